@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: detector frames/sec (whole node) through the shared queue, epix10k2M.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched by
+``torch.distributed.run`` with one rank per GPU.  One STEP = every rank's consumer takes
+``--batch`` frames out of the sharded shared queue and runs the on-GPU peak finder on them.
+Behind it, every rank's producer streams raw epix10k2M frames from a pinned host pool through
+hipMemcpyAsync (side stream) into HBM, calibrates them with the HIP kernels (pedestal + gain
+switching + common mode + mask) directly into ring slots, and the transport routes them to the
+consumer shards (RCCL send/recv over xGMI for N > 1, balanced routing).  W untimed warmup
+steps, then exactly K timed steps bracketed by a barrier + device synchronisation; the time is
+the MAX over ranks; rank 0 prints ONE JSON line.  ``value`` = total frames/s of the node.
+
+Synthetic data: random-init calibration constants and a pre-generated pool of raw frames
+(cycled), because no LCLS data / psana exists offline (BASELINE.json).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import threading
+import time
+
+METRIC = "detector frames/sec (whole node) through SharedQueue, epix10k2M at 1/2/4/8 GPUs"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=32, help="frames per rank per step (consumer batch)")
+    ap.add_argument("--detector", default="epix10k2M")
+    ap.add_argument("--mode", default="calib", choices=["calib", "image", "raw"])
+    ap.add_argument("--common-mode", default="default", help="off | default | flags,thr,maxcorr,npix_min[,bank]")
+    ap.add_argument("--consumer", default="peakfind", choices=["peakfind", "none"])
+    ap.add_argument("--route", default="balanced", choices=["balanced", "local_first", "spread"])
+    ap.add_argument("--queue-size", type=int, default=400, help="logical queue capacity (README.md:20 example)")
+    ap.add_argument("--source", default="host", choices=["host", "device"],
+                    help="host: pinned host pool + H2D (real pipeline); device: raw frames already in HBM")
+    ap.add_argument("--chunk", type=int, default=16, help="frames per producer kernel launch / H2D copy")
+    ap.add_argument("--pool-frames", type=int, default=64)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from psana_ray_amd.config import CommonModeParams, PeakFinderParams
+    from psana_ray_amd.models import Calibrator, Mode
+    from psana_ray_amd.parallel.comm import init_groups
+    from psana_ray_amd.parallel.launch import bind_numa_to_device, detect
+    from psana_ray_amd.pipeline import PeakFinderConsumer, ProducerPipeline
+    from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
+    from psana_ray_amd.source import SyntheticRun
+
+    li = detect()
+    world, rank = li.size, li.rank
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"bench.py: --gpus {args.gpus} needs a launcher (torch.distributed.run) with one rank per GPU",
+                  file=sys.stderr)
+            return 2
+    if not torch.cuda.is_available():
+        print("bench.py needs a HIP device", file=sys.stderr)
+        return 2
+    device = torch.device(f"cuda:{li.local_rank % torch.cuda.device_count()}")
+    torch.cuda.set_device(device)
+    numa = bind_numa_to_device(device)
+
+    comm = None
+    coord = None
+    if world > 1:
+        comm = init_groups(rank, world, device)
+        coord = dist.new_group(backend="gloo")
+
+    def barrier():
+        if coord is not None:
+            dist.barrier(group=coord)
+
+    mode = Mode(args.mode)
+    cm = CommonModeParams.parse(args.common_mode) if mode != Mode.raw else None
+    src = SyntheticRun("synthetic", 0, args.detector, rank=rank, size=world, pool_frames=args.pool_frames,
+                       pinned=(args.source == "host"), gen_device=str(device))
+    cal = Calibrator(src.consts, device, mode, common_mode=cm)
+    share = max(1, math.ceil(args.queue_size / world))
+    producer_slots = 2 * args.chunk + args.batch
+    ring = FrameRing(cal.out_shape, cal.out_dtype, device, producer_slots, share)
+    ep = QueueEndpoint(ring, rank, world, comm, route=args.route, max_offer=64)
+    if args.source == "device":
+        # raw pool resident in HBM: isolates the GPU pipeline from PCIe (secondary number)
+        dev_pool = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(device)
+
+        class _DevSrc:
+            spec = src.spec
+            calibrated = False
+
+            def __init__(self):
+                self.k = 0
+
+            def next_events(self, n):
+                from psana_ray_amd.source.synthetic import RawEvent
+                out = []
+                for _ in range(n):
+                    j = self.k % dev_pool.shape[0]
+                    out.append(RawEvent(rank + self.k * world, self.k, dev_pool[j], int(dev_pool[j].data_ptr()), 9.5))
+                    self.k += 1
+                return out
+
+        source = _DevSrc()
+    else:
+        source = src
+    prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk)
+    consumer = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=args.batch) \
+        if args.consumer == "peakfind" else None
+
+    stop = threading.Event()
+    ep.start()
+    pt = threading.Thread(target=prod.run, kwargs=dict(stop=stop), name="producer", daemon=True)
+    pt.start()
+
+    def consume(n_frames):
+        got = 0
+        while got < n_frames:
+            if consumer is not None:
+                got += consumer.poll(timeout=0.05)
+            else:
+                it = ep.get(timeout=0.05)
+                if it is not None:
+                    it.release()
+                    got += 1
+            if ep.failed is not None:
+                raise RuntimeError(f"transport failed: {ep.failed!r}")
+        return got
+
+    def sync():
+        torch.cuda.synchronize(device)
+
+    B = args.batch
+    consume(args.warmup * B)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    p0 = prod.frames
+    consume(args.steps * B)
+    sync()
+    t1 = time.perf_counter()
+    p1 = prod.frames
+    barrier()
+    dt = t1 - t0
+    if coord is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=coord)
+        dt = float(t[0])
+    stop.set()
+    # drain until every producer's EOS arrived
+    while True:
+        try:
+            if consumer is not None:
+                consumer.poll(timeout=0.05)
+            else:
+                it = ep.get(timeout=0.05)
+                if it is not None:
+                    it.release()
+        except EndOfStream:
+            break
+        if ep.failed is not None:
+            break
+    pt.join(timeout=60)
+    ep.join(timeout=60)
+    peaks = consumer.synchronize() if consumer is not None else 0
+    total = world * args.steps * B
+    value = total / dt
+    st = ep.stats()
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * dt / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "float32" if mode != Mode.raw else "uint16",
+        "data": "synthetic (random-init calibration constants, pre-generated raw epix10k2M pool cycled "
+                + ("from pinned host memory via hipMemcpyAsync)" if args.source == "host" else "from HBM)"),
+        "config": {
+            "model": args.detector,
+            "global_batch": world * B,
+            "seq_len": None,
+            "parallelism": f"dp{world}",
+            "frame_shape": list(cal.out_shape),
+            "mode": args.mode,
+            "common_mode": args.common_mode,
+            "consumer": args.consumer,
+            "route": args.route,
+            "queue_size": args.queue_size,
+            "source": args.source,
+            "chunk": args.chunk,
+        },
+        "extra": {
+            "producer_frames_per_s_rank0": round((p1 - p0) / max(dt, 1e-9), 1),
+            "frame_bytes": ring.frame_bytes,
+            "GB_per_s_out": round(value * ring.frame_bytes / 1e9, 2),
+            "peaks_found_rank0": peaks,
+            "queue_full_waits_rank0": prod.full_waits,
+            "transport_rounds_rank0": st.get("rounds", 0),
+            "transport_round_ms_rank0": round(st.get("round_ms", 0.0), 3),
+            "bytes_sent_rank0": st.get("bytes_sent", 0),
+            "numa_node": numa,
+        },
+    }
+    if rank == 0:
+        line = json.dumps(result)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

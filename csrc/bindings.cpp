@@ -1,0 +1,174 @@
+// pybind11 bindings of psana_ray_amd._C.  Device buffers and streams cross the boundary as
+// integers (tensor.data_ptr(), torch.cuda.current_stream().cuda_stream), so this module does
+// not depend on the torch C++ ABI; the Python layer validates shapes/dtypes/devices first.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "common.h"
+#include "runtime.h"
+
+namespace py = pybind11;
+
+namespace pr {
+void launch_calib_basic(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, int64_t npix, int kind,
+                        uint64_t stream);
+void launch_calib_image(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, int64_t npix, int kind,
+                        uint64_t idx, int64_t nout, uint64_t stream);
+void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t pflags, int kind,
+                     int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
+                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream);
+size_t cm_lds_bytes(int asic_rows, int asic_cols);
+void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nout, uint64_t omask,
+                     uint64_t stream);
+void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
+                     float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
+                     uint64_t summary, uint64_t stream);
+}  // namespace pr
+
+using pr::FramePtrs;
+
+static FramePtrs make_ptrs(const std::vector<uint64_t>& in, const std::vector<uint64_t>& out) {
+  pr::check(in.size() == out.size(), "input/output pointer lists differ in length");
+  pr::check(!in.empty() && (int)in.size() <= pr::kMaxFrames, "1..32 frames per launch");
+  FramePtrs fp{};
+  for (size_t i = 0; i < in.size(); ++i) {
+    pr::check(in[i] != 0 && out[i] != 0, "null frame pointer");
+    fp.in[i] = in[i];
+    fp.out[i] = out[i];
+  }
+  return fp;
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "psana_ray_amd native extension: gfx950 HIP kernels + host runtime";
+  m.attr("MAX_FRAMES_PER_LAUNCH") = pr::kMaxFrames;
+  m.attr("KIND_EPIX10KA") = (int)pr::kEpix10ka;
+  m.attr("KIND_JUNGFRAU") = (int)pr::kJungfrau;
+  m.attr("KIND_PLAIN") = (int)pr::kPlain;
+
+  m.def("calib_basic",
+        [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t ped, uint64_t gf,
+           int64_t npix, int kind, uint64_t stream) {
+          pr::launch_calib_basic(make_ptrs(in, out), (int)in.size(), ped, gf, npix, kind, stream);
+        },
+        py::arg("raw_ptrs"), py::arg("out_ptrs"), py::arg("ped"), py::arg("gf"), py::arg("npix"),
+        py::arg("kind"), py::arg("stream"));
+  m.def("calib_image",
+        [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t ped, uint64_t gf,
+           int64_t npix, int kind, uint64_t idx, int64_t nout, uint64_t stream) {
+          pr::launch_calib_image(make_ptrs(in, out), (int)in.size(), ped, gf, npix, kind, idx, nout, stream);
+        },
+        py::arg("raw_ptrs"), py::arg("out_ptrs"), py::arg("ped"), py::arg("gf"), py::arg("npix"),
+        py::arg("kind"), py::arg("idx"), py::arg("nout"), py::arg("stream"));
+  m.def("calib_cm",
+        [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t ped, uint64_t gf,
+           uint64_t pflags, int kind, int n_panels, int panel_rows, int panel_cols, int asic_rows,
+           int asic_cols, float thr, float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream) {
+          pr::launch_calib_cm(make_ptrs(in, out), (int)in.size(), ped, gf, pflags, kind, n_panels, panel_rows,
+                              panel_cols, asic_rows, asic_cols, thr, maxcorr, npix_min, flags, bank_cols, stream);
+        },
+        py::arg("raw_ptrs"), py::arg("out_ptrs"), py::arg("ped"), py::arg("gf"), py::arg("pflags"),
+        py::arg("kind"), py::arg("n_panels"), py::arg("panel_rows"), py::arg("panel_cols"),
+        py::arg("asic_rows"), py::arg("asic_cols"), py::arg("thr"), py::arg("maxcorr"), py::arg("npix_min"),
+        py::arg("flags"), py::arg("bank_cols"), py::arg("stream"));
+  m.def("cm_lds_bytes", &pr::cm_lds_bytes);
+  m.def("assemble",
+        [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t idx, int64_t nout,
+           uint64_t omask, uint64_t stream) {
+          pr::launch_assemble(make_ptrs(in, out), (int)in.size(), idx, nout, omask, stream);
+        },
+        py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("idx"), py::arg("nout"), py::arg("omask"),
+        py::arg("stream"));
+  m.def("peakfind",
+        [](const std::vector<uint64_t>& in, int n_panels, int rows, int cols, float thr_peak, float son_min,
+           int radius, int max_peaks, uint64_t peaks, uint64_t counts, uint64_t summary, uint64_t stream) {
+          std::vector<uint64_t> dummy(in.size(), 1);
+          pr::launch_peakfind(make_ptrs(in, dummy), (int)in.size(), n_panels, rows, cols, thr_peak, son_min,
+                              radius, max_peaks, peaks, counts, summary, stream);
+        },
+        py::arg("in_ptrs"), py::arg("n_panels"), py::arg("rows"), py::arg("cols"), py::arg("thr_peak"),
+        py::arg("son_min"), py::arg("radius"), py::arg("max_peaks"), py::arg("peaks"), py::arg("counts"),
+        py::arg("summary"), py::arg("stream"));
+
+  m.def("memcpy_h2d_async", &pr::memcpy_h2d_async, py::arg("dst"), py::arg("src"), py::arg("bytes"),
+        py::arg("stream"));
+  m.def("memcpy_h2d_batch", &pr::memcpy_h2d_batch, py::arg("dst"), py::arg("src"), py::arg("bytes"),
+        py::arg("stream"));
+
+  py::class_<pr::PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())
+      .def(py::init<size_t>(), py::arg("bytes"))
+      .def_property_readonly("ptr", &pr::PinnedBuffer::ptr)
+      .def_property_readonly("nbytes", &pr::PinnedBuffer::bytes)
+      .def_buffer([](pr::PinnedBuffer& b) -> py::buffer_info {
+        return py::buffer_info(b.raw(), 1, py::format_descriptor<uint8_t>::format(), 1, {(py::ssize_t)b.bytes()},
+                               {(py::ssize_t)1});
+      });
+
+  py::class_<pr::SlotHeader>(m, "SlotHeader")
+      .def(py::init<>())
+      .def(py::init([](int64_t rank, int64_t idx, int64_t gevt, double pe, int64_t aux) {
+             pr::SlotHeader h;
+             h.rank = rank;
+             h.idx = idx;
+             h.gevt = gevt;
+             h.photon_energy = pe;
+             h.aux = aux;
+             return h;
+           }),
+           py::arg("rank"), py::arg("idx"), py::arg("gevt"), py::arg("photon_energy"), py::arg("aux") = 0)
+      .def_readwrite("rank", &pr::SlotHeader::rank)
+      .def_readwrite("idx", &pr::SlotHeader::idx)
+      .def_readwrite("gevt", &pr::SlotHeader::gevt)
+      .def_readwrite("photon_energy", &pr::SlotHeader::photon_energy)
+      .def_readwrite("aux", &pr::SlotHeader::aux);
+
+  py::class_<pr::PoolStats>(m, "PoolStats")
+      .def_readonly("produced", &pr::PoolStats::produced)
+      .def_readonly("routed_local", &pr::PoolStats::routed_local)
+      .def_readonly("sent", &pr::PoolStats::sent)
+      .def_readonly("received", &pr::PoolStats::received)
+      .def_readonly("got", &pr::PoolStats::got)
+      .def_readonly("released", &pr::PoolStats::released)
+      .def_readonly("produce_full", &pr::PoolStats::produce_full);
+
+  using SP = pr::SlotPool;
+  py::class_<SP>(m, "SlotPool")
+      .def(py::init<int, int, int>(), py::arg("producer_budget"), py::arg("consumer_budget"), py::arg("device"))
+      .def_property_readonly("n_slots", &SP::n_slots)
+      .def_property_readonly("producer_budget", &SP::producer_budget)
+      .def_property_readonly("consumer_budget", &SP::consumer_budget)
+      .def("try_acquire_produce", &SP::try_acquire_produce)
+      .def("acquire_produce", &SP::acquire_produce, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
+      .def("commit_produce", &SP::commit_produce, py::arg("slot"), py::arg("header"), py::arg("stream"))
+      .def("abort_produce", &SP::abort_produce)
+      .def("produced", &SP::produced, py::arg("max_n"))
+      .def("n_produced", &SP::n_produced)
+      .def("producer_held", &SP::producer_held)
+      .def("route_local", &SP::route_local)
+      .def("begin_send", &SP::begin_send)
+      .def("end_send", &SP::end_send, py::arg("slot"), py::arg("stream"))
+      .def("credits", &SP::credits)
+      .def("begin_recv", &SP::begin_recv)
+      .def("end_recv", &SP::end_recv, py::arg("slot"), py::arg("header"), py::arg("stream"))
+      .def("try_get", &SP::try_get)
+      .def("get", &SP::get, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
+      .def("release", &SP::release, py::arg("slot"), py::arg("stream"))
+      .def("n_ready", &SP::n_ready)
+      .def("consumer_held", &SP::consumer_held)
+      .def("wait_ready_on", &SP::wait_ready_on, py::arg("slot"), py::arg("stream"))
+      .def("wait_free_on", &SP::wait_free_on, py::arg("slot"), py::arg("stream"))
+      .def("sync_ready", &SP::sync_ready, py::call_guard<py::gil_scoped_release>())
+      .def("header", &SP::header)
+      .def("state", &SP::state)
+      .def("stats", &SP::stats)
+      .def("wake_all", &SP::wake_all);
+
+  py::class_<pr::RawRunReader>(m, "RawRunReader")
+      .def(py::init<const std::string&, int>(), py::arg("path"), py::arg("n_threads") = 4)
+      .def_property_readonly("n_events", &pr::RawRunReader::n_events)
+      .def_property_readonly("frame_bytes", &pr::RawRunReader::frame_bytes)
+      .def_property_readonly("record_bytes", &pr::RawRunReader::record_bytes)
+      .def_property_readonly("header_bytes", &pr::RawRunReader::header_bytes)
+      .def("read", &pr::RawRunReader::read, py::arg("events"), py::arg("dst_ptrs"),
+           py::call_guard<py::gil_scoped_release>());
+}

@@ -1,0 +1,220 @@
+// K-01 / K-02 / K-04: fused gain-decode + pedestal subtraction + gain factor + pixel mask.
+// K-05 (fused variant): the same math evaluated directly at assembled-image positions.
+//
+// Reference parity: psana-ray never calibrates itself; it receives already calibrated frames
+// from psana_wrapper.iter_events(mode) (psana_ray/producer.py:88, mode chosen at :156-159) and
+// then applies `np.where(mask, data, 0)` (producer.py:92-95).  Here the whole chain is one
+// memory-bound streaming pass on the GPU.
+//
+// Design (MI355X):
+//  * one thread owns 8 consecutive pixels: one 16-B raw load + two 16-B f32 stores per frame
+//    (Guideline 13: 16 B / lane).
+//  * the per-pixel constants (pedestal and gain-factor for every candidate gain, the mask
+//    folded into the gain factor) are loaded ONCE per thread and reused for every frame of the
+//    batch (up to kMaxFrames per launch), so constant traffic is amortised over the batch and
+//    the kernel streams raw-in + f32-out only: 6 B / pixel / frame.
+//  * per-frame pointers travel in the kernel-argument block, so outputs can be scattered HBM
+//    ring slots (no packing copy).
+#include "common.h"
+
+namespace pr {
+
+template <int KIND>
+struct KindTraits;
+template <>
+struct KindTraits<kEpix10ka> { static constexpr int NT = 2; };
+template <>
+struct KindTraits<kJungfrau> { static constexpr int NT = 3; };
+template <>
+struct KindTraits<kPlain> { static constexpr int NT = 1; };
+
+template <int NT>
+__device__ __forceinline__ float pick(const float (&t)[NT][8], int i, int c) {
+  if constexpr (NT == 1) {
+    return t[0][i];
+  } else if constexpr (NT == 2) {
+    return c ? t[1][i] : t[0][i];
+  } else {
+    return c == 0 ? t[0][i] : (c == 1 ? t[1][i] : t[2][i]);
+  }
+}
+
+template <int KIND, int NT>
+__device__ __forceinline__ void calib8(const uint4 r, const float (&p)[NT][8],
+                                       const float (&g)[NT][8], float4& o0, float4& o1) {
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  float o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t raw = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+    bool valid;
+    const int c = decode_cand(raw, KIND, valid);
+    const float adu = decode_adu(raw, KIND);
+    const float v = (adu - pick<NT>(p, i, c)) * pick<NT>(g, i, c);
+    o[i] = valid ? v : 0.0f;
+  }
+  o0 = make_float4(o[0], o[1], o[2], o[3]);
+  o1 = make_float4(o[4], o[5], o[6], o[7]);
+}
+
+template <int NT>
+__device__ __forceinline__ void load_tab8(const float* __restrict__ tab, int64_t npix, int64_t pix0,
+                                          float (&t)[NT][8]) {
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    const float4 a = *reinterpret_cast<const float4*>(tab + k * npix + pix0);
+    const float4 b = *reinterpret_cast<const float4*>(tab + k * npix + pix0 + 4);
+    t[k][0] = a.x; t[k][1] = a.y; t[k][2] = a.z; t[k][3] = a.w;
+    t[k][4] = b.x; t[k][5] = b.y; t[k][6] = b.z; t[k][7] = b.w;
+  }
+}
+
+// raw frames: u16 [npix] each (fp.in[f]); outputs: f32 [npix] each (fp.out[f]).
+template <int KIND>
+__global__ __launch_bounds__(256) void calib_basic_kernel(const FramePtrs fp, const int nframes,
+                                                          const float* __restrict__ ped,
+                                                          const float* __restrict__ gf,
+                                                          const int64_t npix) {
+  constexpr int NT = KindTraits<KIND>::NT;
+  const int64_t nvec = npix >> 3;
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= nvec) return;
+  const int64_t pix0 = v * 8;
+  float p[NT][8], g[NT][8];
+  load_tab8<NT>(ped, npix, pix0, p);
+  load_tab8<NT>(gf, npix, pix0, g);
+
+  int f = 0;
+  // 4 frames in flight per thread: 4 independent 16-B loads before the first use.
+  for (; f + 4 <= nframes; f += 4) {
+    uint4 r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      r[k] = ld_nt_u4(reinterpret_cast<const uint4*>(fp.in[f + k]) + v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float4 o0, o1;
+      calib8<KIND, NT>(r[k], p, g, o0, o1);
+      float4* out = reinterpret_cast<float4*>(fp.out[f + k]) + 2 * v;
+      out[0] = o0;
+      out[1] = o1;
+    }
+  }
+  for (; f < nframes; ++f) {
+    const uint4 r = ld_nt_u4(reinterpret_cast<const uint4*>(fp.in[f]) + v);
+    float4 o0, o1;
+    calib8<KIND, NT>(r, p, g, o0, o1);
+    float4* out = reinterpret_cast<float4*>(fp.out[f]) + 2 * v;
+    out[0] = o0;
+    out[1] = o1;
+  }
+}
+
+// Fused raw -> assembled image (image mode without common mode).  One thread owns 4
+// consecutive output pixels; idx[o] is the flat source pixel of output o or -1 (gap).
+// Constants are gathered once per thread and reused over the frame batch.
+template <int KIND>
+__global__ __launch_bounds__(256) void calib_image_kernel(const FramePtrs fp, const int nframes,
+                                                          const float* __restrict__ ped,
+                                                          const float* __restrict__ gf,
+                                                          const int64_t npix,
+                                                          const int32_t* __restrict__ idx,
+                                                          const int64_t nout) {
+  constexpr int NT = KindTraits<KIND>::NT;
+  const int64_t o0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (o0 >= nout) return;
+  int32_t src[4];
+  float p[NT][4], g[NT][4];
+  const bool full = (o0 + 4 <= nout);
+  if (full) {
+    const int4 s = *reinterpret_cast<const int4*>(idx + o0);
+    src[0] = s.x; src[1] = s.y; src[2] = s.z; src[3] = s.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) src[i] = (o0 + i < nout) ? idx[o0 + i] : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      p[k][i] = src[i] >= 0 ? ped[k * npix + src[i]] : 0.0f;
+      g[k][i] = src[i] >= 0 ? gf[k * npix + src[i]] : 0.0f;
+    }
+  }
+  for (int f = 0; f < nframes; ++f) {
+    const uint16_t* raw = reinterpret_cast<const uint16_t*>(fp.in[f]);
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float val = 0.0f;
+      if (src[i] >= 0) {
+        const uint32_t r = raw[src[i]];
+        bool valid;
+        const int c = decode_cand(r, KIND, valid);
+        float pp, gg;
+        if constexpr (NT == 1) {
+          pp = p[0][i]; gg = g[0][i];
+        } else if constexpr (NT == 2) {
+          pp = c ? p[1][i] : p[0][i]; gg = c ? g[1][i] : g[0][i];
+        } else {
+          pp = c == 0 ? p[0][i] : (c == 1 ? p[1][i] : p[2][i]);
+          gg = c == 0 ? g[0][i] : (c == 1 ? g[1][i] : g[2][i]);
+        }
+        val = valid ? (decode_adu(r, KIND) - pp) * gg : 0.0f;
+      }
+      o[i] = val;
+    }
+    float* out = reinterpret_cast<float*>(fp.out[f]);
+    if (full) {
+      *reinterpret_cast<float4*>(out + o0) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+      for (int i = 0; i < 4 && o0 + i < nout; ++i) out[o0 + i] = o[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------------------
+void launch_calib_basic(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, int64_t npix,
+                        int kind, uint64_t stream) {
+  check(nframes >= 1 && nframes <= kMaxFrames, "calib_basic: nframes out of range");
+  check(npix % 8 == 0, "calib_basic: npix must be a multiple of 8");
+  check(aligned16(ped) && aligned16(gf), "calib_basic: constant tables must be 16-B aligned");
+  for (int f = 0; f < nframes; ++f)
+    check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_basic: frame buffers must be 16-B aligned");
+  const int64_t nvec = npix / 8;
+  const dim3 grid((unsigned)((nvec + 255) / 256));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float* P = reinterpret_cast<const float*>(ped);
+  const float* G = reinterpret_cast<const float*>(gf);
+  switch (kind) {
+    case kEpix10ka: hipLaunchKernelGGL(calib_basic_kernel<kEpix10ka>, grid, dim3(256), 0, s, fp, nframes, P, G, npix); break;
+    case kJungfrau: hipLaunchKernelGGL(calib_basic_kernel<kJungfrau>, grid, dim3(256), 0, s, fp, nframes, P, G, npix); break;
+    case kPlain: hipLaunchKernelGGL(calib_basic_kernel<kPlain>, grid, dim3(256), 0, s, fp, nframes, P, G, npix); break;
+    default: check(false, "calib_basic: unknown gain kind");
+  }
+  hip_check(hipGetLastError(), "calib_basic launch");
+}
+
+void launch_calib_image(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, int64_t npix,
+                        int kind, uint64_t idx, int64_t nout, uint64_t stream) {
+  check(nframes >= 1 && nframes <= kMaxFrames, "calib_image: nframes out of range");
+  check(aligned16(idx), "calib_image: index map must be 16-B aligned");
+  for (int f = 0; f < nframes; ++f) check(aligned16(fp.out[f]), "calib_image: outputs must be 16-B aligned");
+  const int64_t nthr = (nout + 3) / 4;
+  const dim3 grid((unsigned)((nthr + 255) / 256));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float* P = reinterpret_cast<const float*>(ped);
+  const float* G = reinterpret_cast<const float*>(gf);
+  const int32_t* I = reinterpret_cast<const int32_t*>(idx);
+  switch (kind) {
+    case kEpix10ka: hipLaunchKernelGGL(calib_image_kernel<kEpix10ka>, grid, dim3(256), 0, s, fp, nframes, P, G, npix, I, nout); break;
+    case kJungfrau: hipLaunchKernelGGL(calib_image_kernel<kJungfrau>, grid, dim3(256), 0, s, fp, nframes, P, G, npix, I, nout); break;
+    case kPlain: hipLaunchKernelGGL(calib_image_kernel<kPlain>, grid, dim3(256), 0, s, fp, nframes, P, G, npix, I, nout); break;
+    default: check(false, "calib_image: unknown gain kind");
+  }
+  hip_check(hipGetLastError(), "calib_image launch");
+}
+
+}  // namespace pr

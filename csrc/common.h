@@ -1,0 +1,69 @@
+// Shared definitions for the psana_ray_amd HIP kernels (gfx950 / CDNA4 only).
+//
+// Everything here is written for 64-lane wavefronts and launched on caller-provided
+// hipStream_t handles (the Python layer passes torch's current stream as an integer),
+// so the extension has no dependency on the torch C++ ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+namespace pr {
+
+constexpr int kWave = 64;
+// Max frames per launch: per-frame input/output pointers travel in the kernel argument
+// block (2 * 32 * 8 B = 512 B), so ring slots need not be contiguous.
+constexpr int kMaxFrames = 32;
+
+struct FramePtrs {
+  uint64_t in[kMaxFrames];
+  uint64_t out[kMaxFrames];
+};
+
+// Gain decoding families (parameters, not verified psana facts).
+//  kEpix10ka: ADU = raw & 0x3FFF; bit 14 selects candidate table b (auto-ranging switched)
+//             vs a.  Candidates per pixel are pre-resolved from the pixel gain config on
+//             the host (FH/FM/FL/AHL/AML -> (a, b) gain indices), so the kernel sees 2 tables.
+//  kJungfrau: ADU = raw & 0x3FFF; gain bits = raw >> 14: 0 -> G0, 1 -> G1, 3 -> G2,
+//             2 -> invalid (pixel output 0).  3 tables.
+//  kPlain:    ADU = raw (no gain bits), 1 table.
+enum GainKind : int { kEpix10ka = 0, kJungfrau = 1, kPlain = 2 };
+
+__device__ __forceinline__ int decode_cand(uint32_t raw, int kind, bool& valid) {
+  valid = true;
+  if (kind == kEpix10ka) return (raw >> 14) & 1;
+  if (kind == kJungfrau) {
+    uint32_t g = raw >> 14;
+    valid = (g != 2u);
+    return g == 3u ? 2 : (int)(g & 1u);
+  }
+  return 0;
+}
+
+__device__ __forceinline__ float decode_adu(uint32_t raw, int kind) {
+  return (float)(kind == kPlain ? raw : (raw & 0x3FFFu));
+}
+
+inline void check(bool ok, const std::string& msg) {
+  if (!ok) throw std::runtime_error("psana_ray_amd: " + msg);
+}
+
+inline void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("psana_ray_amd HIP error in ") + what + ": " +
+                             hipGetErrorString(e));
+}
+
+inline bool aligned16(uint64_t p) { return (p & 15u) == 0; }
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// 16-B streaming (non-temporal) load: data read exactly once (raw frames).
+__device__ __forceinline__ uint4 ld_nt_u4(const void* p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+}  // namespace pr

@@ -1,0 +1,354 @@
+// K-03 common-mode correction, fused with K-01/K-02/K-04 in ONE pass over HBM.
+//
+// Reference parity: psana applies common mode inside det.calib (reached through
+// psana_wrapper.iter_events, psana_ray/producer.py:88); psana-ray itself has no numerics.
+// Semantics implemented here (psana "mode 7"-like, every knob a parameter):
+//   v = ADU - ped[gain]                                   (pre-gain, ADU domain)
+//   eligible = good-mask && gain in the CM gain set
+//   rows:  for every ASIC row and every bank of `bank_cols` columns, median of the eligible
+//          pixels with |v| < thr; if count >= npix_min and |median| <= maxcorr, subtract it
+//          from every eligible pixel of that row-bank segment
+//   cols:  then the same per ASIC column (all ASIC rows)
+//   out = v * gain_factor   (mask folded into the gain factor -> masked pixels are 0)
+// Median = numpy semantics (mean of the two middle elements for an even count).
+//
+// MI355X design: one 1024-thread workgroup (16 waves) owns one (frame, ASIC) tile.  The
+// whole pre-gain tile lives in LDS (176 x 193 f32 incl. a 1-float row pad that makes column
+// reads bank-conflict free, + 4 bits of per-pixel state = 152.8 KB of the 160 KB), so HBM is
+// touched exactly once: raw u16 in, f32 out.  Medians are exact: every row-bank segment
+// (<= 64 px) is one wave-register bitonic sort, every column (<= 256 px) a 4-register bitonic
+// sort across the wave, with DPP / ds_swizzle lane exchanges (no LDS round trips).
+#include "common.h"
+
+namespace pr {
+
+// ---- lane exchange: y = x from lane (lane ^ J) -----------------------------------------
+template <int J>
+__device__ __forceinline__ float xor_lane(float x) {
+  const int xi = __float_as_int(x);
+  int yi;
+  if constexpr (J == 1) {
+    yi = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    yi = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4 || J == 8 || J == 16) {
+    yi = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (J << 10));  // bitmask mode, xor J in 32-lane groups
+  } else {
+    static_assert(J == 32, "xor_lane: J must be a power of two < 64");
+    yi = __shfl_xor(xi, 32);
+  }
+  return __int_as_float(yi);
+}
+
+// ---- bitonic sort of NR independent 64-element sequences (element index = lane) --------
+template <int K, int J, int NR>
+__device__ __forceinline__ void seg_step(float (&x)[NR], int lane) {
+  const bool up = (lane & K) == 0;
+  const bool lower = (lane & J) == 0;
+  const bool take_min = (lower == up);
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const float y = xor_lane<J>(x[r]);
+    x[r] = take_min ? fminf(x[r], y) : fmaxf(x[r], y);
+  }
+}
+template <int K, int J, int NR>
+__device__ __forceinline__ void seg_merge(float (&x)[NR], int lane) {
+  seg_step<K, J, NR>(x, lane);
+  if constexpr (J > 1) seg_merge<K, J / 2, NR>(x, lane);
+}
+template <int K, int NR>
+__device__ __forceinline__ void seg_sort_from(float (&x)[NR], int lane) {
+  seg_merge<K, K / 2, NR>(x, lane);
+  if constexpr (K < 64) seg_sort_from<K * 2, NR>(x, lane);
+}
+
+// ---- bitonic sort of ONE 256-element sequence held as x[r] at element r*64 + lane -------
+template <int K, int J>
+__device__ __forceinline__ void col_step(float (&x)[4], int lane) {
+  if constexpr (J >= 64) {
+    constexpr int JR = J / 64;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if ((r & JR) == 0) {
+        const int q = r | JR;
+        const bool up = ((r * 64) & K) == 0;
+        const float lo = fminf(x[r], x[q]);
+        const float hi = fmaxf(x[r], x[q]);
+        x[r] = up ? lo : hi;
+        x[q] = up ? hi : lo;
+      }
+    }
+  } else {
+    const bool lower = (lane & J) == 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool up = ((r * 64 + lane) & K) == 0;
+      const float y = xor_lane<J>(x[r]);
+      x[r] = (lower == up) ? fminf(x[r], y) : fmaxf(x[r], y);
+    }
+  }
+}
+template <int K, int J>
+__device__ __forceinline__ void col_merge(float (&x)[4], int lane) {
+  col_step<K, J>(x, lane);
+  if constexpr (J > 1) col_merge<K, J / 2>(x, lane);
+}
+template <int K>
+__device__ __forceinline__ void col_sort_from(float (&x)[4], int lane) {
+  col_merge<K, K / 2>(x, lane);
+  if constexpr (K < 256) col_sort_from<K * 2>(x, lane);
+}
+
+__device__ __forceinline__ float lane_value(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+
+// numpy-median of the `cnt` smallest (sorted) values; element e lives in register e>>6, lane e&63.
+__device__ __forceinline__ float median_sorted4(const float (&x)[4], int cnt) {
+  const int i0 = __builtin_amdgcn_readfirstlane((cnt - 1) >> 1);
+  const int i1 = __builtin_amdgcn_readfirstlane(cnt >> 1);
+  const int r0 = i0 >> 6, r1 = i1 >> 6;
+  const float s0 = r0 == 0 ? x[0] : (r0 == 1 ? x[1] : (r0 == 2 ? x[2] : x[3]));
+  const float s1 = r1 == 0 ? x[0] : (r1 == 1 ? x[1] : (r1 == 2 ? x[2] : x[3]));
+  const float a = lane_value(s0, i0 & 63);
+  const float b = lane_value(s1, i1 & 63);
+  return (a + b) * 0.5f;
+}
+
+struct CmParams {
+  float thr;        // |v| < thr participates in the median estimate
+  float maxcorr;    // a correction with |median| > maxcorr is not applied
+  int npix_min;     // minimum participating pixels for a correction
+  int flags;        // bit0: rows by bank, bit1: columns
+  int bank_cols;    // columns per bank (<= 64, divides the ASIC width)
+};
+
+struct TileGeom {
+  int panel_rows, panel_cols;  // H, W of one panel
+  int asic_rows, asic_cols;    // R, C of one ASIC tile
+  int asics_per_col, asics_per_row;  // H / R, W / C
+  int64_t npix;                // pixels per frame
+};
+
+// per-pixel nibble in LDS: bits0-1 candidate, bit2 good, bit3 cm-eligible
+template <int KIND>
+__global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, const float* __restrict__ ped,
+                                                        const float* __restrict__ gf,
+                                                        const uint8_t* __restrict__ pflags,
+                                                        const TileGeom tg, const CmParams cp) {
+  constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int R = tg.asic_rows, C = tg.asic_cols, LD = C + 1;
+  float* tile = reinterpret_cast<float*>(smem);
+  uint32_t* nib = reinterpret_cast<uint32_t*>(smem + (((size_t)R * LD * 4 + 15) & ~(size_t)15));
+  const int C8 = C >> 3;
+
+  const int asic = blockIdx.x;
+  const int f = blockIdx.y;
+  const int per_panel = tg.asics_per_col * tg.asics_per_row;
+  const int panel = asic / per_panel;
+  const int ar = (asic % per_panel) / tg.asics_per_row;
+  const int ac = (asic % per_panel) % tg.asics_per_row;
+  const int64_t base = (int64_t)panel * tg.panel_rows * tg.panel_cols +
+                       (int64_t)ar * R * tg.panel_cols + (int64_t)ac * C;
+  const uint16_t* raw = reinterpret_cast<const uint16_t*>(fp.in[f]);
+  float* out = reinterpret_cast<float*>(fp.out[f]);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int nwaves = blockDim.x >> 6;
+
+  // ---- phase 1: decode + pedestal into LDS ---------------------------------------------
+  for (int i = tid; i < R * C8; i += blockDim.x) {
+    const int r = i / C8, c = (i % C8) * 8;
+    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
+    const uint4 rw = ld_nt_u4(raw + pix);
+    const uint2 fl = *reinterpret_cast<const uint2*>(pflags + pix);
+    const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
+    const uint32_t fw[2] = {fl.x, fl.y};
+    float pa[NT][8];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      const float4 a = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix);
+      const float4 b = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix + 4);
+      pa[k][0] = a.x; pa[k][1] = a.y; pa[k][2] = a.z; pa[k][3] = a.w;
+      pa[k][4] = b.x; pa[k][5] = b.y; pa[k][6] = b.z; pa[k][7] = b.w;
+    }
+    uint32_t nb = 0;
+    float* trow = tile + r * LD + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t rv = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+      const uint32_t pf = (fw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      bool valid;
+      const int cand = decode_cand(rv, KIND, valid);
+      float pp;
+      if constexpr (NT == 1) pp = pa[0][j];
+      else if constexpr (NT == 2) pp = cand ? pa[1][j] : pa[0][j];
+      else pp = cand == 0 ? pa[0][j] : (cand == 1 ? pa[1][j] : pa[2][j]);
+      const bool good = valid && (pf & 1u);
+      const bool elig = good && ((pf >> (1 + cand)) & 1u);
+      trow[j] = decode_adu(rv, KIND) - pp;
+      nb |= (uint32_t)(cand | (good ? 4 : 0) | (elig ? 8 : 0)) << (4 * j);
+    }
+    nib[r * C8 + (c >> 3)] = nb;
+  }
+  __syncthreads();
+
+  const float INF = __int_as_float(0x7f800000);
+
+  // ---- phase 2a: row common mode per bank segment ---------------------------------------
+  if (cp.flags & 1) {
+    const int L = cp.bank_cols;
+    const int nbanks = C / L;
+    for (int r = wave; r < R; r += nwaves) {
+      float* trow = tile + r * LD;
+      for (int b0 = 0; b0 < nbanks; b0 += 4) {
+        float x[4];
+        float v[4];
+        bool el[4];
+        int cnt[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = (b0 + j) * L + lane;
+          const bool in = (b0 + j < nbanks) && (lane < L);
+          v[j] = in ? trow[col] : 0.0f;
+          el[j] = in && ((nib[r * C8 + (col >> 3)] >> (4 * (col & 7) + 3)) & 1u);
+          const bool part = el[j] && (fabsf(v[j]) < cp.thr);
+          x[j] = part ? v[j] : INF;
+          cnt[j] = __popcll(__ballot(part));
+        }
+        seg_sort_from<2, 4>(x, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (cnt[j] >= cp.npix_min && cnt[j] > 0) {
+            const int i0 = __builtin_amdgcn_readfirstlane((cnt[j] - 1) >> 1);
+            const int i1 = __builtin_amdgcn_readfirstlane(cnt[j] >> 1);
+            const float med = (lane_value(x[j], i0) + lane_value(x[j], i1)) * 0.5f;
+            if (fabsf(med) <= cp.maxcorr && el[j]) trow[(b0 + j) * L + lane] = v[j] - med;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- phase 2b: column common mode -------------------------------------------------------
+  if (cp.flags & 2) {
+    for (int c = wave; c < C; c += nwaves) {
+      float x[4], v[4];
+      bool el[4];
+      int cnt = 0;
+      const uint32_t shift = 4 * (c & 7) + 3;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = k * 64 + lane;
+        const bool in = r < R;
+        v[k] = in ? tile[r * LD + c] : 0.0f;
+        el[k] = in && ((nib[r * C8 + (c >> 3)] >> shift) & 1u);
+        const bool part = el[k] && (fabsf(v[k]) < cp.thr);
+        x[k] = part ? v[k] : INF;
+        cnt += __popcll(__ballot(part));
+      }
+      col_sort_from<2>(x, lane);
+      if (cnt >= cp.npix_min && cnt > 0) {
+        const float med = median_sorted4(x, cnt);
+        if (fabsf(med) <= cp.maxcorr) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (el[k]) tile[(k * 64 + lane) * LD + c] = v[k] - med;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- phase 3: gain factor + mask, store -------------------------------------------------
+  for (int i = tid; i < R * C8; i += blockDim.x) {
+    const int r = i / C8, c = (i % C8) * 8;
+    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
+    const uint32_t nb = nib[i];
+    float ga[NT][8];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      const float4 a = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix);
+      const float4 b = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix + 4);
+      ga[k][0] = a.x; ga[k][1] = a.y; ga[k][2] = a.z; ga[k][3] = a.w;
+      ga[k][4] = b.x; ga[k][5] = b.y; ga[k][6] = b.z; ga[k][7] = b.w;
+    }
+    const float* trow = tile + r * LD + c;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t q = (nb >> (4 * j)) & 0xFu;
+      const int cand = q & 3;
+      float gg;
+      if constexpr (NT == 1) gg = ga[0][j];
+      else if constexpr (NT == 2) gg = cand ? ga[1][j] : ga[0][j];
+      else gg = cand == 0 ? ga[0][j] : (cand == 1 ? ga[1][j] : ga[2][j]);
+      o[j] = (q & 4u) ? trow[j] * gg : 0.0f;
+    }
+    float4* op = reinterpret_cast<float4*>(out + pix);
+    op[0] = make_float4(o[0], o[1], o[2], o[3]);
+    op[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
+size_t cm_lds_bytes(int asic_rows, int asic_cols) {
+  const size_t tile = (((size_t)asic_rows * (asic_cols + 1) * 4) + 15) & ~(size_t)15;
+  return tile + (size_t)asic_rows * (asic_cols / 8) * 4;
+}
+
+void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t pflags,
+                     int kind, int n_panels, int panel_rows, int panel_cols, int asic_rows,
+                     int asic_cols, float thr, float maxcorr, int npix_min, int flags,
+                     int bank_cols, uint64_t stream) {
+  check(nframes >= 1 && nframes <= kMaxFrames, "calib_cm: nframes out of range");
+  check(asic_rows >= 1 && asic_rows <= 256, "calib_cm: ASIC rows must be in [1, 256]");
+  check(asic_cols % 8 == 0 && asic_cols >= 8, "calib_cm: ASIC cols must be a multiple of 8");
+  check(panel_rows % asic_rows == 0 && panel_cols % asic_cols == 0, "calib_cm: panel not tiled by ASICs");
+  check(bank_cols >= 1 && bank_cols <= 64 && asic_cols % bank_cols == 0,
+        "calib_cm: bank_cols must be <= 64 and divide the ASIC width");
+  check(panel_cols % 8 == 0, "calib_cm: panel cols must be a multiple of 8");
+  const size_t lds = cm_lds_bytes(asic_rows, asic_cols);
+  check(lds <= 160 * 1024, "calib_cm: ASIC tile does not fit in 160 KiB of LDS");
+  check(aligned16(ped) && aligned16(gf) && (pflags & 7) == 0, "calib_cm: misaligned constant tables");
+  for (int f = 0; f < nframes; ++f)
+    check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_cm: frame buffers must be 16-B aligned");
+  TileGeom tg;
+  tg.panel_rows = panel_rows;
+  tg.panel_cols = panel_cols;
+  tg.asic_rows = asic_rows;
+  tg.asic_cols = asic_cols;
+  tg.asics_per_col = panel_rows / asic_rows;
+  tg.asics_per_row = panel_cols / asic_cols;
+  tg.npix = (int64_t)n_panels * panel_rows * panel_cols;
+  CmParams cp{thr, maxcorr, npix_min, flags, bank_cols};
+  const dim3 grid((unsigned)(n_panels * tg.asics_per_col * tg.asics_per_row), (unsigned)nframes);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float* P = reinterpret_cast<const float*>(ped);
+  const float* G = reinterpret_cast<const float*>(gf);
+  const uint8_t* F = reinterpret_cast<const uint8_t*>(pflags);
+  switch (kind) {
+    case kEpix10ka:
+      hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kEpix10ka>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
+      hipLaunchKernelGGL(calib_cm_kernel<kEpix10ka>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp);
+      break;
+    case kJungfrau:
+      hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kJungfrau>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
+      hipLaunchKernelGGL(calib_cm_kernel<kJungfrau>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp);
+      break;
+    case kPlain:
+      hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kPlain>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
+      hipLaunchKernelGGL(calib_cm_kernel<kPlain>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp);
+      break;
+    default: check(false, "calib_cm: unknown gain kind");
+  }
+  hip_check(hipGetLastError(), "calib_cm launch");
+}
+
+}  // namespace pr

@@ -1,0 +1,424 @@
+#include "runtime.h"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <future>
+#include <stdexcept>
+
+#include "common.h"
+
+namespace pr {
+
+// ---------------------------------------------------------------------------------------
+PinnedBuffer::PinnedBuffer(size_t bytes) : bytes_(bytes) {
+  check(bytes > 0, "PinnedBuffer: size must be > 0");
+  hip_check(hipHostMalloc(&ptr_, bytes, hipHostMallocDefault), "hipHostMalloc");
+}
+
+PinnedBuffer::~PinnedBuffer() {
+  if (ptr_) (void)hipHostFree(ptr_);
+}
+
+// ---------------------------------------------------------------------------------------
+SlotPool::SlotPool(int producer_budget, int consumer_budget, int device)
+    : pb_(producer_budget), cb_(consumer_budget), n_(producer_budget + consumer_budget), device_(device) {
+  check(producer_budget >= 0 && consumer_budget >= 0 && n_ > 0, "SlotPool: budgets must be >= 0 and sum > 0");
+  state_.assign(n_, kFree);
+  hdr_.resize(n_);
+  free_ev_valid_.assign(n_, 0);
+  for (int i = 0; i < n_; ++i) free_list_.push_back(i);
+  if (device_ >= 0) {
+    set_device();
+    ready_ev_.resize(n_);
+    free_ev_.resize(n_);
+    for (int i = 0; i < n_; ++i) {
+      hip_check(hipEventCreateWithFlags(&ready_ev_[i], hipEventDisableTiming), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&free_ev_[i], hipEventDisableTiming), "hipEventCreate");
+    }
+  }
+}
+
+SlotPool::~SlotPool() {
+  if (device_ >= 0) {
+    set_device();
+    for (auto e : ready_ev_) (void)hipEventDestroy(e);
+    for (auto e : free_ev_) (void)hipEventDestroy(e);
+  }
+}
+
+void SlotPool::set_device() const {
+  if (device_ >= 0) hip_check(hipSetDevice(device_), "hipSetDevice");
+}
+
+void SlotPool::check_slot(int slot) const {
+  check(slot >= 0 && slot < n_, "SlotPool: slot index out of range");
+}
+
+void SlotPool::record(hipEvent_t ev, uint64_t stream) const {
+  hip_check(hipEventRecord(ev, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord");
+}
+
+static std::string state_msg(const char* op, int want, int got) {
+  return std::string("SlotPool.") + op + ": slot in state " + std::to_string(got) + ", expected " +
+         std::to_string(want);
+}
+
+int SlotPool::try_acquire_produce() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (producer_held_ >= pb_ || free_list_.empty()) {
+    ++st_.produce_full;
+    return -1;
+  }
+  const int s = free_list_.front();
+  free_list_.pop_front();
+  state_[s] = kProducing;
+  ++producer_held_;
+  return s;
+}
+
+int SlotPool::acquire_produce(double timeout_s) {
+  std::unique_lock<std::mutex> lk(mu_);
+  const auto pred = [&] { return closed_ || (producer_held_ < pb_ && !free_list_.empty()); };
+  if (!pred()) ++st_.produce_full;
+  if (timeout_s < 0) {
+    cv_produce_.wait(lk, pred);
+  } else if (!cv_produce_.wait_for(lk, std::chrono::duration<double>(timeout_s), pred)) {
+    return -1;
+  }
+  if (closed_) return -1;
+  const int s = free_list_.front();
+  free_list_.pop_front();
+  state_[s] = kProducing;
+  ++producer_held_;
+  return s;
+}
+
+void SlotPool::commit_produce(int slot, const SlotHeader& h, uint64_t stream) {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  check(state_[slot] == kProducing, state_msg("commit_produce", kProducing, state_[slot]));
+  hdr_[slot] = h;
+  if (device_ >= 0) {
+    set_device();
+    record(ready_ev_[slot], stream);
+  }
+  state_[slot] = kProduced;
+  produced_fifo_.push_back(slot);
+  ++st_.produced;
+}
+
+void SlotPool::abort_produce(int slot) {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  check(state_[slot] == kProducing, state_msg("abort_produce", kProducing, state_[slot]));
+  state_[slot] = kFree;
+  --producer_held_;
+  free_list_.push_front(slot);
+  cv_produce_.notify_one();
+}
+
+std::vector<int> SlotPool::produced(int max_n) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<int> out;
+  for (int s : produced_fifo_) {
+    if ((int)out.size() >= max_n) break;
+    out.push_back(s);
+  }
+  return out;
+}
+
+int SlotPool::n_produced() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return (int)produced_fifo_.size();
+}
+
+int SlotPool::producer_held() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return producer_held_;
+}
+
+static void erase_value(std::deque<int>& q, int v) {
+  for (auto it = q.begin(); it != q.end(); ++it)
+    if (*it == v) {
+      q.erase(it);
+      return;
+    }
+  throw std::runtime_error("psana_ray_amd: SlotPool internal FIFO corruption");
+}
+
+void SlotPool::route_local(int slot) {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  check(state_[slot] == kProduced, state_msg("route_local", kProduced, state_[slot]));
+  check(consumer_held_ < cb_, "SlotPool.route_local: no consumer credit");
+  erase_value(produced_fifo_, slot);
+  state_[slot] = kReady;
+  --producer_held_;
+  ++consumer_held_;
+  ready_fifo_.push_back(slot);
+  ++st_.routed_local;
+  cv_ready_.notify_one();
+  cv_produce_.notify_one();
+}
+
+void SlotPool::begin_send(int slot) {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  check(state_[slot] == kProduced, state_msg("begin_send", kProduced, state_[slot]));
+  erase_value(produced_fifo_, slot);
+  state_[slot] = kSending;
+}
+
+void SlotPool::end_send(int slot, uint64_t stream) {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  check(state_[slot] == kSending, state_msg("end_send", kSending, state_[slot]));
+  if (device_ >= 0) {
+    set_device();
+    record(free_ev_[slot], stream);
+    free_ev_valid_[slot] = 1;
+  }
+  state_[slot] = kFree;
+  --producer_held_;
+  free_list_.push_back(slot);
+  ++st_.sent;
+  cv_produce_.notify_one();
+}
+
+int SlotPool::credits() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return cb_ - consumer_held_;
+}
+
+int SlotPool::begin_recv() {
+  std::lock_guard<std::mutex> lk(mu_);
+  check(consumer_held_ < cb_, "SlotPool.begin_recv: no consumer credit");
+  check(!free_list_.empty(), "SlotPool.begin_recv: no free slot");
+  const int s = free_list_.front();
+  free_list_.pop_front();
+  state_[s] = kReceiving;
+  ++consumer_held_;
+  return s;
+}
+
+void SlotPool::end_recv(int slot, const SlotHeader& h, uint64_t stream) {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  check(state_[slot] == kReceiving, state_msg("end_recv", kReceiving, state_[slot]));
+  hdr_[slot] = h;
+  if (device_ >= 0) {
+    set_device();
+    record(ready_ev_[slot], stream);
+  }
+  state_[slot] = kReady;
+  ready_fifo_.push_back(slot);
+  ++st_.received;
+  cv_ready_.notify_one();
+}
+
+int SlotPool::try_get() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (ready_fifo_.empty()) return -1;
+  const int s = ready_fifo_.front();
+  ready_fifo_.pop_front();
+  state_[s] = kLeased;
+  ++st_.got;
+  return s;
+}
+
+int SlotPool::get(double timeout_s) {
+  std::unique_lock<std::mutex> lk(mu_);
+  const auto pred = [&] { return closed_ || !ready_fifo_.empty(); };
+  if (timeout_s < 0) {
+    cv_ready_.wait(lk, pred);
+  } else if (!cv_ready_.wait_for(lk, std::chrono::duration<double>(timeout_s), pred)) {
+    return -1;
+  }
+  if (ready_fifo_.empty()) return -1;
+  const int s = ready_fifo_.front();
+  ready_fifo_.pop_front();
+  state_[s] = kLeased;
+  ++st_.got;
+  return s;
+}
+
+void SlotPool::release(int slot, uint64_t stream) {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  check(state_[slot] == kLeased, state_msg("release", kLeased, state_[slot]));
+  if (device_ >= 0) {
+    set_device();
+    record(free_ev_[slot], stream);
+    free_ev_valid_[slot] = 1;
+  }
+  state_[slot] = kFree;
+  --consumer_held_;
+  free_list_.push_back(slot);
+  ++st_.released;
+  cv_produce_.notify_one();
+}
+
+int SlotPool::n_ready() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return (int)ready_fifo_.size();
+}
+
+int SlotPool::consumer_held() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return consumer_held_;
+}
+
+void SlotPool::wait_ready_on(int slot, uint64_t stream) const {
+  check_slot(slot);
+  if (device_ < 0) return;
+  set_device();
+  hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ready_ev_[slot], 0), "hipStreamWaitEvent");
+}
+
+void SlotPool::wait_free_on(int slot, uint64_t stream) const {
+  check_slot(slot);
+  if (device_ < 0) return;
+  bool valid;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    valid = free_ev_valid_[slot] != 0;
+  }
+  if (!valid) return;
+  set_device();
+  hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), free_ev_[slot], 0), "hipStreamWaitEvent");
+}
+
+void SlotPool::sync_ready(int slot) const {
+  check_slot(slot);
+  if (device_ < 0) return;
+  set_device();
+  hip_check(hipEventSynchronize(ready_ev_[slot]), "hipEventSynchronize");
+}
+
+SlotHeader SlotPool::header(int slot) const {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  return hdr_[slot];
+}
+
+int SlotPool::state(int slot) const {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  return state_[slot];
+}
+
+PoolStats SlotPool::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return st_;
+}
+
+void SlotPool::wake_all() {
+  std::lock_guard<std::mutex> lk(mu_);
+  closed_ = true;
+  cv_produce_.notify_all();
+  cv_ready_.notify_all();
+}
+
+// ---------------------------------------------------------------------------------------
+namespace {
+struct RunHeader {
+  char magic[8];
+  uint32_t version;
+  uint32_t header_bytes;
+  char det[64];
+  uint32_t ndim;
+  uint32_t pad0;
+  uint64_t shape[4];
+  uint32_t dtype_bytes;
+  uint32_t pad1;
+  uint64_t n_events;
+  uint64_t record_bytes;
+};
+constexpr int64_t kRecordHeaderBytes = 32;
+
+void pread_full(int fd, void* dst, size_t n, off_t off) {
+  char* p = static_cast<char*>(dst);
+  while (n > 0) {
+    const ssize_t r = ::pread(fd, p, n, off);
+    if (r < 0 && errno == EINTR) continue;
+    check(r > 0, "RawRunReader: short read");
+    p += r;
+    n -= (size_t)r;
+    off += r;
+  }
+}
+}  // namespace
+
+RawRunReader::RawRunReader(const std::string& path, int n_threads) : n_threads_(n_threads < 1 ? 1 : n_threads) {
+  fd_ = ::open(path.c_str(), O_RDONLY);
+  check(fd_ >= 0, "RawRunReader: cannot open " + path);
+  RunHeader h;
+  pread_full(fd_, &h, sizeof(h), 0);
+  check(std::memcmp(h.magic, "PRAWRUN1", 8) == 0, "RawRunReader: bad magic in " + path);
+  header_bytes_ = h.header_bytes;
+  n_events_ = (int64_t)h.n_events;
+  record_bytes_ = (int64_t)h.record_bytes;
+  frame_bytes_ = record_bytes_ - kRecordHeaderBytes;
+  check(frame_bytes_ > 0, "RawRunReader: bad record size");
+}
+
+RawRunReader::~RawRunReader() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+std::vector<std::pair<int64_t, double>> RawRunReader::read(const std::vector<int64_t>& events,
+                                                           const std::vector<uint64_t>& dst_ptrs) {
+  check(events.size() == dst_ptrs.size(), "RawRunReader.read: events / dst size mismatch");
+  const size_t n = events.size();
+  std::vector<std::pair<int64_t, double>> meta(n);
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      check(events[i] >= 0 && events[i] < n_events_, "RawRunReader.read: event index out of range");
+      const off_t off = (off_t)(header_bytes_ + events[i] * record_bytes_);
+      int64_t rh[4];
+      pread_full(fd_, rh, sizeof(rh), off);
+      double pe;
+      std::memcpy(&pe, &rh[1], sizeof(double));
+      meta[i] = {rh[0], pe};
+      pread_full(fd_, reinterpret_cast<void*>(dst_ptrs[i]), (size_t)frame_bytes_, off + kRecordHeaderBytes);
+    }
+  };
+  const int nt = (int)std::min<size_t>((size_t)n_threads_, n);
+  std::vector<std::future<void>> fs;
+  for (int t = 1; t < nt; ++t) fs.push_back(std::async(std::launch::async, work));
+  work();
+  for (auto& f : fs) f.get();
+  return meta;
+}
+
+// ---------------------------------------------------------------------------------------
+// hipMemcpyDefault: pinned host -> HBM (the staging path) or HBM -> HBM (device-resident source)
+void memcpy_h2d_async(uint64_t dst, uint64_t src, size_t bytes, uint64_t stream) {
+  hip_check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), bytes,
+                           hipMemcpyDefault, reinterpret_cast<hipStream_t>(stream)),
+            "hipMemcpyAsync");
+}
+
+void memcpy_h2d_batch(const std::vector<uint64_t>& dst, const std::vector<uint64_t>& src, size_t bytes,
+                      uint64_t stream) {
+  check(dst.size() == src.size(), "memcpy_h2d_batch: size mismatch");
+  // coalesce runs that are contiguous on both sides into one copy
+  size_t i = 0;
+  while (i < dst.size()) {
+    size_t j = i + 1;
+    while (j < dst.size() && dst[j] == dst[j - 1] + bytes && src[j] == src[j - 1] + bytes) ++j;
+    memcpy_h2d_async(dst[i], src[i], bytes * (j - i), stream);
+    i = j;
+  }
+}
+
+}  // namespace pr

@@ -1,0 +1,161 @@
+// Native host runtime of psana_ray_amd: pinned staging memory, the HBM slot pool that backs
+// the sharded shared queue, and the raw-run file reader (the data loader).
+//
+// Reference parity:
+//  * SlotPool replaces the single-threaded Ray actor `Queue` (psana_ray/shared_queue.py:4-31):
+//    bounded capacity with put->False backpressure (Q-4), FIFO get, non-blocking get->None,
+//    size().  Unlike the actor it is sharded (one pool per GPU), lock-protected for many
+//    threads, and every slot carries HIP events so producers, the RCCL transport and
+//    consumers order on-device work without host synchronisation.
+//  * PinnedBuffer / memcpy_h2d_async implement the "stage raw events into pinned host pages
+//    with hipMemcpyAsync on a side stream" path that replaces psana's CPU-side numpy frames
+//    (psana_ray/producer.py:88).
+//  * RawRunReader is the native event reader behind the raw-run file source (stands in for
+//    psana's XTC reader when psana is absent).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace pr {
+
+// ---------------------------------------------------------------------------------------
+class PinnedBuffer {
+ public:
+  explicit PinnedBuffer(size_t bytes);
+  ~PinnedBuffer();
+  PinnedBuffer(const PinnedBuffer&) = delete;
+  PinnedBuffer& operator=(const PinnedBuffer&) = delete;
+  uint64_t ptr() const { return reinterpret_cast<uint64_t>(ptr_); }
+  size_t bytes() const { return bytes_; }
+  void* raw() const { return ptr_; }
+
+ private:
+  void* ptr_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+// ---------------------------------------------------------------------------------------
+enum SlotState : int {
+  kFree = 0,
+  kProducing = 1,
+  kProduced = 2,
+  kSending = 3,
+  kReceiving = 4,
+  kReady = 5,
+  kLeased = 6,
+};
+
+struct SlotHeader {
+  int64_t rank = -1;        // producer rank (reference item field 0)
+  int64_t idx = -1;         // rank-local event index (reference item field 1)
+  int64_t gevt = -1;        // global event id (new: lets consumers dedupe / order)
+  double photon_energy = 0; // NaN encodes None (Q-16)
+  int64_t aux = 0;          // free for the caller (e.g. timestamp)
+};
+
+struct PoolStats {
+  int64_t produced = 0, routed_local = 0, sent = 0, received = 0, got = 0, released = 0;
+  int64_t produce_full = 0;  // acquire attempts refused because the producer budget was full
+};
+
+class SlotPool {
+ public:
+  // device < 0: host-only pool (no events).  n_slots = producer_budget + consumer_budget.
+  SlotPool(int producer_budget, int consumer_budget, int device);
+  ~SlotPool();
+  SlotPool(const SlotPool&) = delete;
+  SlotPool& operator=(const SlotPool&) = delete;
+
+  int n_slots() const { return n_; }
+  int producer_budget() const { return pb_; }
+  int consumer_budget() const { return cb_; }
+
+  // producer side
+  int try_acquire_produce();
+  int acquire_produce(double timeout_s);  // -1 on timeout
+  void commit_produce(int slot, const SlotHeader& h, uint64_t stream);
+  void abort_produce(int slot);
+  std::vector<int> produced(int max_n) const;  // FIFO order, not popped
+  int n_produced() const;
+  int producer_held() const;
+
+  // routing outcomes
+  void route_local(int slot);
+  void begin_send(int slot);
+  void end_send(int slot, uint64_t stream);
+
+  // consumer side
+  int credits() const;
+  int begin_recv();
+  void end_recv(int slot, const SlotHeader& h, uint64_t stream);
+  int try_get();
+  int get(double timeout_s);
+  void release(int slot, uint64_t stream);
+  int n_ready() const;
+  int consumer_held() const;
+
+  // ordering helpers
+  void wait_ready_on(int slot, uint64_t stream) const;  // stream waits for the slot's data
+  void wait_free_on(int slot, uint64_t stream) const;   // stream waits until the slot may be rewritten
+  void sync_ready(int slot) const;                      // host waits for the slot's data
+  SlotHeader header(int slot) const;
+  int state(int slot) const;
+  PoolStats stats() const;
+  void wake_all();  // wake blocked waiters (shutdown)
+
+ private:
+  void set_device() const;
+  void check_slot(int slot) const;
+  void record(hipEvent_t ev, uint64_t stream) const;
+
+  int pb_, cb_, n_, device_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_produce_, cv_ready_;
+  std::vector<int> state_;
+  std::vector<SlotHeader> hdr_;
+  std::vector<hipEvent_t> ready_ev_, free_ev_;
+  std::vector<char> free_ev_valid_;
+  std::deque<int> free_list_, produced_fifo_, ready_fifo_;
+  int producer_held_ = 0, consumer_held_ = 0;
+  bool closed_ = false;
+  PoolStats st_;
+};
+
+// ---------------------------------------------------------------------------------------
+// Raw-run file: fixed-size records so event i is at header_bytes + i * record_bytes.
+//   file header (4096 B): magic "PRAWRUN1", u32 version, u32 header_bytes, char det[64],
+//   u32 ndim, u64 shape[4], u32 dtype_bytes, u64 n_events, u64 record_bytes
+//   record: i64 gevt, f64 photon_energy, i64 timestamp, i64 reserved, then the raw frame
+class RawRunReader {
+ public:
+  RawRunReader(const std::string& path, int n_threads);
+  ~RawRunReader();
+  int64_t n_events() const { return n_events_; }
+  int64_t frame_bytes() const { return frame_bytes_; }
+  int64_t record_bytes() const { return record_bytes_; }
+  int64_t header_bytes() const { return header_bytes_; }
+  // Synchronously reads events[i] into dst_ptrs[i] (frame bytes) using the thread pool and
+  // returns (gevt, photon_energy) per event.
+  std::vector<std::pair<int64_t, double>> read(const std::vector<int64_t>& events,
+                                               const std::vector<uint64_t>& dst_ptrs);
+
+ private:
+  int fd_ = -1;
+  int n_threads_;
+  int64_t n_events_ = 0, frame_bytes_ = 0, record_bytes_ = 0, header_bytes_ = 0;
+};
+
+// ---------------------------------------------------------------------------------------
+void memcpy_h2d_async(uint64_t dst, uint64_t src, size_t bytes, uint64_t stream);
+void memcpy_h2d_batch(const std::vector<uint64_t>& dst, const std::vector<uint64_t>& src, size_t bytes,
+                      uint64_t stream);
+
+}  // namespace pr

@@ -1,0 +1,118 @@
+"""Shared defaults and configuration dataclasses.
+
+One module owns every default so producer and consumer agree (fixes reference quirk Q-3: the
+reference producer defaults ``queue_name='my'`` / ``ray_namespace='default'``
+(psana_ray/producer.py:26-27) while its DataReader defaults ``queue_name='shared_queue'`` /
+``ray_namespace='my'`` (psana_ray/data_reader.py:5), so the documented consumer cannot find the
+documented producer's queue).  The producer CLI keeps the reference's exact flag defaults; the
+consumer side now defaults to the SAME values.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+# --- reference CLI defaults (psana_ray/producer.py:17-33) -------------------------------
+DEFAULT_RAY_ADDRESS = "auto"          # :25
+DEFAULT_RAY_NAMESPACE = "default"     # :26
+DEFAULT_QUEUE_NAME = "my"             # :27
+DEFAULT_QUEUE_SIZE = 100              # :28 (also shared_queue.py:6,33)
+DEFAULT_NUM_CONSUMERS = 1             # :29
+DEFAULT_LOG_LEVEL = "INFO"            # :31
+LOG_LEVELS = ["DEBUG", "INFO", "WARNING", "ERROR", "CRITICAL"]  # :32
+
+# --- reference retry / backoff constants -------------------------------------------------
+BACKOFF_BASE_S = 0.1                  # producer.py:85
+BACKOFF_MAX_S = 2.0                   # producer.py:86
+BACKOFF_JITTER_S = 0.5                # producer.py:109
+TRANSIENT_RETRY_SLEEP_S = 1.0         # producer.py:117
+QUEUE_LOOKUP_RETRIES = 10             # producer.py:35
+QUEUE_LOOKUP_DELAY_S = 1.0            # producer.py:35
+CONSUMER_POLL_SLEEP_S = 1.0           # examples/psana_consumer.py:40
+
+# --- rendezvous ---------------------------------------------------------------------------
+DEFAULT_STORE_PORT = 6379             # the Ray head port of README.md:15, reused for the store
+ENV_ADDRESS = "PSANA_RAY_ADDRESS"
+
+
+def resolve_address(address: Optional[str]) -> tuple[str, int]:
+    """Map the reference's ``--ray_address`` value to a rendezvous ``(host, port)``.
+
+    ``"auto"`` (the reference default) means: ``$PSANA_RAY_ADDRESS`` if set, else
+    ``127.0.0.1:6379``.  ``host``, ``host:port`` and ``ray://host:port`` are accepted.
+    """
+    if address is None or address == "auto":
+        address = os.environ.get(ENV_ADDRESS, f"127.0.0.1:{DEFAULT_STORE_PORT}")
+    if "://" in address:
+        address = address.split("://", 1)[1]
+    if ":" in address:
+        host, port = address.rsplit(":", 1)
+        return host or "127.0.0.1", int(port)
+    return address, DEFAULT_STORE_PORT
+
+
+@dataclass
+class CommonModeParams:
+    """psana "mode 7"-like common-mode parameters (K-03).
+
+    flags: bit0 = rows by bank segment, bit1 = columns (within each ASIC).
+    thr: only pixels with |ADU - pedestal| < thr estimate the median.
+    maxcorr: corrections with |median| > maxcorr are skipped.
+    npix_min: minimum number of participating pixels.
+    """
+
+    flags: int = 3
+    thr: float = 30.0
+    maxcorr: float = 50.0
+    npix_min: int = 10
+    bank_cols: Optional[int] = None   # None -> detector default (epix10ka: 48)
+
+    @staticmethod
+    def parse(text: Optional[str]) -> Optional["CommonModeParams"]:
+        """``"off"``/``None`` -> None; ``"default"`` -> defaults; else ``flags,thr,maxcorr,npix_min[,bank]``."""
+        if text is None or text.lower() in ("", "none", "off", "0"):
+            return None
+        if text.lower() in ("default", "on", "1"):
+            return CommonModeParams()
+        parts = [p.strip() for p in text.split(",")]
+        cm = CommonModeParams(flags=int(parts[0]))
+        if len(parts) > 1:
+            cm.thr = float(parts[1])
+        if len(parts) > 2:
+            cm.maxcorr = float(parts[2]) if parts[2].lower() != "inf" else math.inf
+        if len(parts) > 3:
+            cm.npix_min = int(parts[3])
+        if len(parts) > 4:
+            cm.bank_cols = int(parts[4])
+        return cm
+
+
+@dataclass
+class PeakFinderParams:
+    """K-07 consumer peak finder parameters."""
+
+    thr_peak: float = 20.0   # keV-domain threshold on the calibrated pixel
+    son_min: float = 5.0     # minimum signal-over-noise vs the background ring
+    radius: int = 1          # local-maximum window radius (1 -> 3x3, 2 -> 5x5)
+    max_peaks: int = 2048    # peak records kept per frame
+
+
+@dataclass
+class QueueConfig:
+    """Everything that defines one shared queue instance."""
+
+    queue_name: str = DEFAULT_QUEUE_NAME
+    ray_namespace: str = DEFAULT_RAY_NAMESPACE
+    address: str = DEFAULT_RAY_ADDRESS
+    queue_size: int = DEFAULT_QUEUE_SIZE
+    num_consumers: int = DEFAULT_NUM_CONSUMERS
+    # physical HBM slots are capped by this fraction of free device memory (H-8: queue_size is
+    # a LOGICAL bound, the reference never pre-allocates: shared_queue.py:7)
+    hbm_fraction: float = 0.80
+    producer_slots: int = 64          # calibrated frames a producer may hold un-routed
+    max_offer: int = 64               # frames a producer offers per transport round
+    route: str = "balanced"           # balanced | local_first | spread
+    connect_timeout_s: float = 300.0
+    extra: dict = field(default_factory=dict)

@@ -1,0 +1,158 @@
+"""The calibration "model": raw detector frames -> frames in the requested retrieval mode.
+
+This is the work psana does inside ``PsanaWrapperSmd.iter_events(mode)`` for psana-ray
+(psana_ray/producer.py:88, mode from ``--calib`` at :156-159) plus the reference's own masking
+(:92-95) and ndim fix-up (:96-97), re-designed as gfx950 kernels writing straight into the
+destination buffers (HBM ring slots):
+
+  mode=raw    raw u16 frames, untouched                         -> (P, H, W) uint16
+  mode=calib  K-01..K-04 (+K-03 common mode if enabled)         -> (P, H, W) float32
+  mode=image  the above + K-05 geometry assembly                -> (1, Himg, Wimg) float32
+
+On a CUDA(HIP) device the HIP kernels are mandatory (no silent PyTorch fallback); on
+``device="cpu"`` the fp32 golden model (ops.reference) is the explicit compute path.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..config import CommonModeParams
+from ..ops import kernels, reference
+from .constants import CalibConstants
+from .detector import Mode
+from .geometry import Geometry, make_geometry
+
+
+class Calibrator:
+    def __init__(self, consts: CalibConstants, device, mode: Mode = Mode.calib,
+                 mask: Optional[np.ndarray] = None, common_mode: Optional[CommonModeParams] = None,
+                 geometry: Optional[Geometry] = None):
+        self.consts = consts
+        self.spec = consts.spec
+        self.device = torch.device(device)
+        self.mode = Mode(mode) if not isinstance(mode, Mode) else mode
+        self.cm = common_mode
+        if self.cm is not None and self.cm.bank_cols is None:
+            self.cm = CommonModeParams(self.cm.flags, self.cm.thr, self.cm.maxcorr, self.cm.npix_min,
+                                       self.spec.bank_cols)
+        spec = self.spec
+        # masks: frame-shaped masks fold into the tables; image-shaped ones apply at assembly
+        self.geometry = geometry
+        frame_mask, image_mask = None, None
+        if mask is not None:
+            m = np.asarray(mask)
+            if m.size == spec.npix:
+                frame_mask = m.reshape(spec.frame_shape).astype(bool)
+            else:
+                if self.mode != Mode.image:
+                    raise ValueError(f"mask of shape {m.shape} does not match frame shape {spec.frame_shape}")
+                image_mask = m
+        self.frame_mask = frame_mask
+        if self.mode == Mode.image:
+            self.geometry = geometry or make_geometry(spec)
+            if image_mask is not None and image_mask.size != int(np.prod(self.geometry.image_shape)):
+                raise ValueError(f"image mask of shape {image_mask.shape} does not match image {self.geometry.image_shape}")
+        self.image_mask = image_mask
+
+        self._gpu = self.device.type == "cuda"
+        ped, gf, pflags = consts.device_tables(frame_mask)
+        if self._gpu:
+            kernels._ext.load()  # fail loudly on a GPU box without the extension
+            self.ped = torch.from_numpy(ped).to(self.device)
+            self.gf = torch.from_numpy(gf).to(self.device)
+            self.pflags = torch.from_numpy(pflags).to(self.device)
+            if self.mode == Mode.image:
+                self.idx = torch.from_numpy(self.geometry.index_map()).to(self.device)
+                self.omask = None if image_mask is None else \
+                    torch.from_numpy(np.asarray(image_mask).astype(np.uint8).ravel()).to(self.device)
+            if self.cm is not None:
+                kernels._ext.load().cm_lds_bytes(spec.asic_rows, spec.asic_cols)
+        self._scratch: Optional[torch.Tensor] = None
+
+    # ------------------------------------------------------------------------------------
+    @property
+    def out_shape(self):
+        if self.mode == Mode.image:
+            return (1, *self.geometry.image_shape)
+        return self.spec.frame_shape
+
+    @property
+    def out_dtype(self):
+        return torch.uint16 if self.mode == Mode.raw else torch.float32
+
+    @property
+    def out_frame_bytes(self) -> int:
+        return int(np.prod(self.out_shape)) * (2 if self.mode == Mode.raw else 4)
+
+    def _scratch_frames(self, n: int) -> List[torch.Tensor]:
+        if self._scratch is None or self._scratch.shape[0] < n:
+            self._scratch = torch.empty((max(n, kernels.MAX_FRAMES), *self.spec.frame_shape), dtype=torch.float32,
+                                        device=self.device)
+        return [self._scratch[i] for i in range(n)]
+
+    def run(self, raw: Sequence[torch.Tensor], out: Sequence[torch.Tensor], stream=None) -> None:
+        """Calibrate ``raw[i]`` (uint16, frame shape) into ``out[i]`` (``out_shape``) on ``stream``."""
+        if len(raw) != len(out):
+            raise ValueError("raw/out length mismatch")
+        if not raw:
+            return
+        if not self._gpu:
+            self._run_reference(raw, out)
+            return
+        kind = self.spec.kernel_kind
+        if self.mode == Mode.raw:
+            ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
+            with ctx:
+                for r, o in zip(raw, out):
+                    o.copy_(r.view(o.shape), non_blocking=True)
+            return
+        if self.mode == Mode.calib:
+            if self.cm is None:
+                kernels.calib_basic(raw, out, self.ped, self.gf, kind, stream)
+            else:
+                kernels.calib_cm(raw, out, self.ped, self.gf, self.pflags, kind, self.spec, self.cm, stream)
+            return
+        # image mode
+        if self.cm is None and self.image_mask is None:
+            kernels.calib_image(raw, out, self.ped, self.gf, kind, self.idx, stream)
+            return
+        for a in range(0, len(raw), kernels.MAX_FRAMES):
+            b = min(len(raw), a + kernels.MAX_FRAMES)
+            tmp = self._scratch_frames(b - a)
+            if self.cm is None:
+                kernels.calib_basic(raw[a:b], tmp, self.ped, self.gf, kind, stream)
+            else:
+                kernels.calib_cm(raw[a:b], tmp, self.ped, self.gf, self.pflags, kind, self.spec, self.cm, stream)
+            kernels.assemble(tmp, out[a:b], self.idx, self.spec.npix, self.omask, stream)
+
+    def _run_reference(self, raw, out):
+        if self.mode == Mode.raw:
+            for r, o in zip(raw, out):
+                o.copy_(r.view(o.shape))
+            return
+        batch = torch.stack([r.view(self.spec.frame_shape) for r in raw])
+        cal = reference.calibrate_reference(batch, self.consts, self.frame_mask, self.cm)
+        if self.mode == Mode.image:
+            cal = reference.assemble_reference(cal, self.geometry.rows, self.geometry.cols,
+                                               self.geometry.image_shape, self.image_mask)
+        for i, o in enumerate(out):
+            o.copy_(cal[i].view(o.shape))
+
+    def __call__(self, raw: torch.Tensor, stream=None) -> torch.Tensor:
+        """Convenience: [F, P, H, W] (or [P, H, W]) uint16 -> newly allocated output batch."""
+        if raw.dim() == 3:
+            raw = raw.unsqueeze(0)
+        out = torch.empty((raw.shape[0], *self.out_shape), dtype=self.out_dtype, device=raw.device)
+        self.run([raw[i] for i in range(raw.shape[0])], [out[i] for i in range(raw.shape[0])], stream)
+        return out
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

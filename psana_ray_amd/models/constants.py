@@ -1,0 +1,117 @@
+"""Per-run calibration constants (pedestals, gains, status, gain configuration).
+
+psana reads these from its calibration database for ``(exp, run, detector)``; psana-ray reaches
+them only implicitly through ``iter_events(mode)`` (psana_ray/producer.py:88) and
+``create_bad_pixel_mask()`` (:81).  Offline there is no calibration DB, so constants are
+random-initialised with physically plausible magnitudes (BASELINE.json: "random-init calibration
+constants"), deterministically from a seed derived from ``(exp, run, detector)``.
+
+``device_tables`` packs them into the kernel layout: per candidate gain table ``c`` and pixel
+``p`` -> pedestal ``ped[c, p]`` and gain factor ``gf[c, p] = mask[p] / gain[g(c, p)]``, plus a
+per-pixel flag byte (bit0 output mask, bit1+c common-mode eligible for candidate c).
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+from .detector import EPIX_CAND_A, EPIX_CAND_B, DetectorSpec
+
+# nominal gains (ADU per keV) and pedestal levels (ADU); domain values, not psana facts
+_EPIX_GAIN = (16.4, 5.47, 0.164, 16.4, 5.47, 0.164, 0.164)
+_EPIX_PED = (2500.0, 2500.0, 1800.0, 2500.0, 2500.0, 1800.0, 1800.0)
+_JF_GAIN = (41.0, -1.5, -0.11)
+_JF_PED = (3000.0, 14500.0, 15000.0)
+# default common-mode gain set: high / medium gains (epix: FH, FM, AHL-H, AML-M; jungfrau: G0)
+EPIX_CM_GAINS = (0, 1, 3, 4)
+JUNGFRAU_CM_GAINS = (0,)
+
+
+def run_seed(exp: str, run: int, detector: str) -> int:
+    h = hashlib.sha256(f"{exp}/{run}/{detector}".encode()).digest()
+    return int.from_bytes(h[:4], "little")
+
+
+@dataclass
+class CalibConstants:
+    spec: DetectorSpec
+    pedestals: np.ndarray           # [G, P, H, W] float32
+    gains: np.ndarray               # [G, P, H, W] float32 (ADU / keV)
+    status: np.ndarray              # [P, H, W] uint8, nonzero = bad pixel
+    gain_config: Optional[np.ndarray] = None   # epix: [P, H, W] uint8 in 0..4 (FH FM FL AHL AML)
+    cm_gains: Sequence[int] = field(default_factory=tuple)
+
+    @classmethod
+    def random(cls, spec: DetectorSpec, seed: int = 0, bad_fraction: float = 0.005,
+               gain_config: str = "AHL") -> "CalibConstants":
+        """Random-init constants.  ``gain_config``: one of FH FM FL AHL AML or ``"mixed"``."""
+        rng = np.random.default_rng(seed)
+        shape = spec.frame_shape
+        G = spec.n_gains
+        if spec.kind == "epix10ka":
+            gain0, ped0, cmg = _EPIX_GAIN, _EPIX_PED, EPIX_CM_GAINS
+            ped_sd = 150.0
+        elif spec.kind == "jungfrau":
+            gain0, ped0, cmg = _JF_GAIN, _JF_PED, JUNGFRAU_CM_GAINS
+            ped_sd = 200.0
+        else:
+            gain0, ped0, cmg = (1.0,), (100.0,), (0,)
+            ped_sd = 5.0
+        ped = np.empty((G, *shape), np.float32)
+        gains = np.empty((G, *shape), np.float32)
+        for g in range(G):
+            ped[g] = (ped0[g] + ped_sd * rng.standard_normal(shape)).astype(np.float32)
+            gains[g] = (gain0[g] * (1.0 + 0.03 * rng.standard_normal(shape))).astype(np.float32)
+        status = (rng.random(shape) < bad_fraction).astype(np.uint8)
+        cfg = None
+        if spec.kind == "epix10ka":
+            names = ("FH", "FM", "FL", "AHL", "AML")
+            if gain_config == "mixed":
+                cfg = rng.integers(0, 5, size=shape, dtype=np.uint8)
+            else:
+                cfg = np.full(shape, names.index(gain_config), np.uint8)
+        return cls(spec, ped, gains, status, cfg, tuple(cmg))
+
+    # ------------------------------------------------------------------------------------
+    def create_bad_pixel_mask(self) -> np.ndarray:
+        """psana_wrapper.create_bad_pixel_mask() equivalent (producer.py:81): truthy = good."""
+        return (self.status == 0).astype(np.uint8)
+
+    def candidate_gain_index(self) -> np.ndarray:
+        """[NC, P, H, W] gain-range index of each kernel candidate table."""
+        s = self.spec
+        if s.kind == "epix10ka":
+            a = np.asarray(EPIX_CAND_A, np.int64)[self.gain_config]
+            b = np.asarray(EPIX_CAND_B, np.int64)[self.gain_config]
+            return np.stack([a, b])
+        if s.kind == "jungfrau":
+            return np.stack([np.full(s.frame_shape, g, np.int64) for g in range(3)])
+        return np.zeros((1, *s.frame_shape), np.int64)
+
+    def device_tables(self, mask: Optional[np.ndarray] = None):
+        """Kernel tables: ``ped [NC, npix]``, ``gf [NC, npix]`` (mask folded), ``pflags [npix]``.
+
+        ``mask`` is the combined output mask (bad-pixel & manual, truthy = keep) in frame shape;
+        None keeps every pixel (the reference applies masks only when asked, producer.py:92-95).
+        """
+        s = self.spec
+        cand = self.candidate_gain_index()                     # [NC, P, H, W]
+        ped = np.take_along_axis(self.pedestals, cand, axis=0)  # [NC, P, H, W]
+        gain = np.take_along_axis(self.gains, cand, axis=0)
+        keep = np.ones(s.frame_shape, bool) if mask is None else np.asarray(mask).astype(bool)
+        keep = np.broadcast_to(keep, s.frame_shape)
+        gf = np.where(keep[None], np.float32(1.0) / gain, np.float32(0.0)).astype(np.float32)
+        status_good = self.status == 0
+        flags = keep.astype(np.uint8).copy()
+        cm_set = np.zeros(max(s.n_gains, 1), bool)
+        cm_set[list(self.cm_gains)] = True
+        for c in range(cand.shape[0]):
+            elig = keep & status_good & cm_set[cand[c]]
+            flags |= (elig.astype(np.uint8) << (1 + c))
+        npix = s.npix
+        return (np.ascontiguousarray(ped.reshape(-1, npix)),
+                np.ascontiguousarray(gf.reshape(-1, npix)),
+                np.ascontiguousarray(flags.reshape(npix)))

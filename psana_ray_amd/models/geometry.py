@@ -1,0 +1,104 @@
+"""Panel geometry and the image-assembly index map (K-05).
+
+psana assembles calibrated panels into a 2-D image in image mode (the reference's default mode,
+psana_ray/producer.py:22,156-159; SURVEY E-03 / Appendix B).  Without psana geometry files the
+framework builds a synthetic but realistic layout: each panel is placed by an integer
+90-degree rotation + translation (epix10k2M: four 2x2-panel quads in a pinwheel), so every
+panel pixel lands on exactly one image pixel and scatter == gather exactly.
+
+The GPU kernel consumes the inverse map (image pixel -> flat source pixel, -1 for gaps), a
+deterministic, atomics-free gather.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from .detector import DetectorSpec
+
+
+def _rotate(rr: np.ndarray, cc: np.ndarray, h: int, w: int, k: int):
+    """Rotate pixel coordinates of an h x w block by k*90 degrees; returns (rows, cols, h', w')."""
+    k %= 4
+    if k == 0:
+        return rr, cc, h, w
+    if k == 1:
+        return (w - 1 - cc), rr, w, h
+    if k == 2:
+        return (h - 1 - rr), (w - 1 - cc), h, w
+    return cc, (h - 1 - rr), w, h
+
+
+@dataclass
+class Geometry:
+    spec: DetectorSpec
+    image_shape: tuple
+    rows: np.ndarray  # [P, H, W] int32 image row of each panel pixel
+    cols: np.ndarray  # [P, H, W] int32 image col
+
+    def index_map(self) -> np.ndarray:
+        """Flat gather map of the image: source flat pixel index or -1 (gap)."""
+        himg, wimg = self.image_shape
+        idx = np.full(himg * wimg, -1, dtype=np.int32)
+        dst = (self.rows.astype(np.int64) * wimg + self.cols).ravel()
+        idx[dst] = np.arange(self.spec.npix, dtype=np.int32)
+        return idx
+
+    def pixel_coords_um(self):
+        """(x, y) pixel-centre coordinates in micrometres (psana-style geometry output)."""
+        ps = self.spec.pixel_size_um
+        return self.cols * ps, self.rows * ps
+
+
+def _panel_grid(spec: DetectorSpec, gap: int):
+    """Generic layout: panels on a near-square grid, no rotation."""
+    P, H, W = spec.frame_shape
+    ncol = int(math.ceil(math.sqrt(P)))
+    nrow = int(math.ceil(P / ncol))
+    rr, cc = np.meshgrid(np.arange(H), np.arange(W), indexing="ij")
+    rows = np.empty((P, H, W), np.int32)
+    cols = np.empty((P, H, W), np.int32)
+    for p in range(P):
+        gr, gc = divmod(p, ncol)
+        rows[p] = rr + gr * (H + gap)
+        cols[p] = cc + gc * (W + gap)
+    return rows, cols, (nrow * (H + gap) - gap, ncol * (W + gap) - gap)
+
+
+def _epix_quads(spec: DetectorSpec, gap: int):
+    """epix10k2M-like: 4 quads of 2x2 panels, quad q rotated by q*90 deg (pinwheel)."""
+    P, H, W = spec.frame_shape
+    assert P == 16
+    QH, QW = 2 * H + gap, 2 * W + gap
+    cell = max(QH, QW) + 2 * gap
+    rr, cc = np.meshgrid(np.arange(H), np.arange(W), indexing="ij")
+    rows = np.empty((P, H, W), np.int32)
+    cols = np.empty((P, H, W), np.int32)
+    cell_of_quad = [(0, 0), (0, 1), (1, 1), (1, 0)]  # clockwise around the beam
+    for p in range(P):
+        q, i = divmod(p, 4)
+        qr, qc = divmod(i, 2)
+        yr = rr + qr * (H + gap)
+        xc = cc + qc * (W + gap)
+        yr, xc, qh, qw = _rotate(yr, xc, QH, QW, q)
+        cy, cx = cell_of_quad[q]
+        oy = cy * cell + (cell - qh) // 2
+        ox = cx * cell + (cell - qw) // 2
+        rows[p] = yr + oy
+        cols[p] = xc + ox
+    return rows, cols, (2 * cell, 2 * cell)
+
+
+def make_geometry(spec: DetectorSpec) -> Geometry:
+    gap = spec.panel_gap_px
+    if spec.kind == "epix10ka" and spec.n_panels == 16:
+        rows, cols, shape = _epix_quads(spec, gap)
+    else:
+        rows, cols, shape = _panel_grid(spec, gap)
+    geo = Geometry(spec, tuple(int(s) for s in shape), rows, cols)
+    flat = rows.astype(np.int64) * shape[1] + cols
+    assert np.unique(flat).size == spec.npix, "geometry maps two pixels onto one image pixel"
+    assert rows.min() >= 0 and cols.min() >= 0 and rows.max() < shape[0] and cols.max() < shape[1]
+    return geo

@@ -1,0 +1,52 @@
+"""Loader for the native extension ``psana_ray_amd._C`` (HIP kernels + host runtime).
+
+torch is imported first so the process has exactly one HIP runtime: torch ships
+``libamdhip64.so.7`` and the extension links against the same soname (rpath to torch/lib).
+If the extension is missing and ``hipcc`` is available it is built in-tree on first use; on a
+GPU box a missing/failed extension raises -- GPU ops never silently fall back to PyTorch.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the extension: one HIP runtime per process)
+
+_lock = threading.Lock()
+_mod = None
+_err = None
+
+
+def load(build_if_missing: bool = True):
+    global _mod, _err
+    if _mod is not None:
+        return _mod
+    with _lock:
+        if _mod is not None:
+            return _mod
+        try:
+            if build_if_missing and os.environ.get("PSANA_RAY_AMD_NO_BUILD") != "1":
+                from .. import _build
+
+                _build.build()
+            _mod = importlib.import_module("psana_ray_amd._C")
+            return _mod
+        except Exception as e:  # pragma: no cover - surfaced to the caller
+            _err = e
+            raise RuntimeError(f"psana_ray_amd native extension unavailable: {e}") from e
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except Exception:
+        return False
+
+
+def stream_handle(stream=None) -> int:
+    """Raw hipStream_t of a torch stream (default: the current stream of the current device)."""
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)

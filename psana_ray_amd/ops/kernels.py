@@ -1,0 +1,141 @@
+"""Validated torch-facing wrappers of the gfx950 HIP kernels (K-01..K-05, K-07).
+
+Every wrapper checks device / dtype / shape / contiguity / alignment on the host BEFORE the
+launch (a mis-shaped launch of a hand-written kernel can fault the GPU), splits batches into
+launches of at most ``MAX_FRAMES`` frames, and launches on the given torch stream.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from . import _ext
+
+MAX_FRAMES = 32
+
+
+def _ptr(t: torch.Tensor) -> int:
+    return int(t.data_ptr())
+
+
+def _check_frames(frames: Sequence[torch.Tensor], dtype, numel: int, device, what: str):
+    for t in frames:
+        if t.device != device:
+            raise ValueError(f"{what}: tensor on {t.device}, expected {device}")
+        if t.dtype != dtype:
+            raise ValueError(f"{what}: dtype {t.dtype}, expected {dtype}")
+        if t.numel() != numel:
+            raise ValueError(f"{what}: {t.numel()} elements, expected {numel}")
+        if not t.is_contiguous():
+            raise ValueError(f"{what}: tensor must be contiguous")
+        if t.data_ptr() % 16:
+            raise ValueError(f"{what}: tensor must be 16-byte aligned")
+
+
+def _validate_index_map(idx: torch.Tensor, npix: int, what: str):
+    """One-time (cached on the tensor) host check that the gather map stays inside the frame."""
+    if getattr(idx, "_pr_checked_npix", None) == npix:
+        return
+    if idx.dtype != torch.int32 or not idx.is_contiguous() or idx.data_ptr() % 16:
+        raise ValueError(f"{what}: idx must be a contiguous, 16-B aligned int32 tensor")
+    if idx.numel() and (int(idx.max()) >= npix or int(idx.min()) < -1):
+        raise ValueError(f"{what}: index map points outside the frame")
+    idx._pr_checked_npix = npix
+
+
+def _chunks(n: int):
+    for i in range(0, n, MAX_FRAMES):
+        yield i, min(n, i + MAX_FRAMES)
+
+
+def calib_basic(raw: Sequence[torch.Tensor], out: Sequence[torch.Tensor], ped: torch.Tensor, gf: torch.Tensor,
+                kind: int, stream: Optional[torch.cuda.Stream] = None):
+    C = _ext.load()
+    npix = ped.shape[1]
+    dev = ped.device
+    _check_frames(raw, torch.uint16, npix, dev, "calib_basic raw")
+    _check_frames(out, torch.float32, npix, dev, "calib_basic out")
+    if len(raw) != len(out):
+        raise ValueError("calib_basic: raw/out length mismatch")
+    s = _ext.stream_handle(stream)
+    for a, b in _chunks(len(raw)):
+        C.calib_basic([_ptr(t) for t in raw[a:b]], [_ptr(t) for t in out[a:b]], _ptr(ped), _ptr(gf), npix, kind, s)
+
+
+def calib_image(raw, out, ped, gf, kind, idx: torch.Tensor, stream=None):
+    C = _ext.load()
+    npix = ped.shape[1]
+    dev = ped.device
+    nout = idx.numel()
+    _check_frames(raw, torch.uint16, npix, dev, "calib_image raw")
+    _check_frames(out, torch.float32, nout, dev, "calib_image out")
+    if idx.device != dev:
+        raise ValueError("calib_image: idx must be on the kernel device")
+    _validate_index_map(idx, npix, "calib_image")
+    s = _ext.stream_handle(stream)
+    for a, b in _chunks(len(raw)):
+        C.calib_image([_ptr(t) for t in raw[a:b]], [_ptr(t) for t in out[a:b]], _ptr(ped), _ptr(gf), npix, kind,
+                      _ptr(idx), nout, s)
+
+
+def calib_cm(raw, out, ped, gf, pflags, kind, spec, cm, stream=None):
+    C = _ext.load()
+    npix = ped.shape[1]
+    dev = ped.device
+    _check_frames(raw, torch.uint16, npix, dev, "calib_cm raw")
+    _check_frames(out, torch.float32, npix, dev, "calib_cm out")
+    if pflags.dtype != torch.uint8 or pflags.numel() != npix:
+        raise ValueError("calib_cm: pflags must be uint8[npix]")
+    bank = cm.bank_cols or spec.bank_cols
+    lds = C.cm_lds_bytes(spec.asic_rows, spec.asic_cols)
+    if lds > 160 * 1024:
+        raise ValueError(f"common mode: ASIC tile {spec.asic_rows}x{spec.asic_cols} needs {lds} B of LDS (>160 KiB)")
+    s = _ext.stream_handle(stream)
+    for a, b in _chunks(len(raw)):
+        C.calib_cm([_ptr(t) for t in raw[a:b]], [_ptr(t) for t in out[a:b]], _ptr(ped), _ptr(gf), _ptr(pflags), kind,
+                   spec.n_panels, spec.panel_rows, spec.panel_cols, spec.asic_rows, spec.asic_cols,
+                   float(cm.thr), float(cm.maxcorr), int(cm.npix_min), int(cm.flags), int(bank), s)
+
+
+def assemble(frames, out, idx: torch.Tensor, npix: int, omask: Optional[torch.Tensor] = None, stream=None):
+    C = _ext.load()
+    dev = idx.device
+    nout = idx.numel()
+    _check_frames(frames, torch.float32, npix, dev, "assemble in")
+    _check_frames(out, torch.float32, nout, dev, "assemble out")
+    _validate_index_map(idx, npix, "assemble")
+    if omask is not None and (omask.dtype != torch.uint8 or omask.numel() != nout or omask.device != dev):
+        raise ValueError("assemble: omask must be uint8[nout] on the kernel device")
+    s = _ext.stream_handle(stream)
+    for a, b in _chunks(len(frames)):
+        C.assemble([_ptr(t) for t in frames[a:b]], [_ptr(t) for t in out[a:b]], _ptr(idx), nout,
+                   0 if omask is None else _ptr(omask), s)
+
+
+def peakfind(frames: Sequence[torch.Tensor], shape, params, peaks: torch.Tensor, counts: torch.Tensor,
+             summary: torch.Tensor, stream=None):
+    """frames: F tensors of ``shape`` = (P, H, W) f32.  Outputs (zeroed here, on the stream):
+    peaks [F, max_peaks, 8] f32, counts [F] int32, summary [F, 2] f32."""
+    C = _ext.load()
+    P, H, W = shape
+    F = len(frames)
+    if F == 0:
+        return
+    dev = frames[0].device
+    _check_frames(frames, torch.float32, P * H * W, dev, "peakfind in")
+    if peaks.shape != (F, params.max_peaks, 8) or peaks.dtype != torch.float32:
+        raise ValueError("peakfind: peaks must be float32 [F, max_peaks, 8]")
+    if counts.shape != (F,) or counts.dtype != torch.int32:
+        raise ValueError("peakfind: counts must be int32 [F]")
+    if summary.shape != (F, 2) or summary.dtype != torch.float32:
+        raise ValueError("peakfind: summary must be float32 [F, 2]")
+    if params.radius not in (1, 2):
+        raise ValueError("peakfind: radius must be 1 or 2")
+    s = _ext.stream_handle(stream)
+    with torch.cuda.stream(stream) if stream is not None else torch.cuda.stream(torch.cuda.current_stream()):
+        counts.zero_()
+        summary.zero_()
+    for a, b in _chunks(F):
+        C.peakfind([_ptr(t) for t in frames[a:b]], P, H, W, float(params.thr_peak), float(params.son_min),
+                   int(params.radius), int(params.max_peaks), _ptr(peaks[a]), _ptr(counts[a:]), _ptr(summary[a]), s)

@@ -1,0 +1,242 @@
+"""Producer and consumer pipelines (the per-rank engines behind the CLIs and ``bench.py``).
+
+Producer (replaces psana_ray/producer.py:78-117, ``produce_data``):
+    source events (pinned host pages) --hipMemcpyAsync, side stream--> raw HBM chunk buffers
+    --calibration kernels, compute stream--> HBM ring slots --commit--> sharded queue
+  * triple-buffered raw chunks: the H2D copy of chunk k+1 overlaps the kernels of chunk k;
+    everything is ordered with HIP events, the host never waits for the device except on
+    backpressure (no free slot) -- which replaces the reference's sleep-based exponential
+    backoff (producer.py:105-111) with a condition-variable wait;
+  * masks (bad-pixel via ``create_bad_pixel_mask()``, manual ``.npy``; truthy keeps,
+    producer.py:81-82,92-95) are folded into the kernel tables once, not applied per event;
+  * frames are written straight into the destination slot (no intermediate copies).
+
+Consumer: drains this rank's shard in batches and runs the on-GPU peak finder (K-07) on a
+consumer stream, releasing slots stream-ordered (BASELINE config 5).
+"""
+from __future__ import annotations
+
+import collections
+import logging
+import time
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .config import PeakFinderParams
+from .models.calibrator import Calibrator
+from .ops import _ext, kernels
+from .queue.endpoint import EndOfStream, FrameItem, QueueEndpoint
+
+log = logging.getLogger(__name__)
+
+
+class ProducerPipeline:
+    def __init__(self, source, calibrator: Optional[Calibrator], endpoint: QueueEndpoint, rank: int = 0,
+                 chunk: int = 16, n_raw_buffers: int = 3, acquire_timeout_s: float = 1.0,
+                 log_every: int = 0):
+        self.source = source
+        self.cal = calibrator
+        self.ep = endpoint
+        self.rank = rank
+        self.chunk = min(chunk, kernels.MAX_FRAMES)
+        self.device = endpoint.ring.device
+        self.gpu = self.device.type == "cuda"
+        self.acquire_timeout_s = acquire_timeout_s
+        self.log_every = log_every
+        self.frames = 0
+        self.full_waits = 0
+        self.t_first = None
+        self.calibrated_source = getattr(source, "calibrated", False)
+        spec = getattr(source, "spec", None)
+        if self.gpu and not self.calibrated_source:
+            _ext.load()
+            self.h2d = torch.cuda.Stream(device=self.device)
+            self.compute = torch.cuda.Stream(device=self.device)
+            self.raw_bufs = torch.empty((n_raw_buffers, self.chunk, *spec.frame_shape), dtype=torch.uint16,
+                                        device=self.device)
+            self.buf_free = [torch.cuda.Event() for _ in range(n_raw_buffers)]
+            self.buf_used = [False] * n_raw_buffers
+            self.h2d_done = [torch.cuda.Event() for _ in range(n_raw_buffers)]
+        self._k = 0
+        self._inflight = collections.deque()
+        self._reuses = hasattr(source, "n_staging")
+
+    # --------------------------------------------------------------------------------
+    def _acquire(self, n: int, stream) -> List[int]:
+        slots = []
+        while len(slots) < n:
+            s = self.ep.acquire(timeout=self.acquire_timeout_s, stream=stream)
+            if s is None:
+                self.full_waits += 1
+                if self.full_waits % 50 == 1:
+                    log.info("Rank %d: Queue is full, waiting...", self.rank)  # producer.py:106
+                continue
+            slots.append(s)
+        return slots
+
+    def step(self) -> int:
+        """Produce up to ``chunk`` frames.  Returns the number produced (0 = source exhausted)."""
+        if self.t_first is None:
+            self.t_first = time.perf_counter()
+        if self.calibrated_source:
+            return self._step_calibrated()
+        if self._reuses and self.gpu:
+            # the source refills pinned staging slots: keep its ring ahead of in-flight copies
+            max_inflight = max(1, self.source.n_staging // self.chunk - 1)
+            while len(self._inflight) >= max_inflight:
+                self._inflight.popleft().synchronize()
+        evs = self.source.next_events(self.chunk)
+        if not evs:
+            return 0
+        n = len(evs)
+        if self.gpu:
+            C = _ext.load()
+            b = self._k % len(self.raw_bufs)
+            self._k += 1
+            buf = self.raw_bufs[b]
+            if self.buf_used[b]:
+                self.h2d.wait_event(self.buf_free[b])
+            self.buf_used[b] = True
+            nbytes = evs[0].raw.nbytes
+            C.memcpy_h2d_batch([int(buf[i].data_ptr()) for i in range(n)], [int(e.host_ptr) for e in evs], nbytes,
+                               int(self.h2d.cuda_stream))
+            self.h2d_done[b].record(self.h2d)
+            if self._reuses:
+                ev = torch.cuda.Event()
+                ev.record(self.h2d)
+                self._inflight.append(ev)
+            slots = self._acquire(n, self.compute)
+            self.compute.wait_event(self.h2d_done[b])
+            outs = [self.ep.slot_tensor(s) for s in slots]
+            self.cal.run([buf[i] for i in range(n)], outs, self.compute)
+            self.buf_free[b].record(self.compute)
+            for s, e in zip(slots, evs):
+                self.ep.commit(s, self.rank, e.idx, e.gevt, e.photon_energy, self.compute)
+        else:
+            slots = self._acquire(n, None)
+            raw = [torch.from_numpy(np.ascontiguousarray(e.raw).view(np.int16)).view(torch.uint16) for e in evs]
+            outs = [self.ep.slot_tensor(s) for s in slots]
+            self.cal.run(raw, outs)
+            for s, e in zip(slots, evs):
+                self.ep.commit(s, self.rank, e.idx, e.gevt, e.photon_energy)
+        self.frames += n
+        if self.log_every and self.frames % self.log_every < n:
+            log.info("Rank %d produced: idx=%d | shape=%s | photon_energy=%s", self.rank, evs[-1].idx,
+                     tuple(self.ep.ring.frame_shape), evs[-1].photon_energy)
+        return n
+
+    def _step_calibrated(self) -> int:
+        """psana path: frames arrive calibrated on the host; upload into the slot."""
+        if not hasattr(self, "_it"):
+            from .models.detector import Mode
+
+            self._it = enumerate(self.source.iter_events(self.cal.mode if self.cal else Mode.calib))
+        try:
+            idx, (data, pe) = next(self._it)
+        except StopIteration:
+            return 0
+        if data.ndim == 2:
+            data = data[None]
+        (s,) = self._acquire(1, None)
+        self.ep.slot_tensor(s).copy_(torch.from_numpy(np.ascontiguousarray(data, dtype=np.float32)))
+        if self.gpu:
+            torch.cuda.current_stream(self.device).synchronize()
+        self.ep.commit(s, self.rank, idx, idx, pe)
+        self.frames += 1
+        return 1
+
+    def run(self, max_steps: Optional[int] = None, stop=None) -> int:
+        """Produce until the source ends, ``max_steps`` events (per rank, Q-6) or ``stop`` is set."""
+        while not (stop is not None and stop.is_set()):
+            if max_steps is not None and self.frames >= max_steps:
+                log.info("Rank %d: Reached max_steps %d, terminating", self.rank, max_steps)
+                break
+            if max_steps is not None and not self.calibrated_source:
+                self.chunk = max(1, min(self.chunk, max_steps - self.frames))
+            if self.step() == 0:
+                break
+        if self.gpu and not self.calibrated_source:
+            self.compute.synchronize()
+        self.ep.finish()
+        return self.frames
+
+
+class PeakFinderConsumer:
+    """Consumer engine: batches of leased slots -> K-07 peak finder -> stream-ordered release."""
+
+    def __init__(self, endpoint: QueueEndpoint, frame_shape, params: Optional[PeakFinderParams] = None,
+                 batch: int = 16, keep_results: bool = False):
+        self.ep = endpoint
+        self.params = params or PeakFinderParams()
+        self.batch = min(batch, kernels.MAX_FRAMES)
+        self.device = endpoint.ring.device
+        self.gpu = self.device.type == "cuda"
+        self.shape = tuple(frame_shape)
+        self.frames = 0
+        self.peaks_total = 0
+        self.keep_results = keep_results
+        self.results = []
+        if self.gpu:
+            self.stream = torch.cuda.Stream(device=self.device)
+            B = self.batch
+            self._nbuf = 3
+            self.peaks = torch.empty((self._nbuf, B, self.params.max_peaks, 8), dtype=torch.float32, device=self.device)
+            self.counts = torch.zeros((self._nbuf, B), dtype=torch.int32, device=self.device)
+            self.summary = torch.zeros((self._nbuf, B, 2), dtype=torch.float32, device=self.device)
+            self.count_acc = torch.zeros((), dtype=torch.int64, device=self.device)
+            self._b = 0
+
+    def process(self, items: List[FrameItem]):
+        n = len(items)
+        if n == 0:
+            return
+        if self.gpu:
+            b = self._b % self._nbuf
+            self._b += 1
+            with torch.cuda.stream(self.stream):
+                kernels.peakfind([it.data for it in items], self.shape, self.params, self.peaks[b, :n],
+                                 self.counts[b, :n], self.summary[b, :n], self.stream)
+                self.count_acc += self.counts[b, :n].clamp(max=self.params.max_peaks).sum()
+                if self.keep_results:
+                    self.results.append((self.peaks[b, :n].clone(), self.counts[b, :n].clone(),
+                                         [(it.rank, it.idx, it.gevt) for it in items]))
+            for it in items:
+                it.release(self.stream)
+        else:
+            from .ops import reference
+
+            frames = torch.stack([it.data.reshape(self.shape) for it in items])
+            peaks, _summary = reference.peakfind_reference(frames, self.params)
+            self.peaks_total += sum(int(p.shape[0]) for p in peaks)
+            if self.keep_results:
+                self.results.append((peaks, [(it.rank, it.idx, it.gevt) for it in items]))
+            for it in items:
+                it.release()
+        self.frames += n
+
+    def poll(self, timeout: float = 0.05) -> int:
+        """Take up to ``batch`` ready frames (waiting up to ``timeout`` for the first) and process
+        them.  Returns frames processed; raises EndOfStream at the end of the stream."""
+        items: List[FrameItem] = []
+        it = self.ep.get(timeout=timeout, stream=self.stream if self.gpu else None)
+        if it is None:
+            return 0
+        items.append(it)
+        while len(items) < self.batch:
+            try:
+                nxt = self.ep.get(timeout=0.0, stream=self.stream if self.gpu else None)
+            except EndOfStream:
+                break
+            if nxt is None:
+                break
+            items.append(nxt)
+        self.process(items)
+        return len(items)
+
+    def synchronize(self):
+        if self.gpu:
+            self.stream.synchronize()
+            self.peaks_total = int(self.count_acc.item())
+        return self.peaks_total

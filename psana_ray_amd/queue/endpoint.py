@@ -1,0 +1,335 @@
+"""One rank's endpoint of the sharded shared queue (producer and/or consumer roles).
+
+Reference contract being replaced (psana_ray/shared_queue.py, producer.py, data_reader.py):
+  * producers ``put([rank, idx, data, photon_energy])``; a full queue returns False and the
+    producer backs off (producer.py:98-111) -- here ``acquire()`` hands out an HBM slot only when
+    the producer has budget, blocking on a condition variable instead of sleeping;
+  * consumers ``get()`` non-blocking, None when empty (data_reader.py:31-37);
+  * end of stream was a ``None`` sentinel indistinguishable from "empty" (Q-2) and depended on a
+    global MPI Barrier (producer.py:120, hang risk Q-7) -- here every producer advertises its own
+    EOS in the control round once all its frames are routed; a consumer raises
+    :class:`EndOfStream` after EOS from every producer and an empty shard.  No barrier.
+  * a dead queue actor raised RayActorError -> DataReaderError (data_reader.py:36-37) -- here a
+    failed control/data exchange (peer died) raises :class:`QueuePeerError`.
+
+Transport (world > 1): a progress thread runs rounds -- all-gather (offers, credits, headers) on
+the gloo control group, deterministic routing (parallel.routing), then one grouped RCCL
+send/recv exchange of the frames on a dedicated stream.  World == 1: frames are routed locally
+(zero copy: the calibration kernel already wrote them into the consumer's slot).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import struct
+import threading
+import time
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..ops import _ext
+from ..parallel.routing import plan_round
+from .ring import FrameRing
+
+log = logging.getLogger(__name__)
+
+F_PRODUCER, F_CONSUMER, F_EOS, F_CLOSED, F_FAILED = 1, 2, 4, 8, 16
+HDR = 4          # fixed words per control vector
+PER_OFFER = 4    # rank, idx, gevt, photon-energy bits
+
+
+class QueueError(RuntimeError):
+    pass
+
+
+class QueueClosed(QueueError):
+    """The queue no longer accepts frames (all consumers left, or the endpoint was closed)."""
+
+
+class QueuePeerError(QueueError):
+    """A peer process / the transport failed (the reference's 'Queue actor is dead')."""
+
+
+class EndOfStream(QueueError):
+    """Every producer finished and this consumer's shard is drained."""
+
+
+def _pe_bits(pe: Optional[float]) -> int:
+    return struct.unpack("<q", struct.pack("<d", float("nan") if pe is None else float(pe)))[0]
+
+
+def _pe_from_bits(b: int) -> Optional[float]:
+    v = struct.unpack("<d", struct.pack("<q", int(b)))[0]
+    return None if math.isnan(v) else v
+
+
+@dataclass
+class FrameItem:
+    """A frame leased from the ring.  ``data`` is a view of the HBM slot: call ``release()``
+    (or use ``with``) when done, or ``to_list(copy=True)`` for a reference-style owned item."""
+
+    endpoint: "QueueEndpoint"
+    slot: int
+    rank: int
+    idx: int
+    gevt: int
+    photon_energy: Optional[float]
+    data: torch.Tensor
+    _released: bool = False
+
+    def release(self, stream=None):
+        if not self._released:
+            self._released = True
+            self.endpoint.release(self.slot, stream)
+
+    def to_list(self, copy: bool = True):
+        """``[rank, idx, data, photon_energy]`` -- the reference item (producer.py:101)."""
+        data = self.data.clone() if copy else self.data
+        if copy:
+            self.release()
+        return [self.rank, self.idx, data, self.photon_energy]
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.release()
+        return False
+
+
+class QueueEndpoint:
+    def __init__(self, ring: FrameRing, rank: int = 0, world: int = 1, comm=None,
+                 producer_ranks: Optional[Sequence[int]] = None, consumer_ranks: Optional[Sequence[int]] = None,
+                 route: str = "balanced", max_offer: int = 64, is_producer: bool = True, is_consumer: bool = True):
+        self.ring = ring
+        self.pool = ring.pool
+        self.rank, self.world, self.comm = rank, world, comm
+        self.is_producer, self.is_consumer = is_producer, is_consumer
+        self.producer_ranks = list(range(world)) if producer_ranks is None else list(producer_ranks)
+        self.consumer_ranks = list(range(world)) if consumer_ranks is None else list(consumer_ranks)
+        self.route = route
+        self.max_offer = max_offer
+        self.gpu = ring.device.type == "cuda"
+        self._lock = threading.Lock()
+        self._producer_finished = not is_producer
+        self._consumer_closed = not is_consumer
+        self._eos_from: set = set()
+        self._transport_done = comm is None and False
+        self._failed: Optional[BaseException] = None
+        self._consumers_gone = False
+        self._round = 0
+        self._thread: Optional[threading.Thread] = None
+        self._stop = threading.Event()
+        self.rounds = 0
+        self.round_time_s = 0.0
+        self.frames_routed = 0
+        if comm is None and world != 1:
+            raise ValueError("world > 1 needs a Comm")
+
+    # ------------------------------------------------------------------------ helpers
+    def _stream(self, stream) -> int:
+        if not self.gpu:
+            return 0
+        return _ext.stream_handle(stream)
+
+    def _raise_if_failed(self):
+        if self._failed is not None:
+            raise QueuePeerError(f"shared queue transport failed: {self._failed!r}") from self._failed
+
+    # ------------------------------------------------------------------------ producer
+    def acquire(self, timeout: Optional[float] = None, stream=None) -> Optional[int]:
+        """A free slot for the next calibrated frame, or None on timeout (queue full).
+        ``stream`` (default: current) is ordered after the slot's previous readers."""
+        self._raise_if_failed()
+        if self._consumers_gone:
+            raise QueueClosed("no consumer is attached to the queue any more")
+        if timeout is not None and timeout <= 0:
+            s = self.pool.try_acquire_produce()
+        else:
+            s = self.pool.acquire_produce(-1.0 if timeout is None else float(timeout))
+        if s < 0:
+            self._raise_if_failed()
+            return None
+        self.pool.wait_free_on(s, self._stream(stream))
+        return s
+
+    def slot_tensor(self, slot: int) -> torch.Tensor:
+        return self.ring.slot(slot)
+
+    def commit(self, slot: int, rank: int, idx: int, gevt: int, photon_energy: Optional[float], stream=None):
+        C = _ext.load()
+        h = C.SlotHeader(int(rank), int(idx), int(gevt), float("nan") if photon_energy is None else float(photon_energy))
+        self.pool.commit_produce(slot, h, self._stream(stream))
+        if self.comm is None:
+            self._pump_local()
+
+    def abort(self, slot: int):
+        self.pool.abort_produce(slot)
+
+    def finish(self):
+        """This rank's producer has no more events (its EOS is advertised once drained)."""
+        self._producer_finished = True
+        if self.comm is None:
+            self._pump_local()
+
+    # ------------------------------------------------------------------------ consumer
+    def get(self, timeout: float = 0.0, stream=None) -> Optional[FrameItem]:
+        """Next frame (FIFO within this shard) or None if none arrives within ``timeout``.
+        Raises EndOfStream once every producer finished and the shard is drained."""
+        if self.comm is None:
+            self._pump_local()
+        s = self.pool.try_get() if timeout <= 0 else self.pool.get(float(timeout))
+        if s < 0:
+            if self.comm is None:
+                self._pump_local()
+                s = self.pool.try_get()
+            if s < 0:
+                self._raise_if_failed()
+                if self.stream_done and self.pool.n_ready() == 0:
+                    raise EndOfStream("all producers finished and the queue shard is drained")
+                return None
+        self.pool.wait_ready_on(s, self._stream(stream))
+        h = self.pool.header(s)
+        pe = None if math.isnan(h.photon_energy) else h.photon_energy
+        return FrameItem(self, s, h.rank, h.idx, h.gevt, pe, self.ring.slot(s))
+
+    def release(self, slot: int, stream=None):
+        self.pool.release(slot, self._stream(stream))
+        if self.comm is None:
+            self._pump_local()
+
+    def close_consumer(self):
+        self._consumer_closed = True
+
+    @property
+    def stream_done(self) -> bool:
+        if self.comm is None:
+            return self._producer_finished and self.pool.n_produced() == 0
+        return self._transport_done
+
+    def size(self) -> int:
+        """Frames ready in this shard (reference Queue.size, shared_queue.py:26-31)."""
+        return self.pool.n_ready()
+
+    # ------------------------------------------------------------------------ local routing
+    def _pump_local(self):
+        with self._lock:
+            while self.pool.credits() > 0:
+                slots = self.pool.produced(1)
+                if not slots:
+                    break
+                self.pool.route_local(slots[0])
+                self.frames_routed += 1
+
+    # ------------------------------------------------------------------------ transport rounds
+    def _control_vector(self, offers: List[int]) -> np.ndarray:
+        v = np.zeros(HDR + PER_OFFER * self.max_offer, dtype=np.int64)
+        flags = (F_PRODUCER if self.is_producer else 0) | (F_CONSUMER if self.is_consumer else 0)
+        if self._producer_finished and not offers and self.pool.n_produced() == 0:
+            flags |= F_EOS
+        if self._consumer_closed:
+            flags |= F_CLOSED
+        credits = 0 if self._consumer_closed else self.pool.credits()
+        v[0], v[1], v[2], v[3] = len(offers), credits, flags, self._round
+        for i, s in enumerate(offers):
+            h = self.pool.header(s)
+            b = HDR + PER_OFFER * i
+            v[b], v[b + 1], v[b + 2], v[b + 3] = h.rank, h.idx, h.gevt, _pe_bits(
+                None if math.isnan(h.photon_energy) else h.photon_energy)
+        return v
+
+    def step(self) -> int:
+        """Run ONE transport round (collective: every rank must call it).  Returns frames moved."""
+        t0 = time.perf_counter()
+        C = _ext.load()
+        comm = self.comm
+        offers = self.pool.produced(self.max_offer) if self.is_producer else []
+        allv = comm.allgather_ctrl(self._control_vector(offers))
+        flags = allv[:, 2]
+        offer_n = [int(x) for x in allv[:, 0]]
+        credits = [int(x) for x in allv[:, 1]]
+        for r in range(self.world):
+            if flags[r] & F_EOS:
+                self._eos_from.add(r)
+        consumers_alive = [r for r in range(self.world) if (flags[r] & F_CONSUMER) and not (flags[r] & F_CLOSED)]
+        self._consumers_gone = len(consumers_alive) == 0
+        plan = plan_round(offer_n, credits, self._round, self.route)
+        me = self.rank
+        sends, recvs, recv_meta, send_slots = [], [], [], []
+        sh = comm.stream_handle
+        for k, (p, i, c) in enumerate(plan):
+            if p == me and c == me:
+                self.pool.route_local(offers[i])
+            elif p == me:
+                s = offers[i]
+                self.pool.begin_send(s)
+                self.pool.wait_ready_on(s, sh)
+                sends.append((self.ring.slot(s), c, k))
+                send_slots.append(s)
+            elif c == me:
+                s = self.pool.begin_recv()
+                self.pool.wait_free_on(s, sh)
+                recvs.append((self.ring.slot(s), p, k))
+                b = HDR + PER_OFFER * i
+                row = allv[p]
+                recv_meta.append((s, C.SlotHeader(int(row[b]), int(row[b + 1]), int(row[b + 2]),
+                                                  float("nan") if _pe_from_bits(row[b + 3]) is None
+                                                  else _pe_from_bits(row[b + 3]))))
+        comm.exchange(sends, recvs)
+        for s in send_slots:
+            self.pool.end_send(s, sh)
+        for s, h in recv_meta:
+            self.pool.end_recv(s, h, sh)
+        self._round += 1
+        self.rounds += 1
+        self.frames_routed += len(plan)
+        self.round_time_s += time.perf_counter() - t0
+        if all(r in self._eos_from for r in self.producer_ranks):
+            self._transport_done = True
+        return len(plan)
+
+    def _loop(self):
+        if self.gpu:
+            torch.cuda.set_device(self.ring.device)
+        idle = 0.0
+        try:
+            while not self._transport_done:
+                moved = self.step()
+                if moved == 0:
+                    idle = min(2e-3, idle * 2 if idle else 5e-5)
+                    time.sleep(idle)
+                else:
+                    idle = 0.0
+        except BaseException as e:  # noqa: BLE001 - surfaced to both roles
+            self._failed = e
+            log.error("rank %d: shared-queue transport failed: %r", self.rank, e)
+        finally:
+            self.pool.wake_all()
+
+    def start(self):
+        if self.comm is None or self._thread is not None:
+            return self
+        self._thread = threading.Thread(target=self._loop, name=f"psana-ray-transport-{self.rank}", daemon=True)
+        self._thread.start()
+        return self
+
+    def join(self, timeout: Optional[float] = None) -> bool:
+        if self._thread is None:
+            return True
+        self._thread.join(timeout)
+        return not self._thread.is_alive()
+
+    @property
+    def failed(self) -> Optional[BaseException]:
+        return self._failed
+
+    def stats(self) -> dict:
+        d = self.ring.stats()
+        d.update(rounds=self.rounds, frames_routed=self.frames_routed,
+                 round_ms=1e3 * self.round_time_s / max(1, self.rounds))
+        if self.comm is not None:
+            d.update(bytes_sent=self.comm.bytes_sent, bytes_recv=self.comm.bytes_recv)
+        return d

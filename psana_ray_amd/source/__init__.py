@@ -1,0 +1,36 @@
+"""Event sources: synthetic detector, raw-run files (native reader), optional psana adapter."""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+from .psana_adapter import PsanaWrapperSource, psana_available
+from .rawfile import RawFileRun, make_synthetic_run, run_path, write_run
+from .synthetic import RawEvent, SyntheticRun, generate_raw
+
+ENV_DATA_DIR = "PSANA_RAY_DATA"
+
+
+def open_source(exp: str, run: int, detector_name: str, rank: int = 0, size: int = 1,
+                n_events: Optional[int] = None, pinned: bool = False, pool_frames: int = 32,
+                data_dir: Optional[str] = None, **kw):
+    """Pick the event source for ``(exp, run, detector_name)``:
+
+    1. a raw-run file ``$PSANA_RAY_DATA/<exp>/r<run>/<detector>.praw`` if it exists;
+    2. the synthetic detector for ``--exp synthetic`` (or whenever psana is unavailable);
+    3. the real psana_wrapper otherwise (import-gated).
+    """
+    data_dir = data_dir or os.environ.get(ENV_DATA_DIR)
+    if data_dir:
+        p = run_path(data_dir, exp, run, detector_name)
+        if p.exists():
+            return RawFileRun(p, detector_name, exp=exp, run=run, rank=rank, size=size, pinned=pinned,
+                              n_events=n_events)
+    if exp != "synthetic" and psana_available():
+        return PsanaWrapperSource(exp, run, detector_name)
+    return SyntheticRun(exp, run, detector_name, rank=rank, size=size, n_events=n_events,
+                        pool_frames=pool_frames, pinned=pinned, **kw)
+
+
+__all__ = ["RawEvent", "SyntheticRun", "RawFileRun", "PsanaWrapperSource", "open_source", "generate_raw",
+           "write_run", "make_synthetic_run", "run_path", "psana_available"]

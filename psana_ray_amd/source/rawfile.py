@@ -1,0 +1,111 @@
+"""Raw-run files: the on-disk event format read by the native ``RawRunReader`` (C++ thread pool).
+
+Stands in for psana's XTC2 reader (the reference's events come from psana via
+``PsanaWrapperSmd``, psana_ray/producer.py:150-154).  Fixed-size records make event ``i``
+addressable at ``header_bytes + i * record_bytes`` so every producer rank reads its shard
+(``i % size == rank``, P-01) with positional reads straight into pinned staging buffers.
+
+Layout (little endian): a 4096-byte file header ``PRAWRUN1`` (see csrc/runtime.h) followed by
+records ``[i64 gevt, f64 photon_energy, i64 timestamp, i64 reserved, raw frame bytes]``.
+"""
+from __future__ import annotations
+
+import os
+import struct
+from pathlib import Path
+from typing import List, Optional
+
+import numpy as np
+
+from ..models.constants import CalibConstants, run_seed
+from ..models.detector import DetectorSpec, get_detector
+from .synthetic import RawEvent, generate_raw
+
+HEADER_BYTES = 4096
+RECORD_HEADER = 32
+
+
+def run_path(data_dir: str, exp: str, run: int, detector: str) -> Path:
+    return Path(data_dir) / exp / f"r{run:04d}" / f"{detector}.praw"
+
+
+def write_run(path, spec: DetectorSpec, frames: np.ndarray, photon_energy: np.ndarray, first_gevt: int = 0):
+    """Write frames [n, P, H, W] uint16 as a raw-run file."""
+    path = Path(path)
+    path.parent.mkdir(parents=True, exist_ok=True)
+    n = frames.shape[0]
+    frame_bytes = spec.raw_frame_bytes
+    rec = RECORD_HEADER + frame_bytes
+    hdr = bytearray(HEADER_BYTES)
+    shape = list(spec.frame_shape) + [0] * (4 - len(spec.frame_shape))
+    struct.pack_into("<8sII64sII4QII2Q", hdr, 0, b"PRAWRUN1", 1, HEADER_BYTES,
+                     spec.name.encode()[:63], len(spec.frame_shape), 0, *shape, 2, 0, n, rec)
+    with open(path, "wb") as f:
+        f.write(hdr)
+        for i in range(n):
+            f.write(struct.pack("<qdqq", first_gevt + i, float(photon_energy[i]), i, 0))
+            f.write(np.ascontiguousarray(frames[i], dtype=np.uint16).tobytes())
+
+
+def make_synthetic_run(data_dir: str, exp: str, run: int, detector: str, n_events: int, chunk: int = 16) -> Path:
+    """Materialise a synthetic run on disk (``psana-ray-mkrun``)."""
+    spec = get_detector(detector)
+    consts = CalibConstants.random(spec, seed=run_seed(exp, run, spec.name))
+    path = run_path(data_dir, exp, run, spec.name)
+    frames_all, pe_all = [], []
+    for a in range(0, n_events, chunk):
+        fr, pe = generate_raw(consts, min(chunk, n_events - a), seed=run_seed(exp, run, spec.name) + 7 + a)
+        frames_all.append(fr)
+        pe_all.append(pe)
+    write_run(path, spec, np.concatenate(frames_all), np.concatenate(pe_all))
+    return path
+
+
+class RawFileRun:
+    """Event source over a raw-run file, read by the native thread-pool reader into pinned
+    staging buffers (ring of ``staging`` frames; callers must not reuse a staged frame before
+    its H2D copy completed -- the producer pipeline waits on the copy event)."""
+
+    def __init__(self, path, detector_name: str, exp: str = "file", run: int = 0, rank: int = 0, size: int = 1,
+                 staging: int = 64, n_threads: int = 4, pinned: bool = True, n_events: Optional[int] = None):
+        from ..ops import _ext
+
+        C = _ext.load()
+        self.spec = get_detector(detector_name)
+        self.exp, self.run = exp, run
+        self.reader = C.RawRunReader(str(path), n_threads)
+        if self.reader.frame_bytes != self.spec.raw_frame_bytes:
+            raise ValueError(f"{path}: frame size {self.reader.frame_bytes} != {self.spec.name} raw frame")
+        self.rank, self.size = rank, size
+        total = self.reader.n_events if n_events is None else min(n_events, self.reader.n_events)
+        self.n_events = total
+        self.consts = CalibConstants.random(self.spec, seed=run_seed(exp, run, self.spec.name))
+        nbytes = staging * self.spec.raw_frame_bytes
+        if pinned:
+            self._buf = C.PinnedBuffer(nbytes)
+            self.staging = np.frombuffer(self._buf, dtype=np.uint16).reshape(staging, *self.spec.frame_shape)
+        else:
+            self.staging = np.empty((staging, *self.spec.frame_shape), np.uint16)
+        self.n_staging = staging
+        self._cursor = 0
+        self._slot = 0
+
+    def create_bad_pixel_mask(self) -> np.ndarray:
+        return self.consts.create_bad_pixel_mask()
+
+    def n_local_events(self) -> int:
+        return max(0, (self.n_events - self.rank + self.size - 1) // self.size)
+
+    def next_events(self, n: int) -> List[RawEvent]:
+        n = min(n, self.n_local_events() - self._cursor, self.n_staging)
+        if n <= 0:
+            return []
+        ks = list(range(self._cursor, self._cursor + n))
+        gevts = [self.rank + k * self.size for k in ks]
+        slots = [(self._slot + i) % self.n_staging for i in range(n)]
+        ptrs = [self.staging[s].ctypes.data for s in slots]
+        meta = self.reader.read(gevts, ptrs)
+        self._cursor += n
+        self._slot = (self._slot + n) % self.n_staging
+        return [RawEvent(int(m[0]), k, self.staging[s], p, None if np.isnan(m[1]) else float(m[1]))
+                for k, s, p, m in zip(ks, slots, ptrs, meta)]

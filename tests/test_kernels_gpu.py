@@ -1,0 +1,153 @@
+"""HIP kernels vs the fp32 PyTorch golden models (ops.reference) on a real MI355X."""
+import numpy as np
+import pytest
+import torch
+
+from psana_ray_amd.config import CommonModeParams, PeakFinderParams
+from psana_ray_amd.models import CalibConstants, Calibrator, Mode, get_detector, make_geometry
+from psana_ray_amd.ops import kernels, reference
+from psana_ray_amd.source import generate_raw
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(det, n, seed=0, gain_config="mixed"):
+    spec = get_detector(det)
+    consts = CalibConstants.random(spec, seed=seed, gain_config=gain_config, bad_fraction=0.02)
+    raw, _ = generate_raw(consts, n, seed=seed + 1)
+    return spec, consts, torch.from_numpy(raw.view(np.int16)).view(torch.uint16)
+
+
+def _mask(spec, seed=3):
+    rng = np.random.default_rng(seed)
+    return (rng.random(spec.frame_shape) > 0.05).astype(np.uint8)
+
+
+def _assert_equal(a, b, what):
+    a, b = a.cpu(), b.cpu()
+    diff = (a - b).abs().max().item()
+    assert torch.equal(a, b), f"{what}: max |diff| = {diff}"
+
+
+@pytest.mark.parametrize("det", ["tiny_epix", "tiny_jungfrau", "tiny_plain", "epix10k2M", "jungfrau4M"])
+@pytest.mark.parametrize("masked", [False, True])
+def test_calib_basic_bitwise(cuda_device, det, masked):
+    n = 3 if det in ("epix10k2M", "jungfrau4M") else 37   # 37 > 32 exercises launch chunking
+    spec, consts, raw = _setup(det, n)
+    mask = _mask(spec) if masked else None
+    cal = Calibrator(consts, cuda_device, Mode.calib, mask=mask)
+    out = cal(raw.to(cuda_device))
+    torch.cuda.synchronize()
+    ref = reference.calibrate_reference(raw.to(torch.int32), consts, mask)
+    _assert_equal(out, ref, f"calib {det}")
+
+
+@pytest.mark.parametrize("det", ["tiny_epix", "epix10k2M"])
+@pytest.mark.parametrize("flags", [1, 2, 3])
+def test_common_mode_bitwise(cuda_device, det, flags):
+    n = 2 if det == "epix10k2M" else 5
+    spec, consts, raw = _setup(det, n, seed=11, gain_config="mixed")
+    cm = CommonModeParams(flags=flags, thr=30.0, maxcorr=50.0, npix_min=5)
+    mask = _mask(spec)
+    cal = Calibrator(consts, cuda_device, Mode.calib, mask=mask, common_mode=cm)
+    out = cal(raw.to(cuda_device))
+    torch.cuda.synchronize()
+    ref = reference.calibrate_reference(raw.to(torch.int32), consts, mask, cal.cm)
+    base = reference.calibrate_reference(raw.to(torch.int32), consts, mask, None)
+    assert (ref - base).abs().max() > 0, "common mode changed nothing: test data too weak"
+    _assert_equal(out, ref, f"cm{flags} {det}")
+
+
+def test_common_mode_even_odd_and_empty_segments(cuda_device):
+    """Hand-built tile: even/odd participant counts, all-masked rows, |median| > maxcorr."""
+    spec = get_detector("tiny_epix")
+    consts = CalibConstants.random(spec, seed=5, gain_config="FH", bad_fraction=0.0)
+    consts.pedestals[:] = 0.0
+    consts.gains[:] = 1.0
+    rng = np.random.default_rng(0)
+    adu = rng.integers(0, 40, size=(4, *spec.frame_shape)).astype(np.uint16)
+    adu[0, 0, 0, :8] = 1000           # bank fully above threshold -> no correction
+    adu[1, 0, 3, 8:16] = 200          # |median| > maxcorr -> skipped
+    raw = torch.from_numpy(adu.view(np.int16)).view(torch.uint16)
+    mask = np.ones(spec.frame_shape, np.uint8)
+    mask[0, 5, :] = 0                 # fully masked row
+    mask[1, :, 7] = 0                 # masked column
+    mask[0, 6, 1::2] = 0              # even/odd counts per bank
+    cm = CommonModeParams(flags=3, thr=100.0, maxcorr=60.0, npix_min=3)
+    cal = Calibrator(consts, cuda_device, Mode.calib, mask=mask, common_mode=cm)
+    out = cal(raw.to(cuda_device))
+    torch.cuda.synchronize()
+    ref = reference.calibrate_reference(raw.to(torch.int32), consts, mask, cal.cm)
+    _assert_equal(out, ref, "cm edge cases")
+
+
+@pytest.mark.parametrize("det,cm", [("tiny_epix", None), ("tiny_epix", "3,30,50,5"), ("epix10k2M", None),
+                                    ("epix10k2M", "default"), ("tiny_jungfrau", None)])
+def test_image_mode_matches_scatter(cuda_device, det, cm):
+    spec, consts, raw = _setup(det, 2, seed=21)
+    cmp = CommonModeParams.parse(cm)
+    cal = Calibrator(consts, cuda_device, Mode.image, common_mode=cmp)
+    out = cal(raw.to(cuda_device))
+    torch.cuda.synchronize()
+    geo = cal.geometry
+    calib = reference.calibrate_reference(raw.to(torch.int32), consts, None, cal.cm)
+    ref = reference.assemble_reference(calib, geo.rows, geo.cols, geo.image_shape)
+    assert out.shape == (2, 1, *geo.image_shape)
+    _assert_equal(out, ref, f"image {det}")
+
+
+def test_image_mask_applied_after_assembly(cuda_device):
+    spec, consts, raw = _setup("tiny_epix", 3, seed=4)
+    geo = make_geometry(spec)
+    imask = (np.random.default_rng(1).random(geo.image_shape) > 0.3).astype(np.uint8)
+    cal = Calibrator(consts, cuda_device, Mode.image, mask=imask)
+    out = cal(raw.to(cuda_device))
+    torch.cuda.synchronize()
+    calib = reference.calibrate_reference(raw.to(torch.int32), consts, None, None)
+    ref = reference.assemble_reference(calib, geo.rows, geo.cols, geo.image_shape, imask)
+    _assert_equal(out, ref, "image mask")
+
+
+def _sorted_peaks(p):
+    p = p.cpu()
+    if p.numel() == 0:
+        return p
+    q = p[:, :3].to(torch.int64)
+    key = q[:, 0] * 100_000_000 + q[:, 1] * 10_000 + q[:, 2]
+    return p[torch.argsort(key)]
+
+
+@pytest.mark.parametrize("radius", [1, 2])
+@pytest.mark.parametrize("det", ["tiny_epix", "epix10k2M"])
+def test_peakfind_vs_reference(cuda_device, det, radius):
+    spec, consts, raw = _setup(det, 3, seed=8, gain_config="AHL")
+    frames = reference.calibrate_reference(raw.to(torch.int32), consts, None, None)
+    params = PeakFinderParams(thr_peak=15.0, son_min=4.0, radius=radius, max_peaks=4096)
+    F = frames.shape[0]
+    d = frames.to(cuda_device).contiguous()
+    peaks = torch.zeros((F, params.max_peaks, 8), dtype=torch.float32, device=cuda_device)
+    counts = torch.zeros(F, dtype=torch.int32, device=cuda_device)
+    summary = torch.zeros((F, 2), dtype=torch.float32, device=cuda_device)
+    kernels.peakfind([d[i] for i in range(F)], spec.frame_shape, params, peaks, counts, summary)
+    torch.cuda.synchronize()
+    ref_peaks, ref_summary = reference.peakfind_reference(frames, params)
+    for f in range(F):
+        n = int(counts[f])
+        assert n == ref_peaks[f].shape[0], f"frame {f}: {n} peaks vs reference {ref_peaks[f].shape[0]}"
+        assert n > 0
+        got = _sorted_peaks(peaks[f, :n])
+        exp = _sorted_peaks(ref_peaks[f])
+        assert torch.equal(got[:, :4], exp[:, :4])
+        assert torch.allclose(got[:, 4:], exp[:, 4:], rtol=1e-4, atol=1e-3)
+    assert torch.equal(summary[:, 0].cpu(), ref_summary[:, 0])
+    assert torch.allclose(summary[:, 1].cpu(), ref_summary[:, 1], rtol=1e-4)
+
+
+def test_kernel_rejects_bad_shapes(cuda_device):
+    spec, consts, raw = _setup("tiny_epix", 1)
+    cal = Calibrator(consts, cuda_device, Mode.calib)
+    bad_out = torch.empty(10, device=cuda_device)
+    with pytest.raises(ValueError):
+        kernels.calib_basic([raw[0].to(cuda_device)], [bad_out], cal.ped, cal.gf, spec.kernel_kind)
+    with pytest.raises(ValueError):
+        kernels.calib_basic([raw[0]], [torch.empty(spec.npix)], cal.ped, cal.gf, spec.kernel_kind)
