@@ -61,6 +61,7 @@ def main(argv=None):
     from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
     from psana_ray_amd.source import SyntheticRun
 
+    sys.setswitchinterval(5e-4)   # short GIL hand-off: transport / consumer threads stay responsive
     li = detect()
     world, rank = li.size, li.rank
     if world != args.gpus:
@@ -100,10 +101,18 @@ def main(argv=None):
 
         class _DevSrc:
             spec = src.spec
+            size = world
             calibrated = False
 
             def __init__(self):
                 self.k = 0
+
+            def cycled_frames(self):
+                return [int(dev_pool[j].data_ptr()) for j in range(dev_pool.shape[0])], \
+                    [float(v) for v in src.pool_pe]
+
+            def n_local_events(self):
+                return None
 
             def next_events(self, n):
                 from psana_ray_amd.source.synthetic import RawEvent
@@ -130,7 +139,7 @@ def main(argv=None):
         got = 0
         while got < n_frames:
             if consumer is not None:
-                got += consumer.poll(timeout=0.05)
+                got += consumer.poll(timeout=0.05, max_items=n_frames - got)
             else:
                 it = ep.get(timeout=0.05)
                 if it is not None:
@@ -149,11 +158,11 @@ def main(argv=None):
     barrier()
     sync()
     t0 = time.perf_counter()
-    p0 = prod.frames
+    p0 = prod.produced
     consume(args.steps * B)
     sync()
     t1 = time.perf_counter()
-    p1 = prod.frames
+    p1 = prod.produced
     barrier()
     dt = t1 - t0
     if coord is not None:

@@ -9,21 +9,8 @@
 
 namespace py = pybind11;
 
-namespace pr {
-void launch_calib_basic(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, int64_t npix, int kind,
-                        uint64_t stream);
-void launch_calib_image(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, int64_t npix, int kind,
-                        uint64_t idx, int64_t nout, uint64_t stream);
-void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t pflags, int kind,
-                     int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
-                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream);
-size_t cm_lds_bytes(int asic_rows, int asic_cols);
-void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nout, uint64_t omask,
-                     uint64_t stream);
-void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
-                     float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
-                     uint64_t summary, uint64_t stream);
-}  // namespace pr
+#include "engine.h"
+#include "kernels.h"
 
 using pr::FramePtrs;
 
@@ -72,6 +59,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("asic_rows"), py::arg("asic_cols"), py::arg("thr"), py::arg("maxcorr"), py::arg("npix_min"),
         py::arg("flags"), py::arg("bank_cols"), py::arg("stream"));
   m.def("cm_lds_bytes", &pr::cm_lds_bytes);
+  m.def("xor_lane_selftest", &pr::launch_xor_selftest, py::arg("out"), py::arg("stream"));
   m.def("assemble",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t idx, int64_t nout,
            uint64_t omask, uint64_t stream) {
@@ -161,7 +149,55 @@ PYBIND11_MODULE(_C, m) {
       .def("header", &SP::header)
       .def("state", &SP::state)
       .def("stats", &SP::stats)
-      .def("wake_all", &SP::wake_all);
+      .def("wake_all", &SP::wake_all)
+      .def("wake_producers", &SP::wake_producers)
+      .def("closed", &SP::closed)
+      .def("set_auto_route", &SP::set_auto_route)
+      .def("get_batch", &SP::get_batch, py::arg("max_n"), py::arg("timeout_s"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("release_batch", &SP::release_batch, py::arg("slots"), py::arg("stream"))
+      .def("headers", &SP::headers);
+
+  py::class_<pr::CalibPlan>(m, "CalibPlan")
+      .def(py::init<>())
+      .def_readwrite("mode", &pr::CalibPlan::mode)
+      .def_readwrite("kind", &pr::CalibPlan::kind)
+      .def_readwrite("npix", &pr::CalibPlan::npix)
+      .def_readwrite("ped", &pr::CalibPlan::ped)
+      .def_readwrite("gf", &pr::CalibPlan::gf)
+      .def_readwrite("pflags", &pr::CalibPlan::pflags)
+      .def_readwrite("n_panels", &pr::CalibPlan::n_panels)
+      .def_readwrite("panel_rows", &pr::CalibPlan::panel_rows)
+      .def_readwrite("panel_cols", &pr::CalibPlan::panel_cols)
+      .def_readwrite("asic_rows", &pr::CalibPlan::asic_rows)
+      .def_readwrite("asic_cols", &pr::CalibPlan::asic_cols)
+      .def_readwrite("thr", &pr::CalibPlan::thr)
+      .def_readwrite("maxcorr", &pr::CalibPlan::maxcorr)
+      .def_readwrite("npix_min", &pr::CalibPlan::npix_min)
+      .def_readwrite("cm_flags", &pr::CalibPlan::cm_flags)
+      .def_readwrite("bank_cols", &pr::CalibPlan::bank_cols)
+      .def_readwrite("use_cm", &pr::CalibPlan::use_cm)
+      .def_readwrite("idx", &pr::CalibPlan::idx)
+      .def_readwrite("nout", &pr::CalibPlan::nout)
+      .def_readwrite("omask", &pr::CalibPlan::omask)
+      .def_readwrite("scratch", &pr::CalibPlan::scratch)
+      .def_readwrite("raw_frame_bytes", &pr::CalibPlan::raw_frame_bytes)
+      .def_readwrite("out_frame_bytes", &pr::CalibPlan::out_frame_bytes);
+  m.def("run_calib_plan", &pr::run_calib_plan, py::arg("plan"), py::arg("in_ptrs"), py::arg("out_ptrs"),
+        py::arg("stream"));
+
+  py::class_<pr::ProducerEngine>(m, "ProducerEngine")
+      .def(py::init<pr::SlotPool*, uint64_t, int64_t, int, const pr::CalibPlan&, int, int, int64_t, int64_t>(),
+           py::arg("pool"), py::arg("ring_base"), py::arg("slot_bytes"), py::arg("device"), py::arg("plan"),
+           py::arg("chunk"), py::arg("n_raw_bufs"), py::arg("rank"), py::arg("size"), py::keep_alive<1, 2>())
+      .def("set_cycled_source", &pr::ProducerEngine::set_cycled_source, py::arg("frames"), py::arg("photon_energy"))
+      .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"))
+      .def("request_stop", &pr::ProducerEngine::request_stop)
+      .def("join", &pr::ProducerEngine::join, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("running", &pr::ProducerEngine::running)
+      .def_property_readonly("frames", &pr::ProducerEngine::frames)
+      .def_property_readonly("full_waits", &pr::ProducerEngine::full_waits)
+      .def("error", &pr::ProducerEngine::error);
 
   py::class_<pr::RawRunReader>(m, "RawRunReader")
       .def(py::init<const std::string&, int>(), py::arg("path"), py::arg("n_threads") = 4)

@@ -17,27 +17,55 @@
 // reads bank-conflict free, + 4 bits of per-pixel state = 152.8 KB of the 160 KB), so HBM is
 // touched exactly once: raw u16 in, f32 out.  Medians are exact: every row-bank segment
 // (<= 64 px) is one wave-register bitonic sort, every column (<= 256 px) a 4-register bitonic
-// sort across the wave, with DPP / ds_swizzle lane exchanges (no LDS round trips).
+// sort across the wave, with DPP / permlane-swap lane exchanges (VALU only, no LDS round trips).
 #include "common.h"
 
 namespace pr {
 
-// ---- lane exchange: y = x from lane (lane ^ J) -----------------------------------------
+// ---- lane exchange: y = x from lane (lane ^ J), VALU-only (no LDS-pipe round trip) ----
+//  J = 1, 2 : one DPP quad_perm
+//  J = 4, 8 : DPP row_shl:J / row_shr:J (16-lane rows) + lane select
+//  J = 16   : gfx950 v_permlane16_swap (swaps odd rows of vdst with even rows of src)
+//  J = 32   : gfx950 v_permlane32_swap (swaps the upper half of vdst with the lower of src)
 template <int J>
-__device__ __forceinline__ float xor_lane(float x) {
+__device__ __forceinline__ float xor_lane(float x, int lane) {
   const int xi = __float_as_int(x);
   int yi;
   if constexpr (J == 1) {
     yi = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
   } else if constexpr (J == 2) {
     yi = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  } else if constexpr (J == 4 || J == 8 || J == 16) {
-    yi = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (J << 10));  // bitmask mode, xor J in 32-lane groups
+  } else if constexpr (J == 4 || J == 8) {
+    const int up = __builtin_amdgcn_update_dpp(0, xi, 0x100 + J, 0xF, 0xF, false);  // row_shl:J
+    const int dn = __builtin_amdgcn_update_dpp(0, xi, 0x110 + J, 0xF, 0xF, false);  // row_shr:J
+    yi = (lane & J) ? dn : up;
+  } else if constexpr (J == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)xi, (unsigned)xi, false, false);
+    yi = (int)((lane & 16) ? r[0] : r[1]);
   } else {
     static_assert(J == 32, "xor_lane: J must be a power of two < 64");
-    yi = __shfl_xor(xi, 32);
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)xi, (unsigned)xi, false, false);
+    yi = (int)((lane & 32) ? r[0] : r[1]);
   }
   return __int_as_float(yi);
+}
+
+// Self-test of the exchanges: out[j * 64 + lane] = source lane seen by `lane` for J = 1 << j.
+__global__ void xor_lane_selftest_kernel(int* out) {
+  const int lane = threadIdx.x & 63;
+  const float x = (float)lane;
+  out[0 * 64 + lane] = (int)xor_lane<1>(x, lane);
+  out[1 * 64 + lane] = (int)xor_lane<2>(x, lane);
+  out[2 * 64 + lane] = (int)xor_lane<4>(x, lane);
+  out[3 * 64 + lane] = (int)xor_lane<8>(x, lane);
+  out[4 * 64 + lane] = (int)xor_lane<16>(x, lane);
+  out[5 * 64 + lane] = (int)xor_lane<32>(x, lane);
+}
+
+void launch_xor_selftest(uint64_t out, uint64_t stream) {
+  hipLaunchKernelGGL(xor_lane_selftest_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<int*>(out));
+  hip_check(hipGetLastError(), "xor selftest launch");
 }
 
 // ---- bitonic sort of NR independent 64-element sequences (element index = lane) --------
@@ -48,7 +76,7 @@ __device__ __forceinline__ void seg_step(float (&x)[NR], int lane) {
   const bool take_min = (lower == up);
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
-    const float y = xor_lane<J>(x[r]);
+    const float y = xor_lane<J>(x[r], lane);
     x[r] = take_min ? fminf(x[r], y) : fmaxf(x[r], y);
   }
 }
@@ -84,7 +112,7 @@ __device__ __forceinline__ void col_step(float (&x)[4], int lane) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const bool up = ((r * 64 + lane) & K) == 0;
-      const float y = xor_lane<J>(x[r]);
+      const float y = xor_lane<J>(x[r], lane);
       x[r] = (lower == up) ? fminf(x[r], y) : fmaxf(x[r], y);
     }
   }

@@ -1,0 +1,206 @@
+#include "engine.h"
+
+#include <chrono>
+#include <stdexcept>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace pr {
+
+static FramePtrs ptrs_of(const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, size_t a, size_t b) {
+  FramePtrs fp{};
+  for (size_t i = a; i < b; ++i) {
+    fp.in[i - a] = in[i];
+    fp.out[i - a] = out[i];
+  }
+  return fp;
+}
+
+void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const std::vector<uint64_t>& out,
+                    uint64_t stream) {
+  check(in.size() == out.size(), "run_calib_plan: in/out size mismatch");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  for (size_t a = 0; a < in.size(); a += kMaxFrames) {
+    const size_t b = std::min(in.size(), a + (size_t)kMaxFrames);
+    const int n = (int)(b - a);
+    switch (p.mode) {
+      case kPlanRawCopy:
+        for (size_t i = a; i < b; ++i)
+          hip_check(hipMemcpyAsync(reinterpret_cast<void*>(out[i]), reinterpret_cast<const void*>(in[i]),
+                                   (size_t)p.raw_frame_bytes, hipMemcpyDeviceToDevice, s),
+                    "raw copy");
+        break;
+      case kPlanCalib:
+        launch_calib_basic(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.npix, p.kind, stream);
+        break;
+      case kPlanCalibCm:
+        launch_calib_cm(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.pflags, p.kind, p.n_panels, p.panel_rows,
+                        p.panel_cols, p.asic_rows, p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags,
+                        p.bank_cols, stream);
+        break;
+      case kPlanImageFused:
+        launch_calib_image(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.npix, p.kind, p.idx, p.nout, stream);
+        break;
+      case kPlanImageScratch: {
+        check(p.scratch != 0, "run_calib_plan: image plan without scratch");
+        std::vector<uint64_t> tmp(n);
+        for (int i = 0; i < n; ++i) tmp[i] = p.scratch + (uint64_t)i * (uint64_t)p.npix * 4u;
+        std::vector<uint64_t> ina(in.begin() + a, in.begin() + b), outa(out.begin() + a, out.begin() + b);
+        if (p.use_cm)
+          launch_calib_cm(ptrs_of(ina, tmp, 0, n), n, p.ped, p.gf, p.pflags, p.kind, p.n_panels, p.panel_rows,
+                          p.panel_cols, p.asic_rows, p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags,
+                          p.bank_cols, stream);
+        else
+          launch_calib_basic(ptrs_of(ina, tmp, 0, n), n, p.ped, p.gf, p.npix, p.kind, stream);
+        launch_assemble(ptrs_of(tmp, outa, 0, n), n, p.idx, p.nout, p.omask, stream);
+        break;
+      }
+      default:
+        check(false, "run_calib_plan: unknown plan mode");
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+ProducerEngine::ProducerEngine(SlotPool* pool, uint64_t ring_base, int64_t slot_bytes, int device,
+                               const CalibPlan& plan, int chunk, int n_raw_bufs, int64_t rank, int64_t size)
+    : pool_(pool), ring_base_(ring_base), slot_bytes_(slot_bytes), device_(device), plan_(plan),
+      chunk_(std::max(1, std::min(chunk, kMaxFrames))), n_raw_bufs_(std::max(2, n_raw_bufs)), rank_(rank),
+      size_(size) {
+  check(pool != nullptr && device >= 0, "ProducerEngine needs a device SlotPool");
+  check(plan.raw_frame_bytes > 0 && plan.raw_frame_bytes % 16 == 0, "ProducerEngine: bad raw frame size");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
+  hip_check(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate");
+  buf_free_.resize(n_raw_bufs_);
+  h2d_done_.resize(n_raw_bufs_);
+  for (int i = 0; i < n_raw_bufs_; ++i) {
+    hip_check(hipEventCreateWithFlags(&buf_free_[i], hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&h2d_done_[i], hipEventDisableTiming), "hipEventCreate");
+  }
+  hip_check(hipMalloc(&raw_bufs_, (size_t)n_raw_bufs_ * chunk_ * plan.raw_frame_bytes), "hipMalloc raw chunks");
+}
+
+ProducerEngine::~ProducerEngine() {
+  stop_.store(true);
+  pool_->wake_producers();
+  if (thread_.joinable()) thread_.join();
+  (void)hipSetDevice(device_);
+  if (h2d_) (void)hipStreamSynchronize(h2d_);
+  if (compute_) (void)hipStreamSynchronize(compute_);
+  for (auto e : buf_free_) (void)hipEventDestroy(e);
+  for (auto e : h2d_done_) (void)hipEventDestroy(e);
+  if (raw_bufs_) (void)hipFree(raw_bufs_);
+  if (h2d_) (void)hipStreamDestroy(h2d_);
+  if (compute_) (void)hipStreamDestroy(compute_);
+}
+
+void ProducerEngine::set_cycled_source(const std::vector<uint64_t>& frames, const std::vector<double>& pe) {
+  check(!running_.load(), "ProducerEngine: cannot change the source while running");
+  check(!frames.empty() && frames.size() == pe.size(), "ProducerEngine: bad cycled source");
+  src_frames_ = frames;
+  src_pe_ = pe;
+}
+
+void ProducerEngine::start(int64_t n_local_events, int64_t max_steps) {
+  check(!src_frames_.empty(), "ProducerEngine: no source");
+  check(!running_.load() && !thread_.joinable(), "ProducerEngine: already started");
+  stop_.store(false);
+  running_.store(true);
+  thread_ = std::thread([this, n_local_events, max_steps] { loop(n_local_events, max_steps); });
+}
+
+bool ProducerEngine::join(double timeout_s) {
+  if (!thread_.joinable()) return true;
+  const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  while (running_.load()) {
+    if (timeout_s >= 0 && std::chrono::steady_clock::now() >= t_end) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  thread_.join();
+  return true;
+}
+
+std::string ProducerEngine::error() const {
+  std::lock_guard<std::mutex> lk(err_mu_);
+  return error_;
+}
+
+void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps) {
+  try {
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    int64_t limit = n_local_events;
+    if (max_steps >= 0 && (limit < 0 || max_steps < limit)) limit = max_steps;
+    const uint64_t stream_c = reinterpret_cast<uint64_t>(compute_);
+    std::vector<char> used(n_raw_bufs_, 0);
+    int64_t k = 0;  // rank-local event index
+    int64_t chunk_no = 0;
+    std::vector<uint64_t> in, out;
+    std::vector<int> slots;
+    while (!stop_.load()) {
+      int n = chunk_;
+      if (limit >= 0) n = (int)std::min<int64_t>(n, limit - k);
+      if (n <= 0) break;
+      const int b = (int)(chunk_no++ % n_raw_bufs_);
+      char* buf = static_cast<char*>(raw_bufs_) + (size_t)b * chunk_ * plan_.raw_frame_bytes;
+      if (used[b]) hip_check(hipStreamWaitEvent(h2d_, buf_free_[b], 0), "wait buf free");
+      used[b] = 1;
+      // stage: coalesce host-contiguous runs into single copies
+      const size_t nsrc = src_frames_.size();
+      int i = 0;
+      while (i < n) {
+        const uint64_t s0 = src_frames_[(k + i) % nsrc];
+        int j = i + 1;
+        while (j < n && src_frames_[(k + j) % nsrc] == s0 + (uint64_t)(j - i) * plan_.raw_frame_bytes) ++j;
+        hip_check(hipMemcpyAsync(buf + (size_t)i * plan_.raw_frame_bytes, reinterpret_cast<const void*>(s0),
+                                 (size_t)(j - i) * plan_.raw_frame_bytes, hipMemcpyDefault, h2d_),
+                  "stage copy");
+        i = j;
+      }
+      hip_check(hipEventRecord(h2d_done_[b], h2d_), "record h2d");
+      // acquire destination slots (backpressure)
+      slots.clear();
+      while ((int)slots.size() < n && !stop_.load()) {
+        const int s = pool_->acquire_produce(0.05);
+        if (s < 0) {
+          if (pool_->closed()) break;
+          full_waits_.fetch_add(1);
+          continue;
+        }
+        pool_->wait_free_on(s, stream_c);
+        slots.push_back(s);
+      }
+      if ((int)slots.size() < n) {  // stopped while waiting
+        for (int s : slots) pool_->abort_produce(s);
+        break;
+      }
+      hip_check(hipStreamWaitEvent(compute_, h2d_done_[b], 0), "wait h2d");
+      in.resize(n);
+      out.resize(n);
+      for (int q = 0; q < n; ++q) {
+        in[q] = reinterpret_cast<uint64_t>(buf) + (uint64_t)q * plan_.raw_frame_bytes;
+        out[q] = ring_base_ + (uint64_t)slots[q] * (uint64_t)slot_bytes_;
+      }
+      run_calib_plan(plan_, in, out, stream_c);
+      hip_check(hipEventRecord(buf_free_[b], compute_), "record buf free");
+      for (int q = 0; q < n; ++q) {
+        SlotHeader h;
+        h.rank = rank_;
+        h.idx = k + q;
+        h.gevt = rank_ + (k + q) * size_;
+        h.photon_energy = src_pe_[(k + q) % src_pe_.size()];
+        pool_->commit_produce(slots[q], h, stream_c);
+      }
+      k += n;
+      frames_.fetch_add(n);
+    }
+    hip_check(hipStreamSynchronize(compute_), "final sync");
+  } catch (const std::exception& e) {
+    std::lock_guard<std::mutex> lk(err_mu_);
+    error_ = e.what();
+  }
+  running_.store(false);
+}
+
+}  // namespace pr

@@ -1,0 +1,95 @@
+// Native producer engine + calibration-plan dispatcher.
+//
+// Reference parity: psana_ray/producer.py:78-117 (produce_data) is a Python loop that, per
+// event, calls psana (CPU calibration), applies masks, and performs a blocking Ray RPC.  Here
+// the per-chunk loop is a C++ thread (no interpreter, no GIL): pinned host frames ->
+// hipMemcpyAsync on a side stream -> calibration kernels on a compute stream writing straight
+// into HBM ring slots -> commit into the SlotPool (event-ordered, no host sync).  Backpressure
+// is a condition-variable wait inside SlotPool::acquire_produce (replaces the sleep-based
+// exponential backoff of producer.py:105-111).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "runtime.h"
+
+namespace pr {
+
+enum PlanMode : int {
+  kPlanRawCopy = 0,     // mode=raw: copy raw frames into the slot
+  kPlanCalib = 1,       // K-01/02/04
+  kPlanCalibCm = 2,     // K-01..K-04 with K-03 common mode
+  kPlanImageFused = 3,  // K-01/02/04 evaluated at image positions (no scratch)
+  kPlanImageScratch = 4 // calib (+cm if use_cm) into scratch, then K-05 assemble (+image mask)
+};
+
+struct CalibPlan {
+  int mode = kPlanCalib;
+  int kind = 0;
+  int64_t npix = 0;
+  uint64_t ped = 0, gf = 0, pflags = 0;
+  int n_panels = 0, panel_rows = 0, panel_cols = 0, asic_rows = 0, asic_cols = 0;
+  float thr = 0, maxcorr = 0;
+  int npix_min = 0, cm_flags = 0, bank_cols = 0;
+  int use_cm = 0;
+  uint64_t idx = 0;
+  int64_t nout = 0;
+  uint64_t omask = 0;
+  uint64_t scratch = 0;  // >= kMaxFrames * npix f32 (kPlanImageScratch)
+  int64_t raw_frame_bytes = 0;
+  int64_t out_frame_bytes = 0;
+};
+
+// Launch the plan for n frames (any n; split into kMaxFrames launches) on `stream`.
+void run_calib_plan(const CalibPlan& plan, const std::vector<uint64_t>& in, const std::vector<uint64_t>& out,
+                    uint64_t stream);
+
+class ProducerEngine {
+ public:
+  ProducerEngine(SlotPool* pool, uint64_t ring_base, int64_t slot_bytes, int device, const CalibPlan& plan,
+                 int chunk, int n_raw_bufs, int64_t rank, int64_t size);
+  ~ProducerEngine();
+  ProducerEngine(const ProducerEngine&) = delete;
+  ProducerEngine& operator=(const ProducerEngine&) = delete;
+
+  // cycled source: frame k of this rank reads host_frames[k % n] (pinned host or device memory)
+  void set_cycled_source(const std::vector<uint64_t>& frames, const std::vector<double>& photon_energy);
+  void start(int64_t n_local_events, int64_t max_steps);  // n_local_events < 0: endless
+  void request_stop() { stop_.store(true); }
+  bool join(double timeout_s);   // true when the thread has exited
+  bool running() const { return running_.load(); }
+  int64_t frames() const { return frames_.load(); }
+  int64_t full_waits() const { return full_waits_.load(); }
+  std::string error() const;
+
+ private:
+  void loop(int64_t n_local_events, int64_t max_steps);
+
+  SlotPool* pool_;
+  uint64_t ring_base_;
+  int64_t slot_bytes_;
+  int device_;
+  CalibPlan plan_;
+  int chunk_;
+  int n_raw_bufs_;
+  int64_t rank_, size_;
+  std::vector<uint64_t> src_frames_;
+  std::vector<double> src_pe_;
+  hipStream_t h2d_ = nullptr, compute_ = nullptr;
+  std::vector<hipEvent_t> buf_free_, h2d_done_;
+  void* raw_bufs_ = nullptr;
+  std::thread thread_;
+  std::atomic<bool> stop_{false}, running_{false};
+  std::atomic<int64_t> frames_{0}, full_waits_{0};
+  mutable std::mutex err_mu_;
+  std::string error_;
+};
+
+}  // namespace pr

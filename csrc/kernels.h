@@ -1,0 +1,24 @@
+// Host launchers of the gfx950 kernels (definitions in the .hip files).
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace pr {
+void launch_calib_basic(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, int64_t npix, int kind,
+                        uint64_t stream);
+void launch_calib_image(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, int64_t npix, int kind,
+                        uint64_t idx, int64_t nout, uint64_t stream);
+void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t pflags, int kind,
+                     int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
+                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream);
+size_t cm_lds_bytes(int asic_rows, int asic_cols);
+void launch_xor_selftest(uint64_t out, uint64_t stream);
+void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nout, uint64_t omask,
+                     uint64_t stream);
+void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
+                     float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
+                     uint64_t summary, uint64_t stream);
+}  // namespace pr

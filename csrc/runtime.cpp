@@ -111,6 +111,7 @@ void SlotPool::commit_produce(int slot, const SlotHeader& h, uint64_t stream) {
   state_[slot] = kProduced;
   produced_fifo_.push_back(slot);
   ++st_.produced;
+  if (auto_route_) route_pending_locked();
 }
 
 void SlotPool::abort_produce(int slot) {
@@ -261,6 +262,7 @@ void SlotPool::release(int slot, uint64_t stream) {
   --consumer_held_;
   free_list_.push_back(slot);
   ++st_.released;
+  if (auto_route_) route_pending_locked();
   cv_produce_.notify_one();
 }
 
@@ -316,6 +318,94 @@ int SlotPool::state(int slot) const {
 PoolStats SlotPool::stats() const {
   std::lock_guard<std::mutex> lk(mu_);
   return st_;
+}
+
+void SlotPool::route_pending_locked() {
+  bool any = false;
+  while (consumer_held_ < cb_ && !produced_fifo_.empty()) {
+    const int s = produced_fifo_.front();
+    produced_fifo_.pop_front();
+    state_[s] = kReady;
+    --producer_held_;
+    ++consumer_held_;
+    ready_fifo_.push_back(s);
+    ++st_.routed_local;
+    any = true;
+  }
+  if (any) {
+    cv_ready_.notify_all();
+    cv_produce_.notify_all();
+  }
+}
+
+void SlotPool::set_auto_route(bool on) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto_route_ = on;
+  if (on) route_pending_locked();
+}
+
+int SlotPool::pop_ready_locked() {
+  const int s = ready_fifo_.front();
+  ready_fifo_.pop_front();
+  state_[s] = kLeased;
+  ++st_.got;
+  return s;
+}
+
+std::vector<int> SlotPool::get_batch(int max_n, double timeout_s, uint64_t stream) {
+  std::vector<int> out;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    const auto pred = [&] { return closed_ || !ready_fifo_.empty(); };
+    if (timeout_s > 0 && !pred()) cv_ready_.wait_for(lk, std::chrono::duration<double>(timeout_s), pred);
+    while ((int)out.size() < max_n && !ready_fifo_.empty()) out.push_back(pop_ready_locked());
+  }
+  if (device_ >= 0 && !out.empty()) {
+    set_device();
+    for (int s : out)
+      hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ready_ev_[s], 0), "hipStreamWaitEvent");
+  }
+  return out;
+}
+
+void SlotPool::release_batch(const std::vector<int>& slots, uint64_t stream) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (device_ >= 0) set_device();
+  for (int slot : slots) {
+    check_slot(slot);
+    check(state_[slot] == kLeased, state_msg("release_batch", kLeased, state_[slot]));
+    if (device_ >= 0) {
+      record(free_ev_[slot], stream);
+      free_ev_valid_[slot] = 1;
+    }
+    state_[slot] = kFree;
+    --consumer_held_;
+    free_list_.push_back(slot);
+    ++st_.released;
+  }
+  if (auto_route_) route_pending_locked();
+  cv_produce_.notify_all();
+}
+
+std::vector<SlotHeader> SlotPool::headers(const std::vector<int>& slots) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<SlotHeader> out;
+  out.reserve(slots.size());
+  for (int s : slots) {
+    check_slot(s);
+    out.push_back(hdr_[s]);
+  }
+  return out;
+}
+
+void SlotPool::wake_producers() {
+  std::lock_guard<std::mutex> lk(mu_);
+  cv_produce_.notify_all();
+}
+
+bool SlotPool::closed() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return closed_;
 }
 
 void SlotPool::wake_all() {

@@ -110,11 +110,24 @@ class SlotPool {
   int state(int slot) const;
   PoolStats stats() const;
   void wake_all();  // wake blocked waiters (shutdown)
+  void wake_producers();
+  bool closed() const;
+
+  // single-process mode: PRODUCED frames are routed to this pool's own consumer as soon as
+  // consumer credit exists (on commit and on release), entirely in native code
+  void set_auto_route(bool on);
+
+  // batched consumer calls (one native call per batch instead of one per frame)
+  std::vector<int> get_batch(int max_n, double timeout_s, uint64_t stream);
+  void release_batch(const std::vector<int>& slots, uint64_t stream);
+  std::vector<SlotHeader> headers(const std::vector<int>& slots) const;
 
  private:
   void set_device() const;
   void check_slot(int slot) const;
   void record(hipEvent_t ev, uint64_t stream) const;
+  void route_pending_locked();
+  int pop_ready_locked();
 
   int pb_, cb_, n_, device_;
   mutable std::mutex mu_;
@@ -126,6 +139,7 @@ class SlotPool {
   std::deque<int> free_list_, produced_fifo_, ready_fifo_;
   int producer_held_ = 0, consumer_held_ = 0;
   bool closed_ = false;
+  bool auto_route_ = false;
   PoolStats st_;
 };
 

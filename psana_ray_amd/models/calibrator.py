@@ -59,18 +59,24 @@ class Calibrator:
 
         self._gpu = self.device.type == "cuda"
         ped, gf, pflags = consts.device_tables(frame_mask)
+        self.plan = None
         if self._gpu:
-            kernels._ext.load()  # fail loudly on a GPU box without the extension
+            C = kernels._ext.load()  # fail loudly on a GPU box without the extension
             self.ped = torch.from_numpy(ped).to(self.device)
             self.gf = torch.from_numpy(gf).to(self.device)
             self.pflags = torch.from_numpy(pflags).to(self.device)
+            self.idx = None
+            self.omask = None
             if self.mode == Mode.image:
                 self.idx = torch.from_numpy(self.geometry.index_map()).to(self.device)
+                kernels._validate_index_map(self.idx, spec.npix, "Calibrator")
                 self.omask = None if image_mask is None else \
                     torch.from_numpy(np.asarray(image_mask).astype(np.uint8).ravel()).to(self.device)
             if self.cm is not None:
-                kernels._ext.load().cm_lds_bytes(spec.asic_rows, spec.asic_cols)
-        self._scratch: Optional[torch.Tensor] = None
+                lds = C.cm_lds_bytes(spec.asic_rows, spec.asic_cols)
+                if lds > 160 * 1024:
+                    raise ValueError(f"common mode: ASIC tile {spec.asic_rows}x{spec.asic_cols} needs {lds} B of LDS")
+            self.plan = self._make_plan(C)
 
     # ------------------------------------------------------------------------------------
     @property
@@ -87,12 +93,6 @@ class Calibrator:
     def out_frame_bytes(self) -> int:
         return int(np.prod(self.out_shape)) * (2 if self.mode == Mode.raw else 4)
 
-    def _scratch_frames(self, n: int) -> List[torch.Tensor]:
-        if self._scratch is None or self._scratch.shape[0] < n:
-            self._scratch = torch.empty((max(n, kernels.MAX_FRAMES), *self.spec.frame_shape), dtype=torch.float32,
-                                        device=self.device)
-        return [self._scratch[i] for i in range(n)]
-
     def run(self, raw: Sequence[torch.Tensor], out: Sequence[torch.Tensor], stream=None) -> None:
         """Calibrate ``raw[i]`` (uint16, frame shape) into ``out[i]`` (``out_shape``) on ``stream``."""
         if len(raw) != len(out):
@@ -102,31 +102,50 @@ class Calibrator:
         if not self._gpu:
             self._run_reference(raw, out)
             return
-        kind = self.spec.kernel_kind
+        for r in raw:
+            if r.dtype != torch.uint16 or r.numel() != self.spec.npix or not r.is_contiguous() or r.device != self.device:
+                raise ValueError("Calibrator.run: raw frames must be contiguous uint16 frames on the calibrator device")
+        for o in out:
+            if o.dtype != self.out_dtype or o.numel() * o.element_size() != self.out_frame_bytes or \
+                    not o.is_contiguous() or o.device != self.device or o.data_ptr() % 16:
+                raise ValueError("Calibrator.run: outputs must be contiguous, 16-B aligned frames of out_shape")
+        self.run_ptrs([int(r.data_ptr()) for r in raw], [int(o.data_ptr()) for o in out], stream)
+
+    def run_ptrs(self, raw_ptrs, out_ptrs, stream=None) -> None:
+        """Pointer-level entry (buffers already validated by the caller, e.g. ring slots)."""
+        from ..ops import _ext
+
+        _ext.load().run_calib_plan(self.plan, list(raw_ptrs), list(out_ptrs), _ext.stream_handle(stream))
+
+    def _make_plan(self, C):
+        spec = self.spec
+        p = C.CalibPlan()
+        p.kind = spec.kernel_kind
+        p.npix = spec.npix
+        p.ped, p.gf, p.pflags = int(self.ped.data_ptr()), int(self.gf.data_ptr()), int(self.pflags.data_ptr())
+        p.n_panels, p.panel_rows, p.panel_cols = spec.n_panels, spec.panel_rows, spec.panel_cols
+        p.asic_rows, p.asic_cols = spec.asic_rows, spec.asic_cols
+        p.raw_frame_bytes = spec.raw_frame_bytes
+        p.out_frame_bytes = self.out_frame_bytes
+        if self.cm is not None:
+            p.use_cm = 1
+            p.thr, p.maxcorr = float(self.cm.thr), float(self.cm.maxcorr)
+            p.npix_min, p.cm_flags, p.bank_cols = int(self.cm.npix_min), int(self.cm.flags), int(self.cm.bank_cols)
         if self.mode == Mode.raw:
-            ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
-            with ctx:
-                for r, o in zip(raw, out):
-                    o.copy_(r.view(o.shape), non_blocking=True)
-            return
-        if self.mode == Mode.calib:
-            if self.cm is None:
-                kernels.calib_basic(raw, out, self.ped, self.gf, kind, stream)
+            p.mode = 0
+        elif self.mode == Mode.calib:
+            p.mode = 2 if self.cm is not None else 1
+        else:
+            p.idx, p.nout = int(self.idx.data_ptr()), int(self.idx.numel())
+            if self.cm is None and self.omask is None:
+                p.mode = 3
             else:
-                kernels.calib_cm(raw, out, self.ped, self.gf, self.pflags, kind, self.spec, self.cm, stream)
-            return
-        # image mode
-        if self.cm is None and self.image_mask is None:
-            kernels.calib_image(raw, out, self.ped, self.gf, kind, self.idx, stream)
-            return
-        for a in range(0, len(raw), kernels.MAX_FRAMES):
-            b = min(len(raw), a + kernels.MAX_FRAMES)
-            tmp = self._scratch_frames(b - a)
-            if self.cm is None:
-                kernels.calib_basic(raw[a:b], tmp, self.ped, self.gf, kind, stream)
-            else:
-                kernels.calib_cm(raw[a:b], tmp, self.ped, self.gf, self.pflags, kind, self.spec, self.cm, stream)
-            kernels.assemble(tmp, out[a:b], self.idx, self.spec.npix, self.omask, stream)
+                p.mode = 4
+                self._scratch = torch.empty((kernels.MAX_FRAMES, *spec.frame_shape), dtype=torch.float32,
+                                            device=self.device)
+                p.scratch = int(self._scratch.data_ptr())
+                p.omask = 0 if self.omask is None else int(self.omask.data_ptr())
+        return p
 
     def _run_reference(self, raw, out):
         if self.mode == Mode.raw:
@@ -150,9 +169,3 @@ class Calibrator:
         return out
 
 
-class _nullctx:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False

