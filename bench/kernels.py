@@ -28,7 +28,7 @@ from psana_ray_amd.source import SyntheticRun
 HBM_ROOF = 6.29e12
 
 
-def timeit(fn, iters=20, warmup=3):
+def timeit(fn, iters=20, warmup=10):
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -80,6 +80,14 @@ def main(argv=None):
     cal = Calibrator(src.consts, dev, Mode.calib)
     if want("calib_basic"):
         report("calib_basic", timeit(lambda: cal.run(rl, ol), a.iters), F * npix * 6)
+    if want("calib_cm_ab"):
+        import os
+        calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
+        for rnd in range(3):   # interleaved A/B in one process (methodology rule 24)
+            os.environ["PSANA_RAY_CM_GENERIC"] = "1"
+            report(f"calib_cm(generic bitonic) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
+            os.environ["PSANA_RAY_CM_GENERIC"] = "0"
+            report(f"calib_cm(sort networks) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
     if want("calib_cm"):
         calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
         report("calib_cm(rows+cols)", timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)

@@ -33,9 +33,9 @@ __device__ __forceinline__ float pick(const float (&t)[NT][8], int i, int c) {
   if constexpr (NT == 1) {
     return t[0][i];
   } else if constexpr (NT == 2) {
-    return c ? t[1][i] : t[0][i];
+    return bsel(c != 0, t[1][i], t[0][i]);
   } else {
-    return c == 0 ? t[0][i] : (c == 1 ? t[1][i] : t[2][i]);
+    return bsel(c == 0, t[0][i], bsel(c == 1, t[1][i], t[2][i]));
   }
 }
 
@@ -155,10 +155,10 @@ __global__ __launch_bounds__(256) void calib_image_kernel(const FramePtrs fp, co
         if constexpr (NT == 1) {
           pp = p[0][i]; gg = g[0][i];
         } else if constexpr (NT == 2) {
-          pp = c ? p[1][i] : p[0][i]; gg = c ? g[1][i] : g[0][i];
+          pp = bsel(c != 0, p[1][i], p[0][i]); gg = bsel(c != 0, g[1][i], g[0][i]);
         } else {
-          pp = c == 0 ? p[0][i] : (c == 1 ? p[1][i] : p[2][i]);
-          gg = c == 0 ? g[0][i] : (c == 1 ? g[1][i] : g[2][i]);
+          pp = bsel(c == 0, p[0][i], bsel(c == 1, p[1][i], p[2][i]));
+          gg = bsel(c == 0, g[0][i], bsel(c == 1, g[1][i], g[2][i]));
         }
         val = valid ? (decode_adu(r, KIND) - pp) * gg : 0.0f;
       }

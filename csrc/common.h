@@ -58,6 +58,14 @@ inline void hip_check(hipError_t e, const char* what) {
 
 inline bool aligned16(uint64_t p) { return (p & 15u) == 0; }
 
+// Register-only select.  A plain `c ? t[1][i] : t[0][i]` lets LLVM fold the select into an
+// indexed access t[c][i], which forces the whole register table into scratch/LDS; the integer
+// blend keeps both operands in VGPRs.
+__device__ __forceinline__ float bsel(bool c, float a, float b) {
+  const int m = -(int)c;
+  return __int_as_float((__float_as_int(a) & m) | (__float_as_int(b) & ~m));
+}
+
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 // 16-B streaming (non-temporal) load: data read exactly once (raw frames).

@@ -19,6 +19,9 @@
 // (<= 64 px) is one wave-register bitonic sort, every column (<= 256 px) a 4-register bitonic
 // sort across the wave, with DPP / permlane-swap lane exchanges (VALU only, no LDS round trips).
 #include "common.h"
+#include "sortnet.h"
+
+#include <cstdlib>
 
 namespace pr {
 
@@ -213,8 +216,8 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
       const int cand = decode_cand(rv, KIND, valid);
       float pp;
       if constexpr (NT == 1) pp = pa[0][j];
-      else if constexpr (NT == 2) pp = cand ? pa[1][j] : pa[0][j];
-      else pp = cand == 0 ? pa[0][j] : (cand == 1 ? pa[1][j] : pa[2][j]);
+      else if constexpr (NT == 2) pp = bsel(cand != 0, pa[1][j], pa[0][j]);
+      else pp = bsel(cand == 0, pa[0][j], bsel(cand == 1, pa[1][j], pa[2][j]));
       const bool good = valid && (pf & 1u);
       const bool elig = good && ((pf >> (1 + cand)) & 1u);
       trow[j] = decode_adu(rv, KIND) - pp;
@@ -313,14 +316,254 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
       const int cand = q & 3;
       float gg;
       if constexpr (NT == 1) gg = ga[0][j];
-      else if constexpr (NT == 2) gg = cand ? ga[1][j] : ga[0][j];
-      else gg = cand == 0 ? ga[0][j] : (cand == 1 ? ga[1][j] : ga[2][j]);
+      else if constexpr (NT == 2) gg = bsel(cand != 0, ga[1][j], ga[0][j]);
+      else gg = bsel(cand == 0, ga[0][j], bsel(cand == 1, ga[1][j], ga[2][j]));
       o[j] = (q & 4u) ? trow[j] * gg : 0.0f;
     }
     float4* op = reinterpret_cast<float4*>(out + pix);
     op[0] = make_float4(o[0], o[1], o[2], o[3]);
     op[1] = make_float4(o[4], o[5], o[6], o[7]);
   }
+}
+
+
+// ==========================================================================================
+// Fast path: per-lane in-register sorting networks (no cross-lane traffic in the sorts).
+//
+//  rows:    ONE lane owns one (row, bank) segment of L pixels; the lane sorts its L values with a
+//           pruned Batcher network (L=48: 384 comparators = 768 VALU) -- 64 segments per wave
+//           instruction instead of one.
+//  columns: TWO lanes (an even/odd pair) own one column, M = ceil(R/2) rows each; each sorts its
+//           half in registers (M=88: 957 comparators), then both evaluate the merge-path
+//           identity  kth(A u B) = min_i max(A[i-1], B[k-i])  with the partner's registers
+//           fetched by one DPP quad_perm each (all register indices compile-time).
+//  Balanced +-inf padding: of the u non-participating elements, the first floor(u/2) become
+//           -inf and the rest +inf.  The numpy median of the participating values then sits at
+//           FIXED sorted positions (N/2-1, N/2 for even N), so no runtime register indexing.
+// ==========================================================================================
+__device__ __forceinline__ float dpp_xor1(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
+}
+
+template <int N>
+__device__ __forceinline__ void fixed_median_pos(int cnt, int& lo, int& hi) {
+  // positions of the lower/upper numpy-median elements after balanced +-inf padding of N slots
+  const int u = N - cnt, a = u >> 1;
+  lo = a + ((cnt - 1) >> 1);
+  hi = a + (cnt >> 1);
+}
+
+template <int KIND, int L, int M>
+__global__ __launch_bounds__(512) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
+                                                            const float* __restrict__ gf,
+                                                            const uint8_t* __restrict__ pflags,
+                                                            const TileGeom tg, const CmParams cp) {
+  constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int R = tg.asic_rows, C = tg.asic_cols, LD = C + 1;
+  float* tile = reinterpret_cast<float*>(smem);
+  uint32_t* nib = reinterpret_cast<uint32_t*>(smem + (((size_t)R * LD * 4 + 15) & ~(size_t)15));
+  const int C8 = C >> 3;
+  const int asic = blockIdx.x;
+  const int f = blockIdx.y;
+  const int per_panel = tg.asics_per_col * tg.asics_per_row;
+  const int panel = asic / per_panel;
+  const int ar = (asic % per_panel) / tg.asics_per_row;
+  const int ac = (asic % per_panel) % tg.asics_per_row;
+  const int64_t base = (int64_t)panel * tg.panel_rows * tg.panel_cols + (int64_t)ar * R * tg.panel_cols +
+                       (int64_t)ac * C;
+  const uint16_t* raw = reinterpret_cast<const uint16_t*>(fp.in[f]);
+  float* out = reinterpret_cast<float*>(fp.out[f]);
+  const int tid = threadIdx.x;
+  const float INF = __int_as_float(0x7f800000);
+
+  // ---- phase 1: decode + pedestal into LDS (same as the generic kernel) -------------------
+  for (int i = tid; i < R * C8; i += blockDim.x) {
+    const int r = i / C8, c = (i % C8) * 8;
+    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
+    const uint4 rw = ld_nt_u4(raw + pix);
+    const uint2 fl = *reinterpret_cast<const uint2*>(pflags + pix);
+    const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
+    const uint32_t fw[2] = {fl.x, fl.y};
+    float pa[NT][8];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      const float4 a = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix);
+      const float4 b = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix + 4);
+      pa[k][0] = a.x; pa[k][1] = a.y; pa[k][2] = a.z; pa[k][3] = a.w;
+      pa[k][4] = b.x; pa[k][5] = b.y; pa[k][6] = b.z; pa[k][7] = b.w;
+    }
+    uint32_t nb = 0;
+    float* trow = tile + r * LD + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t rv = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+      const uint32_t pf = (fw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      bool valid;
+      const int cand = decode_cand(rv, KIND, valid);
+      float pp;
+      if constexpr (NT == 1) pp = pa[0][j];
+      else if constexpr (NT == 2) pp = bsel(cand != 0, pa[1][j], pa[0][j]);
+      else pp = bsel(cand == 0, pa[0][j], bsel(cand == 1, pa[1][j], pa[2][j]));
+      const bool good = valid && (pf & 1u);
+      const bool elig = good && ((pf >> (1 + cand)) & 1u);
+      trow[j] = decode_adu(rv, KIND) - pp;
+      nb |= (uint32_t)(cand | (good ? 4 : 0) | (elig ? 8 : 0)) << (4 * j);
+    }
+    nib[r * C8 + (c >> 3)] = nb;
+  }
+  __syncthreads();
+
+  // ---- phase 2a: rows by bank, one lane per segment ----------------------------------------
+  // Non-participating elements are first marked NaN (a per-element select, no bit masks: 64-bit
+  // mask extraction per element pushed the sorts into scratch), then turned into the balanced
+  // -inf / +inf padding by a running counter.
+  const float QNAN = __int_as_float(0x7fc00000);
+  if (cp.flags & 1) {
+    const int nbank = C / L;
+    for (int sgi = tid; sgi < R * nbank; sgi += blockDim.x) {
+      const int b = sgi / R, r = sgi % R;           // consecutive lanes -> consecutive rows: no bank conflicts
+      float* seg = tile + r * LD + b * L;
+      const uint32_t* nrow = nib + r * C8;
+      float x[L];
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const int col = b * L + j;
+        const float v = seg[j];
+        const bool el = (nrow[col >> 3] >> (4 * (col & 7) + 3)) & 1u;
+        const bool pt = el && (fabsf(v) < cp.thr);
+        cnt += pt ? 1 : 0;
+        x[j] = pt ? v : QNAN;
+      }
+      const int a = (L - cnt) >> 1;
+      int ninv = 0;
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const bool inv = x[j] != x[j];
+        x[j] = inv ? (ninv < a ? -INF : INF) : x[j];
+        ninv += inv ? 1 : 0;
+      }
+      asm volatile("" ::: "memory");   // keep the write-back's LDS reads below the sort (VGPR pressure)
+      sort_regs<L>(x);
+      asm volatile("" ::: "memory");
+      // numpy median at fixed positions: lower = a + (cnt-1)/2, upper = a + cnt/2, which only
+      // depend on the parity of cnt (L even: L/2-1 | L/2; L odd: (L-1)/2 | (L-3)/2,(L-1)/2)
+      float s_lo, s_hi;
+      if constexpr ((L & 1) == 0) {
+        s_lo = x[L / 2 - 1];
+        s_hi = (cnt & 1) ? x[L / 2 - 1] : x[L / 2];
+      } else {
+        s_lo = (cnt & 1) ? x[(L - 1) / 2] : x[(L - 3) / 2];
+        s_hi = x[(L - 1) / 2];
+      }
+      const float med = (s_lo + s_hi) * 0.5f;
+      if (cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const int col = b * L + j;
+          if ((nrow[col >> 3] >> (4 * (col & 7) + 3)) & 1u) seg[j] -= med;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- phase 2b: columns, two lanes per column ---------------------------------------------
+  if (cp.flags & 2) {
+    const int nwork = 2 * C;
+    for (int w = tid; w < ((nwork + 63) / 64) * 64; w += blockDim.x) {
+      // whole waves iterate together (the DPP exchange needs both lanes of a pair)
+      const bool act = w < nwork;
+      const int c = act ? (w >> 1) : 0;
+      const int h = w & 1;
+      const uint32_t shift = 4 * (c & 7) + 3;
+      float x[M];
+      int my_cnt = 0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int r = h * M + i;
+        const bool in = act && r < R;
+        const float v = in ? tile[r * LD + c] : 0.0f;
+        const bool el = in && ((nib[r * C8 + (c >> 3)] >> shift) & 1u);
+        const bool pt = el && (fabsf(v) < cp.thr);
+        my_cnt += pt ? 1 : 0;
+        x[i] = pt ? v : QNAN;
+        if ((i & 15) == 15) asm volatile("" ::: "memory");   // cap loads in flight (VGPR pressure)
+      }
+      const int other_cnt = __builtin_amdgcn_update_dpp(0, my_cnt, 0xB1, 0xF, 0xF, false);
+      const int cnt = my_cnt + other_cnt;
+      const int a = (2 * M - cnt) >> 1;
+      const int my_inv = M - my_cnt, other_inv = M - other_cnt;
+      // the even lane owns the first non-participating elements of the column
+      const int neg_budget = h == 0 ? min(my_inv, a) : max(0, a - other_inv);
+      int ninv = 0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const bool inv = x[i] != x[i];
+        x[i] = inv ? (ninv < neg_budget ? -INF : INF) : x[i];
+        ninv += inv ? 1 : 0;
+      }
+      asm volatile("" ::: "memory");
+      sort_regs<M>(x);
+      asm volatile("" ::: "memory");
+      // merge-path k-th of the union for k = M-1 and k = M (both lanes compute both)
+      float k_lo = fminf(x[M - 1], dpp_xor1(x[M - 1]));   // i = M and i = 0 terms
+      float k_hi = __int_as_float(0x7f800000);
+#pragma unroll
+      for (int i = 1; i < M; ++i) k_lo = fminf(k_lo, fmaxf(x[i - 1], dpp_xor1(x[M - 1 - i])));
+#pragma unroll
+      for (int i = 1; i <= M; ++i) k_hi = fminf(k_hi, fmaxf(x[i - 1], dpp_xor1(x[M - i])));
+      // 2M slots: lower median at M-1; upper at M (even count) or M-1 (odd count)
+      const float med = (k_lo + ((cnt & 1) ? k_lo : k_hi)) * 0.5f;
+      asm volatile("" ::: "memory");
+      if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          const int r = h * M + i;
+          if (r < R && ((nib[r * C8 + (c >> 3)] >> shift) & 1u)) tile[r * LD + c] -= med;
+          if ((i & 15) == 15) asm volatile("" ::: "memory");
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- phase 3: gain factor + mask, store ---------------------------------------------------
+  for (int i = tid; i < R * C8; i += blockDim.x) {
+    const int r = i / C8, c = (i % C8) * 8;
+    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
+    const uint32_t nb = nib[i];
+    float ga[NT][8];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      const float4 a = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix);
+      const float4 b = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix + 4);
+      ga[k][0] = a.x; ga[k][1] = a.y; ga[k][2] = a.z; ga[k][3] = a.w;
+      ga[k][4] = b.x; ga[k][5] = b.y; ga[k][6] = b.z; ga[k][7] = b.w;
+    }
+    const float* trow = tile + r * LD + c;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t q = (nb >> (4 * j)) & 0xFu;
+      const int cand = q & 3;
+      float gg;
+      if constexpr (NT == 1) gg = ga[0][j];
+      else if constexpr (NT == 2) gg = bsel(cand != 0, ga[1][j], ga[0][j]);
+      else gg = bsel(cand == 0, ga[0][j], bsel(cand == 1, ga[1][j], ga[2][j]));
+      o[j] = (q & 4u) ? trow[j] * gg : 0.0f;
+    }
+    float4* op = reinterpret_cast<float4*>(out + pix);
+    op[0] = make_float4(o[0], o[1], o[2], o[3]);
+    op[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
+// PSANA_RAY_CM_GENERIC=1 forces the generic wave-bitonic kernel (A/B benchmarking, read per launch)
+static bool cm_force_generic() {
+  const char* e = getenv("PSANA_RAY_CM_GENERIC");
+  return e != nullptr && e[0] == '1';
 }
 
 size_t cm_lds_bytes(int asic_rows, int asic_cols) {
@@ -358,6 +601,21 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   const float* P = reinterpret_cast<const float*>(ped);
   const float* G = reinterpret_cast<const float*>(gf);
   const uint8_t* F = reinterpret_cast<const uint8_t*>(pflags);
+  const int M = (asic_rows + 1) / 2;
+  bool done = false;
+#define PR_CM_NET(KIND_, L_, M_)                                                                      \
+  if (!done && kind == KIND_ && bank_cols == L_ && M == M_ && !cm_force_generic()) {                  \
+    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<KIND_, L_, M_>,                     \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");   \
+    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_>), grid, dim3(512), lds, s, fp, P, G, F, tg, cp); \
+    done = true;                                                                                      \
+  }
+  PR_CM_NET(kEpix10ka, 48, 88)
+  PR_CM_NET(kEpix10ka, 8, 8)
+  PR_CM_NET(kPlain, 32, 64)
+  PR_CM_NET(kPlain, 8, 4)
+#undef PR_CM_NET
+  if (!done) {
   switch (kind) {
     case kEpix10ka:
       hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kEpix10ka>,
@@ -375,6 +633,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
       hipLaunchKernelGGL(calib_cm_kernel<kPlain>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp);
       break;
     default: check(false, "calib_cm: unknown gain kind");
+  }
   }
   hip_check(hipGetLastError(), "calib_cm launch");
 }
