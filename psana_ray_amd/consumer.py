@@ -1,0 +1,131 @@
+"""``psana-ray-consumer``: installed consumer entry point (the reference only ships
+examples/psana_consumer.py and never installs it, SURVEY R-14 / Q-9).
+
+    psana-ray-consumer [consumer_id] [--queue_name my] [--ray_namespace default] [--task peakfind]
+
+Joins the queue session through :class:`~psana_ray_amd.data_reader.DataReader` (same defaults as
+the producer, fixing Q-3), reads ``[rank, idx, data, photon_energy]`` items (4 fields, fixing the
+example's 3-field unpack, Q-1) until the explicit end of stream (fixing Q-2), and runs a task:
+``print`` (the reference example's behaviour), ``peakfind`` (on-GPU K-07 peak finder over
+zero-copy leased batches) or ``none``.  ``--out`` writes the peak lists to an ``.npz``.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import signal
+import sys
+import time
+
+from .config import DEFAULT_LOG_LEVEL, DEFAULT_QUEUE_NAME, DEFAULT_RAY_ADDRESS, DEFAULT_RAY_NAMESPACE, LOG_LEVELS
+
+log = logging.getLogger("psana_ray_amd.consumer")
+
+
+def build_parser():
+    ap = argparse.ArgumentParser(description="psana-ray consumer")
+    ap.add_argument("consumer_id", nargs="?", type=int, default=None,
+                    help="consumer id (examples/psana_consumer.py:51); default: claim the next free id")
+    ap.add_argument("--ray_address", type=str, default=DEFAULT_RAY_ADDRESS)
+    ap.add_argument("--ray_namespace", type=str, default=DEFAULT_RAY_NAMESPACE)
+    ap.add_argument("--queue_name", type=str, default=DEFAULT_QUEUE_NAME)
+    ap.add_argument("--device", type=str, default=None)
+    ap.add_argument("--task", type=str, default="print", choices=["print", "peakfind", "none"])
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--max_frames", type=int, default=None)
+    ap.add_argument("--thr_peak", type=float, default=20.0)
+    ap.add_argument("--son_min", type=float, default=5.0)
+    ap.add_argument("--out", type=str, default=None, help="write peaks (npz) when --task peakfind")
+    ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--log_level", type=str, default=DEFAULT_LOG_LEVEL, choices=LOG_LEVELS)
+    return ap
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
+    logging.basicConfig(level=getattr(logging, args.log_level), format="%(asctime)s - %(levelname)s - %(message)s")
+    import numpy as np
+    import torch
+
+    from .config import PeakFinderParams
+    from .data_reader import DataReader, DataReaderError, EndOfStream
+
+    stop = {"flag": False}
+
+    def handler(sig, frame):
+        print("Ctrl+C pressed. Shutting down...")
+        stop["flag"] = True
+
+    signal.signal(signal.SIGINT, handler)
+    t0 = time.time()
+    n = 0
+    peaks_total = 0
+    records = []
+    with DataReader(args.ray_address, args.queue_name, args.ray_namespace, consumer_id=args.consumer_id,
+                    device=args.device, timeout_s=args.timeout) as reader:
+        cid = reader.consumer_id
+        pf = None
+        if args.task == "peakfind":
+            from .ops import kernels
+
+            params = PeakFinderParams(thr_peak=args.thr_peak, son_min=args.son_min)
+        while not stop["flag"] and (args.max_frames is None or n < args.max_frames):
+            try:
+                if args.task == "peakfind" and reader.endpoint is not None:
+                    items = reader.read_batch(args.batch, timeout=1.0)
+                    if not items:
+                        continue
+                    shape = tuple(items[0].data.shape)
+                    dev = items[0].data.device
+                    F = len(items)
+                    if dev.type == "cuda":
+                        pk = torch.empty((F, params.max_peaks, 8), dtype=torch.float32, device=dev)
+                        cnt = torch.zeros(F, dtype=torch.int32, device=dev)
+                        sm = torch.zeros((F, 2), dtype=torch.float32, device=dev)
+                        kernels.peakfind([it.data for it in items], shape, params, pk, cnt, sm)
+                        cnt_h = cnt.cpu()
+                        for i, it in enumerate(items):
+                            k = min(int(cnt_h[i]), params.max_peaks)
+                            peaks_total += k
+                            if args.out:
+                                records.append((it.rank, it.idx, it.gevt, pk[i, :k].cpu().numpy()))
+                    else:
+                        from .ops import reference
+
+                        pl, _ = reference.peakfind_reference(torch.stack([it.data for it in items]), params)
+                        for it, p in zip(items, pl):
+                            peaks_total += p.shape[0]
+                            if args.out:
+                                records.append((it.rank, it.idx, it.gevt, p.numpy()))
+                    for it in items:
+                        it.release()
+                    n += F
+                else:
+                    result = reader.read(timeout=1.0)
+                    if result is None:
+                        print(f"Consumer {cid} waiting for data...")
+                        continue
+                    rank, idx, data, photon_energy = result
+                    if args.task == "print":
+                        print(f"Consumer {cid} processed: rank={rank} | idx={idx} | shape={tuple(data.shape)} "
+                              f"| photon_energy={photon_energy}")
+                    n += 1
+            except EndOfStream:
+                log.info("Consumer %s: end of stream", cid)
+                break
+            except DataReaderError as e:
+                print(f"DataReader error: {e}")
+                print("Queue actor is dead. Exiting...")
+                return 1
+    dt = time.time() - t0
+    log.info("Consumer %s: %d frames in %.2f s (%.1f frames/s), %d peaks", cid, n, dt, n / max(dt, 1e-9), peaks_total)
+    if args.out and records:
+        counts = np.array([r[3].shape[0] for r in records], dtype=np.int64)
+        np.savez(args.out, rank=np.array([r[0] for r in records]), idx=np.array([r[1] for r in records]),
+                 gevt=np.array([r[2] for r in records]), counts=counts,
+                 peaks=np.concatenate([r[3].reshape(-1, 8) for r in records]).astype(np.float32))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

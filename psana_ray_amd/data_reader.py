@@ -1,0 +1,204 @@
+"""Consumer client: ``DataReader`` (reference parity: psana_ray/data_reader.py:4-48).
+
+Same surface as the reference -- ``DataReader(address, queue_name, ray_namespace)``,
+``connect()``, ``read()``, ``close()``, context manager, ``DataReaderError`` -- with these
+MI355X-native semantics:
+
+* ``connect()`` joins the queue session at the rendezvous store (``address``; the reference's
+  ``ray.init`` + ``ray.get_actor``, data_reader.py:11-24), gets this consumer's HBM ring shard and
+  starts the transport thread (frames arrive by RCCL send/recv over xGMI, or gloo on the CPU).
+  Defaults come from ONE shared module, so they match the producer's (fixes Q-3).
+* ``read()`` is non-blocking by default and returns None when nothing is ready (data_reader.py:35);
+  items are the reference's ``[rank, idx, data, photon_energy]`` (4 fields, producer.py:101; the
+  reference example's 3-field unpack is quirk Q-1), ``data`` a torch tensor on the consumer's
+  device (``as_numpy=True`` for a host ndarray).  ``read(timeout=s)`` waits event-driven.
+* end of stream is distinct from "empty" (fixes Q-2): once every producer finished and the shard
+  is drained, ``read()`` raises :class:`EndOfStream` -- a ``DataReaderError`` subclass, so the
+  reference's consumer loop (``except DataReaderError: break``) terminates cleanly -- and
+  ``reader.done`` becomes True.
+* a dead peer raises ``DataReaderError("Queue peer is dead.")`` (data_reader.py:36-37).
+* ``close()`` releases only what this reader created (fixes Q-13).
+* ``lease()`` / ``read_batch()`` give zero-copy access to HBM slots for GPU consumers (H-9).
+
+``queue_name`` / ``ray_namespace`` may also name an in-process :mod:`cpu queue
+<psana_ray_amd.queue.cpu_queue>` created with ``create_queue`` (BASELINE config 1); it is used
+when it exists in this process.
+"""
+from __future__ import annotations
+
+import logging
+import math
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .config import DEFAULT_QUEUE_NAME, DEFAULT_RAY_ADDRESS, DEFAULT_RAY_NAMESPACE
+from .queue.endpoint import EndOfStream as _QueueEOS
+from .queue.endpoint import FrameItem, QueuePeerError
+
+log = logging.getLogger(__name__)
+
+
+class DataReaderError(Exception):
+    """Custom exception for DataReader errors (data_reader.py:46-48)."""
+
+
+class EndOfStream(DataReaderError):
+    """Every producer finished and this consumer's queue shard is drained."""
+
+
+class DataReader:
+    def __init__(self, address: str = DEFAULT_RAY_ADDRESS, queue_name: str = DEFAULT_QUEUE_NAME,
+                 ray_namespace: str = DEFAULT_RAY_NAMESPACE, consumer_id: Optional[int] = None,
+                 device: Optional[str] = None, as_numpy: bool = False, timeout_s: float = 300.0):
+        self.address = address
+        self.queue_name = queue_name
+        self.ray_namespace = ray_namespace
+        self.consumer_id = consumer_id
+        self.device_req = device
+        self.as_numpy = as_numpy
+        self.timeout_s = timeout_s
+        self._queue = None       # the reference's actor handle slot: endpoint or in-process queue
+        self._local = None
+        self._sess = None
+        self._comm = None
+        self._done = False
+        self.frames_read = 0
+
+    # ------------------------------------------------------------------------------------
+    def connect(self):
+        if self._queue is not None:
+            return self
+        from .queue.cpu_queue import get_queue
+
+        try:   # in-process queue (config 1)
+            self._local = get_queue(self.queue_name, self.ray_namespace)
+            self._queue = self._local
+            return self
+        except ValueError:
+            pass
+        try:
+            self._connect_distributed()
+        except Exception as e:
+            print(f"Error getting queue: {e}")   # data_reader.py:22
+            self.close()
+            raise
+        return self
+
+    def _connect_distributed(self):
+        from .parallel.launch import device_for, detect
+        from .parallel.rendezvous import consumer_join, form_world, open_store
+        from .queue.endpoint import QueueEndpoint
+        from .queue.ring import FrameRing, physical_slots
+
+        store = open_store(self.address, host_if_absent=False, timeout_s=self.timeout_s)
+        sess = consumer_join(store, self.ray_namespace, self.queue_name, self.consumer_id, self.timeout_s)
+        meta = sess.meta
+        if meta.device_kind == "cuda":
+            if self.device_req:
+                device = torch.device(self.device_req)
+            else:
+                n = max(1, torch.cuda.device_count())
+                device = torch.device(f"cuda:{(meta.n_producers + sess.role_index) % n}")
+            torch.cuda.set_device(device)
+        else:
+            device = torch.device("cpu")
+        comm = form_world(sess, device, self.timeout_s)
+        dtype = {"float32": torch.float32, "uint16": torch.uint16}[meta.dtype]
+        frame_bytes = int(np.prod(meta.frame_shape)) * (4 if meta.dtype == "float32" else 2)
+        share = max(1, math.ceil(meta.queue_size / max(1, meta.n_consumers)))
+        slots = physical_slots(share, frame_bytes, device, 0.8)
+        ring = FrameRing(meta.frame_shape, dtype, device, 0, slots)
+        ep = QueueEndpoint(ring, sess.rank, sess.world, comm, producer_ranks=sess.producer_ranks,
+                           consumer_ranks=sess.consumer_ranks, route=meta.extra.get("route", "balanced"),
+                           max_offer=int(meta.extra.get("max_offer", 64)), is_producer=False, is_consumer=True)
+        ep.start()
+        self._sess, self._comm, self._queue = sess, comm, ep
+        self.consumer_id = sess.role_index
+        log.info("consumer %d joined queue %s/%s as rank %d of %d on %s (%d slots)", sess.role_index,
+                 self.ray_namespace, self.queue_name, sess.rank, sess.world, device, slots)
+
+    # ------------------------------------------------------------------------------------
+    @property
+    def done(self) -> bool:
+        return self._done
+
+    @property
+    def endpoint(self):
+        return self._queue if self._local is None else None
+
+    def _check(self):
+        if self._queue is None:
+            raise RuntimeError("DataReader is not connected. Call connect() first.")   # data_reader.py:33
+
+    def lease(self, timeout: float = 0.0, stream=None) -> Optional[FrameItem]:
+        """Zero-copy: the next frame as a leased HBM slot (release it, or use ``with``)."""
+        self._check()
+        if self._local is not None:
+            raise DataReaderError("lease() needs the distributed HBM queue")
+        try:
+            it = self._queue.get(timeout=timeout, stream=stream)
+        except _QueueEOS as e:
+            self._done = True
+            raise EndOfStream(str(e)) from e
+        except QueuePeerError as e:
+            raise DataReaderError("Queue peer is dead.") from e
+        if it is not None:
+            self.frames_read += 1
+        return it
+
+    def read(self, timeout: float = 0.0):
+        """``[rank, idx, data, photon_energy]`` or None (nothing ready within ``timeout``)."""
+        self._check()
+        if self._local is not None:
+            item = self._local.get(timeout=timeout or None)
+            if item is not None:
+                self.frames_read += 1
+            return item
+        it = self.lease(timeout)
+        if it is None:
+            return None
+        rank, idx, data, pe = it.to_list(copy=True)
+        if self.as_numpy:
+            data = data.cpu().numpy()
+        return [rank, idx, data, pe]
+
+    def read_batch(self, max_n: int, timeout: float = 0.0) -> List[FrameItem]:
+        """Up to ``max_n`` leased frames in one call (zero-copy GPU consumers)."""
+        out: List[FrameItem] = []
+        while len(out) < max_n:
+            try:
+                it = self.lease(timeout if not out else 0.0)
+            except EndOfStream:
+                if out:
+                    break
+                raise
+            if it is None:
+                break
+            out.append(it)
+        return out
+
+    def close(self):
+        ep = self.endpoint
+        if ep is not None:
+            ep.close_consumer()
+            # stay in the collective rounds until the producers' EOS so peers never see a
+            # half-finished world; a reader closed early just stops taking frames
+            ep.join(timeout=self.timeout_s)
+            try:
+                import torch.distributed as dist
+
+                if dist.is_initialized():
+                    dist.destroy_process_group()
+            except Exception:  # noqa: BLE001
+                pass
+        self._queue = None
+        self._local = None
+
+    def __enter__(self):
+        self.connect()
+        return self
+
+    def __exit__(self, exc_type, exc_val, exc_tb):
+        self.close()

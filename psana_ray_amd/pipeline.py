@@ -188,9 +188,7 @@ class ProducerPipeline:
         self.engine.start(-1 if n_local is None else int(n_local), -1 if max_steps is None else int(max_steps))
         try:
             while not self.engine.join(0.05):
-                if stop is not None and stop.is_set():
-                    self.engine.request_stop()
-                if self.ep.failed is not None:
+                if (stop is not None and stop.is_set()) or self.ep.failed is not None or self.ep._consumers_gone:
                     self.engine.request_stop()
         finally:
             self.engine.request_stop()
@@ -203,6 +201,11 @@ class ProducerPipeline:
         self.ep.finish()
         if err:
             raise RuntimeError(f"producer engine failed: {err}")
+        self.ep._raise_if_failed()
+        if self.ep._consumers_gone:
+            from .queue.endpoint import QueueClosed
+
+            raise QueueClosed("no consumer is attached to the queue any more")
         return self.frames
 
 

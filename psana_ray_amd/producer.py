@@ -1,0 +1,259 @@
+"""``psana-ray-producer``: MPI-launched producer ranks streaming calibrated detector frames into
+the shared queue (reference parity: psana_ray/producer.py, console script setup.py:22-26).
+
+    mpirun -n 4 psana-ray-producer --exp mfxl1038923 --run 58 --detector_name epix10k2M --queue_size 400
+
+The 13 reference flags keep their exact names, types and defaults (producer.py:17-33; SURVEY
+2.6).  Image mode stays the default; ``--calib`` selects per-panel frames (Q-11).  Additive
+flags (``--device``, ``--common_mode``, ``--consumer_task``, ...) have defaults that reproduce
+the reference behaviour.  Rank/size come from the MPI launcher environment (no mpi4py).
+
+Per rank: event source (psana / raw-run file / synthetic) -> pinned host pages -> hipMemcpyAsync
+on a side stream -> gfx950 calibration kernels (pedestal, gain switching, common mode, masks,
+geometry) writing into HBM ring slots -> sharded queue -> consumers, with explicit per-producer
+end-of-stream (no global barrier, Q-7/Q-8) and SIGINT handling on every rank (Q-14).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import math
+import signal
+import sys
+import threading
+import traceback
+from typing import Optional
+
+import numpy as np
+
+from .config import (BACKOFF_BASE_S, BACKOFF_JITTER_S, BACKOFF_MAX_S, DEFAULT_LOG_LEVEL, DEFAULT_NUM_CONSUMERS,
+                     DEFAULT_QUEUE_NAME, DEFAULT_QUEUE_SIZE, DEFAULT_RAY_ADDRESS, DEFAULT_RAY_NAMESPACE, LOG_LEVELS,
+                     QUEUE_LOOKUP_DELAY_S, QUEUE_LOOKUP_RETRIES, CommonModeParams, PeakFinderParams)
+
+log = logging.getLogger("psana_ray_amd.producer")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    parser = argparse.ArgumentParser(description="PsanaWrapper Data Producer")
+    # ---- reference flags: identical names / types / defaults (psana_ray/producer.py:19-32)
+    parser.add_argument("--exp", type=str, required=True, help="Experiment name")
+    parser.add_argument("--run", type=int, required=True, help="Run number")
+    parser.add_argument("--detector_name", type=str, required=True, help="Detector name")
+    parser.add_argument("--calib", action="store_true", help="Use calib mode")
+    parser.add_argument("--uses_bad_pixel_mask", action="store_true", help="Use bad pixel mask")
+    parser.add_argument("--manual_mask_path", type=str, default=None, help="Path to a manual mask in npy")
+    parser.add_argument("--ray_address", type=str, default=DEFAULT_RAY_ADDRESS, help="Address of the Ray cluster")
+    parser.add_argument("--ray_namespace", type=str, default=DEFAULT_RAY_NAMESPACE,
+                        help="Ray namespace to use for both queues")
+    parser.add_argument("--queue_name", type=str, default=DEFAULT_QUEUE_NAME, help="Queue name")
+    parser.add_argument("--queue_size", type=int, default=DEFAULT_QUEUE_SIZE, help="Maximum queue size")
+    parser.add_argument("--num_consumers", type=int, default=DEFAULT_NUM_CONSUMERS,
+                        help="Number of consumer processes expected.")
+    parser.add_argument("--max_steps", type=int, default=None, help="Maximum number of steps before terminating")
+    parser.add_argument("--log_level", type=str, default=DEFAULT_LOG_LEVEL, choices=LOG_LEVELS, help="Logging level")
+    # ---- additive flags (MI355X framework)
+    g = parser.add_argument_group("psana_ray_amd")
+    g.add_argument("--device", type=str, default="auto", help="auto | cpu | cuda[:i] (auto: GPU local_rank)")
+    g.add_argument("--mode", type=str, default=None, choices=["raw", "calib", "image"],
+                   help="override the retrieval mode (default: image, or calib with --calib)")
+    g.add_argument("--common_mode", type=str, default="off",
+                   help="common-mode correction: off | default | flags,thr,maxcorr,npix_min[,bank_cols]")
+    g.add_argument("--num_events", type=int, default=None, help="events in a synthetic run (default: endless)")
+    g.add_argument("--data_dir", type=str, default=None, help="raw-run files directory (or $PSANA_RAY_DATA)")
+    g.add_argument("--chunk", type=int, default=16, help="frames per H2D copy / kernel launch")
+    g.add_argument("--route", type=str, default="balanced", choices=["balanced", "local_first", "spread"])
+    g.add_argument("--consumer_task", type=str, default="none", choices=["none", "peakfind"],
+                   help="also consume on every producer rank (co-located consumer, BASELINE config 5)")
+    g.add_argument("--producer_slots", type=int, default=64, help="calibrated frames a rank may hold un-routed")
+    g.add_argument("--hbm_fraction", type=float, default=0.8, help="cap of free HBM used for ring slots")
+    g.add_argument("--timeout", type=float, default=300.0, help="rendezvous / peer timeout in seconds")
+    g.add_argument("--local", action="store_true",
+                   help="single-process queue: no rendezvous; requires --consumer_task (no external consumers)")
+    return parser
+
+
+def parse_arguments(argv=None):
+    return build_parser().parse_args(argv)
+
+
+def backoff_delays(retries: int):
+    """The reference's full-queue backoff schedule (producer.py:84-111): 0.1, 0.2, 0.4, 0.8, 1.6, then
+    2.0 s forever, each plus U(0, 0.5) s jitter.  Returns (delay without jitter, jitter bound)."""
+    delay = min(BACKOFF_MAX_S, BACKOFF_BASE_S * (2 ** retries))
+    return delay, BACKOFF_JITTER_S
+
+
+def initialize_queue(ray_address, ray_namespace, queue_name, queue_size, rank, size, num_consumers, frame_shape,
+                     dtype, device_kind, extra=None, max_retries=QUEUE_LOOKUP_RETRIES,
+                     retry_delay=QUEUE_LOOKUP_DELAY_S, timeout_s=300.0):
+    """Join (rank 0: create) the queue session; None on failure (producer.py:35-71)."""
+    from .parallel.rendezvous import SessionMeta, open_store, producer_join
+
+    try:
+        store = open_store(ray_address, host_if_absent=(rank == 0), timeout_s=timeout_s, retries=max_retries,
+                           retry_delay_s=retry_delay)
+        meta = SessionMeta(int(queue_size), int(size), int(num_consumers), tuple(frame_shape), dtype, device_kind,
+                           extra=dict(extra or {}))
+        sess = producer_join(store, ray_namespace, queue_name, rank, size, meta, timeout_s)
+        log.info("Rank %d: Successfully connected to shared queue.", rank)
+        return sess
+    except Exception as e:  # noqa: BLE001 - reference: log + None (producer.py:69-71)
+        log.error("Rank %d: Error in initialize_queue: %s", rank, e)
+        return None
+
+
+initialize_ray = initialize_queue   # reference name (producer.py:35), kept for API parity
+
+
+def load_masks(source, uses_bad_pixel_mask: bool, manual_mask_path: Optional[str]):
+    """Combined mask (truthy keeps, producer.py:81-82,92-95): bad-pixel AND manual."""
+    mask = None
+    if uses_bad_pixel_mask:
+        mask = np.asarray(source.create_bad_pixel_mask()).astype(bool)
+    if manual_mask_path is not None:
+        manual = np.load(manual_mask_path).astype(bool)   # allow_pickle stays False
+        if mask is None:
+            mask = manual
+        elif manual.shape == mask.shape:
+            mask = mask & manual
+        else:
+            raise ValueError(f"manual mask {manual.shape} and bad-pixel mask {mask.shape} differ in shape")
+    return mask
+
+
+def produce_data(pipeline, max_steps=None, stop=None):
+    """Run one rank's producer pipeline (producer.py:78-130); returns frames produced."""
+    from .queue.endpoint import QueueClosed, QueuePeerError
+
+    try:
+        return pipeline.run(max_steps=max_steps, stop=stop)
+    except QueuePeerError:
+        log.error("Rank %d: Queue peer is dead. Exiting...", pipeline.rank)   # producer.py:113
+        return pipeline.frames
+    except QueueClosed:
+        log.error("Rank %d: No consumer attached any more. Exiting...", pipeline.rank)
+        pipeline.ep.finish()
+        return pipeline.frames
+
+
+def main(argv=None) -> int:
+    args = parse_arguments(argv)
+    logging.basicConfig(level=getattr(logging, args.log_level),
+                        format="%(asctime)s - %(levelname)s - %(message)s")   # producer.py:135-136
+    import torch
+
+    from .models.calibrator import Calibrator
+    from .models.detector import Mode
+    from .parallel.launch import bind_numa_to_device, detect, device_for
+    from .parallel.rendezvous import Heartbeat, finish_session, form_world
+    from .pipeline import PeakFinderConsumer, ProducerPipeline
+    from .queue.endpoint import EndOfStream, QueueEndpoint
+    from .queue.ring import FrameRing, physical_slots
+    from .source import open_source
+
+    li = detect()
+    rank, size = li.rank, li.size
+    device = device_for(li.local_rank, args.device)
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+        bind_numa_to_device(device)
+    stop = threading.Event()
+
+    def signal_handler(sig, frame):   # every rank (Q-14): stop producing, advertise EOS, exit cleanly
+        log.error("Ctrl+C pressed. Shutting down...")
+        stop.set()
+
+    signal.signal(signal.SIGINT, signal_handler)
+
+    mode = Mode(args.mode) if args.mode else (Mode.calib if args.calib else Mode.image)   # producer.py:156-159
+    source = open_source(args.exp, args.run, args.detector_name, rank=rank, size=size, n_events=args.num_events,
+                         pinned=device.type == "cuda", data_dir=args.data_dir)
+    mask = load_masks(source, args.uses_bad_pixel_mask, args.manual_mask_path)
+    cm = CommonModeParams.parse(args.common_mode) if mode != Mode.raw else None
+    calibrator = Calibrator(source.consts, device, mode, mask=mask, common_mode=cm) \
+        if not getattr(source, "calibrated", False) else None
+    frame_shape = calibrator.out_shape if calibrator else tuple(source.spec.frame_shape)
+    dtype = "uint16" if mode == Mode.raw else "float32"
+    co_consumer = args.consumer_task != "none"
+    frame_bytes = int(np.prod(frame_shape)) * (2 if mode == Mode.raw else 4)
+
+    sess = None
+    comm = None
+    hb = None
+    try:
+        if args.local or (size == 1 and args.num_consumers == 0):
+            if not co_consumer:
+                log.error("--local needs --consumer_task (nobody would read the queue)")
+                return 2
+            ring = FrameRing(frame_shape, torch.float32 if dtype == "float32" else torch.uint16, device,
+                             args.producer_slots, physical_slots(args.queue_size, frame_bytes, device,
+                                                                 args.hbm_fraction, args.producer_slots))
+            ep = QueueEndpoint(ring)
+        else:
+            n_consumer_ranks = args.num_consumers
+            sess = initialize_queue(args.ray_address, args.ray_namespace, args.queue_name, args.queue_size, rank,
+                                    size, n_consumer_ranks, frame_shape, dtype, device.type,
+                                    extra={"route": args.route, "co_consumers": co_consumer},
+                                    timeout_s=args.timeout)
+            if sess is None:
+                return 1
+            if rank == 0:
+                hb = Heartbeat(sess.store, args.ray_namespace, args.queue_name)
+            comm = form_world(sess, device, args.timeout)
+            consumers = sess.consumer_ranks + (sess.producer_ranks if co_consumer else [])
+            n_cons = max(1, len(consumers))
+            share = max(1, math.ceil(args.queue_size / n_cons)) if co_consumer else 0
+            cslots = physical_slots(share, frame_bytes, device, args.hbm_fraction, args.producer_slots) if share else 0
+            ring = FrameRing(frame_shape, torch.float32 if dtype == "float32" else torch.uint16, device,
+                             args.producer_slots, cslots)
+            ep = QueueEndpoint(ring, sess.rank, sess.world, comm, producer_ranks=sess.producer_ranks,
+                               consumer_ranks=sorted(consumers), route=args.route, is_producer=True,
+                               is_consumer=co_consumer)
+            ep.start()
+        pipe = ProducerPipeline(source, calibrator, ep, rank=rank, chunk=args.chunk,
+                                log_every=1 if logging.getLogger().isEnabledFor(logging.DEBUG) else 0)
+        cons_thread = None
+        stats = {}
+        if co_consumer:
+            cons = PeakFinderConsumer(ep, frame_shape, PeakFinderParams())
+
+            def consume():
+                while True:
+                    try:
+                        cons.poll(timeout=0.1)
+                    except EndOfStream:
+                        break
+                stats["peaks"] = cons.synchronize()
+                stats["consumed"] = cons.frames
+
+            cons_thread = threading.Thread(target=consume, name="co-consumer", daemon=True)
+            cons_thread.start()
+        n = produce_data(pipe, max_steps=args.max_steps, stop=stop)
+        log.info("Rank %d: produced %d frames", rank, n)
+        if cons_thread is not None:
+            cons_thread.join()
+            log.info("Rank %d: co-located consumer processed %d frames, %d peaks", rank, stats.get("consumed", 0),
+                     stats.get("peaks", 0))
+        ep.join(timeout=args.timeout)
+        return 0
+    except Exception as e:
+        log.error("Rank %d: Unhandled exception in main: %s", rank, e)   # producer.py:163-166
+        log.error("Traceback:")
+        log.error(traceback.format_exc())
+        raise
+    finally:
+        if hb is not None:
+            hb.stop()
+        if sess is not None:
+            finish_session(sess)
+        try:
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+if __name__ == "__main__":
+    sys.exit(main())
