@@ -227,6 +227,8 @@ def main(argv=None):
             "transport_round_ms_rank0": round(st.get("round_ms", 0.0), 3),
             "bytes_sent_rank0": st.get("bytes_sent", 0),
             "numa_node": numa,
+            "producer_host_s_stage_acquire_launch_commit_total": (
+                [round(x, 4) for x in prod.engine.timing()] if prod.engine is not None else None),
         },
     }
     if rank == 0:

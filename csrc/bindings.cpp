@@ -156,7 +156,13 @@ PYBIND11_MODULE(_C, m) {
       .def("get_batch", &SP::get_batch, py::arg("max_n"), py::arg("timeout_s"), py::arg("stream"),
            py::call_guard<py::gil_scoped_release>())
       .def("release_batch", &SP::release_batch, py::arg("slots"), py::arg("stream"))
-      .def("headers", &SP::headers);
+      .def("headers", &SP::headers)
+      .def("acquire_batch", &SP::acquire_batch, py::arg("n"), py::arg("timeout_s"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("commit_batch", &SP::commit_batch, py::arg("slots"), py::arg("headers"), py::arg("stream"))
+      .def("end_send_batch", &SP::end_send_batch, py::arg("slots"), py::arg("stream"))
+      .def("end_recv_batch", &SP::end_recv_batch, py::arg("slots"), py::arg("headers"), py::arg("stream"))
+      .def_property_readonly("event_records", &SP::event_records);
 
   py::class_<pr::CalibPlan>(m, "CalibPlan")
       .def(py::init<>())
@@ -197,7 +203,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("running", &pr::ProducerEngine::running)
       .def_property_readonly("frames", &pr::ProducerEngine::frames)
       .def_property_readonly("full_waits", &pr::ProducerEngine::full_waits)
-      .def("error", &pr::ProducerEngine::error);
+      .def("error", &pr::ProducerEngine::error)
+      .def("timing", &pr::ProducerEngine::timing);
 
   py::class_<pr::RawRunReader>(m, "RawRunReader")
       .def(py::init<const std::string&, int>(), py::arg("path"), py::arg("n_threads") = 4)

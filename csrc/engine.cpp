@@ -122,59 +122,81 @@ bool ProducerEngine::join(double timeout_s) {
   return true;
 }
 
+std::vector<double> ProducerEngine::timing() const {
+  std::lock_guard<std::mutex> lk(err_mu_);
+  return {t_stage_, t_acquire_, t_launch_, t_commit_, t_total_};
+}
+
 std::string ProducerEngine::error() const {
   std::lock_guard<std::mutex> lk(err_mu_);
   return error_;
 }
 
 void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps) {
+  using clk = std::chrono::steady_clock;
+  auto secs = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
+  const auto t_begin = clk::now();
   try {
     hip_check(hipSetDevice(device_), "hipSetDevice");
     int64_t limit = n_local_events;
     if (max_steps >= 0 && (limit < 0 || max_steps < limit)) limit = max_steps;
     const uint64_t stream_c = reinterpret_cast<uint64_t>(compute_);
     std::vector<char> used(n_raw_bufs_, 0);
-    int64_t k = 0;  // rank-local event index
-    int64_t chunk_no = 0;
     std::vector<uint64_t> in, out;
     std::vector<int> slots;
-    while (!stop_.load()) {
-      int n = chunk_;
-      if (limit >= 0) n = (int)std::min<int64_t>(n, limit - k);
-      if (n <= 0) break;
-      const int b = (int)(chunk_no++ % n_raw_bufs_);
+    std::vector<SlotHeader> hdrs;
+    const size_t nsrc = src_frames_.size();
+    // host-side software pipeline: the copy of chunk c+1 is queued on the side stream BEFORE
+    // chunk c waits for slots / launches, so the copy engine never runs dry behind host work
+    auto stage = [&](int64_t k0, int n, int b) {
       char* buf = static_cast<char*>(raw_bufs_) + (size_t)b * chunk_ * plan_.raw_frame_bytes;
       if (used[b]) hip_check(hipStreamWaitEvent(h2d_, buf_free_[b], 0), "wait buf free");
       used[b] = 1;
-      // stage: coalesce host-contiguous runs into single copies
-      const size_t nsrc = src_frames_.size();
       int i = 0;
-      while (i < n) {
-        const uint64_t s0 = src_frames_[(k + i) % nsrc];
+      while (i < n) {   // coalesce host-contiguous runs into single copies
+        const uint64_t s0 = src_frames_[(k0 + i) % nsrc];
         int j = i + 1;
-        while (j < n && src_frames_[(k + j) % nsrc] == s0 + (uint64_t)(j - i) * plan_.raw_frame_bytes) ++j;
+        while (j < n && src_frames_[(k0 + j) % nsrc] == s0 + (uint64_t)(j - i) * plan_.raw_frame_bytes) ++j;
         hip_check(hipMemcpyAsync(buf + (size_t)i * plan_.raw_frame_bytes, reinterpret_cast<const void*>(s0),
                                  (size_t)(j - i) * plan_.raw_frame_bytes, hipMemcpyDefault, h2d_),
                   "stage copy");
         i = j;
       }
       hip_check(hipEventRecord(h2d_done_[b], h2d_), "record h2d");
-      // acquire destination slots (backpressure)
+    };
+    auto chunk_len = [&](int64_t k0) -> int {
+      int n = chunk_;
+      if (limit >= 0) n = (int)std::max<int64_t>(0, std::min<int64_t>(n, limit - k0));
+      return n;
+    };
+    int64_t k = 0;       // first event of the current chunk
+    int64_t chunk_no = 0;
+    int n = chunk_len(0);
+    if (n > 0) {
+      const auto t0 = clk::now();
+      stage(0, n, 0);
+      t_stage_ += secs(t0, clk::now());
+    }
+    while (n > 0 && !stop_.load()) {
+      const int b = (int)(chunk_no % n_raw_bufs_);
+      const int64_t k_next = k + n;
+      const int n_next = chunk_len(k_next);
+      auto t0 = clk::now();
+      if (n_next > 0) stage(k_next, n_next, (int)((chunk_no + 1) % n_raw_bufs_));
+      auto t1 = clk::now();
+      t_stage_ += secs(t0, t1);
       slots.clear();
-      while ((int)slots.size() < n && !stop_.load()) {
-        const int s = pool_->acquire_produce(0.05);
-        if (s < 0) {
+      while (slots.empty() && !stop_.load()) {   // all n slots at once, one event wait per batch
+        slots = pool_->acquire_batch(n, 0.05, stream_c);
+        if (slots.empty()) {
           if (pool_->closed()) break;
           full_waits_.fetch_add(1);
-          continue;
         }
-        pool_->wait_free_on(s, stream_c);
-        slots.push_back(s);
       }
-      if ((int)slots.size() < n) {  // stopped while waiting
-        for (int s : slots) pool_->abort_produce(s);
-        break;
-      }
+      auto t2 = clk::now();
+      t_acquire_ += secs(t1, t2);
+      if ((int)slots.size() < n) break;   // stopped while waiting
+      char* buf = static_cast<char*>(raw_bufs_) + (size_t)b * chunk_ * plan_.raw_frame_bytes;
       hip_check(hipStreamWaitEvent(compute_, h2d_done_[b], 0), "wait h2d");
       in.resize(n);
       out.resize(n);
@@ -184,21 +206,31 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps) {
       }
       run_calib_plan(plan_, in, out, stream_c);
       hip_check(hipEventRecord(buf_free_[b], compute_), "record buf free");
+      auto t3 = clk::now();
+      t_launch_ += secs(t2, t3);
+      hdrs.resize(n);
       for (int q = 0; q < n; ++q) {
-        SlotHeader h;
-        h.rank = rank_;
-        h.idx = k + q;
-        h.gevt = rank_ + (k + q) * size_;
-        h.photon_energy = src_pe_[(k + q) % src_pe_.size()];
-        pool_->commit_produce(slots[q], h, stream_c);
+        hdrs[q].rank = rank_;
+        hdrs[q].idx = k + q;
+        hdrs[q].gevt = rank_ + (k + q) * size_;
+        hdrs[q].photon_energy = src_pe_[(k + q) % src_pe_.size()];
       }
-      k += n;
+      pool_->commit_batch(slots, hdrs, stream_c);   // one ready event for the whole chunk
+      t_commit_ += secs(t3, clk::now());
       frames_.fetch_add(n);
+      k = k_next;
+      n = n_next;
+      ++chunk_no;
     }
     hip_check(hipStreamSynchronize(compute_), "final sync");
+    hip_check(hipStreamSynchronize(h2d_), "final sync");
   } catch (const std::exception& e) {
     std::lock_guard<std::mutex> lk(err_mu_);
     error_ = e.what();
+  }
+  {
+    std::lock_guard<std::mutex> lk(err_mu_);
+    t_total_ = secs(t_begin, clk::now());
   }
   running_.store(false);
 }

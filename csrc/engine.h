@@ -68,6 +68,8 @@ class ProducerEngine {
   int64_t frames() const { return frames_.load(); }
   int64_t full_waits() const { return full_waits_.load(); }
   std::string error() const;
+  // host-side time (seconds) spent per loop part: [stage copies, acquire slots, launch kernels, commit, total]
+  std::vector<double> timing() const;
 
  private:
   void loop(int64_t n_local_events, int64_t max_steps);
@@ -88,6 +90,7 @@ class ProducerEngine {
   std::thread thread_;
   std::atomic<bool> stop_{false}, running_{false};
   std::atomic<int64_t> frames_{0}, full_waits_{0};
+  double t_stage_ = 0, t_acquire_ = 0, t_launch_ = 0, t_commit_ = 0, t_total_ = 0;
   mutable std::mutex err_mu_;
   std::string error_;
 };

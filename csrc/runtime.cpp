@@ -31,24 +31,23 @@ SlotPool::SlotPool(int producer_budget, int consumer_budget, int device)
   check(producer_budget >= 0 && consumer_budget >= 0 && n_ > 0, "SlotPool: budgets must be >= 0 and sum > 0");
   state_.assign(n_, kFree);
   hdr_.resize(n_);
-  free_ev_valid_.assign(n_, 0);
+  ready_ref_.resize(n_);
+  free_ref_.resize(n_);
   for (int i = 0; i < n_; ++i) free_list_.push_back(i);
   if (device_ >= 0) {
     set_device();
-    ready_ev_.resize(n_);
-    free_ev_.resize(n_);
-    for (int i = 0; i < n_; ++i) {
-      hip_check(hipEventCreateWithFlags(&ready_ev_[i], hipEventDisableTiming), "hipEventCreate");
-      hip_check(hipEventCreateWithFlags(&free_ev_[i], hipEventDisableTiming), "hipEventCreate");
-    }
+    const int ne = std::max(256, 4 * n_);
+    ev_.resize(ne);
+    ev_gen_.assign(ne, 0);
+    for (int i = 0; i < ne; ++i)
+      hip_check(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
   }
 }
 
 SlotPool::~SlotPool() {
   if (device_ >= 0) {
     set_device();
-    for (auto e : ready_ev_) (void)hipEventDestroy(e);
-    for (auto e : free_ev_) (void)hipEventDestroy(e);
+    for (auto e : ev_) (void)hipEventDestroy(e);
   }
 }
 
@@ -60,8 +59,21 @@ void SlotPool::check_slot(int slot) const {
   check(slot >= 0 && slot < n_, "SlotPool: slot index out of range");
 }
 
-void SlotPool::record(hipEvent_t ev, uint64_t stream) const {
-  hip_check(hipEventRecord(ev, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord");
+SlotPool::EvRef SlotPool::record_shared_locked(uint64_t stream) {
+  EvRef r;
+  if (device_ < 0) return r;
+  set_device();
+  r.idx = ev_next_;
+  ev_next_ = (ev_next_ + 1) % (int)ev_.size();
+  r.gen = ++ev_gen_[r.idx];
+  hip_check(hipEventRecord(ev_[r.idx], reinterpret_cast<hipStream_t>(stream)), "hipEventRecord");
+  ++ev_records_;
+  return r;
+}
+
+void SlotPool::wait_ref(const EvRef& r, uint64_t stream) const {
+  if (device_ < 0 || r.idx < 0) return;
+  hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ev_[r.idx], 0), "hipStreamWaitEvent");
 }
 
 static std::string state_msg(const char* op, int want, int got) {
@@ -104,10 +116,7 @@ void SlotPool::commit_produce(int slot, const SlotHeader& h, uint64_t stream) {
   std::lock_guard<std::mutex> lk(mu_);
   check(state_[slot] == kProducing, state_msg("commit_produce", kProducing, state_[slot]));
   hdr_[slot] = h;
-  if (device_ >= 0) {
-    set_device();
-    record(ready_ev_[slot], stream);
-  }
+  ready_ref_[slot] = record_shared_locked(stream);
   state_[slot] = kProduced;
   produced_fifo_.push_back(slot);
   ++st_.produced;
@@ -180,11 +189,7 @@ void SlotPool::end_send(int slot, uint64_t stream) {
   check_slot(slot);
   std::lock_guard<std::mutex> lk(mu_);
   check(state_[slot] == kSending, state_msg("end_send", kSending, state_[slot]));
-  if (device_ >= 0) {
-    set_device();
-    record(free_ev_[slot], stream);
-    free_ev_valid_[slot] = 1;
-  }
+  free_ref_[slot] = record_shared_locked(stream);
   state_[slot] = kFree;
   --producer_held_;
   free_list_.push_back(slot);
@@ -213,10 +218,7 @@ void SlotPool::end_recv(int slot, const SlotHeader& h, uint64_t stream) {
   std::lock_guard<std::mutex> lk(mu_);
   check(state_[slot] == kReceiving, state_msg("end_recv", kReceiving, state_[slot]));
   hdr_[slot] = h;
-  if (device_ >= 0) {
-    set_device();
-    record(ready_ev_[slot], stream);
-  }
+  ready_ref_[slot] = record_shared_locked(stream);
   state_[slot] = kReady;
   ready_fifo_.push_back(slot);
   ++st_.received;
@@ -253,11 +255,7 @@ void SlotPool::release(int slot, uint64_t stream) {
   check_slot(slot);
   std::lock_guard<std::mutex> lk(mu_);
   check(state_[slot] == kLeased, state_msg("release", kLeased, state_[slot]));
-  if (device_ >= 0) {
-    set_device();
-    record(free_ev_[slot], stream);
-    free_ev_valid_[slot] = 1;
-  }
+  free_ref_[slot] = record_shared_locked(stream);
   state_[slot] = kFree;
   --consumer_held_;
   free_list_.push_back(slot);
@@ -279,28 +277,129 @@ int SlotPool::consumer_held() const {
 void SlotPool::wait_ready_on(int slot, uint64_t stream) const {
   check_slot(slot);
   if (device_ < 0) return;
+  EvRef r;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!ref_live_locked(ready_ref_[slot])) return;
+    r = ready_ref_[slot];
+  }
   set_device();
-  hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ready_ev_[slot], 0), "hipStreamWaitEvent");
+  wait_ref(r, stream);
 }
 
 void SlotPool::wait_free_on(int slot, uint64_t stream) const {
   check_slot(slot);
   if (device_ < 0) return;
-  bool valid;
+  EvRef r;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    valid = free_ev_valid_[slot] != 0;
+    if (!ref_live_locked(free_ref_[slot])) return;
+    r = free_ref_[slot];
   }
-  if (!valid) return;
   set_device();
-  hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), free_ev_[slot], 0), "hipStreamWaitEvent");
+  wait_ref(r, stream);
 }
 
 void SlotPool::sync_ready(int slot) const {
   check_slot(slot);
   if (device_ < 0) return;
+  hipEvent_t e;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!ref_live_locked(ready_ref_[slot])) return;
+    e = ev_[ready_ref_[slot].idx];
+  }
   set_device();
-  hip_check(hipEventSynchronize(ready_ev_[slot]), "hipEventSynchronize");
+  hip_check(hipEventSynchronize(e), "hipEventSynchronize");
+}
+
+std::vector<int> SlotPool::acquire_batch(int n, double timeout_s, uint64_t stream) {
+  std::vector<int> out;
+  std::vector<EvRef> waits;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    const auto pred = [&] { return closed_ || (producer_held_ + n <= pb_ && (int)free_list_.size() >= n); };
+    if (!pred()) {
+      ++st_.produce_full;
+      if (timeout_s < 0) cv_produce_.wait(lk, pred);
+      else if (!cv_produce_.wait_for(lk, std::chrono::duration<double>(timeout_s), pred)) return out;
+    }
+    if (closed_) return out;
+    for (int i = 0; i < n; ++i) {
+      const int s = free_list_.front();
+      free_list_.pop_front();
+      state_[s] = kProducing;
+      ++producer_held_;
+      out.push_back(s);
+      const EvRef r = free_ref_[s];
+      if (!ref_live_locked(r)) continue;
+      bool dup = false;
+      for (const auto& w : waits) dup |= (w.idx == r.idx && w.gen == r.gen);
+      if (!dup) waits.push_back(r);
+    }
+  }
+  if (device_ >= 0 && !waits.empty()) {
+    set_device();
+    for (const auto& w : waits) wait_ref(w, stream);
+  }
+  return out;
+}
+
+void SlotPool::commit_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream) {
+  check(slots.size() == hdrs.size(), "commit_batch: size mismatch");
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kProducing, state_msg("commit_batch", kProducing, state_[s]));
+  }
+  const EvRef r = record_shared_locked(stream);
+  for (size_t i = 0; i < slots.size(); ++i) {
+    const int s = slots[i];
+    hdr_[s] = hdrs[i];
+    ready_ref_[s] = r;
+    state_[s] = kProduced;
+    produced_fifo_.push_back(s);
+    ++st_.produced;
+  }
+  if (auto_route_) route_pending_locked();
+}
+
+void SlotPool::end_send_batch(const std::vector<int>& slots, uint64_t stream) {
+  if (slots.empty()) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kSending, state_msg("end_send_batch", kSending, state_[s]));
+  }
+  const EvRef r = record_shared_locked(stream);
+  for (int s : slots) {
+    free_ref_[s] = r;
+    state_[s] = kFree;
+    --producer_held_;
+    free_list_.push_back(s);
+    ++st_.sent;
+  }
+  cv_produce_.notify_all();
+}
+
+void SlotPool::end_recv_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream) {
+  check(slots.size() == hdrs.size(), "end_recv_batch: size mismatch");
+  if (slots.empty()) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kReceiving, state_msg("end_recv_batch", kReceiving, state_[s]));
+  }
+  const EvRef r = record_shared_locked(stream);
+  for (size_t i = 0; i < slots.size(); ++i) {
+    const int s = slots[i];
+    hdr_[s] = hdrs[i];
+    ready_ref_[s] = r;
+    state_[s] = kReady;
+    ready_fifo_.push_back(s);
+    ++st_.received;
+  }
+  cv_ready_.notify_all();
 }
 
 SlotHeader SlotPool::header(int slot) const {
@@ -354,30 +453,37 @@ int SlotPool::pop_ready_locked() {
 
 std::vector<int> SlotPool::get_batch(int max_n, double timeout_s, uint64_t stream) {
   std::vector<int> out;
+  std::vector<EvRef> waits;
   {
     std::unique_lock<std::mutex> lk(mu_);
     const auto pred = [&] { return closed_ || !ready_fifo_.empty(); };
     if (timeout_s > 0 && !pred()) cv_ready_.wait_for(lk, std::chrono::duration<double>(timeout_s), pred);
-    while ((int)out.size() < max_n && !ready_fifo_.empty()) out.push_back(pop_ready_locked());
+    while ((int)out.size() < max_n && !ready_fifo_.empty()) {
+      const int s = pop_ready_locked();
+      out.push_back(s);
+      const EvRef r = ready_ref_[s];
+      if (!ref_live_locked(r)) continue;
+      bool dup = false;
+      for (const auto& w : waits) dup |= (w.idx == r.idx && w.gen == r.gen);
+      if (!dup) waits.push_back(r);
+    }
   }
-  if (device_ >= 0 && !out.empty()) {
+  if (device_ >= 0 && !waits.empty()) {
     set_device();
-    for (int s : out)
-      hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ready_ev_[s], 0), "hipStreamWaitEvent");
+    for (const auto& w : waits) wait_ref(w, stream);
   }
   return out;
 }
 
 void SlotPool::release_batch(const std::vector<int>& slots, uint64_t stream) {
   std::lock_guard<std::mutex> lk(mu_);
-  if (device_ >= 0) set_device();
   for (int slot : slots) {
     check_slot(slot);
     check(state_[slot] == kLeased, state_msg("release_batch", kLeased, state_[slot]));
-    if (device_ >= 0) {
-      record(free_ev_[slot], stream);
-      free_ev_valid_[slot] = 1;
-    }
+  }
+  const EvRef r = record_shared_locked(stream);
+  for (int slot : slots) {
+    free_ref_[slot] = r;
     state_[slot] = kFree;
     --consumer_held_;
     free_list_.push_back(slot);

@@ -117,15 +117,29 @@ class SlotPool {
   // consumer credit exists (on commit and on release), entirely in native code
   void set_auto_route(bool on);
 
-  // batched consumer calls (one native call per batch instead of one per frame)
+  // batched calls: one native call AND one HIP event record per batch instead of per frame
   std::vector<int> get_batch(int max_n, double timeout_s, uint64_t stream);
   void release_batch(const std::vector<int>& slots, uint64_t stream);
   std::vector<SlotHeader> headers(const std::vector<int>& slots) const;
+  std::vector<int> acquire_batch(int n, double timeout_s, uint64_t stream);  // all n or none
+  void commit_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream);
+  void end_send_batch(const std::vector<int>& slots, uint64_t stream);
+  void end_recv_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream);
+  int64_t event_records() const { return ev_records_; }
 
  private:
   void set_device() const;
   void check_slot(int slot) const;
-  void record(hipEvent_t ev, uint64_t stream) const;
+  // Shared event ring: a batch records ONE event and every slot of the batch references it as
+  // (index, generation).  A reference whose generation was overwritten is treated as complete:
+  // the ring holds >= 4x the slots, so an event is re-recorded only after thousands of batches.
+  struct EvRef {
+    int idx = -1;
+    uint64_t gen = 0;
+  };
+  EvRef record_shared_locked(uint64_t stream);
+  void wait_ref(const EvRef& r, uint64_t stream) const;
+  bool ref_live_locked(const EvRef& r) const { return r.idx >= 0 && ev_gen_[r.idx] == r.gen; }
   void route_pending_locked();
   int pop_ready_locked();
 
@@ -134,8 +148,11 @@ class SlotPool {
   std::condition_variable cv_produce_, cv_ready_;
   std::vector<int> state_;
   std::vector<SlotHeader> hdr_;
-  std::vector<hipEvent_t> ready_ev_, free_ev_;
-  std::vector<char> free_ev_valid_;
+  std::vector<hipEvent_t> ev_;
+  std::vector<uint64_t> ev_gen_;
+  int ev_next_ = 0;
+  int64_t ev_records_ = 0;
+  std::vector<EvRef> ready_ref_, free_ref_;
   std::deque<int> free_list_, produced_fifo_, ready_fifo_;
   int producer_held_ = 0, consumer_held_ = 0;
   bool closed_ = false;

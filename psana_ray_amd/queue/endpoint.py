@@ -281,10 +281,9 @@ class QueueEndpoint:
                                                   float("nan") if _pe_from_bits(row[b + 3]) is None
                                                   else _pe_from_bits(row[b + 3]))))
         comm.exchange(sends, recvs)
-        for s in send_slots:
-            self.pool.end_send(s, sh)
-        for s, h in recv_meta:
-            self.pool.end_recv(s, h, sh)
+        # one HIP event per direction per round (not one per frame)
+        self.pool.end_send_batch(send_slots, sh)
+        self.pool.end_recv_batch([s for s, _ in recv_meta], [h for _, h in recv_meta], sh)
         self._round += 1
         self.rounds += 1
         self.frames_routed += len(plan)
