@@ -12,6 +12,11 @@ namespace py = pybind11;
 #include "engine.h"
 #include "kernels.h"
 
+namespace pr {
+std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers, const std::vector<int64_t>& credits,
+                                       int64_t round_id, int policy);
+}
+
 using pr::FramePtrs;
 
 static FramePtrs make_ptrs(const std::vector<uint64_t>& in, const std::vector<uint64_t>& out) {
@@ -78,6 +83,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("son_min"), py::arg("radius"), py::arg("max_peaks"), py::arg("peaks"), py::arg("counts"),
         py::arg("summary"), py::arg("stream"));
 
+  m.def("plan_round", &pr::plan_round_native, py::arg("offers"), py::arg("credits"), py::arg("round_id"),
+        py::arg("policy"), "flattened (producer, offer_index, consumer) triples");
   m.def("memcpy_h2d_async", &pr::memcpy_h2d_async, py::arg("dst"), py::arg("src"), py::arg("bytes"),
         py::arg("stream"));
   m.def("memcpy_h2d_batch", &pr::memcpy_h2d_batch, py::arg("dst"), py::arg("src"), py::arg("bytes"),
@@ -160,6 +167,8 @@ PYBIND11_MODULE(_C, m) {
       .def("acquire_batch", &SP::acquire_batch, py::arg("n"), py::arg("timeout_s"), py::arg("stream"),
            py::call_guard<py::gil_scoped_release>())
       .def("commit_batch", &SP::commit_batch, py::arg("slots"), py::arg("headers"), py::arg("stream"))
+      .def("begin_send_batch", &SP::begin_send_batch, py::arg("slots"), py::arg("stream"))
+      .def("begin_recv_batch", &SP::begin_recv_batch, py::arg("n"), py::arg("stream"))
       .def("end_send_batch", &SP::end_send_batch, py::arg("slots"), py::arg("stream"))
       .def("end_recv_batch", &SP::end_recv_batch, py::arg("slots"), py::arg("headers"), py::arg("stream"))
       .def_property_readonly("event_records", &SP::event_records);

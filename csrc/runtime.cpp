@@ -364,6 +364,57 @@ void SlotPool::commit_batch(const std::vector<int>& slots, const std::vector<Slo
   if (auto_route_) route_pending_locked();
 }
 
+void SlotPool::begin_send_batch(const std::vector<int>& slots, uint64_t stream) {
+  std::vector<EvRef> waits;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int s : slots) {
+      check_slot(s);
+      check(state_[s] == kProduced, state_msg("begin_send_batch", kProduced, state_[s]));
+    }
+    for (int s : slots) {
+      erase_value(produced_fifo_, s);
+      state_[s] = kSending;
+      const EvRef r = ready_ref_[s];
+      if (!ref_live_locked(r)) continue;
+      bool dup = false;
+      for (const auto& w : waits) dup |= (w.idx == r.idx && w.gen == r.gen);
+      if (!dup) waits.push_back(r);
+    }
+  }
+  if (device_ >= 0 && !waits.empty()) {
+    set_device();
+    for (const auto& w : waits) wait_ref(w, stream);
+  }
+}
+
+std::vector<int> SlotPool::begin_recv_batch(int n, uint64_t stream) {
+  std::vector<int> out;
+  std::vector<EvRef> waits;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    check(consumer_held_ + n <= cb_, "SlotPool.begin_recv_batch: not enough consumer credit");
+    check((int)free_list_.size() >= n, "SlotPool.begin_recv_batch: not enough free slots");
+    for (int i = 0; i < n; ++i) {
+      const int s = free_list_.front();
+      free_list_.pop_front();
+      state_[s] = kReceiving;
+      ++consumer_held_;
+      out.push_back(s);
+      const EvRef r = free_ref_[s];
+      if (!ref_live_locked(r)) continue;
+      bool dup = false;
+      for (const auto& w : waits) dup |= (w.idx == r.idx && w.gen == r.gen);
+      if (!dup) waits.push_back(r);
+    }
+  }
+  if (device_ >= 0 && !waits.empty()) {
+    set_device();
+    for (const auto& w : waits) wait_ref(w, stream);
+  }
+  return out;
+}
+
 void SlotPool::end_send_batch(const std::vector<int>& slots, uint64_t stream) {
   if (slots.empty()) return;
   std::lock_guard<std::mutex> lk(mu_);

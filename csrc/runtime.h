@@ -123,6 +123,8 @@ class SlotPool {
   std::vector<SlotHeader> headers(const std::vector<int>& slots) const;
   std::vector<int> acquire_batch(int n, double timeout_s, uint64_t stream);  // all n or none
   void commit_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream);
+  void begin_send_batch(const std::vector<int>& slots, uint64_t stream);   // + stream waits for their data
+  std::vector<int> begin_recv_batch(int n, uint64_t stream);              // + stream waits for free slots
   void end_send_batch(const std::vector<int>& slots, uint64_t stream);
   void end_recv_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream);
   int64_t event_records() const { return ev_records_; }

@@ -31,12 +31,12 @@ import numpy as np
 import torch
 
 from ..ops import _ext
-from ..parallel.routing import plan_round
 from .ring import FrameRing
 
 log = logging.getLogger(__name__)
 
 F_PRODUCER, F_CONSUMER, F_EOS, F_CLOSED, F_FAILED = 1, 2, 4, 8, 16
+_POLICY_CODE = {"balanced": 0, "local_first": 1, "spread": 2}
 HDR = 4          # fixed words per control vector
 PER_OFFER = 4    # rank, idx, gevt, photon-energy bits
 
@@ -258,39 +258,44 @@ class QueueEndpoint:
                 self._eos_from.add(r)
         consumers_alive = [r for r in range(self.world) if (flags[r] & F_CONSUMER) and not (flags[r] & F_CLOSED)]
         self._consumers_gone = len(consumers_alive) == 0
-        plan = plan_round(offer_n, credits, self._round, self.route)
+        flat = C.plan_round(offer_n, credits, self._round, _POLICY_CODE[self.route])
         me = self.rank
-        sends, recvs, recv_meta, send_slots = [], [], [], []
         sh = comm.stream_handle
-        for k, (p, i, c) in enumerate(plan):
-            if p == me and c == me:
-                self.pool.route_local(offers[i])
-            elif p == me:
-                s = offers[i]
-                self.pool.begin_send(s)
-                self.pool.wait_ready_on(s, sh)
-                sends.append((self._views[s], c, k))
-                send_slots.append(s)
+        local, send_slots, send_dst, recv_src, recv_hdr = [], [], [], [], []
+        n_plan = len(flat) // 3
+        for k in range(n_plan):
+            p, i, c = flat[3 * k], flat[3 * k + 1], flat[3 * k + 2]
+            if p == me:
+                if c == me:
+                    local.append(offers[i])
+                else:
+                    send_slots.append(offers[i])
+                    send_dst.append((c, k))
             elif c == me:
-                s = self.pool.begin_recv()
-                self.pool.wait_free_on(s, sh)
-                recvs.append((self._views[s], p, k))
                 b = HDR + PER_OFFER * i
                 row = allv[p]
-                recv_meta.append((s, C.SlotHeader(int(row[b]), int(row[b + 1]), int(row[b + 2]),
-                                                  float("nan") if _pe_from_bits(row[b + 3]) is None
-                                                  else _pe_from_bits(row[b + 3]))))
+                pe = _pe_from_bits(row[b + 3])
+                recv_src.append((p, k))
+                recv_hdr.append(C.SlotHeader(int(row[b]), int(row[b + 1]), int(row[b + 2]),
+                                             float("nan") if pe is None else pe))
+        for s in local:
+            self.pool.route_local(s)
+        self.pool.begin_send_batch(send_slots, sh)          # comm stream waits for the frames' data
+        recv_slots = self.pool.begin_recv_batch(len(recv_src), sh) if recv_src else []
+        views = self._views
+        sends = [(views[s], c, k) for s, (c, k) in zip(send_slots, send_dst)]
+        recvs = [(views[s], p, k) for s, (p, k) in zip(recv_slots, recv_src)]
         comm.exchange(sends, recvs)
         # one HIP event per direction per round (not one per frame)
         self.pool.end_send_batch(send_slots, sh)
-        self.pool.end_recv_batch([s for s, _ in recv_meta], [h for _, h in recv_meta], sh)
+        self.pool.end_recv_batch(recv_slots, recv_hdr, sh)
         self._round += 1
         self.rounds += 1
-        self.frames_routed += len(plan)
+        self.frames_routed += n_plan
         self.round_time_s += time.perf_counter() - t0
         if all(r in self._eos_from for r in self.producer_ranks):
             self._transport_done = True
-        return len(plan)
+        return n_plan
 
     def _loop(self):
         if self.gpu:

@@ -63,3 +63,17 @@ def test_spread_round_robins():
 def test_unknown_policy():
     with pytest.raises(ValueError):
         plan_round([1], [1], 0, "nope")
+
+
+@pytest.mark.parametrize("policy", POLICIES)
+def test_native_plan_matches_python_reference(native, policy):
+    code = {"balanced": 0, "local_first": 1, "spread": 2}[policy]
+    rng = random.Random(7)
+    for _ in range(400):
+        world = rng.randint(1, 8)
+        offers = [rng.randint(0, 64) for _ in range(world)]
+        credits = [rng.randint(0, 50) for _ in range(world)]
+        rid = rng.randint(0, 1000)
+        flat = native.plan_round(offers, credits, rid, code)
+        got = [tuple(flat[i:i + 3]) for i in range(0, len(flat), 3)]
+        assert got == plan_round(offers, credits, rid, policy)
