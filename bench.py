@@ -92,7 +92,8 @@ def main(argv=None):
                        pinned=(args.source == "host"), gen_device=str(device))
     cal = Calibrator(src.consts, device, mode, common_mode=cm)
     share = max(1, math.ceil(args.queue_size / world))
-    producer_slots = 2 * args.chunk + args.batch
+    # slack for frames waiting to be routed / in flight over xGMI (a round can hold max_offer frames)
+    producer_slots = 4 * args.chunk + args.batch + (64 if world > 1 else 0)
     ring = FrameRing(cal.out_shape, cal.out_dtype, device, producer_slots, share)
     ep = QueueEndpoint(ring, rank, world, comm, route=args.route, max_offer=64)
     if args.source == "device":
@@ -237,8 +238,18 @@ def main(argv=None):
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    sys.stdout.flush()
     if world > 1:
-        dist.destroy_process_group()
+        # never let a communicator teardown hang the run after the result line
+        clean = ep.failed is None and not pt.is_alive()
+        wd = threading.Timer(60.0, lambda: os._exit(0 if clean else 3))
+        wd.daemon = True
+        wd.start()
+        if clean:
+            dist.destroy_process_group()
+        wd.cancel()
+        if not clean:
+            os._exit(3)
     return 0
 
 
