@@ -44,6 +44,8 @@ def parse(argv=None):
     ap.add_argument("--chunk", type=int, default=16, help="frames per producer kernel launch / H2D copy")
     ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: protocol rehearsal with gloo and the golden models (tests only; not a benchmark)")
     return ap.parse_args(argv)
 
 
@@ -69,12 +71,17 @@ def main(argv=None):
             print(f"bench.py: --gpus {args.gpus} needs a launcher (torch.distributed.run) with one rank per GPU",
                   file=sys.stderr)
             return 2
-    if not torch.cuda.is_available():
-        print("bench.py needs a HIP device", file=sys.stderr)
-        return 2
-    device = torch.device(f"cuda:{li.local_rank % torch.cuda.device_count()}")
-    torch.cuda.set_device(device)
-    numa = bind_numa_to_device(device)
+    if args.device == "cpu":
+        device = torch.device("cpu")
+        numa = None
+    else:
+        if not torch.cuda.is_available():
+            print("bench.py needs a HIP device", file=sys.stderr)
+            return 2
+        device = torch.device(f"cuda:{li.local_rank % torch.cuda.device_count()}")
+        torch.cuda.set_device(device)
+        numa = bind_numa_to_device(device)
+    gpu = device.type == "cuda"
 
     comm = None
     coord = None
@@ -89,7 +96,7 @@ def main(argv=None):
     mode = Mode(args.mode)
     cm = CommonModeParams.parse(args.common_mode) if mode != Mode.raw else None
     src = SyntheticRun("synthetic", 0, args.detector, rank=rank, size=world, pool_frames=args.pool_frames,
-                       pinned=(args.source == "host"), gen_device=str(device))
+                       pinned=(args.source == "host" and gpu), gen_device=str(device))
     cal = Calibrator(src.consts, device, mode, common_mode=cm)
     share = max(1, math.ceil(args.queue_size / world))
     # slack for frames waiting to be routed / in flight over xGMI (a round can hold max_offer frames)
@@ -151,7 +158,8 @@ def main(argv=None):
         return got
 
     def sync():
-        torch.cuda.synchronize(device)
+        if gpu:
+            torch.cuda.synchronize(device)
 
     B = args.batch
     consume(args.warmup * B)
@@ -203,7 +211,8 @@ def main(argv=None):
         "vs_baseline": None,
         "dtype": "float32" if mode != Mode.raw else "uint16",
         "data": "synthetic (random-init calibration constants, pre-generated raw epix10k2M pool cycled "
-                + ("from pinned host memory via hipMemcpyAsync)" if args.source == "host" else "from HBM)"),
+                + ("from pinned host memory via hipMemcpyAsync)" if args.source == "host" and gpu
+                   else "from HBM)" if gpu else "on the CPU; gloo protocol rehearsal, not a benchmark)"),
         "config": {
             "model": args.detector,
             "global_batch": world * B,
