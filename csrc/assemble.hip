@@ -30,13 +30,13 @@ __global__ __launch_bounds__(256) void assemble_kernel(const FramePtrs fp, const
       if (o0 + i < nout && omask[o0 + i] == 0) src[i] = -1;
   }
   for (int f = 0; f < nframes; ++f) {
-    const float* in = reinterpret_cast<const float*>(fp.in[f]);
+    const PR_GLOBAL float* in = gin<float>(fp.in[f]);
     float o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = src[i] >= 0 ? in[src[i]] : 0.0f;
-    float* out = reinterpret_cast<float*>(fp.out[f]);
+    PR_GLOBAL float* out = gout<float>(fp.out[f]);
     if (full) {
-      *reinterpret_cast<float4*>(out + o0) = make_float4(o[0], o[1], o[2], o[3]);
+      st_f4((PR_GLOBAL float4*)(out + o0), make_float4(o[0], o[1], o[2], o[3]));
     } else {
       for (int i = 0; i < 4 && o0 + i < nout; ++i) out[o0 + i] = o[i];
     }

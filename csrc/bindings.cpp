@@ -64,6 +64,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("asic_rows"), py::arg("asic_cols"), py::arg("thr"), py::arg("maxcorr"), py::arg("npix_min"),
         py::arg("flags"), py::arg("bank_cols"), py::arg("stream"));
   m.def("cm_lds_bytes", &pr::cm_lds_bytes);
+  m.def("convert_u16_f32",
+        [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, int64_t npix, uint64_t stream) {
+          pr::launch_convert_u16_f32(make_ptrs(in, out), (int)in.size(), npix, stream);
+        },
+        "bandwidth reference: u16 -> f32 streaming copy (same traffic as calib_basic)");
   m.def("xor_lane_selftest", &pr::launch_xor_selftest, py::arg("out"), py::arg("stream"));
   m.def("assemble",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t idx, int64_t nout,

@@ -17,6 +17,9 @@
 //    ring slots (no packing copy).
 #include "common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace pr {
 
 template <int KIND>
@@ -70,44 +73,140 @@ __device__ __forceinline__ void load_tab8(const float* __restrict__ tab, int64_t
 }
 
 // raw frames: u16 [npix] each (fp.in[f]); outputs: f32 [npix] each (fp.out[f]).
+//
+// Frames are processed in groups of 4 with the NEXT group's raw loads issued before the current
+// group's stores (register double buffer): on CDNA4 `vmcnt` counts stores too, so without this
+// every group's load wait also drained the previous group's stores (store + load latency in
+// series).  blockIdx.y splits the frame batch into groups of FPB frames for more waves in flight
+// (the constants are then re-read once per group, from L2 / Infinity Cache).
 template <int KIND>
 __global__ __launch_bounds__(256) void calib_basic_kernel(const FramePtrs fp, const int nframes,
                                                           const float* __restrict__ ped,
                                                           const float* __restrict__ gf,
-                                                          const int64_t npix) {
+                                                          const int64_t npix, const int fpb) {
   constexpr int NT = KindTraits<KIND>::NT;
   const int64_t nvec = npix >> 3;
   const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (v >= nvec) return;
+  const int f_begin = blockIdx.y * fpb;
+  const int f_end = min(nframes, f_begin + fpb);
   const int64_t pix0 = v * 8;
   float p[NT][8], g[NT][8];
   load_tab8<NT>(ped, npix, pix0, p);
   load_tab8<NT>(gf, npix, pix0, g);
 
-  int f = 0;
-  // 4 frames in flight per thread: 4 independent 16-B loads before the first use.
-  for (; f + 4 <= nframes; f += 4) {
-    uint4 r[4];
+  uint4 cur[4], nxt[4];
+  int f = f_begin;
+  const int n0 = min(4, f_end - f);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      r[k] = ld_nt_u4(reinterpret_cast<const uint4*>(fp.in[f + k]) + v);
+  for (int k = 0; k < 4; ++k)
+    if (k < n0) cur[k] = ld_nt_u4(gin<uint4>(fp.in[f + k]) + v);
+  while (f < f_end) {
+    const int n = min(4, f_end - f);
+    const int fn = f + 4;
+    const int nn = min(4, f_end - fn);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)   // prefetch the next group before this group's stores
+      if (k < nn) nxt[k] = ld_nt_u4(gin<uint4>(fp.in[fn + k]) + v);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float4 o0, o1;
-      calib8<KIND, NT>(r[k], p, g, o0, o1);
-      float4* out = reinterpret_cast<float4*>(fp.out[f + k]) + 2 * v;
-      out[0] = o0;
-      out[1] = o1;
+      if (k < n) {
+        float4 o0, o1;
+        calib8<KIND, NT>(cur[k], p, g, o0, o1);
+        PR_GLOBAL float4* out = gout<float4>(fp.out[f + k]) + 2 * v;
+        st_f4(out, o0);
+        st_f4(out + 1, o1);
+      }
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    f = fn;
   }
-  for (; f < nframes; ++f) {
-    const uint4 r = ld_nt_u4(reinterpret_cast<const uint4*>(fp.in[f]) + v);
-    float4 o0, o1;
-    calib8<KIND, NT>(r, p, g, o0, o1);
-    float4* out = reinterpret_cast<float4*>(fp.out[f]) + 2 * v;
-    out[0] = o0;
-    out[1] = o1;
+}
+
+// 4-pixel-per-lane layout: 8-B raw loads and 16-B stores, consecutive lanes on consecutive
+// 16-B output chunks, so every store instruction writes 1 KB contiguous (whole 128-B lines).
+template <int NT>
+__device__ __forceinline__ void load_tab4(const float* __restrict__ tab, int64_t npix, int64_t pix0,
+                                          float (&t)[NT][4]) {
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    const float4 a = *reinterpret_cast<const float4*>(tab + k * npix + pix0);
+    t[k][0] = a.x; t[k][1] = a.y; t[k][2] = a.z; t[k][3] = a.w;
   }
+}
+
+template <int KIND, int NT>
+__device__ __forceinline__ float4 calib4(const uint2 r, const float (&p)[NT][4], const float (&g)[NT][4]) {
+  const uint32_t w[2] = {r.x, r.y};
+  float o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t raw = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+    bool valid;
+    const int c = decode_cand(raw, KIND, valid);
+    float pp, gg;
+    if constexpr (NT == 1) {
+      pp = p[0][i]; gg = g[0][i];
+    } else if constexpr (NT == 2) {
+      pp = bsel(c != 0, p[1][i], p[0][i]); gg = bsel(c != 0, g[1][i], g[0][i]);
+    } else {
+      pp = bsel(c == 0, p[0][i], bsel(c == 1, p[1][i], p[2][i]));
+      gg = bsel(c == 0, g[0][i], bsel(c == 1, g[1][i], g[2][i]));
+    }
+    const float v = (decode_adu(raw, KIND) - pp) * gg;
+    o[i] = valid ? v : 0.0f;
+  }
+  return make_float4(o[0], o[1], o[2], o[3]);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void calib_basic4_kernel(const FramePtrs fp, const int nframes,
+                                                           const float* __restrict__ ped,
+                                                           const float* __restrict__ gf,
+                                                           const int64_t npix, const int fpb) {
+  constexpr int NT = KindTraits<KIND>::NT;
+  const int64_t nq = npix >> 2;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const int f_begin = blockIdx.y * fpb;
+  const int f_end = min(nframes, f_begin + fpb);
+  const int64_t pix0 = q * 4;
+  float p[NT][4], g[NT][4];
+  load_tab4<NT>(ped, npix, pix0, p);
+  load_tab4<NT>(gf, npix, pix0, g);
+  int f = f_begin;
+  for (; f + 8 <= f_end; f += 8) {
+    uint2 r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      r[k] = ld_nt_u2(gin<uint2>(fp.in[f + k]) + q);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st_f4(gout<float4>(fp.out[f + k]) + q, calib4<KIND, NT>(r[k], p, g));
+  }
+  for (; f < f_end; ++f) {
+    st_f4(gout<float4>(fp.out[f]) + q, calib4<KIND, NT>(ld_nt_u2(gin<uint2>(fp.in[f]) + q), p, g));
+  }
+}
+
+// Bandwidth reference for the same traffic mix (u16 in, f32 out, no calibration math).
+__global__ __launch_bounds__(256) void convert_u16_f32_kernel(const FramePtrs fp, const int nframes,
+                                                              const int64_t npix) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (npix >> 2)) return;
+  for (int f = blockIdx.y * 8; f < min(nframes, (int)blockIdx.y * 8 + 8); ++f) {
+    const uint2 x = ld_nt_u2(gin<uint2>(fp.in[f]) + q);
+    st_f4(gout<float4>(fp.out[f]) + q,
+          make_float4((float)(x.x & 0xFFFF), (float)(x.x >> 16), (float)(x.y & 0xFFFF), (float)(x.y >> 16)));
+  }
+}
+
+void launch_convert_u16_f32(const FramePtrs& fp, int nframes, int64_t npix, uint64_t stream) {
+  const dim3 grid((unsigned)((npix / 4 + 255) / 256), (unsigned)((nframes + 7) / 8));
+  hipLaunchKernelGGL(convert_u16_f32_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), fp, nframes,
+                     npix);
+  hip_check(hipGetLastError(), "convert launch");
 }
 
 // Fused raw -> assembled image (image mode without common mode).  One thread owns 4
@@ -142,7 +241,7 @@ __global__ __launch_bounds__(256) void calib_image_kernel(const FramePtrs fp, co
     }
   }
   for (int f = 0; f < nframes; ++f) {
-    const uint16_t* raw = reinterpret_cast<const uint16_t*>(fp.in[f]);
+    const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[f]);
     float o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -164,9 +263,9 @@ __global__ __launch_bounds__(256) void calib_image_kernel(const FramePtrs fp, co
       }
       o[i] = val;
     }
-    float* out = reinterpret_cast<float*>(fp.out[f]);
+    PR_GLOBAL float* out = gout<float>(fp.out[f]);
     if (full) {
-      *reinterpret_cast<float4*>(out + o0) = make_float4(o[0], o[1], o[2], o[3]);
+      st_f4((PR_GLOBAL float4*)(out + o0), make_float4(o[0], o[1], o[2], o[3]));
     } else {
       for (int i = 0; i < 4 && o0 + i < nout; ++i) out[o0 + i] = o[i];
     }
@@ -184,14 +283,31 @@ void launch_calib_basic(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t
   for (int f = 0; f < nframes; ++f)
     check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_basic: frame buffers must be 16-B aligned");
   const int64_t nvec = npix / 8;
-  const dim3 grid((unsigned)((nvec + 255) / 256));
+  const char* lay = getenv("PSANA_RAY_CALIB_LAYOUT");
+  const bool layout8 = lay && lay[0] == '8';
+  // frames per block-group: the 4-px layout streams a whole batch per block (tables loaded once;
+  // 2.42 vs 2.72 us/frame at 8, profiles/kernels_r1.jsonl). PSANA_RAY_CALIB_FPB overrides (A/B).
+  int fpb = layout8 ? 8 : kMaxFrames;
+  if (const char* e = getenv("PSANA_RAY_CALIB_FPB")) fpb = std::max(1, atoi(e));
+  const dim3 grid((unsigned)((nvec + 255) / 256), (unsigned)((nframes + fpb - 1) / fpb));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float* P = reinterpret_cast<const float*>(ped);
   const float* G = reinterpret_cast<const float*>(gf);
+  if (!layout8) {   // default: 4-pixel-per-lane layout
+    const dim3 g4((unsigned)((npix / 4 + 255) / 256), (unsigned)((nframes + fpb - 1) / fpb));
+    switch (kind) {
+      case kEpix10ka: hipLaunchKernelGGL(calib_basic4_kernel<kEpix10ka>, g4, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
+      case kJungfrau: hipLaunchKernelGGL(calib_basic4_kernel<kJungfrau>, g4, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
+      case kPlain: hipLaunchKernelGGL(calib_basic4_kernel<kPlain>, g4, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
+      default: check(false, "calib_basic: unknown gain kind");
+    }
+    hip_check(hipGetLastError(), "calib_basic launch");
+    return;
+  }
   switch (kind) {
-    case kEpix10ka: hipLaunchKernelGGL(calib_basic_kernel<kEpix10ka>, grid, dim3(256), 0, s, fp, nframes, P, G, npix); break;
-    case kJungfrau: hipLaunchKernelGGL(calib_basic_kernel<kJungfrau>, grid, dim3(256), 0, s, fp, nframes, P, G, npix); break;
-    case kPlain: hipLaunchKernelGGL(calib_basic_kernel<kPlain>, grid, dim3(256), 0, s, fp, nframes, P, G, npix); break;
+    case kEpix10ka: hipLaunchKernelGGL(calib_basic_kernel<kEpix10ka>, grid, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
+    case kJungfrau: hipLaunchKernelGGL(calib_basic_kernel<kJungfrau>, grid, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
+    case kPlain: hipLaunchKernelGGL(calib_basic_kernel<kPlain>, grid, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
     default: check(false, "calib_basic: unknown gain kind");
   }
   hip_check(hipGetLastError(), "calib_basic launch");

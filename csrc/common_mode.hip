@@ -183,8 +183,8 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
   const int ac = (asic % per_panel) % tg.asics_per_row;
   const int64_t base = (int64_t)panel * tg.panel_rows * tg.panel_cols +
                        (int64_t)ar * R * tg.panel_cols + (int64_t)ac * C;
-  const uint16_t* raw = reinterpret_cast<const uint16_t*>(fp.in[f]);
-  float* out = reinterpret_cast<float*>(fp.out[f]);
+  const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[f]);
+  PR_GLOBAL float* out = gout<float>(fp.out[f]);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
   for (int i = tid; i < R * C8; i += blockDim.x) {
     const int r = i / C8, c = (i % C8) * 8;
     const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
-    const uint4 rw = ld_nt_u4(raw + pix);
+    const uint4 rw = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
     const uint2 fl = *reinterpret_cast<const uint2*>(pflags + pix);
     const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
     const uint32_t fw[2] = {fl.x, fl.y};
@@ -320,9 +320,9 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
       else gg = bsel(cand == 0, ga[0][j], bsel(cand == 1, ga[1][j], ga[2][j]));
       o[j] = (q & 4u) ? trow[j] * gg : 0.0f;
     }
-    float4* op = reinterpret_cast<float4*>(out + pix);
-    op[0] = make_float4(o[0], o[1], o[2], o[3]);
-    op[1] = make_float4(o[4], o[5], o[6], o[7]);
+    PR_GLOBAL float4* op = (PR_GLOBAL float4*)(out + pix);
+    st_f4(op, make_float4(o[0], o[1], o[2], o[3]));
+    st_f4(op + 1, make_float4(o[4], o[5], o[6], o[7]));
   }
 }
 
@@ -372,8 +372,8 @@ __global__ __launch_bounds__(512) void calib_cm_net_kernel(const FramePtrs fp, c
   const int ac = (asic % per_panel) % tg.asics_per_row;
   const int64_t base = (int64_t)panel * tg.panel_rows * tg.panel_cols + (int64_t)ar * R * tg.panel_cols +
                        (int64_t)ac * C;
-  const uint16_t* raw = reinterpret_cast<const uint16_t*>(fp.in[f]);
-  float* out = reinterpret_cast<float*>(fp.out[f]);
+  const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[f]);
+  PR_GLOBAL float* out = gout<float>(fp.out[f]);
   const int tid = threadIdx.x;
   const float INF = __int_as_float(0x7f800000);
 
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(512) void calib_cm_net_kernel(const FramePtrs fp, c
   for (int i = tid; i < R * C8; i += blockDim.x) {
     const int r = i / C8, c = (i % C8) * 8;
     const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
-    const uint4 rw = ld_nt_u4(raw + pix);
+    const uint4 rw = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
     const uint2 fl = *reinterpret_cast<const uint2*>(pflags + pix);
     const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
     const uint32_t fw[2] = {fl.x, fl.y};
@@ -554,9 +554,9 @@ __global__ __launch_bounds__(512) void calib_cm_net_kernel(const FramePtrs fp, c
       else gg = bsel(cand == 0, ga[0][j], bsel(cand == 1, ga[1][j], ga[2][j]));
       o[j] = (q & 4u) ? trow[j] * gg : 0.0f;
     }
-    float4* op = reinterpret_cast<float4*>(out + pix);
-    op[0] = make_float4(o[0], o[1], o[2], o[3]);
-    op[1] = make_float4(o[4], o[5], o[6], o[7]);
+    PR_GLOBAL float4* op = (PR_GLOBAL float4*)(out + pix);
+    st_f4(op, make_float4(o[0], o[1], o[2], o[3]));
+    st_f4(op + 1, make_float4(o[4], o[5], o[6], o[7]));
   }
 }
 

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void peakfind_kernel(const FramePtrs fp, const
   const int panel = blockIdx.x / (tiles_x * tiles_y);
   const int trem = blockIdx.x % (tiles_x * tiles_y);
   const int ty0 = (trem / tiles_x) * kPfTY, tx0 = (trem % tiles_x) * kPfTX;
-  const float* img = reinterpret_cast<const float*>(fp.in[f]) + (int64_t)panel * pp.rows * pp.cols;
+  const PR_GLOBAL float* img = gin<float>(fp.in[f]) + (int64_t)panel * pp.rows * pp.cols;
   const float NaN = __int_as_float(0x7fc00000);
 
   for (int i = threadIdx.x; i < LH * LW; i += 256) {

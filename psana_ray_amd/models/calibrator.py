@@ -77,6 +77,7 @@ class Calibrator:
                 if lds > 160 * 1024:
                     raise ValueError(f"common mode: ASIC tile {spec.asic_rows}x{spec.asic_cols} needs {lds} B of LDS")
             self.plan = self._make_plan(C)
+        self._out_frame_bytes = self.out_frame_bytes
 
     # ------------------------------------------------------------------------------------
     @property
@@ -102,12 +103,15 @@ class Calibrator:
         if not self._gpu:
             self._run_reference(raw, out)
             return
+        # cheap per-tensor checks (this runs per batch on the host; keep it well under a kernel's time)
+        npix, ofb, odt = self.spec.npix, self._out_frame_bytes, self.out_dtype
+        di = self.device.index if self.device.index is not None else torch.cuda.current_device()
         for r in raw:
-            if r.dtype != torch.uint16 or r.numel() != self.spec.npix or not r.is_contiguous() or r.device != self.device:
+            if r.dtype is not torch.uint16 or r.numel() != npix or not r.is_contiguous() or r.get_device() != di:
                 raise ValueError("Calibrator.run: raw frames must be contiguous uint16 frames on the calibrator device")
         for o in out:
-            if o.dtype != self.out_dtype or o.numel() * o.element_size() != self.out_frame_bytes or \
-                    not o.is_contiguous() or o.device != self.device or o.data_ptr() % 16:
+            if o.dtype is not odt or o.numel() * o.element_size() != ofb or not o.is_contiguous() or \
+                    o.get_device() != di or o.data_ptr() % 16:
                 raise ValueError("Calibrator.run: outputs must be contiguous, 16-B aligned frames of out_shape")
         self.run_ptrs([int(r.data_ptr()) for r in raw], [int(o.data_ptr()) for o in out], stream)
 
