@@ -44,6 +44,10 @@ def parse(argv=None):
     ap.add_argument("--chunk", type=int, default=16, help="frames per producer kernel launch / H2D copy")
     ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--hbm-fraction", type=float, default=0.8, help="cap of free HBM used for queue slots")
+    ap.add_argument("--loopback", action="store_true",
+                    help="N=1 only: route frames through the multi-GPU transport (gloo control round + RCCL "
+                         "send/recv to self) instead of the zero-copy local route; exercises the N>1 data path")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: protocol rehearsal with gloo and the golden models (tests only; not a benchmark)")
     return ap.parse_args(argv)
@@ -61,6 +65,7 @@ def main(argv=None):
     from psana_ray_amd.parallel.launch import bind_numa_to_device, detect
     from psana_ray_amd.pipeline import PeakFinderConsumer, ProducerPipeline
     from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
+    from psana_ray_amd.queue.ring import physical_slots
     from psana_ray_amd.source import SyntheticRun
 
     sys.setswitchinterval(5e-4)   # short GIL hand-off: transport / consumer threads stay responsive
@@ -88,6 +93,12 @@ def main(argv=None):
     if world > 1:
         comm = init_groups(rank, world, device)
         coord = dist.new_group(backend="gloo")
+    elif args.loopback:
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        comm = init_groups(0, 1, device, master_addr="127.0.0.1", master_port=port)
 
     def barrier():
         if coord is not None:
@@ -100,9 +111,12 @@ def main(argv=None):
     cal = Calibrator(src.consts, device, mode, common_mode=cm)
     share = max(1, math.ceil(args.queue_size / world))
     # slack for frames waiting to be routed / in flight over xGMI (a round can hold max_offer frames)
-    producer_slots = 4 * args.chunk + args.batch + (64 if world > 1 else 0)
-    ring = FrameRing(cal.out_shape, cal.out_dtype, device, producer_slots, share)
-    ep = QueueEndpoint(ring, rank, world, comm, route=args.route, max_offer=64)
+    producer_slots = 4 * args.chunk + args.batch + (64 if comm is not None else 0)
+    # queue_size is the LOGICAL capacity (deque(maxlen), shared_queue.py:7); physical HBM slots are
+    # capped by free memory (config 4: Jungfrau-16M x 400000 would need 26.8 TB)
+    cslots = physical_slots(share, cal.out_frame_bytes, device, args.hbm_fraction, producer_slots)
+    ring = FrameRing(cal.out_shape, cal.out_dtype, device, producer_slots, cslots)
+    ep = QueueEndpoint(ring, rank, world, comm, route=args.route, max_offer=64, loopback=args.loopback)
     if args.source == "device":
         # raw pool resident in HBM: isolates the GPU pipeline from PCIe (secondary number)
         dev_pool = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(device)
@@ -226,10 +240,13 @@ def main(argv=None):
             "queue_size": args.queue_size,
             "source": args.source,
             "chunk": args.chunk,
+            "loopback": args.loopback,
         },
         "extra": {
             "producer_frames_per_s_rank0": round((p1 - p0) / max(dt, 1e-9), 1),
             "frame_bytes": ring.frame_bytes,
+            "queue_slots_physical_rank0": cslots,
+            "ring_GB_rank0": round(ring.storage.numel() * ring.storage.element_size() / 1e9, 1),
             "GB_per_s_out": round(value * ring.frame_bytes / 1e9, 2),
             "peaks_found_rank0": peaks,
             "queue_full_waits_rank0": prod.full_waits,
@@ -248,7 +265,7 @@ def main(argv=None):
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     sys.stdout.flush()
-    if world > 1:
+    if comm is not None:
         # never let a communicator teardown hang the run after the result line
         clean = ep.failed is None and not pt.is_alive()
         wd = threading.Timer(60.0, lambda: os._exit(0 if clean else 3))

@@ -141,13 +141,19 @@ def main(argv=None):
         report("assemble", timeit(lambda: kernels.assemble(ol, il, cali.idx, npix), a.iters),
                F * (npix * 4 + nout * 4))
     if want("peakfind"):
+        import os
         cal.run(rl, ol)
         p = PeakFinderParams()
         peaks = torch.empty((F, p.max_peaks, 8), dtype=torch.float32, device=dev)
         counts = torch.zeros(F, dtype=torch.int32, device=dev)
         summ = torch.zeros((F, 2), dtype=torch.float32, device=dev)
-        report("peakfind", timeit(lambda: kernels.peakfind(ol, spec.frame_shape, p, peaks, counts, summ), a.iters),
-               F * npix * 4, {"peaks_per_frame": float(counts.float().mean())})
+        for rnd in range(2):   # interleaved A/B in one process
+            for ver in ("v1", "v2"):
+                os.environ["PSANA_RAY_PF_V1"] = "1" if ver == "v1" else "0"
+                report(f"peakfind({ver}) r{rnd}",
+                       timeit(lambda: kernels.peakfind(ol, spec.frame_shape, p, peaks, counts, summ), a.iters),
+                       F * npix * 4, {"peaks_per_frame": float(counts.float().mean())})
+        os.environ.pop("PSANA_RAY_PF_V1", None)
     if want("h2d"):
         C = _ext.load()
         hp = src.pool

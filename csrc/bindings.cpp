@@ -1,6 +1,8 @@
 // pybind11 bindings of psana_ray_amd._C.  Device buffers and streams cross the boundary as
 // integers (tensor.data_ptr(), torch.cuda.current_stream().cuda_stream), so this module does
 // not depend on the torch C++ ABI; the Python layer validates shapes/dtypes/devices first.
+#include <algorithm>
+
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -11,6 +13,7 @@ namespace py = pybind11;
 
 #include "engine.h"
 #include "kernels.h"
+#include "trace.h"
 
 namespace pr {
 std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers, const std::vector<int64_t>& credits,
@@ -64,6 +67,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("asic_rows"), py::arg("asic_cols"), py::arg("thr"), py::arg("maxcorr"), py::arg("npix_min"),
         py::arg("flags"), py::arg("bank_cols"), py::arg("stream"));
   m.def("cm_lds_bytes", &pr::cm_lds_bytes);
+  m.def("cm_tile_cols", &pr::cm_tile_cols);
+  m.def("roctx_enabled", &pr::trace::enabled);
+  m.def("roctx_push", [](const std::string& n) { pr::trace::push(n.c_str()); });
+  m.def("roctx_pop", &pr::trace::pop);
+  m.def("roctx_mark", [](const std::string& n) { pr::trace::mark(n.c_str()); });
   m.def("convert_u16_f32",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, int64_t npix, uint64_t stream) {
           pr::launch_convert_u16_f32(make_ptrs(in, out), (int)in.size(), npix, stream);
@@ -79,14 +87,41 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream"));
   m.def("peakfind",
         [](const std::vector<uint64_t>& in, int n_panels, int rows, int cols, float thr_peak, float son_min,
-           int radius, int max_peaks, uint64_t peaks, uint64_t counts, uint64_t summary, uint64_t stream) {
-          std::vector<uint64_t> dummy(in.size(), 1);
-          pr::launch_peakfind(make_ptrs(in, dummy), (int)in.size(), n_panels, rows, cols, thr_peak, son_min,
-                              radius, max_peaks, peaks, counts, summary, stream);
+           int radius, int max_peaks, uint64_t peaks, uint64_t counts, uint64_t summary, uint64_t stream,
+           uint64_t total) {
+          pr::launch_peakfind(make_ptrs(in, in), (int)in.size(), n_panels, rows, cols, thr_peak, son_min,
+                              radius, max_peaks, peaks, counts, summary, total, stream);
         },
         py::arg("in_ptrs"), py::arg("n_panels"), py::arg("rows"), py::arg("cols"), py::arg("thr_peak"),
         py::arg("son_min"), py::arg("radius"), py::arg("max_peaks"), py::arg("peaks"), py::arg("counts"),
-        py::arg("summary"), py::arg("stream"));
+        py::arg("summary"), py::arg("stream"), py::arg("total") = 0);
+  // consumer hot path: ring slots -> zeroed per-batch outputs -> peak finder, one native call
+  m.def("peakfind_slots",
+        [](uint64_t base, int64_t slot_bytes, const std::vector<int>& slots, int n_panels, int rows, int cols,
+           float thr_peak, float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
+           uint64_t summary, uint64_t total, uint64_t stream) {
+          const int n = (int)slots.size();
+          pr::check(n >= 1, "peakfind_slots: no slots");
+          pr::check(base != 0 && slot_bytes >= (int64_t)n_panels * rows * cols * 4, "peakfind_slots: bad ring");
+          hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+          pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(counts), 0, (size_t)n * 4, s), "zero counts");
+          pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(summary), 0, (size_t)n * 8, s), "zero summary");
+          for (int a = 0; a < n; a += pr::kMaxFrames) {
+            const int m = std::min(pr::kMaxFrames, n - a);
+            std::vector<uint64_t> in(m);
+            for (int i = 0; i < m; ++i) {
+              pr::check(slots[a + i] >= 0, "peakfind_slots: negative slot");
+              in[i] = base + (uint64_t)slots[a + i] * (uint64_t)slot_bytes;
+            }
+            pr::launch_peakfind(make_ptrs(in, in), m, n_panels, rows, cols, thr_peak, son_min, radius, max_peaks,
+                                peaks + (uint64_t)a * max_peaks * 32, counts + (uint64_t)a * 4,
+                                summary + (uint64_t)a * 8, total, stream);
+          }
+        },
+        py::arg("base"), py::arg("slot_bytes"), py::arg("slots"), py::arg("n_panels"), py::arg("rows"),
+        py::arg("cols"), py::arg("thr_peak"), py::arg("son_min"), py::arg("radius"), py::arg("max_peaks"),
+        py::arg("peaks"), py::arg("counts"), py::arg("summary"), py::arg("total"), py::arg("stream"),
+        py::call_guard<py::gil_scoped_release>());
 
   m.def("plan_round", &pr::plan_round_native, py::arg("offers"), py::arg("credits"), py::arg("round_id"),
         py::arg("policy"), "flattened (producer, offer_index, consumer) triples");
@@ -211,7 +246,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("pool"), py::arg("ring_base"), py::arg("slot_bytes"), py::arg("device"), py::arg("plan"),
            py::arg("chunk"), py::arg("n_raw_bufs"), py::arg("rank"), py::arg("size"), py::keep_alive<1, 2>())
       .def("set_cycled_source", &pr::ProducerEngine::set_cycled_source, py::arg("frames"), py::arg("photon_energy"))
-      .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"))
+      .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"), py::arg("k0") = 0)
       .def("request_stop", &pr::ProducerEngine::request_stop)
       .def("join", &pr::ProducerEngine::join, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &pr::ProducerEngine::running)

@@ -571,6 +571,18 @@ size_t cm_lds_bytes(int asic_rows, int asic_cols) {
   return tile + (size_t)asic_rows * (asic_cols / 8) * 4;
 }
 
+// Width of the LDS tile a workgroup owns.  Row medians are per bank segment and column medians
+// need whole columns, so an ASIC may be cut into full-height stripes whose width is a multiple
+// of the bank width without changing any median (Jungfrau: 256x256 ASIC = 289 KB > 160 KiB ->
+// two 256x128 stripes of 145 KB).  0 = no stripe fits.
+int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols) {
+  for (int w = asic_cols; w >= bank_cols; --w) {
+    if (asic_cols % w || w % bank_cols || w % 8) continue;
+    if (cm_lds_bytes(asic_rows, w) <= 160 * 1024) return w;
+  }
+  return 0;
+}
+
 void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t pflags,
                      int kind, int n_panels, int panel_rows, int panel_cols, int asic_rows,
                      int asic_cols, float thr, float maxcorr, int npix_min, int flags,
@@ -582,8 +594,9 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   check(bank_cols >= 1 && bank_cols <= 64 && asic_cols % bank_cols == 0,
         "calib_cm: bank_cols must be <= 64 and divide the ASIC width");
   check(panel_cols % 8 == 0, "calib_cm: panel cols must be a multiple of 8");
+  asic_cols = cm_tile_cols(asic_rows, asic_cols, bank_cols);
+  check(asic_cols > 0, "calib_cm: no full-height ASIC stripe fits in 160 KiB of LDS");
   const size_t lds = cm_lds_bytes(asic_rows, asic_cols);
-  check(lds <= 160 * 1024, "calib_cm: ASIC tile does not fit in 160 KiB of LDS");
   check(aligned16(ped) && aligned16(gf) && (pflags & 7) == 0, "calib_cm: misaligned constant tables");
   for (int f = 0; f < nframes; ++f)
     check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_cm: frame buffers must be 16-B aligned");

@@ -1,4 +1,5 @@
 #include "engine.h"
+#include "trace.h"
 
 #include <chrono>
 #include <stdexcept>
@@ -103,12 +104,13 @@ void ProducerEngine::set_cycled_source(const std::vector<uint64_t>& frames, cons
   src_pe_ = pe;
 }
 
-void ProducerEngine::start(int64_t n_local_events, int64_t max_steps) {
+void ProducerEngine::start(int64_t n_local_events, int64_t max_steps, int64_t k0) {
   check(!src_frames_.empty(), "ProducerEngine: no source");
+  check(k0 >= 0, "ProducerEngine: negative start event");
   check(!running_.load() && !thread_.joinable(), "ProducerEngine: already started");
   stop_.store(false);
   running_.store(true);
-  thread_ = std::thread([this, n_local_events, max_steps] { loop(n_local_events, max_steps); });
+  thread_ = std::thread([this, n_local_events, max_steps, k0] { loop(n_local_events, max_steps, k0); });
 }
 
 bool ProducerEngine::join(double timeout_s) {
@@ -132,14 +134,15 @@ std::string ProducerEngine::error() const {
   return error_;
 }
 
-void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps) {
+void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0) {
   using clk = std::chrono::steady_clock;
   auto secs = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
   const auto t_begin = clk::now();
   try {
     hip_check(hipSetDevice(device_), "hipSetDevice");
+    // absolute rank-local event bound: [k0, limit)
     int64_t limit = n_local_events;
-    if (max_steps >= 0 && (limit < 0 || max_steps < limit)) limit = max_steps;
+    if (max_steps >= 0 && (limit < 0 || k0 + max_steps < limit)) limit = k0 + max_steps;
     const uint64_t stream_c = reinterpret_cast<uint64_t>(compute_);
     std::vector<char> used(n_raw_bufs_, 0);
     std::vector<uint64_t> in, out;
@@ -169,23 +172,28 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps) {
       if (limit >= 0) n = (int)std::max<int64_t>(0, std::min<int64_t>(n, limit - k0));
       return n;
     };
-    int64_t k = 0;       // first event of the current chunk
+    int64_t k = k0;      // first event of the current chunk
     int64_t chunk_no = 0;
-    int n = chunk_len(0);
+    int n = chunk_len(k0);
     if (n > 0) {
       const auto t0 = clk::now();
-      stage(0, n, 0);
+      stage(k0, n, 0);
       t_stage_ += secs(t0, clk::now());
     }
     while (n > 0 && !stop_.load()) {
       const int b = (int)(chunk_no % n_raw_bufs_);
       const int64_t k_next = k + n;
       const int n_next = chunk_len(k_next);
+      trace::Range chunk_range("producer.chunk");
       auto t0 = clk::now();
-      if (n_next > 0) stage(k_next, n_next, (int)((chunk_no + 1) % n_raw_bufs_));
+      if (n_next > 0) {
+        trace::Range r("producer.stage_h2d");
+        stage(k_next, n_next, (int)((chunk_no + 1) % n_raw_bufs_));
+      }
       auto t1 = clk::now();
       t_stage_ += secs(t0, t1);
       slots.clear();
+      trace::push("producer.acquire");
       while (slots.empty() && !stop_.load()) {   // all n slots at once, one event wait per batch
         slots = pool_->acquire_batch(n, 0.05, stream_c);
         if (slots.empty()) {
@@ -193,6 +201,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps) {
           full_waits_.fetch_add(1);
         }
       }
+      trace::pop();
       auto t2 = clk::now();
       t_acquire_ += secs(t1, t2);
       if ((int)slots.size() < n) break;   // stopped while waiting
@@ -204,7 +213,10 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps) {
         in[q] = reinterpret_cast<uint64_t>(buf) + (uint64_t)q * plan_.raw_frame_bytes;
         out[q] = ring_base_ + (uint64_t)slots[q] * (uint64_t)slot_bytes_;
       }
-      run_calib_plan(plan_, in, out, stream_c);
+      {
+        trace::Range r("producer.launch_calib");
+        run_calib_plan(plan_, in, out, stream_c);
+      }
       hip_check(hipEventRecord(buf_free_[b], compute_), "record buf free");
       auto t3 = clk::now();
       t_launch_ += secs(t2, t3);

@@ -61,7 +61,8 @@ class ProducerEngine {
 
   // cycled source: frame k of this rank reads host_frames[k % n] (pinned host or device memory)
   void set_cycled_source(const std::vector<uint64_t>& frames, const std::vector<double>& photon_energy);
-  void start(int64_t n_local_events, int64_t max_steps);  // n_local_events < 0: endless
+  // rank-local events [k0, n_local_events) (n_local_events < 0: endless), at most max_steps of them
+  void start(int64_t n_local_events, int64_t max_steps, int64_t k0 = 0);
   void request_stop() { stop_.store(true); }
   bool join(double timeout_s);   // true when the thread has exited
   bool running() const { return running_.load(); }
@@ -72,7 +73,7 @@ class ProducerEngine {
   std::vector<double> timing() const;
 
  private:
-  void loop(int64_t n_local_events, int64_t max_steps);
+  void loop(int64_t n_local_events, int64_t max_steps, int64_t k0);
 
   SlotPool* pool_;
   uint64_t ring_base_;

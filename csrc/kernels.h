@@ -15,11 +15,12 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
                      int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
                      float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream);
 size_t cm_lds_bytes(int asic_rows, int asic_cols);
+int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols);
 void launch_convert_u16_f32(const FramePtrs& fp, int nframes, int64_t npix, uint64_t stream);
 void launch_xor_selftest(uint64_t out, uint64_t stream);
 void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nout, uint64_t omask,
                      uint64_t stream);
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
                      float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
-                     uint64_t summary, uint64_t stream);
+                     uint64_t summary, uint64_t total, uint64_t stream);
 }  // namespace pr

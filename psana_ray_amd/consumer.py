@@ -37,6 +37,8 @@ def build_parser():
     ap.add_argument("--son_min", type=float, default=5.0)
     ap.add_argument("--out", type=str, default=None, help="write peaks (npz) when --task peakfind")
     ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--metrics_interval", type=float, default=10.0, help="seconds between rate lines; 0 disables")
+    ap.add_argument("--metrics_json", type=str, default=None, help="append per-interval metrics as JSON lines")
     ap.add_argument("--log_level", type=str, default=DEFAULT_LOG_LEVEL, choices=LOG_LEVELS)
     return ap
 
@@ -61,9 +63,18 @@ def main(argv=None) -> int:
     n = 0
     peaks_total = 0
     records = []
+    from .utils.metrics import Registry, Reporter
+
+    registry = Registry()
+    registry.register("consumer", lambda: {"frames_consumed": n, "peaks": peaks_total})
+    reporter = None
     with DataReader(args.ray_address, args.queue_name, args.ray_namespace, consumer_id=args.consumer_id,
                     device=args.device, timeout_s=args.timeout) as reader:
         cid = reader.consumer_id
+        if reader.endpoint is not None:
+            registry.register("queue", reader.endpoint.metrics)
+        reporter = Reporter(registry, rank=cid if cid is not None else 0, interval=args.metrics_interval,
+                            json_path=args.metrics_json).start()
         pf = None
         if args.task == "peakfind":
             from .ops import kernels
@@ -117,6 +128,8 @@ def main(argv=None) -> int:
                 print(f"DataReader error: {e}")
                 print("Queue actor is dead. Exiting...")
                 return 1
+    if reporter is not None:
+        reporter.stop(final_sample=args.metrics_interval > 0 or args.metrics_json is not None)
     dt = time.time() - t0
     log.info("Consumer %s: %d frames in %.2f s (%.1f frames/s), %d peaks", cid, n, dt, n / max(dt, 1e-9), peaks_total)
     if args.out and records:

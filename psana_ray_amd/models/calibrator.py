@@ -73,9 +73,9 @@ class Calibrator:
                 self.omask = None if image_mask is None else \
                     torch.from_numpy(np.asarray(image_mask).astype(np.uint8).ravel()).to(self.device)
             if self.cm is not None:
-                lds = C.cm_lds_bytes(spec.asic_rows, spec.asic_cols)
-                if lds > 160 * 1024:
-                    raise ValueError(f"common mode: ASIC tile {spec.asic_rows}x{spec.asic_cols} needs {lds} B of LDS")
+                if C.cm_tile_cols(spec.asic_rows, spec.asic_cols, int(self.cm.bank_cols)) == 0:
+                    raise ValueError(f"common mode: no full-height stripe of the {spec.asic_rows}x{spec.asic_cols} "
+                                     f"ASIC (bank {self.cm.bank_cols}) fits in 160 KiB of LDS")
             self.plan = self._make_plan(C)
         self._out_frame_bytes = self.out_frame_bytes
 

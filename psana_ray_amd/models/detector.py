@@ -96,6 +96,7 @@ EPIX10K2M = register(
 EPIX10KA = register(DetectorSpec("epix10ka", "epix10ka", 1, 352, 384, 176, 192, 48, 100.0), "epix10ka_1panel")
 JUNGFRAU16M = register(DetectorSpec("jungfrau16M", "jungfrau", 32, 512, 1024, 256, 256, 64, 75.0), "jungfrau16m")
 JUNGFRAU4M = register(DetectorSpec("jungfrau4M", "jungfrau", 8, 512, 1024, 256, 256, 64, 75.0), "jungfrau4m")
+JUNGFRAU05M = register(DetectorSpec("jungfrau05M", "jungfrau", 1, 512, 1024, 256, 256, 64, 75.0), "jungfrau05m")
 # BASELINE config 1: synthetic 256x256 float-like frames without gain switching
 PLAIN256 = register(DetectorSpec("plain256", "plain", 1, 256, 256, 128, 128, 32, 100.0), "synthetic256")
 # small detectors for CPU tests (same kernels, same code paths)

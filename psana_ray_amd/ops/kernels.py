@@ -88,9 +88,9 @@ def calib_cm(raw, out, ped, gf, pflags, kind, spec, cm, stream=None):
     if pflags.dtype != torch.uint8 or pflags.numel() != npix:
         raise ValueError("calib_cm: pflags must be uint8[npix]")
     bank = cm.bank_cols or spec.bank_cols
-    lds = C.cm_lds_bytes(spec.asic_rows, spec.asic_cols)
-    if lds > 160 * 1024:
-        raise ValueError(f"common mode: ASIC tile {spec.asic_rows}x{spec.asic_cols} needs {lds} B of LDS (>160 KiB)")
+    if C.cm_tile_cols(spec.asic_rows, spec.asic_cols, int(bank)) == 0:
+        raise ValueError(f"common mode: no full-height stripe of the {spec.asic_rows}x{spec.asic_cols} ASIC "
+                         f"(bank {bank}) fits in 160 KiB of LDS")
     s = _ext.stream_handle(stream)
     for a, b in _chunks(len(raw)):
         C.calib_cm([_ptr(t) for t in raw[a:b]], [_ptr(t) for t in out[a:b]], _ptr(ped), _ptr(gf), _ptr(pflags), kind,
@@ -114,9 +114,10 @@ def assemble(frames, out, idx: torch.Tensor, npix: int, omask: Optional[torch.Te
 
 
 def peakfind(frames: Sequence[torch.Tensor], shape, params, peaks: torch.Tensor, counts: torch.Tensor,
-             summary: torch.Tensor, stream=None):
+             summary: torch.Tensor, stream=None, total: Optional[torch.Tensor] = None):
     """frames: F tensors of ``shape`` = (P, H, W) f32.  Outputs (zeroed here, on the stream):
-    peaks [F, max_peaks, 8] f32, counts [F] int32, summary [F, 2] f32."""
+    peaks [F, max_peaks, 8] f32, counts [F] int32, summary [F, 2] f32.  ``total`` (int64 scalar on
+    the device, optional) is incremented by the number of peak records written."""
     C = _ext.load()
     P, H, W = shape
     F = len(frames)
@@ -132,10 +133,13 @@ def peakfind(frames: Sequence[torch.Tensor], shape, params, peaks: torch.Tensor,
         raise ValueError("peakfind: summary must be float32 [F, 2]")
     if params.radius not in (1, 2):
         raise ValueError("peakfind: radius must be 1 or 2")
+    if total is not None and (total.dtype != torch.int64 or total.numel() != 1 or total.device != dev):
+        raise ValueError("peakfind: total must be an int64 scalar on the frames' device")
     s = _ext.stream_handle(stream)
     with torch.cuda.stream(stream) if stream is not None else torch.cuda.stream(torch.cuda.current_stream()):
         counts.zero_()
         summary.zero_()
     for a, b in _chunks(F):
         C.peakfind([_ptr(t) for t in frames[a:b]], P, H, W, float(params.thr_peak), float(params.son_min),
-                   int(params.radius), int(params.max_peaks), _ptr(peaks[a]), _ptr(counts[a:]), _ptr(summary[a]), s)
+                   int(params.radius), int(params.max_peaks), _ptr(peaks[a]), _ptr(counts[a:]), _ptr(summary[a]), s,
+                   0 if total is None else _ptr(total))

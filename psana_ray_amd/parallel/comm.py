@@ -46,6 +46,18 @@ class Comm:
         GPU: ops are enqueued on ``self.stream``; on return that stream is ordered after their
         completion (``work.wait()`` is a stream dependency for NCCL), so callers record events
         on ``self.stream``.  CPU/gloo: returns after completion."""
+        self.bytes_sent += sum(t.numel() * t.element_size() for t, _, _ in sends)
+        self.bytes_recv += sum(t.numel() * t.element_size() for t, _, _ in recvs)
+        if not self.gpu:
+            # gloo has no send-to-self: loopback pairs (matched in order, like RCCL) are copies
+            own_s = [t for t, peer, _ in sends if peer == self.rank]
+            own_r = [t for t, peer, _ in recvs if peer == self.rank]
+            if len(own_s) != len(own_r):
+                raise RuntimeError("loopback exchange: unmatched self send/recv")
+            for a, b in zip(own_s, own_r):
+                b.copy_(a)
+            sends = [x for x in sends if x[1] != self.rank]
+            recvs = [x for x in recvs if x[1] != self.rank]
         ops = [dist.P2POp(dist.isend, t, peer, group=self.data_group, tag=tag) for t, peer, tag in sends]
         ops += [dist.P2POp(dist.irecv, t, peer, group=self.data_group, tag=tag) for t, peer, tag in recvs]
         if not ops:
@@ -59,8 +71,6 @@ class Comm:
             works = dist.batch_isend_irecv(ops)
             for w in works:
                 w.wait()
-        self.bytes_sent += sum(t.numel() * t.element_size() for t, _, _ in sends)
-        self.bytes_recv += sum(t.numel() * t.element_size() for t, _, _ in recvs)
 
     @property
     def stream_handle(self) -> int:

@@ -28,6 +28,7 @@ from .config import PeakFinderParams
 from .models.calibrator import Calibrator
 from .ops import _ext, kernels
 from .queue.endpoint import EndOfStream, FrameItem, QueueEndpoint
+from .utils.tracing import trace_range
 
 log = logging.getLogger(__name__)
 
@@ -145,7 +146,8 @@ class ProducerPipeline:
         if not hasattr(self, "_it"):
             from .models.detector import Mode
 
-            self._it = enumerate(self.source.iter_events(self.cal.mode if self.cal else Mode.calib))
+            self._it = enumerate(self.source.iter_events(self.cal.mode if self.cal else Mode.calib),
+                                 start=int(getattr(self.source, "_skip", 0)))
         try:
             idx, (data, pe) = next(self._it)
         except StopIteration:
@@ -163,6 +165,15 @@ class ProducerPipeline:
     @property
     def produced(self) -> int:
         return int(self.engine.frames) if self.engine is not None else self.frames
+
+    def metrics(self) -> dict:
+        """Cumulative counters for utils.metrics (sampled, nothing runs per frame)."""
+        d = {"frames_produced": self.produced,
+             "full_waits": int(self.engine.full_waits) if self.engine is not None else self.full_waits}
+        if self.engine is not None:
+            st, acq, launch, commit, total = self.engine.timing()
+            d.update(host_stage_s=st, host_acquire_s=acq, host_launch_s=launch, host_commit_s=commit)
+        return d
 
     def run(self, max_steps: Optional[int] = None, stop=None) -> int:
         """Produce until the source ends, ``max_steps`` events (per rank, Q-6) or ``stop`` is set."""
@@ -185,7 +196,8 @@ class ProducerPipeline:
     def _run_engine(self, max_steps, stop) -> int:
         n_local = self.source.n_local_events() if hasattr(self.source, "n_local_events") else None
         self.t_first = time.perf_counter()
-        self.engine.start(-1 if n_local is None else int(n_local), -1 if max_steps is None else int(max_steps))
+        k0 = int(getattr(self.source, "cursor", 0))   # resume cursor (source.seek / --start_event)
+        self.engine.start(-1 if n_local is None else int(n_local), -1 if max_steps is None else int(max_steps), k0)
         try:
             while not self.engine.join(0.05):
                 if (stop is not None and stop.is_set()) or self.ep.failed is not None or self.ep._consumers_gone:
@@ -243,8 +255,7 @@ class PeakFinderConsumer:
             self._b += 1
             with torch.cuda.stream(self.stream):
                 kernels.peakfind([it.data for it in items], self.shape, self.params, self.peaks[b, :n],
-                                 self.counts[b, :n], self.summary[b, :n], self.stream)
-                self.count_acc += self.counts[b, :n].clamp(max=self.params.max_peaks).sum()
+                                 self.counts[b, :n], self.summary[b, :n], self.stream, total=self.count_acc)
                 if self.keep_results:
                     self.results.append((self.peaks[b, :n].clone(), self.counts[b, :n].clone(),
                                          [(it.rank, it.idx, it.gevt) for it in items]))
@@ -292,21 +303,24 @@ class PeakFinderConsumer:
         self._b += 1
         sh = int(self.stream.cuda_stream)
         P, H, W = self.shape
-        with torch.cuda.stream(self.stream):
-            self.counts[b, :n].zero_()
-            self.summary[b, :n].zero_()
-            C.peakfind([self.ep.slot_ptr(s) for s in slots], P, H, W, float(self.params.thr_peak),
-                       float(self.params.son_min), int(self.params.radius), int(self.params.max_peaks),
-                       int(self.peaks[b].data_ptr()), int(self.counts[b].data_ptr()), int(self.summary[b].data_ptr()),
-                       sh)
-            self.count_acc += self.counts[b, :n].clamp(max=self.params.max_peaks).sum()
+        with trace_range("consumer.peakfind_batch"):
+            # one native call: zero this batch's outputs, run the peak finder on the ring slots,
+            # bump the on-device running peak total (no per-batch torch ops, no host sync)
+            C.peakfind_slots(self.ep._base, self.ep._slot_bytes, slots, P, H, W, float(self.params.thr_peak),
+                             float(self.params.son_min), int(self.params.radius), int(self.params.max_peaks),
+                             int(self.peaks[b].data_ptr()), int(self.counts[b].data_ptr()),
+                             int(self.summary[b].data_ptr()), int(self.count_acc.data_ptr()), sh)
             if self.keep_results:
                 hs = self.ep.pool.headers(slots)
-                self.results.append((self.peaks[b, :n].clone(), self.counts[b, :n].clone(),
-                                     [(h.rank, h.idx, h.gevt) for h in hs]))
+                with torch.cuda.stream(self.stream):
+                    self.results.append((self.peaks[b, :n].clone(), self.counts[b, :n].clone(),
+                                         [(h.rank, h.idx, h.gevt) for h in hs]))
         self.ep.release_batch(slots, self.stream)
         self.frames += n
         return n
+
+    def metrics(self) -> dict:
+        return {"frames_consumed": self.frames}
 
     def synchronize(self):
         if self.gpu:

@@ -67,6 +67,12 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--producer_slots", type=int, default=64, help="calibrated frames a rank may hold un-routed")
     g.add_argument("--hbm_fraction", type=float, default=0.8, help="cap of free HBM used for ring slots")
     g.add_argument("--timeout", type=float, default=300.0, help="rendezvous / peer timeout in seconds")
+    g.add_argument("--start_event", type=int, default=0,
+                   help="resume: first global event id to produce (frames carry gevt, so consumers can dedupe)")
+    g.add_argument("--metrics_interval", type=float, default=10.0,
+                   help="seconds between metric summary lines (rates, queue depth); 0 disables")
+    g.add_argument("--metrics_json", type=str, default=None, help="append per-interval metrics as JSON lines")
+    g.add_argument("--metrics_port", type=int, default=None, help="Prometheus exporter port (if installed)")
     g.add_argument("--local", action="store_true",
                    help="single-process queue: no rendezvous; requires --consumer_task (no external consumers)")
     return parser
@@ -150,6 +156,7 @@ def main(argv=None) -> int:
     from .queue.endpoint import EndOfStream, QueueEndpoint
     from .queue.ring import FrameRing, physical_slots
     from .source import open_source
+    from .utils.metrics import Registry, Reporter
 
     li = detect()
     rank, size = li.rank, li.size
@@ -168,6 +175,12 @@ def main(argv=None) -> int:
     mode = Mode(args.mode) if args.mode else (Mode.calib if args.calib else Mode.image)   # producer.py:156-159
     source = open_source(args.exp, args.run, args.detector_name, rank=rank, size=size, n_events=args.num_events,
                          pinned=device.type == "cuda", data_dir=args.data_dir)
+    if args.start_event:
+        if not hasattr(source, "seek"):
+            log.error("--start_event: source %s cannot seek", type(source).__name__)
+            return 2
+        k0 = source.seek(args.start_event)
+        log.info("Rank %d: resuming at global event %d (local index %d)", rank, args.start_event, k0)
     mask = load_masks(source, args.uses_bad_pixel_mask, args.manual_mask_path)
     cm = CommonModeParams.parse(args.common_mode) if mode != Mode.raw else None
     calibrator = Calibrator(source.consts, device, mode, mask=mask, common_mode=cm) \
@@ -214,8 +227,12 @@ def main(argv=None) -> int:
                                 log_every=1 if logging.getLogger().isEnabledFor(logging.DEBUG) else 0)
         cons_thread = None
         stats = {}
+        registry = Registry()
+        registry.register("producer", pipe.metrics)
+        registry.register("queue", ep.metrics)
         if co_consumer:
             cons = PeakFinderConsumer(ep, frame_shape, PeakFinderParams())
+            registry.register("consumer", cons.metrics)
 
             def consume():
                 while True:
@@ -228,13 +245,18 @@ def main(argv=None) -> int:
 
             cons_thread = threading.Thread(target=consume, name="co-consumer", daemon=True)
             cons_thread.start()
-        n = produce_data(pipe, max_steps=args.max_steps, stop=stop)
-        log.info("Rank %d: produced %d frames", rank, n)
-        if cons_thread is not None:
-            cons_thread.join()
-            log.info("Rank %d: co-located consumer processed %d frames, %d peaks", rank, stats.get("consumed", 0),
-                     stats.get("peaks", 0))
-        ep.join(timeout=args.timeout)
+        reporter = Reporter(registry, rank=rank, interval=args.metrics_interval, json_path=args.metrics_json,
+                            prometheus_port=(args.metrics_port + rank) if args.metrics_port else None).start()
+        try:
+            n = produce_data(pipe, max_steps=args.max_steps, stop=stop)
+            log.info("Rank %d: produced %d frames", rank, n)
+            if cons_thread is not None:
+                cons_thread.join()
+                log.info("Rank %d: co-located consumer processed %d frames, %d peaks", rank,
+                         stats.get("consumed", 0), stats.get("peaks", 0))
+            ep.join(timeout=args.timeout)
+        finally:
+            reporter.stop(final_sample=args.metrics_interval > 0 or args.metrics_json is not None)
         return 0
     except Exception as e:
         log.error("Rank %d: Unhandled exception in main: %s", rank, e)   # producer.py:163-166

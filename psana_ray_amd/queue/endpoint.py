@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from ..ops import _ext
+from ..utils.tracing import trace_range
 from .ring import FrameRing
 
 log = logging.getLogger(__name__)
@@ -103,7 +104,8 @@ class FrameItem:
 class QueueEndpoint:
     def __init__(self, ring: FrameRing, rank: int = 0, world: int = 1, comm=None,
                  producer_ranks: Optional[Sequence[int]] = None, consumer_ranks: Optional[Sequence[int]] = None,
-                 route: str = "balanced", max_offer: int = 64, is_producer: bool = True, is_consumer: bool = True):
+                 route: str = "balanced", max_offer: int = 64, is_producer: bool = True, is_consumer: bool = True,
+                 loopback: bool = False):
         self.ring = ring
         self.pool = ring.pool
         self.rank, self.world, self.comm = rank, world, comm
@@ -112,6 +114,11 @@ class QueueEndpoint:
         self.consumer_ranks = list(range(world)) if consumer_ranks is None else list(consumer_ranks)
         self.route = route
         self.max_offer = max_offer
+        # loopback: frames routed to this rank itself still travel through the data exchange
+        # (RCCL send/recv to self).  Lets a single GPU run the full multi-GPU transport path.
+        self.loopback = bool(loopback)
+        if self.loopback and comm is None:
+            raise ValueError("loopback transport needs a Comm")
         self.gpu = ring.device.type == "cuda"
         self._lock = threading.Lock()
         self._producer_finished = not is_producer
@@ -249,7 +256,8 @@ class QueueEndpoint:
         C = _ext.load()
         comm = self.comm
         offers = self.pool.produced(self.max_offer) if self.is_producer else []
-        allv = comm.allgather_ctrl(self._control_vector(offers))
+        with trace_range("transport.ctrl_allgather"):
+            allv = comm.allgather_ctrl(self._control_vector(offers))
         flags = allv[:, 2]
         offer_n = [int(x) for x in allv[:, 0]]
         credits = [int(x) for x in allv[:, 1]]
@@ -265,13 +273,13 @@ class QueueEndpoint:
         n_plan = len(flat) // 3
         for k in range(n_plan):
             p, i, c = flat[3 * k], flat[3 * k + 1], flat[3 * k + 2]
+            if p == me and c == me and not self.loopback:
+                local.append(offers[i])
+                continue
             if p == me:
-                if c == me:
-                    local.append(offers[i])
-                else:
-                    send_slots.append(offers[i])
-                    send_dst.append((c, k))
-            elif c == me:
+                send_slots.append(offers[i])
+                send_dst.append((c, k))
+            if c == me:
                 b = HDR + PER_OFFER * i
                 row = allv[p]
                 pe = _pe_from_bits(row[b + 3])
@@ -285,7 +293,8 @@ class QueueEndpoint:
         views = self._views
         sends = [(views[s], c, k) for s, (c, k) in zip(send_slots, send_dst)]
         recvs = [(views[s], p, k) for s, (p, k) in zip(recv_slots, recv_src)]
-        comm.exchange(sends, recvs)
+        with trace_range("transport.exchange"):
+            comm.exchange(sends, recvs)
         # one HIP event per direction per round (not one per frame)
         self.pool.end_send_batch(send_slots, sh)
         self.pool.end_recv_batch(recv_slots, recv_hdr, sh)
@@ -331,6 +340,15 @@ class QueueEndpoint:
     @property
     def failed(self) -> Optional[BaseException]:
         return self._failed
+
+    def metrics(self) -> dict:
+        """Gauges + cumulative counters for utils.metrics."""
+        d = {"ready": self.pool.n_ready(), "credits": self.pool.credits(), "rounds": self.rounds,
+             "frames_routed": self.frames_routed if self.comm is not None else self.pool.stats().routed_local}
+        if self.comm is not None:
+            d.update(bytes_sent=self.comm.bytes_sent, bytes_recv=self.comm.bytes_recv,
+                     round_ms=1e3 * self.round_time_s / max(1, self.rounds))
+        return d
 
     def stats(self) -> dict:
         d = self.ring.stats()

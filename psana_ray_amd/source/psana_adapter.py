@@ -37,6 +37,13 @@ class PsanaWrapperSource:
     def create_bad_pixel_mask(self) -> np.ndarray:
         return self.wrapper.create_bad_pixel_mask()
 
+    def seek(self, start_event: int) -> int:
+        """Skip this rank's first ``start_event`` events (psana shards inside its SMD reader)."""
+        self._skip = max(0, int(start_event))
+        return self._skip
+
     def iter_events(self, mode: Mode) -> Iterator[Tuple[np.ndarray, Optional[float]]]:
+        import itertools
+
         m = self._mode_enum.calib if Mode(mode) == Mode.calib else self._mode_enum.image
-        return self.wrapper.iter_events(mode=m)
+        return itertools.islice(self.wrapper.iter_events(mode=m), getattr(self, "_skip", 0), None)

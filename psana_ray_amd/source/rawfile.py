@@ -96,6 +96,17 @@ class RawFileRun:
     def n_local_events(self) -> int:
         return max(0, (self.n_events - self.rank + self.size - 1) // self.size)
 
+    def seek(self, start_event: int) -> int:
+        """Resume at global event ``start_event`` (see synthetic.first_local_event)."""
+        from .synthetic import first_local_event
+
+        self._cursor = first_local_event(start_event, self.rank, self.size)
+        return self._cursor
+
+    @property
+    def cursor(self) -> int:
+        return self._cursor
+
     def next_events(self, n: int) -> List[RawEvent]:
         n = min(n, self.n_local_events() - self._cursor, self.n_staging)
         if n <= 0:

@@ -99,6 +99,12 @@ def generate_raw(consts: CalibConstants, n: int, seed: int, device="cpu", spots=
     return out.to(torch.int32).cpu().numpy().astype(np.uint16), (pe_ev.cpu().numpy()).astype(np.float64)
 
 
+def first_local_event(start_event: int, rank: int, size: int) -> int:
+    """First rank-local index k with global id ``rank + k * size >= start_event`` (round-robin
+    sharding, P-01)."""
+    return max(0, -(-(int(start_event) - rank) // size))
+
+
 class SyntheticRun:
     """psana_wrapper-like source for ``(exp, run, detector_name)`` (``--exp synthetic`` or no psana)."""
 
@@ -138,6 +144,16 @@ class SyntheticRun:
         if self.n_events is None:
             return None
         return max(0, (self.n_events - self.rank + self.size - 1) // self.size)
+
+    def seek(self, start_event: int) -> int:
+        """Resume at global event ``start_event``: this rank's next event is its first one with
+        ``gevt >= start_event``.  Returns that rank-local index."""
+        self._cursor = first_local_event(start_event, self.rank, self.size)
+        return self._cursor
+
+    @property
+    def cursor(self) -> int:
+        return self._cursor
 
     def cycled_frames(self):
         """(host pointers, photon energies) of the cycled pool for the native producer engine:
