@@ -70,9 +70,11 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 // Frame buffers arrive as integer addresses (kernarg FramePtrs).  A pointer made from an integer
-// is GENERIC to the compiler, which then emits FLAT loads/stores -- counted in both vmcnt and
-// lgkmcnt and forcing full drains (measured: 2.7x slower calibration).  Every frame access goes
-// through these address_space(1) (global) views instead.
+// is GENERIC to the compiler, which then emits FLAT loads/stores (tracked by both vmcnt and
+// lgkmcnt).  Every frame access goes through these address_space(1) (global) views so the ISA
+// uses global_load/store with scalar bases and LDS waits stay independent of HBM waits in the
+// LDS-heavy kernels.  (No speed-up of the streaming calib kernel is claimed: the only FLAT-vs-
+// global comparison was taken with host-bound timing and could not separate them.)
 #define PR_GLOBAL __attribute__((address_space(1)))
 template <typename T>
 __device__ __forceinline__ const PR_GLOBAL T* gin(uint64_t p) {
