@@ -272,7 +272,10 @@ def main(argv=None):
         wd.daemon = True
         wd.start()
         if clean:
+            comm.close()
             dist.destroy_process_group()
+        else:
+            comm.abort()
         wd.cancel()
         if not clean:
             os._exit(3)

@@ -14,6 +14,7 @@ namespace py = pybind11;
 #include "engine.h"
 #include "kernels.h"
 #include "trace.h"
+#include "transport.h"
 
 namespace pr {
 std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers, const std::vector<int64_t>& credits,
@@ -129,6 +130,33 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream"));
   m.def("memcpy_h2d_batch", &pr::memcpy_h2d_batch, py::arg("dst"), py::arg("src"), py::arg("bytes"),
         py::arg("stream"));
+
+  m.def("rccl_version", &pr::rccl_version);
+  m.def("rccl_unique_id", [] {
+    const auto v = pr::rccl_unique_id();
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+  });
+  py::class_<pr::RcclTransport>(m, "RcclTransport")
+      .def(py::init([](const py::bytes& id, int rank, int world, int device) {
+             const std::string s = id;
+             std::vector<uint8_t> v(s.begin(), s.end());
+             py::gil_scoped_release nogil;   // ncclCommInitRank blocks until every rank joined
+             return new pr::RcclTransport(v, rank, world, device);
+           }),
+           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
+      .def("exchange", &pr::RcclTransport::exchange, py::arg("send_ptrs"), py::arg("send_peers"),
+           py::arg("recv_ptrs"), py::arg("recv_peers"), py::arg("bytes"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("round", &pr::RcclTransport::round, py::arg("pool"), py::arg("ring_base"), py::arg("slot_bytes"),
+           py::arg("send_slots"), py::arg("send_peers"), py::arg("recv_peers"), py::arg("recv_headers"),
+           py::arg("stream"), py::call_guard<py::gil_scoped_release>())
+      .def("async_error", &pr::RcclTransport::async_error)
+      .def("abort", &pr::RcclTransport::abort, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &pr::RcclTransport::rank)
+      .def_property_readonly("world", &pr::RcclTransport::world)
+      .def_property_readonly("bytes_sent", &pr::RcclTransport::bytes_sent)
+      .def_property_readonly("bytes_recv", &pr::RcclTransport::bytes_recv)
+      .def_property_readonly("groups", &pr::RcclTransport::groups);
 
   py::class_<pr::PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())
       .def(py::init<size_t>(), py::arg("bytes"))

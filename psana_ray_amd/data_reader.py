@@ -186,6 +186,10 @@ class DataReader:
             # stay in the collective rounds until the producers' EOS so peers never see a
             # half-finished world; a reader closed early just stops taking frames
             ep.join(timeout=self.timeout_s)
+            if ep.comm is not None:
+                if ep.failed is not None:
+                    ep.comm.abort()
+                ep.comm.close()
             try:
                 import torch.distributed as dist
 

@@ -1,13 +1,15 @@
 """Communication backends of the sharded shared queue.
 
-Two process groups over the SAME ranks (one process per GPU):
-  * control group -- gloo on the CPU: one small all-gather per transport round carries every
-    rank's (offers, credits, flags, frame headers).  Keeping it off the GPU means a round's
+Two planes over the SAME ranks (one process per GPU):
+  * control -- a gloo process group on the CPU: one small all-gather per transport round carries
+    every rank's (offers, credits, flags, frame headers).  Keeping it off the GPU means a round's
     routing never waits behind the previous round's frame transfers.
-  * data group    -- ``nccl`` (= RCCL over xGMI on MI355X) for HBM frames, or gloo for host
-    frames (CPU tests / BASELINE config 1 over processes).  Frames move with grouped
-    ``isend``/``irecv`` (``batch_isend_irecv`` -> one ncclGroupStart/End per round) issued on a
-    dedicated HIP stream; completion is stream-ordered (no host sync).
+  * data    -- on GPUs a native RCCL communicator (csrc/transport.cpp; id broadcast over the
+    control group): a round's frames move as ONE ncclGroupStart/End of ncclSend/ncclRecv on a
+    dedicated HIP stream, slot bookkeeping and event ordering included, in a single native call
+    with the GIL released (the first version used torch ``batch_isend_irecv``: ~1 torch P2POp
+    per frame in Python capped a round at ~10k frames/s).  On the CPU (tests / BASELINE config 1
+    over processes) gloo ``isend``/``irecv`` of host tensors.
 
 This replaces the reference's data plane -- a synchronous Ray actor RPC per frame through the
 object store (psana_ray/producer.py:101, data_reader.py:35; C-01/C-03) -- and its MPI control
@@ -23,16 +25,46 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, rank: int, world: int, ctrl_group, data_group, device: torch.device):
+    def __init__(self, rank: int, world: int, ctrl_group, data_group, device: torch.device, rccl=None):
         self.rank = rank
         self.world = world
         self.ctrl_group = ctrl_group
         self.data_group = data_group
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
+        self.rccl = rccl
         self.stream = torch.cuda.Stream(device=self.device) if self.gpu else None
-        self.bytes_sent = 0
-        self.bytes_recv = 0
+        self._bytes_sent = 0
+        self._bytes_recv = 0
+
+    @property
+    def bytes_sent(self) -> int:
+        return int(self.rccl.bytes_sent) if self.rccl is not None else self._bytes_sent
+
+    @property
+    def bytes_recv(self) -> int:
+        return int(self.rccl.bytes_recv) if self.rccl is not None else self._bytes_recv
+
+    def round(self, pool, ring_base: int, slot_bytes: int, send_slots, send_peers, recv_peers, recv_headers):
+        """GPU: one fused native transport round (see csrc/transport.h).  Returns the recv slots."""
+        return self.rccl.round(pool, ring_base, slot_bytes, send_slots, send_peers, recv_peers, recv_headers,
+                               self.stream_handle)
+
+    def check_async(self) -> None:
+        if self.rccl is not None:
+            err = self.rccl.async_error()
+            if err:
+                raise RuntimeError(f"RCCL asynchronous error: {err}")
+
+    def abort(self) -> None:
+        """Drop the data communicator without waiting for peers (after a failure)."""
+        if self.rccl is not None:
+            self.rccl.abort()
+
+    def close(self) -> None:
+        if self.rccl is not None:
+            r, self.rccl = self.rccl, None
+            del r   # ncclCommDestroy (waits for this rank's outstanding work only)
 
     def allgather_ctrl(self, vec: np.ndarray) -> np.ndarray:
         t = torch.from_numpy(np.ascontiguousarray(vec, dtype=np.int64))
@@ -43,11 +75,20 @@ class Comm:
     def exchange(self, sends: Sequence[Tuple[torch.Tensor, int, int]], recvs: Sequence[Tuple[torch.Tensor, int, int]]):
         """Issue all (tensor, peer, tag) sends and receives of a round as one group.
 
-        GPU: ops are enqueued on ``self.stream``; on return that stream is ordered after their
-        completion (``work.wait()`` is a stream dependency for NCCL), so callers record events
-        on ``self.stream``.  CPU/gloo: returns after completion."""
-        self.bytes_sent += sum(t.numel() * t.element_size() for t, _, _ in sends)
-        self.bytes_recv += sum(t.numel() * t.element_size() for t, _, _ in recvs)
+        GPU (RCCL): enqueued on ``self.stream``; callers order their events after that stream.
+        All tensors of one call must have the same byte size.  CPU/gloo: returns after completion."""
+        if self.rccl is not None:
+            nb = {t.numel() * t.element_size() for t, _, _ in list(sends) + list(recvs)}
+            if not nb:
+                return
+            if len(nb) != 1:
+                raise ValueError("RCCL exchange: all messages of a round must have the same size")
+            self.rccl.exchange([int(t.data_ptr()) for t, _, _ in sends], [int(p) for _, p, _ in sends],
+                               [int(t.data_ptr()) for t, _, _ in recvs], [int(p) for _, p, _ in recvs],
+                               nb.pop(), self.stream_handle)
+            return
+        self._bytes_sent += sum(t.numel() * t.element_size() for t, _, _ in sends)
+        self._bytes_recv += sum(t.numel() * t.element_size() for t, _, _ in recvs)
         if not self.gpu:
             # gloo has no send-to-self: loopback pairs (matched in order, like RCCL) are copies
             own_s = [t for t, peer, _ in sends if peer == self.rank]
@@ -62,15 +103,9 @@ class Comm:
         ops += [dist.P2POp(dist.irecv, t, peer, group=self.data_group, tag=tag) for t, peer, tag in recvs]
         if not ops:
             return
-        if self.gpu:
-            with torch.cuda.stream(self.stream):
-                works = dist.batch_isend_irecv(ops)
-                for w in works:
-                    w.wait()
-        else:
-            works = dist.batch_isend_irecv(ops)
-            for w in works:
-                w.wait()
+        works = dist.batch_isend_irecv(ops)
+        for w in works:
+            w.wait()
 
     @property
     def stream_handle(self) -> int:
@@ -79,35 +114,32 @@ class Comm:
 
 def init_groups(rank: int, world: int, device, store=None, master_addr: Optional[str] = None,
                 master_port: Optional[int] = None, timeout_s: float = 600.0):
-    """Create (or reuse) the default process group and the control/data groups.
-
-    GPU device -> default group ``nccl`` (bound to the device: eager communicator init) plus a
-    gloo control group; CPU -> gloo for both.  Returns a :class:`Comm`.
-    """
+    """Create (or reuse) the default gloo process group (control plane) and, on a GPU, the native
+    RCCL communicator of the data plane.  Returns a :class:`Comm`."""
     import datetime
 
     device = torch.device(device)
     gpu = device.type == "cuda"
     tmo = datetime.timedelta(seconds=timeout_s)
+    if gpu:
+        torch.cuda.set_device(device)
     if not dist.is_initialized():
         kw = dict(rank=rank, world_size=world, timeout=tmo)
         if store is not None:
             kw["store"] = store
         elif master_addr is not None:
             kw["init_method"] = f"tcp://{master_addr}:{master_port}"
-        if gpu:
-            torch.cuda.set_device(device)
-            dist.init_process_group("nccl", device_id=device, **kw)
-        else:
-            dist.init_process_group("gloo", **kw)
+        dist.init_process_group("gloo", **kw)
+    ctrl = dist.new_group(backend="gloo", timeout=tmo)
+    rccl = None
     if gpu:
-        data = dist.group.WORLD
-        ctrl = dist.new_group(backend="gloo", timeout=tmo)
-        # first collective on the data group involves every rank (batch_isend_irecv requirement)
-        t = torch.ones(1, device=device)
-        dist.all_reduce(t, group=data)
-        torch.cuda.synchronize(device)
-    else:
-        data = dist.group.WORLD
-        ctrl = dist.new_group(backend="gloo", timeout=tmo)
-    return Comm(rank, world, ctrl, data, device)
+        from ..ops import _ext
+
+        C = _ext.load()
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            uid = torch.frombuffer(bytearray(C.rccl_unique_id()), dtype=torch.uint8).clone()
+        dist.broadcast(uid, src=0, group=ctrl)
+        dev_index = device.index if device.index is not None else torch.cuda.current_device()
+        rccl = C.RcclTransport(bytes(uid.numpy().tobytes()), rank, world, dev_index)
+    return Comm(rank, world, ctrl, dist.group.WORLD, device, rccl=rccl)

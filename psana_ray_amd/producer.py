@@ -268,6 +268,10 @@ def main(argv=None) -> int:
             hb.stop()
         if sess is not None:
             finish_session(sess)
+        if comm is not None:
+            if 'ep' in locals() and ep.failed is not None:
+                comm.abort()
+            comm.close()
         try:
             import torch.distributed as dist
 

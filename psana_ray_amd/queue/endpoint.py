@@ -288,16 +288,24 @@ class QueueEndpoint:
                                              float("nan") if pe is None else pe))
         for s in local:
             self.pool.route_local(s)
-        self.pool.begin_send_batch(send_slots, sh)          # comm stream waits for the frames' data
-        recv_slots = self.pool.begin_recv_batch(len(recv_src), sh) if recv_src else []
-        views = self._views
-        sends = [(views[s], c, k) for s, (c, k) in zip(send_slots, send_dst)]
-        recvs = [(views[s], p, k) for s, (p, k) in zip(recv_slots, recv_src)]
-        with trace_range("transport.exchange"):
-            comm.exchange(sends, recvs)
-        # one HIP event per direction per round (not one per frame)
-        self.pool.end_send_batch(send_slots, sh)
-        self.pool.end_recv_batch(recv_slots, recv_hdr, sh)
+        if getattr(comm, "rccl", None) is not None:
+            # GPU: one native call -- slot ordering, ncclGroupStart/Send/Recv/End, completion events
+            if send_slots or recv_src:
+                comm.round(self.pool, self._base, self._slot_bytes, send_slots, [c for c, _ in send_dst],
+                           [p for p, _ in recv_src], recv_hdr)
+            if self.rounds % 64 == 0:
+                comm.check_async()
+        else:
+            self.pool.begin_send_batch(send_slots, sh)          # data-ready ordering
+            recv_slots = self.pool.begin_recv_batch(len(recv_src), sh) if recv_src else []
+            views = self._views
+            sends = [(views[s], c, k) for s, (c, k) in zip(send_slots, send_dst)]
+            recvs = [(views[s], p, k) for s, (p, k) in zip(recv_slots, recv_src)]
+            with trace_range("transport.exchange"):
+                comm.exchange(sends, recvs)
+            # one event per direction per round (not one per frame)
+            self.pool.end_send_batch(send_slots, sh)
+            self.pool.end_recv_batch(recv_slots, recv_hdr, sh)
         self._round += 1
         self.rounds += 1
         self.frames_routed += n_plan
@@ -321,6 +329,10 @@ class QueueEndpoint:
         except BaseException as e:  # noqa: BLE001 - surfaced to both roles
             self._failed = e
             log.error("rank %d: shared-queue transport failed: %r", self.rank, e)
+            try:
+                self.comm.abort()   # RCCL: never leave kernels waiting on a dead peer
+            except Exception:  # noqa: BLE001
+                pass
         finally:
             self.pool.wake_all()
 

@@ -61,8 +61,9 @@ def main(device: str, n: int) -> int:
         return 1
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
-    print(f"LOOPBACK_OK {n} {comm.bytes_sent}")
+    print(f"LOOPBACK_OK {n} {comm.bytes_sent} native={comm.rccl is not None}")
     import torch.distributed as dist
+    comm.close()
     dist.destroy_process_group()
     return 0
 

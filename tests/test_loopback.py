@@ -39,7 +39,7 @@ def test_bench_loopback_cpu():
 def test_loopback_integrity_rccl(native):
     r = _run(["tests/_loopback_worker.py", "cuda:0", "300"], 300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "LOOPBACK_OK 300" in r.stdout
+    assert "LOOPBACK_OK 300" in r.stdout and "native=True" in r.stdout
 
 
 @pytest.mark.gpu
