@@ -44,6 +44,9 @@ def parse(argv=None):
     ap.add_argument("--chunk", type=int, default=16, help="frames per producer kernel launch / H2D copy")
     ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--producers", type=int, default=0,
+                    help="producer ranks P (ranks < P produce, every rank consumes; 0 = all).  BASELINE config 3: "
+                         "--gpus 8 --producers 4")
     ap.add_argument("--hbm-fraction", type=float, default=0.8, help="cap of free HBM used for queue slots")
     ap.add_argument("--loopback", action="store_true",
                     help="N=1 only: route frames through the multi-GPU transport (gloo control round + RCCL "
@@ -106,24 +109,33 @@ def main(argv=None):
 
     mode = Mode(args.mode)
     cm = CommonModeParams.parse(args.common_mode) if mode != Mode.raw else None
-    src = SyntheticRun("synthetic", 0, args.detector, rank=rank, size=world, pool_frames=args.pool_frames,
-                       pinned=(args.source == "host" and gpu), gen_device=str(device))
+    n_prod = args.producers or world
+    if not 1 <= n_prod <= world:
+        print(f"bench.py: --producers must be in [1, {world}]", file=sys.stderr)
+        return 2
+    is_prod = rank < n_prod
+    # producers shard the run round-robin among themselves (P-01); consumer-only ranks need the
+    # calibration constants (same seed) but no raw pool
+    src = SyntheticRun("synthetic", 0, args.detector, rank=rank if is_prod else 0, size=n_prod,
+                       pool_frames=args.pool_frames if is_prod else 1,
+                       pinned=(args.source == "host" and gpu and is_prod), gen_device=str(device))
     cal = Calibrator(src.consts, device, mode, common_mode=cm)
     share = max(1, math.ceil(args.queue_size / world))
     # slack for frames waiting to be routed / in flight over xGMI (a round can hold max_offer frames)
-    producer_slots = 4 * args.chunk + args.batch + (64 if comm is not None else 0)
+    producer_slots = (4 * args.chunk + args.batch + (64 if comm is not None else 0)) if is_prod else 1
     # queue_size is the LOGICAL capacity (deque(maxlen), shared_queue.py:7); physical HBM slots are
     # capped by free memory (config 4: Jungfrau-16M x 400000 would need 26.8 TB)
     cslots = physical_slots(share, cal.out_frame_bytes, device, args.hbm_fraction, producer_slots)
     ring = FrameRing(cal.out_shape, cal.out_dtype, device, producer_slots, cslots)
-    ep = QueueEndpoint(ring, rank, world, comm, route=args.route, max_offer=64, loopback=args.loopback)
+    ep = QueueEndpoint(ring, rank, world, comm, producer_ranks=list(range(n_prod)), route=args.route, max_offer=64,
+                       is_producer=is_prod, loopback=args.loopback)
     if args.source == "device":
         # raw pool resident in HBM: isolates the GPU pipeline from PCIe (secondary number)
         dev_pool = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(device)
 
         class _DevSrc:
             spec = src.spec
-            size = world
+            size = n_prod
             calibrated = False
 
             def __init__(self):
@@ -141,20 +153,21 @@ def main(argv=None):
                 out = []
                 for _ in range(n):
                     j = self.k % dev_pool.shape[0]
-                    out.append(RawEvent(rank + self.k * world, self.k, dev_pool[j], int(dev_pool[j].data_ptr()), 9.5))
+                    out.append(RawEvent(rank + self.k * n_prod, self.k, dev_pool[j], int(dev_pool[j].data_ptr()), 9.5))
                     self.k += 1
                 return out
 
         source = _DevSrc()
     else:
         source = src
-    prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk)
+    prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk) if is_prod else None
     consumer = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=args.batch) \
         if args.consumer == "peakfind" else None
 
     stop = threading.Event()
     ep.start()
-    pt = threading.Thread(target=prod.run, kwargs=dict(stop=stop), name="producer", daemon=True)
+    pt = threading.Thread(target=prod.run if prod is not None else ep.finish, kwargs=dict(stop=stop) if prod else {},
+                          name="producer", daemon=True)
     pt.start()
 
     def consume(n_frames):
@@ -181,11 +194,11 @@ def main(argv=None):
     barrier()
     sync()
     t0 = time.perf_counter()
-    p0 = prod.produced
+    p0 = prod.produced if prod is not None else 0
     consume(args.steps * B)
     sync()
     t1 = time.perf_counter()
-    p1 = prod.produced
+    p1 = prod.produced if prod is not None else 0
     barrier()
     dt = t1 - t0
     if coord is not None:
@@ -241,6 +254,7 @@ def main(argv=None):
             "source": args.source,
             "chunk": args.chunk,
             "loopback": args.loopback,
+            "producer_ranks": n_prod,
         },
         "extra": {
             "producer_frames_per_s_rank0": round((p1 - p0) / max(dt, 1e-9), 1),
@@ -249,13 +263,14 @@ def main(argv=None):
             "ring_GB_rank0": round(ring.storage.numel() * ring.storage.element_size() / 1e9, 1),
             "GB_per_s_out": round(value * ring.frame_bytes / 1e9, 2),
             "peaks_found_rank0": peaks,
-            "queue_full_waits_rank0": prod.full_waits,
+            "queue_full_waits_rank0": prod.full_waits if prod is not None else 0,
             "transport_rounds_rank0": st.get("rounds", 0),
             "transport_round_ms_rank0": round(st.get("round_ms", 0.0), 3),
             "bytes_sent_rank0": st.get("bytes_sent", 0),
             "numa_node": numa,
             "producer_host_s_stage_acquire_launch_commit_total": (
-                [round(x, 4) for x in prod.engine.timing()] if prod.engine is not None else None),
+                [round(x, 4) for x in prod.engine.timing()] if prod is not None and prod.engine is not None
+                else None),
         },
     }
     if rank == 0:

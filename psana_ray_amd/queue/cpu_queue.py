@@ -26,6 +26,7 @@ class Queue:
         self.items: deque = deque(maxlen=maxsize)
         self._lock = threading.Lock()
         self._not_empty = threading.Condition(self._lock)
+        self._not_full = threading.Condition(self._lock)
 
     @property
     def maxsize(self) -> int:
@@ -50,10 +51,20 @@ class Queue:
             with self._lock:
                 if not self.items and timeout:
                     self._not_empty.wait_for(lambda: bool(self.items), timeout=timeout)
-                return self.items.popleft() if self.items else None
+                if not self.items:
+                    return None
+                item = self.items.popleft()
+                self._not_full.notify()
+                return item
         except Exception as e:
             print(f"Error in get: {e}")
             return None
+
+    def wait_not_full(self, timeout: Optional[float] = None) -> bool:
+        """Block until a ``put`` could succeed (event-driven replacement of the producer's
+        exponential backoff, producer.py:105-111).  Returns False on timeout."""
+        with self._lock:
+            return self._not_full.wait_for(lambda: len(self.items) < self.items.maxlen, timeout=timeout)
 
     def size(self) -> int:
         try:

@@ -243,11 +243,15 @@ class QueueEndpoint:
             flags |= F_CLOSED
         credits = 0 if self._consumer_closed else self.pool.credits()
         v[0], v[1], v[2], v[3] = len(offers), credits, flags, self._round
-        for i, s in enumerate(offers):
-            h = self.pool.header(s)
-            b = HDR + PER_OFFER * i
-            v[b], v[b + 1], v[b + 2], v[b + 3] = h.rank, h.idx, h.gevt, _pe_bits(
-                None if math.isnan(h.photon_energy) else h.photon_energy)
+        if offers:
+            hs = self.pool.headers(list(offers))          # one native call for the whole offer list
+            n = len(hs)
+            w = v[HDR:HDR + PER_OFFER * n].reshape(n, PER_OFFER)
+            w[:, 0] = [h.rank for h in hs]
+            w[:, 1] = [h.idx for h in hs]
+            w[:, 2] = [h.gevt for h in hs]
+            # photon energy travels as the int64 bit pattern of the float64 (NaN = None)
+            w[:, 3] = np.array([h.photon_energy for h in hs], dtype=np.float64).view(np.int64)
         return v
 
     def step(self) -> int:

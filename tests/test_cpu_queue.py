@@ -69,3 +69,31 @@ def test_concurrent_producers_consumers_exactly_once():
     for t in ts:
         t.join(30)
     assert sorted(got) == sorted((r, i) for r in range(P) for i in range(N))
+
+
+def test_wait_not_full_wakes_on_get():
+    import threading
+
+    from psana_ray_amd.queue.cpu_queue import Queue
+
+    q = Queue(maxsize=1)
+    assert q.put(1) and not q.put(2)
+    assert q.wait_not_full(0.01) is False
+    t = threading.Timer(0.05, q.get)
+    t.start()
+    assert q.wait_not_full(5.0) is True
+    assert q.put(2)
+
+
+def test_config1_bench_runs():
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "bench/config1_cpu_queue.py", "--frames", "500", "--queue-size", "16"],
+                       cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["frames"] == 500 and d["frames_per_s"] > 0
