@@ -132,14 +132,40 @@ def main(argv=None):
         calc = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams(flags=2))
         report("calib_cm(cols)", timeit(lambda: calc.run(rl, ol), a.iters), F * npix * 6)
     if want("calib_image") and spec.kind != "plain":
-        cali = Calibrator(src.consts, dev, Mode.image)
+        import os
+        C = _ext.load()
+        cals = {}
+        for ver in ("v1", "tiles"):
+            os.environ["PSANA_RAY_IMAGE_V1"] = "1" if ver == "v1" else "0"
+            cals[ver] = Calibrator(src.consts, dev, Mode.image)
+        os.environ.pop("PSANA_RAY_IMAGE_V1", None)
+        cali = cals["tiles"]
+        tm = cali.tile_map
         img = torch.empty((F, *cali.out_shape), dtype=torch.float32, device=dev)
         il = [img[i] for i in range(F)]
         nout = int(np.prod(cali.out_shape))
-        report("calib_image(fused)", timeit(lambda: cali.run(rl, il), a.iters), F * (npix * 2 + nout * 4),
-               {"image_shape": list(cali.out_shape)})
-        report("assemble", timeit(lambda: kernels.assemble(ol, il, cali.idx, npix), a.iters),
-               F * (npix * 4 + nout * 4))
+        rp = [int(t.data_ptr()) for t in rl]
+        op = [int(t.data_ptr()) for t in ol]
+        ip = [int(t.data_ptr()) for t in il]
+        extra = {"image_shape": list(cali.out_shape), "tile_direct_frac": round(tm.direct_px / max(1, tm.staged_px
+                                                                                                    + tm.direct_px), 4)}
+        for rnd in range(2):
+            for ver in ("v1", "tiles"):
+                report(f"calib_image(fused,{ver}) r{rnd}", timeit(lambda: cals[ver].run(rl, il), a.iters),
+                       F * (npix * 2 + nout * 4), extra)
+            for grp in (1, 4, 8):
+                os.environ["PSANA_RAY_IMAGE_GROUPS"] = str(grp)
+                report(f"calib_image(fused,tiles,groups={grp}) r{rnd}", timeit(lambda: cali.run(rl, il), a.iters),
+                       F * (npix * 2 + nout * 4))
+            os.environ.pop("PSANA_RAY_IMAGE_GROUPS", None)
+            report(f"assemble(v1) r{rnd}", timeit(lambda: kernels.assemble(ol, il, cali.idx, npix), a.iters),
+                   F * (npix * 4 + nout * 4))
+            report(f"assemble(tiles) r{rnd}",
+                   timeit(lambda: C.image_tiles(op, ip, False, spec.kernel_kind, 0, 0, npix, spec.panel_rows,
+                                                spec.panel_cols, int(cali._tiles.data_ptr()), tm.n_tiles, tm.tiles_x,
+                                                int(cali._codes.data_ptr()), tm.image_shape[0], tm.image_shape[1],
+                                                _ext.stream_handle()), a.iters),
+                   F * (npix * 4 + nout * 4))
     if want("peakfind"):
         import os
         cal.run(rl, ol)

@@ -69,6 +69,17 @@ PYBIND11_MODULE(_C, m) {
         py::arg("flags"), py::arg("bank_cols"), py::arg("stream"));
   m.def("cm_lds_bytes", &pr::cm_lds_bytes);
   m.def("cm_tile_cols", &pr::cm_tile_cols);
+  m.def("image_tile_shape", [] { return py::make_tuple(pr::image_tile_h(), pr::image_tile_w(), pr::image_tile_stage()); });
+  m.def("image_tiles",
+        [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, bool calib, int kind, uint64_t ped,
+           uint64_t gf, int64_t npix, int panel_rows, int panel_cols, uint64_t tiles, int n_tiles, int tiles_x,
+           uint64_t codes, int img_h, int img_w, uint64_t stream) {
+          pr::launch_image_tiles(make_ptrs(in, out), (int)in.size(), calib, kind, ped, gf, npix, panel_rows,
+                                 panel_cols, tiles, n_tiles, tiles_x, codes, img_h, img_w, stream);
+        },
+        py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("calib"), py::arg("kind"), py::arg("ped"), py::arg("gf"),
+        py::arg("npix"), py::arg("panel_rows"), py::arg("panel_cols"), py::arg("tiles"), py::arg("n_tiles"),
+        py::arg("tiles_x"), py::arg("codes"), py::arg("img_h"), py::arg("img_w"), py::arg("stream"));
   m.def("roctx_enabled", &pr::trace::enabled);
   m.def("roctx_push", [](const std::string& n) { pr::trace::push(n.c_str()); });
   m.def("roctx_pop", &pr::trace::pop);
@@ -265,7 +276,14 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("omask", &pr::CalibPlan::omask)
       .def_readwrite("scratch", &pr::CalibPlan::scratch)
       .def_readwrite("raw_frame_bytes", &pr::CalibPlan::raw_frame_bytes)
-      .def_readwrite("out_frame_bytes", &pr::CalibPlan::out_frame_bytes);
+      .def_readwrite("out_frame_bytes", &pr::CalibPlan::out_frame_bytes)
+      .def_readwrite("use_tiles", &pr::CalibPlan::use_tiles)
+      .def_readwrite("tiles", &pr::CalibPlan::tiles)
+      .def_readwrite("codes", &pr::CalibPlan::codes)
+      .def_readwrite("n_tiles", &pr::CalibPlan::n_tiles)
+      .def_readwrite("tiles_x", &pr::CalibPlan::tiles_x)
+      .def_readwrite("img_h", &pr::CalibPlan::img_h)
+      .def_readwrite("img_w", &pr::CalibPlan::img_w);
   m.def("run_calib_plan", &pr::run_calib_plan, py::arg("plan"), py::arg("in_ptrs"), py::arg("out_ptrs"),
         py::arg("stream"));
 

@@ -41,7 +41,11 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
                         p.bank_cols, stream);
         break;
       case kPlanImageFused:
-        launch_calib_image(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.npix, p.kind, p.idx, p.nout, stream);
+        if (p.use_tiles)
+          launch_image_tiles(ptrs_of(in, out, a, b), n, true, p.kind, p.ped, p.gf, p.npix, p.panel_rows,
+                             p.panel_cols, p.tiles, p.n_tiles, p.tiles_x, p.codes, p.img_h, p.img_w, stream);
+        else
+          launch_calib_image(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.npix, p.kind, p.idx, p.nout, stream);
         break;
       case kPlanImageScratch: {
         check(p.scratch != 0, "run_calib_plan: image plan without scratch");
@@ -54,7 +58,11 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
                           p.bank_cols, stream);
         else
           launch_calib_basic(ptrs_of(ina, tmp, 0, n), n, p.ped, p.gf, p.npix, p.kind, stream);
-        launch_assemble(ptrs_of(tmp, outa, 0, n), n, p.idx, p.nout, p.omask, stream);
+        if (p.use_tiles)
+          launch_image_tiles(ptrs_of(tmp, outa, 0, n), n, false, p.kind, 0, 0, p.npix, p.panel_rows,
+                             p.panel_cols, p.tiles, p.n_tiles, p.tiles_x, p.codes, p.img_h, p.img_w, stream);
+        else
+          launch_assemble(ptrs_of(tmp, outa, 0, n), n, p.idx, p.nout, p.omask, stream);
         break;
       }
       default:

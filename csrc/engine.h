@@ -43,6 +43,10 @@ struct CalibPlan {
   int64_t nout = 0;
   uint64_t omask = 0;
   uint64_t scratch = 0;  // >= kMaxFrames * npix f32 (kPlanImageScratch)
+  // LDS-tiled assembly (csrc/image.hip); use_tiles = 0 falls back to the plain gather kernels
+  int use_tiles = 0;
+  uint64_t tiles = 0, codes = 0;
+  int n_tiles = 0, tiles_x = 0, img_h = 0, img_w = 0;
   int64_t raw_frame_bytes = 0;
   int64_t out_frame_bytes = 0;
 };

@@ -15,6 +15,12 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
                      int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
                      float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream);
 size_t cm_lds_bytes(int asic_rows, int asic_cols);
+void launch_image_tiles(const FramePtrs& fp, int nframes, bool calib, int kind, uint64_t ped, uint64_t gf,
+                        int64_t npix, int panel_rows, int panel_cols, uint64_t tiles, int n_tiles, int tiles_x,
+                        uint64_t codes, int img_h, int img_w, uint64_t stream);
+int image_tile_h();
+int image_tile_w();
+int image_tile_stage();
 int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols);
 void launch_convert_u16_f32(const FramePtrs& fp, int nframes, int64_t npix, uint64_t stream);
 void launch_xor_selftest(uint64_t out, uint64_t stream);

@@ -14,6 +14,7 @@ On a CUDA(HIP) device the HIP kernels are mandatory (no silent PyTorch fallback)
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -23,7 +24,7 @@ from ..config import CommonModeParams
 from ..ops import kernels, reference
 from .constants import CalibConstants
 from .detector import Mode
-from .geometry import Geometry, make_geometry
+from .geometry import Geometry, build_tile_map, make_geometry
 
 
 class Calibrator:
@@ -67,9 +68,17 @@ class Calibrator:
             self.pflags = torch.from_numpy(pflags).to(self.device)
             self.idx = None
             self.omask = None
+            self.tile_map = None
             if self.mode == Mode.image:
-                self.idx = torch.from_numpy(self.geometry.index_map()).to(self.device)
+                imap = self.geometry.index_map()
+                self.idx = torch.from_numpy(imap).to(self.device)
                 kernels._validate_index_map(self.idx, spec.npix, "Calibrator")
+                if os.environ.get("PSANA_RAY_IMAGE_V1") != "1":
+                    # LDS-tiled assembly (csrc/image.hip); the image mask folds into its codes
+                    tm = build_tile_map(imap, spec, self.geometry.image_shape, image_mask)
+                    self.tile_map = tm
+                    self._tiles = torch.from_numpy(tm.tiles).to(self.device)
+                    self._codes = torch.from_numpy(tm.codes).to(self.device)
                 self.omask = None if image_mask is None else \
                     torch.from_numpy(np.asarray(image_mask).astype(np.uint8).ravel()).to(self.device)
             if self.cm is not None:
@@ -141,7 +150,13 @@ class Calibrator:
             p.mode = 2 if self.cm is not None else 1
         else:
             p.idx, p.nout = int(self.idx.data_ptr()), int(self.idx.numel())
-            if self.cm is None and self.omask is None:
+            if self.tile_map is not None:
+                tm = self.tile_map
+                p.use_tiles = 1
+                p.tiles, p.codes = int(self._tiles.data_ptr()), int(self._codes.data_ptr())
+                p.n_tiles, p.tiles_x = tm.n_tiles, tm.tiles_x
+                p.img_h, p.img_w = tm.image_shape
+            if self.cm is None and (self.omask is None or self.tile_map is not None):
                 p.mode = 3
             else:
                 p.mode = 4

@@ -102,3 +102,74 @@ def make_geometry(spec: DetectorSpec) -> Geometry:
     assert np.unique(flat).size == spec.npix, "geometry maps two pixels onto one image pixel"
     assert rows.min() >= 0 and cols.min() >= 0 and rows.max() < shape[0] and cols.max() < shape[1]
     return geo
+
+
+# ------------------------------------------------------------------------------------------
+# Tiled assembly map for csrc/image.hip (LDS-staged gather)
+TILE_H, TILE_W, TILE_STAGE, TILE_LDS = 32, 64, 2048, 2176
+
+
+@dataclass
+class TileMap:
+    """Per-tile staging boxes + per-output-pixel codes (see csrc/image.hip).
+
+    tiles[t] = (panel, r0, c0, h, w, 0, 0, 0): source box staged for output tile t (panel -1:
+    nothing staged); codes[o] >= 0 is the LDS word of output pixel o (row pitch w+1), -1 a gap or
+    masked pixel, <= -2 the source pixel ``-(code+2)`` read directly."""
+
+    image_shape: tuple
+    tiles: np.ndarray      # int32 [n_tiles, 8]
+    codes: np.ndarray      # int32 [img_h * img_w]
+    tiles_x: int
+    staged_px: int
+    direct_px: int
+
+    @property
+    def n_tiles(self) -> int:
+        return int(self.tiles.shape[0])
+
+
+def build_tile_map(index_map: np.ndarray, spec: DetectorSpec, image_shape, image_mask=None,
+                   th: int = TILE_H, tw: int = TILE_W) -> TileMap:
+    """Cut the image into th x tw tiles; per tile, stage the bounding box of the dominant panel's
+    source pixels when it fits (<= TILE_STAGE pixels, padded rows <= TILE_LDS words)."""
+    P, H, W = spec.frame_shape
+    himg, wimg = (int(image_shape[0]), int(image_shape[1]))
+    idx = np.asarray(index_map, dtype=np.int64).reshape(himg, wimg).copy()
+    if image_mask is not None:
+        m = np.asarray(image_mask).reshape(himg, wimg)
+        idx[m == 0] = -1                       # masked pixels become gaps: output 0
+    nty, ntx = -(-himg // th), -(-wimg // tw)
+    tiles = np.zeros((nty * ntx, 8), dtype=np.int32)
+    codes = np.full((himg, wimg), -1, dtype=np.int64)
+    staged = direct = 0
+    ppix = H * W
+    for ty in range(nty):
+        for tx in range(ntx):
+            t = ty * ntx + tx
+            ys, xs = slice(ty * th, min(himg, (ty + 1) * th)), slice(tx * tw, min(wimg, (tx + 1) * tw))
+            sub = idx[ys, xs]
+            valid = sub >= 0
+            tiles[t, 0] = -1
+            if not valid.any():
+                continue
+            pan = np.where(valid, sub // ppix, -1)
+            dom = int(np.bincount(pan[valid]).argmax())
+            sel = pan == dom
+            rem = sub[sel] % ppix
+            r, c = rem // W, rem % W
+            r0, c0 = int(r.min()), int(c.min())
+            bh, bw = int(r.max()) - r0 + 1, int(c.max()) - c0 + 1
+            csub = codes[ys, xs]
+            if bh * bw <= TILE_STAGE and bh * (bw + 1) <= TILE_LDS:
+                tiles[t, :5] = (dom, r0, c0, bh, bw)
+                csub[sel] = (r - r0) * (bw + 1) + (c - c0)
+                other = valid & ~sel
+                staged += int(sel.sum())
+            else:
+                other = valid
+            csub[other] = -2 - sub[other]
+            direct += int(other.sum())
+    if codes.min() < -(2 ** 31):
+        raise ValueError("tile map: source index out of int32 range")
+    return TileMap((himg, wimg), tiles, codes.astype(np.int32).ravel(), ntx, staged, direct)

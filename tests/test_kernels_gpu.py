@@ -82,29 +82,37 @@ def test_common_mode_even_odd_and_empty_segments(cuda_device):
     _assert_equal(out, ref, "cm edge cases")
 
 
+@pytest.mark.parametrize("version", ["tiles", "v1"])
 @pytest.mark.parametrize("det,cm", [("tiny_epix", None), ("tiny_epix", "3,30,50,5"), ("epix10k2M", None),
-                                    ("epix10k2M", "default"), ("tiny_jungfrau", None)])
-def test_image_mode_matches_scatter(cuda_device, det, cm):
-    spec, consts, raw = _setup(det, 2, seed=21)
+                                    ("epix10k2M", "default"), ("tiny_jungfrau", None), ("jungfrau05M", None),
+                                    ("tiny_plain", None)])
+def test_image_mode_matches_scatter(cuda_device, det, cm, version, monkeypatch):
+    monkeypatch.setenv("PSANA_RAY_IMAGE_V1", "1" if version == "v1" else "0")
+    n = 2 if det in ("epix10k2M", "jungfrau05M") else 37   # 37 > 32: launch chunking
+    spec, consts, raw = _setup(det, n, seed=21)
     cmp = CommonModeParams.parse(cm)
     cal = Calibrator(consts, cuda_device, Mode.image, common_mode=cmp)
+    assert (cal.tile_map is not None) == (version == "tiles")
     out = cal(raw.to(cuda_device))
     torch.cuda.synchronize()
     geo = cal.geometry
     calib = reference.calibrate_reference(raw.to(torch.int32), consts, None, cal.cm)
     ref = reference.assemble_reference(calib, geo.rows, geo.cols, geo.image_shape)
-    assert out.shape == (2, 1, *geo.image_shape)
+    assert out.shape == (n, 1, *geo.image_shape)
     _assert_equal(out, ref, f"image {det}")
 
 
-def test_image_mask_applied_after_assembly(cuda_device):
-    spec, consts, raw = _setup("tiny_epix", 3, seed=4)
+@pytest.mark.parametrize("version", ["tiles", "v1"])
+@pytest.mark.parametrize("det,cm", [("tiny_epix", None), ("epix10k2M", None), ("epix10k2M", "default")])
+def test_image_mask_applied_after_assembly(cuda_device, det, cm, version, monkeypatch):
+    monkeypatch.setenv("PSANA_RAY_IMAGE_V1", "1" if version == "v1" else "0")
+    spec, consts, raw = _setup(det, 3, seed=4)
     geo = make_geometry(spec)
     imask = (np.random.default_rng(1).random(geo.image_shape) > 0.3).astype(np.uint8)
-    cal = Calibrator(consts, cuda_device, Mode.image, mask=imask)
+    cal = Calibrator(consts, cuda_device, Mode.image, mask=imask, common_mode=CommonModeParams.parse(cm))
     out = cal(raw.to(cuda_device))
     torch.cuda.synchronize()
-    calib = reference.calibrate_reference(raw.to(torch.int32), consts, None, None)
+    calib = reference.calibrate_reference(raw.to(torch.int32), consts, None, cal.cm)
     ref = reference.assemble_reference(calib, geo.rows, geo.cols, geo.image_shape, imask)
     _assert_equal(out, ref, "image mask")
 

@@ -105,3 +105,47 @@ def test_commonmode_parse():
     assert CommonModeParams.parse("off") is None
     cm = CommonModeParams.parse("1,20,inf,7,24")
     assert cm.flags == 1 and cm.thr == 20 and cm.maxcorr == float("inf") and cm.npix_min == 7 and cm.bank_cols == 24
+
+
+def _emulate_tiles(frame: np.ndarray, tm):
+    """numpy model of csrc/image.hip's use of a TileMap (stage box with pitch w+1, then codes)."""
+    from psana_ray_amd.models.geometry import TILE_H, TILE_W
+
+    himg, wimg = tm.image_shape
+    out = np.zeros(himg * wimg, np.float32)
+    flat = frame.ravel()
+    codes = tm.codes.reshape(himg, wimg)
+    for t in range(tm.n_tiles):
+        ty, tx = divmod(t, tm.tiles_x)
+        ys = slice(ty * TILE_H, min(himg, (ty + 1) * TILE_H))
+        xs = slice(tx * TILE_W, min(wimg, (tx + 1) * TILE_W))
+        cd = codes[ys, xs]
+        p, r0, c0, h, w = tm.tiles[t, :5]
+        stage = np.zeros(h * (w + 1) + 1, np.float32)
+        if p >= 0:
+            box = np.zeros((h, w + 1), np.float32)
+            box[:, :w] = frame[p, r0:r0 + h, c0:c0 + w]
+            stage[:h * (w + 1)] = box.ravel()
+        v = np.zeros(cd.shape, np.float32)
+        v[cd >= 0] = stage[cd[cd >= 0]]
+        v[cd <= -2] = flat[-(cd[cd <= -2].astype(np.int64) + 2)]
+        out.reshape(himg, wimg)[ys, xs] = v
+    return out.reshape(himg, wimg)
+
+
+@pytest.mark.parametrize("det", ["tiny_epix", "epix10k2M", "tiny_jungfrau"])
+@pytest.mark.parametrize("masked", [False, True])
+def test_tile_map_reproduces_assembly(det, masked):
+    from psana_ray_amd.models import get_detector, make_geometry
+    from psana_ray_amd.models.geometry import build_tile_map
+
+    spec = get_detector(det)
+    geo = make_geometry(spec)
+    rng = np.random.default_rng(1)
+    frame = rng.normal(size=spec.frame_shape).astype(np.float32)
+    mask = (rng.random(geo.image_shape) > 0.1).astype(np.uint8) if masked else None
+    tm = build_tile_map(geo.index_map(), spec, geo.image_shape, mask)
+    assert tm.staged_px + tm.direct_px == (spec.npix if mask is None else int((geo.index_map().reshape(geo.image_shape)[mask > 0] >= 0).sum()))
+    ref = reference.assemble_reference(torch.from_numpy(frame)[None], geo.rows, geo.cols, geo.image_shape,
+                                       mask)[0, 0].numpy()
+    np.testing.assert_array_equal(_emulate_tiles(frame, tm), ref)
