@@ -35,7 +35,7 @@ log = logging.getLogger(__name__)
 
 class ProducerPipeline:
     def __init__(self, source, calibrator: Optional[Calibrator], endpoint: QueueEndpoint, rank: int = 0,
-                 chunk: int = 16, n_raw_buffers: int = 6, acquire_timeout_s: float = 1.0,
+                 chunk: int = 32, n_raw_buffers: int = 6, acquire_timeout_s: float = 1.0,
                  log_every: int = 0):
         self.source = source
         self.cal = calibrator
