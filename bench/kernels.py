@@ -119,11 +119,26 @@ def main(argv=None):
     if want("calib_cm_ab"):
         import os
         calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
-        for rnd in range(3):   # interleaved A/B in one process (methodology rule 24)
-            os.environ["PSANA_RAY_CM_GENERIC"] = "1"
-            report(f"calib_cm(generic bitonic) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
-            os.environ["PSANA_RAY_CM_GENERIC"] = "0"
-            report(f"calib_cm(sort networks) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
+        calmem = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams(flags=0))
+        for rnd in range(2):
+            for stripe in ("192", "96", "48"):
+                os.environ["PSANA_RAY_CM_STRIPE"] = stripe
+                report(f"calib_cm(sort networks, stripe={stripe}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
+                       F * npix * 6)
+        os.environ.pop("PSANA_RAY_CM_STRIPE", None)
+        for rnd in range(2):   # interleaved A/B in one process (methodology rule 24)
+            for swz in ("1", "0"):
+                os.environ["PSANA_RAY_CM_SWZ"] = swz
+                os.environ["PSANA_RAY_CM_GENERIC"] = "0"
+                report(f"calib_cm(sort networks, xcd_swizzle={swz}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
+                       F * npix * 6)
+                report(f"calib_cm(memory phases only: flags=0, xcd_swizzle={swz}) r{rnd}",
+                       timeit(lambda: calmem.run(rl, ol), a.iters), F * npix * 6)
+                os.environ["PSANA_RAY_CM_GENERIC"] = "1"
+                report(f"calib_cm(generic bitonic, xcd_swizzle={swz}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
+                       F * npix * 6)
+        os.environ.pop("PSANA_RAY_CM_GENERIC", None)
+        os.environ.pop("PSANA_RAY_CM_SWZ", None)
     if want("calib_cm"):
         calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
         report("calib_cm(rows+cols)", timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)

@@ -58,6 +58,15 @@ inline void hip_check(hipError_t e, const char* what) {
 
 inline bool aligned16(uint64_t p) { return (p & 15u) == 0; }
 
+// Bijective XCD-aware block remap (guide T1): the hardware deals workgroups round-robin over the
+// 8 XCDs (block b and b+8 share an L2), so hand each XCD a CONTIGUOUS range of logical ids.
+// Speed only -- every logical id is still produced exactly once.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
+  constexpr int kXcd = 8;
+  const int q = nwg / kXcd, r = nwg % kXcd, xcd = orig % kXcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / kXcd;
+}
+
 // Register-only select.  A plain `c ? t[1][i] : t[0][i]` lets LLVM fold the select into an
 // indexed access t[c][i], which forces the whole register table into scratch/LDS; the integer
 // blend keeps both operands in VGPRs.

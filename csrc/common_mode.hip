@@ -160,7 +160,19 @@ struct TileGeom {
   int asic_rows, asic_cols;    // R, C of one ASIC tile
   int asics_per_col, asics_per_row;  // H / R, W / C
   int64_t npix;                // pixels per frame
+  int nframes;                 // frames of this launch (grid = n_asics * nframes, 1-D)
+  int swizzle;                 // 1: XCD-aware remap (all frames of an ASIC on one XCD / L2); opt-in
 };
+
+// (asic, frame) of this workgroup.  Frame-minor logical order + the XCD remap put the blocks
+// that read the SAME per-ASIC tables (574 KB for epix) on one XCD, so the tables come from its L2
+// instead of HBM for every frame.
+__device__ __forceinline__ void cm_block_coords(const TileGeom& tg, int& asic, int& f) {
+  const int nwg = (int)gridDim.x;
+  const int id = tg.swizzle ? xcd_swizzle((int)blockIdx.x, nwg) : (int)blockIdx.x;
+  asic = id / tg.nframes;
+  f = id % tg.nframes;
+}
 
 // per-pixel nibble in LDS: bits0-1 candidate, bit2 good, bit3 cm-eligible
 template <int KIND>
@@ -175,8 +187,8 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
   uint32_t* nib = reinterpret_cast<uint32_t*>(smem + (((size_t)R * LD * 4 + 15) & ~(size_t)15));
   const int C8 = C >> 3;
 
-  const int asic = blockIdx.x;
-  const int f = blockIdx.y;
+  int asic, f;
+  cm_block_coords(tg, asic, f);
   const int per_panel = tg.asics_per_col * tg.asics_per_row;
   const int panel = asic / per_panel;
   const int ar = (asic % per_panel) / tg.asics_per_row;
@@ -353,8 +365,8 @@ __device__ __forceinline__ void fixed_median_pos(int cnt, int& lo, int& hi) {
   hi = a + (cnt >> 1);
 }
 
-template <int KIND, int L, int M>
-__global__ __launch_bounds__(512) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
+template <int KIND, int L, int M, int BLOCK>
+__global__ __launch_bounds__(BLOCK, 512 / BLOCK) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
                                                             const float* __restrict__ gf,
                                                             const uint8_t* __restrict__ pflags,
                                                             const TileGeom tg, const CmParams cp) {
@@ -364,8 +376,8 @@ __global__ __launch_bounds__(512) void calib_cm_net_kernel(const FramePtrs fp, c
   float* tile = reinterpret_cast<float*>(smem);
   uint32_t* nib = reinterpret_cast<uint32_t*>(smem + (((size_t)R * LD * 4 + 15) & ~(size_t)15));
   const int C8 = C >> 3;
-  const int asic = blockIdx.x;
-  const int f = blockIdx.y;
+  int asic, f;
+  cm_block_coords(tg, asic, f);
   const int per_panel = tg.asics_per_col * tg.asics_per_row;
   const int panel = asic / per_panel;
   const int ar = (asic % per_panel) / tg.asics_per_row;
@@ -575,8 +587,8 @@ size_t cm_lds_bytes(int asic_rows, int asic_cols) {
 // need whole columns, so an ASIC may be cut into full-height stripes whose width is a multiple
 // of the bank width without changing any median (Jungfrau: 256x256 ASIC = 289 KB > 160 KiB ->
 // two 256x128 stripes of 145 KB).  0 = no stripe fits.
-int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols) {
-  for (int w = asic_cols; w >= bank_cols; --w) {
+int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols, int max_cols) {
+  for (int w = std::min(asic_cols, max_cols > 0 ? max_cols : asic_cols); w >= bank_cols; --w) {
     if (asic_cols % w || w % bank_cols || w % 8) continue;
     if (cm_lds_bytes(asic_rows, w) <= 160 * 1024) return w;
   }
@@ -594,7 +606,28 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   check(bank_cols >= 1 && bank_cols <= 64 && asic_cols % bank_cols == 0,
         "calib_cm: bank_cols must be <= 64 and divide the ASIC width");
   check(panel_cols % 8 == 0, "calib_cm: panel cols must be a multiple of 8");
-  asic_cols = cm_tile_cols(asic_rows, asic_cols, bank_cols);
+  // stripe width: PSANA_RAY_CM_STRIPE caps it (A/B); a stripe of <= 128 columns runs 256-thread
+  // workgroups, two of which fit one CU (LDS <= 80 KB each), so one block's HBM phases overlap
+  // the other's sorts (one 512-thread block per CU cannot overlap anything)
+  // Default: the widest stripe <= 128 columns whose tile fits half the LDS, when a sort-network
+  // instantiation exists for it (epix10k2M: 176x96 stripes, 15.29 vs 15.82 us/frame full width,
+  // 48 columns 22.8; profiles/kernels_r1_cm_stripes.jsonl).
+  const int Mh = (asic_rows + 1) / 2;
+  const bool net256 = !cm_force_generic() &&
+      ((kind == kEpix10ka && bank_cols == 48 && Mh == 88) || (kind == kEpix10ka && bank_cols == 8 && Mh == 8) ||
+       (kind == kPlain && bank_cols == 32 && Mh == 64) || (kind == kPlain && bank_cols == 8 && Mh == 4));
+  int max_w = 0;
+  if (net256) {
+    for (int w = std::min(asic_cols, 128); w >= bank_cols; --w)
+      if (asic_cols % w == 0 && w % bank_cols == 0 && w % 8 == 0 && cm_lds_bytes(asic_rows, w) <= 80 * 1024) {
+        max_w = w;
+        break;
+      }
+  }
+  if (const char* e = getenv("PSANA_RAY_CM_STRIPE"); e && *e) max_w = std::max(0, atoi(e));   // 0: full width
+  const int full_cols = asic_cols;
+  asic_cols = cm_tile_cols(asic_rows, full_cols, bank_cols, max_w);
+  if (asic_cols == 0) asic_cols = cm_tile_cols(asic_rows, full_cols, bank_cols, 0);
   check(asic_cols > 0, "calib_cm: no full-height ASIC stripe fits in 160 KiB of LDS");
   const size_t lds = cm_lds_bytes(asic_rows, asic_cols);
   check(aligned16(ped) && aligned16(gf) && (pflags & 7) == 0, "calib_cm: misaligned constant tables");
@@ -609,24 +642,34 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   tg.asics_per_row = panel_cols / asic_cols;
   tg.npix = (int64_t)n_panels * panel_rows * panel_cols;
   CmParams cp{thr, maxcorr, npix_min, flags, bank_cols};
-  const dim3 grid((unsigned)(n_panels * tg.asics_per_col * tg.asics_per_row), (unsigned)nframes);
+  tg.nframes = nframes;
+  {
+    // XCD-aware placement is OFF by default: measured slower (sort nets 17.4 vs 15.8 us/frame,
+    // memory phases alone 6.5 vs 4.9; profiles/kernels_r1_cm_swizzle.jsonl) -- the per-ASIC tables
+    // are already cache-served under round-robin placement.  PSANA_RAY_CM_SWZ=1 turns it on (A/B).
+    const char* e = getenv("PSANA_RAY_CM_SWZ");
+    tg.swizzle = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  const dim3 grid((unsigned)(n_panels * tg.asics_per_col * tg.asics_per_row * nframes));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float* P = reinterpret_cast<const float*>(ped);
   const float* G = reinterpret_cast<const float*>(gf);
   const uint8_t* F = reinterpret_cast<const uint8_t*>(pflags);
   const int M = (asic_rows + 1) / 2;
   bool done = false;
-#define PR_CM_NET(KIND_, L_, M_)                                                                      \
-  if (!done && kind == KIND_ && bank_cols == L_ && M == M_ && !cm_force_generic()) {                  \
-    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<KIND_, L_, M_>,                     \
+  const bool narrow = asic_cols <= 128;   // 2 lanes per column fit a 256-thread block
+#define PR_CM_NET(KIND_, L_, M_, B_)                                                                  \
+  if (!done && kind == KIND_ && bank_cols == L_ && M == M_ && (B_ == 256) == narrow && !cm_force_generic()) { \
+    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<KIND_, L_, M_, B_>,                 \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");   \
-    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_>), grid, dim3(512), lds, s, fp, P, G, F, tg, cp); \
+    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_, B_>), grid, dim3(B_), lds, s, fp, P, G, F, tg, cp); \
     done = true;                                                                                      \
   }
-  PR_CM_NET(kEpix10ka, 48, 88)
-  PR_CM_NET(kEpix10ka, 8, 8)
-  PR_CM_NET(kPlain, 32, 64)
-  PR_CM_NET(kPlain, 8, 4)
+  PR_CM_NET(kEpix10ka, 48, 88, 512)
+  PR_CM_NET(kEpix10ka, 48, 88, 256)
+  PR_CM_NET(kEpix10ka, 8, 8, 256)
+  PR_CM_NET(kPlain, 32, 64, 256)
+  PR_CM_NET(kPlain, 8, 4, 256)
 #undef PR_CM_NET
   if (!done) {
   switch (kind) {

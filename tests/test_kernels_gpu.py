@@ -42,9 +42,13 @@ def test_calib_basic_bitwise(cuda_device, det, masked):
     _assert_equal(out, ref, f"calib {det}")
 
 
-@pytest.mark.parametrize("det", ["tiny_epix", "epix10k2M", "jungfrau05M"])
+@pytest.mark.parametrize("det,stripe", [("tiny_epix", ""), ("epix10k2M", ""), ("epix10k2M", "0"), ("epix10k2M", "48"),
+                                        ("jungfrau05M", "")])
 @pytest.mark.parametrize("flags", [1, 2, 3])
-def test_common_mode_bitwise(cuda_device, det, flags):
+def test_common_mode_bitwise(cuda_device, det, stripe, flags, monkeypatch):
+    # stripe: PSANA_RAY_CM_STRIPE caps the full-height stripe width ("" default = 96 for epix with
+    # 256-thread blocks, "0" full width with 512-thread blocks, "48" one bank per stripe)
+    monkeypatch.setenv("PSANA_RAY_CM_STRIPE", stripe)
     # jungfrau05M: 256x256 ASICs exceed LDS -> two full-height 256x128 stripes per ASIC
     n = 2 if det in ("epix10k2M", "jungfrau05M") else 5
     spec, consts, raw = _setup(det, n, seed=11, gain_config="mixed")
