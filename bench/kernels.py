@@ -189,12 +189,27 @@ def main(argv=None):
         counts = torch.zeros(F, dtype=torch.int32, device=dev)
         summ = torch.zeros((F, 2), dtype=torch.float32, device=dev)
         for rnd in range(2):   # interleaved A/B in one process
-            for ver in ("v1", "v2"):
+            C = _ext.load()
+            sums = torch.zeros(F, dtype=torch.float32, device=dev)
+            op = [int(t.data_ptr()) for t in ol]
+            for k in (8, 16):
+                for nt in (False, True):
+                    report(f"read_f32 reference (K={k}, nt={int(nt)}) r{rnd}",
+                           timeit(lambda: C.read_f32(op, npix, k, nt, int(sums.data_ptr()), _ext.stream_handle()),
+                                  a.iters), F * npix * 4)
+            for ver, groups in (("v1", ""), ("tiles, 2 frames/block", str(max(1, F // 2))), ("stream K=4", ""),
+                                ("stream K=8", ""), ("stream K=16", "")):
                 os.environ["PSANA_RAY_PF_V1"] = "1" if ver == "v1" else "0"
+                os.environ["PSANA_RAY_PF_VERSION"] = "3" if ver.startswith("stream") else "2"
+                os.environ["PSANA_RAY_PF_K"] = ver.split("=")[1].split()[0] if "K=" in ver else ""
+                os.environ["PSANA_RAY_PF_GROUPS"] = groups
                 report(f"peakfind({ver}) r{rnd}",
                        timeit(lambda: kernels.peakfind(ol, spec.frame_shape, p, peaks, counts, summ), a.iters),
                        F * npix * 4, {"peaks_per_frame": float(counts.float().mean())})
         os.environ.pop("PSANA_RAY_PF_V1", None)
+        os.environ.pop("PSANA_RAY_PF_GROUPS", None)
+        os.environ.pop("PSANA_RAY_PF_VERSION", None)
+        os.environ.pop("PSANA_RAY_PF_K", None)
     if want("h2d"):
         C = _ext.load()
         hp = src.pool

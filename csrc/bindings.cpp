@@ -90,6 +90,11 @@ PYBIND11_MODULE(_C, m) {
           pr::launch_convert_u16_f32(make_ptrs(in, out), (int)in.size(), npix, stream);
         },
         "bandwidth reference: u16 -> f32 streaming copy (same traffic as calib_basic)");
+  m.def("read_f32",
+        [](const std::vector<uint64_t>& in, int64_t npix, int k, bool nt, uint64_t sums, uint64_t stream) {
+          pr::launch_read_f32(make_ptrs(in, in), (int)in.size(), npix, k, nt, sums, stream);
+        },
+        "bandwidth reference: read-only f32 frame sweep (what the peak finder's input read can reach)");
   m.def("xor_lane_selftest", &pr::launch_xor_selftest, py::arg("out"), py::arg("stream"));
   m.def("assemble",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t idx, int64_t nout,

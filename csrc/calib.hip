@@ -209,6 +209,48 @@ void launch_convert_u16_f32(const FramePtrs& fp, int nframes, int64_t npix, uint
   hip_check(hipGetLastError(), "convert launch");
 }
 
+// Read-only bandwidth reference (what a frame-reading consumer kernel can reach): K float4 per
+// lane, block reduction, one atomic per block.  NT = nontemporal loads.
+template <int K, bool NT>
+__global__ __launch_bounds__(256) void read_f32_kernel(const FramePtrs fp, const int64_t n4, float* __restrict__ sums) {
+  __shared__ float red[4];
+  const int f = blockIdx.y;
+  const int64_t q0 = (int64_t)blockIdx.x * 256 * K + threadIdx.x;
+  const PR_GLOBAL f32x4_t* in = gin<f32x4_t>(fp.in[f]);
+  float acc = 0.0f;
+  if ((int64_t)(blockIdx.x + 1) * 256 * K <= n4) {
+    f32x4_t v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = NT ? ld_nt_f4(in + q0 + 256 * k) : in[q0 + 256 * k];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+  } else {
+    for (int k = 0; k < K; ++k)
+      if (q0 + 256 * k < n4) {
+        const f32x4_t v = in[q0 + 256 * k];
+        acc += (v.x + v.y) + (v.z + v.w);
+      }
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(sums + f, red[0] + red[1] + red[2] + red[3]);
+}
+
+void launch_read_f32(const FramePtrs& fp, int nframes, int64_t npix, int k, bool nt, uint64_t sums, uint64_t stream) {
+  check(nframes >= 1 && nframes <= kMaxFrames && npix % 4 == 0, "read_f32: bad arguments");
+  const int64_t n4 = npix / 4;
+  const dim3 grid((unsigned)((n4 + 256 * k - 1) / (256 * k)), (unsigned)nframes);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* S = reinterpret_cast<float*>(sums);
+#define PR_RD(K_, NT_) hipLaunchKernelGGL((read_f32_kernel<K_, NT_>), grid, dim3(256), 0, s, fp, n4, S)
+  if (k == 4) { if (nt) PR_RD(4, true); else PR_RD(4, false); }
+  else if (k == 8) { if (nt) PR_RD(8, true); else PR_RD(8, false); }
+  else { check(k == 16, "read_f32: k must be 4, 8 or 16"); if (nt) PR_RD(16, true); else PR_RD(16, false); }
+#undef PR_RD
+  hip_check(hipGetLastError(), "read_f32 launch");
+}
+
 // Fused raw -> assembled image (image mode without common mode).  One thread owns 4
 // consecutive output pixels; idx[o] is the flat source pixel of output o or -1 (gap).
 // Constants are gathered once per thread and reused over the frame batch.

@@ -106,6 +106,7 @@ __device__ __forceinline__ void st_f4(PR_GLOBAL float4* p, const float4 v) {
   x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
   *(PR_GLOBAL f32x4_t*)p = x;
 }
+__device__ __forceinline__ f32x4_t ld_nt_f4(const PR_GLOBAL f32x4_t* p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ uint2 ld_nt_u2(const PR_GLOBAL uint2* p) {
   const u32x2_t v = __builtin_nontemporal_load((const PR_GLOBAL u32x2_t*)p);
   return make_uint2(v.x, v.y);

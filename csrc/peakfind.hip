@@ -12,11 +12,17 @@
 // Per-frame summary: number of pixels above thr_peak and their sum (hit-finding statistics),
 // reduced wave -> LDS -> one atomic per workgroup.
 //
-// MI355X design: output tiles staged with their halo once in LDS; candidates are rare so the
-// divergent verification path is cheap; one atomic per accepted peak reserves its record slot
-// (and bumps an optional 64-bit running total, so consumers never read counts back per batch).
-// v1 (64x16 tile, 4 px per lane, scalar loads) is kept for A/B (PSANA_RAY_PF_V1=1).
+// MI355X design: candidates are rare in detector frames, so the default (v3 "stream") reads every
+// pixel once with coalesced 16-B loads, thresholds in registers, and sends only the rare
+// candidates through the neighbourhood test (direct, cache-hit reads); one atomic per accepted
+// peak reserves its record slot (and bumps an optional 64-bit running total, so consumers never
+// read counts back per batch).  Versions kept for A/B: PSANA_RAY_PF_VERSION=2 (64x32 LDS halo
+// tiles, frames walked with prefetch), PSANA_RAY_PF_V1=1 (64x16 tiles, scalar loads).
+// epix10k2M: v3 2.21, v2 2.76-2.86, v1 5.88 us/frame (profiles/kernels_r1_peakfind_ab.jsonl).
 #include "common.h"
+
+#include <algorithm>
+#include <cstdlib>
 
 namespace pr {
 
@@ -151,10 +157,10 @@ __global__ __launch_bounds__(256) void peakfind_v1_kernel(const FramePtrs fp, co
 // ---------------------------------------------------------------------------------------------
 constexpr int kPf2TX = 64, kPf2TY = 32, kPf2HX = 4;
 
-template <int RAD>
-__device__ __forceinline__ void pf_candidate(const float (*t)[kPf2TX + 2 * kPf2HX], int cy, int cx, float v,
-                                             const PfParams& pp, int f, int panel, int gy, int gx,
-                                             float* __restrict__ peaks, int* __restrict__ counts,
+// at(dy, dx): neighbour value, NaN outside the panel
+template <int RAD, typename At>
+__device__ __forceinline__ void pf_candidate(const At& at, float v, const PfParams& pp, int f, int panel, int gy,
+                                             int gx, float* __restrict__ peaks, int* __restrict__ counts,
                                              unsigned long long* __restrict__ total) {
   constexpr int H = RAD + 2;
 #pragma unroll
@@ -162,7 +168,7 @@ __device__ __forceinline__ void pf_candidate(const float (*t)[kPf2TX + 2 * kPf2H
 #pragma unroll
     for (int dx = -RAD; dx <= RAD; ++dx) {
       if (dy == 0 && dx == 0) continue;
-      const float n = t[cy + dy][cx + dx];
+      const float n = at(dy, dx);
       if (n != n) continue;
       const bool before = (dy < 0) || (dy == 0 && dx < 0);
       if (before ? !(v > n) : !(v >= n)) return;   // not the strict local max (ties: lower index wins)
@@ -175,7 +181,7 @@ __device__ __forceinline__ void pf_candidate(const float (*t)[kPf2TX + 2 * kPf2H
     for (int dx = -H; dx <= H; ++dx) {
       const int d = max(abs(dy), abs(dx));
       if (d <= RAD) continue;
-      const float n = t[cy + dy][cx + dx];
+      const float n = at(dy, dx);
       if (n != n) continue;
       s += n;
       s2 += n * n;
@@ -191,7 +197,7 @@ __device__ __forceinline__ void pf_candidate(const float (*t)[kPf2TX + 2 * kPf2H
   for (int dy = -RAD; dy <= RAD; ++dy)
 #pragma unroll
     for (int dx = -RAD; dx <= RAD; ++dx) {
-      const float n = t[cy + dy][cx + dx];
+      const float n = at(dy, dx);
       if (n == n) inten += n - bkg;
     }
   const int slot = atomicAdd(counts + f, 1);
@@ -210,7 +216,7 @@ __device__ __forceinline__ void pf_candidate(const float (*t)[kPf2TX + 2 * kPf2H
 }
 
 template <int RAD>
-__global__ __launch_bounds__(256) void peakfind_kernel(const FramePtrs fp, const PfParams pp,
+__global__ __launch_bounds__(256) void peakfind_kernel(const FramePtrs fp, const int nframes, const PfParams pp,
                                                        float* __restrict__ peaks, int* __restrict__ counts,
                                                        float* __restrict__ summary,
                                                        unsigned long long* __restrict__ total) {
@@ -219,44 +225,153 @@ __global__ __launch_bounds__(256) void peakfind_kernel(const FramePtrs fp, const
   constexpr int LW = kPf2TX + 2 * kPf2HX;   // 72 floats = 18 float4 per row
   constexpr int LH = kPf2TY + 2 * H;
   constexpr int Q = LW / 4;
+  constexpr int NLD = (LH * Q + 255) / 256;  // float4 halo loads per thread
   __shared__ __attribute__((aligned(16))) float t[LH][LW];
   __shared__ float red_sum[4];
   __shared__ int red_cnt[4];
 
-  const int f = blockIdx.y;
+  // this workgroup walks frames [fa, fb) of ONE tile; frame f+1's halo is loaded into registers
+  // while frame f is processed from LDS (plain loads stay in flight across the barriers)
+  const int per = (nframes + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int fa = (int)blockIdx.y * per, fb = min(nframes, fa + per);
   const int tiles_x = (pp.cols + kPf2TX - 1) / kPf2TX;
   const int tiles_y = (pp.rows + kPf2TY - 1) / kPf2TY;
   const int panel = blockIdx.x / (tiles_x * tiles_y);
   const int trem = blockIdx.x % (tiles_x * tiles_y);
   const int ty0 = (trem / tiles_x) * kPf2TY, tx0 = (trem % tiles_x) * kPf2TX;
-  const PR_GLOBAL float* img = gin<float>(fp.in[f]) + (int64_t)panel * pp.rows * pp.cols;
+  const int64_t pbase = (int64_t)panel * pp.rows * pp.cols;
   const float NaN = __int_as_float(0x7fc00000);
+  const int tid = threadIdx.x;
 
-  for (int i = threadIdx.x; i < LH * Q; i += 256) {
+  int64_t goff[NLD];   // -1: outside the panel (NaN) or beyond the halo tile
+  int lofs[NLD];
+#pragma unroll
+  for (int j = 0; j < NLD; ++j) {
+    const int i = tid + 256 * j;
     const int ly = i / Q, q = i % Q;
     const int gy = ty0 + ly - H, gx = tx0 - kPf2HX + 4 * q;
-    f32x4_t v = {NaN, NaN, NaN, NaN};
-    if (gy >= 0 && gy < pp.rows && gx >= 0 && gx < pp.cols)
-      v = *(const PR_GLOBAL f32x4_t*)(img + (int64_t)gy * pp.cols + gx);
-    *reinterpret_cast<f32x4_t*>(&t[ly][4 * q]) = v;
+    lofs[j] = i < LH * Q ? ly * LW + 4 * q : -1;
+    goff[j] = (i < LH * Q && gy >= 0 && gy < pp.rows && gx >= 0 && gx < pp.cols)
+                  ? pbase + (int64_t)gy * pp.cols + gx : -1;
   }
-  __syncthreads();
+  f32x4_t pre[NLD];
+  auto load = [&](int f) {
+    const PR_GLOBAL float* img = gin<float>(fp.in[f]);
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) {
+      f32x4_t v = {NaN, NaN, NaN, NaN};
+      if (goff[j] >= 0) v = *(const PR_GLOBAL f32x4_t*)(img + goff[j]);
+      pre[j] = v;
+    }
+  };
 
-  const int x = threadIdx.x & 63;
-  const int y0 = threadIdx.x >> 6;
+  const int x = tid & 63;
+  const int y0 = tid >> 6;
   const int gx = tx0 + x;
+  const int lane = tid & 63, wave = tid >> 6;
+  if (fa < fb) load(fa);
+  for (int f = fa; f < fb; ++f) {
+#pragma unroll
+    for (int j = 0; j < NLD; ++j)
+      if (lofs[j] >= 0) *reinterpret_cast<f32x4_t*>(&t[0][0] + lofs[j]) = pre[j];
+    __syncthreads();
+    if (f + 1 < fb) load(f + 1);
+    float above_sum = 0.0f;
+    int above_cnt = 0;
+    if (gx < pp.cols) {
+#pragma unroll
+      for (int k = 0; k < kPf2TY / 4; ++k) {
+        const int y = y0 + 4 * k;
+        const float v = t[y + H][x + kPf2HX];   // NaN below the panel edge -> rejected
+        if (!(v > pp.thr_peak)) continue;
+        above_sum += v;
+        ++above_cnt;
+        const int cy = y + H, cx = x + kPf2HX;
+        pf_candidate<RAD>([&](int dy, int dx) { return t[cy + dy][cx + dx]; }, v, pp, f, panel, ty0 + y, gx, peaks,
+                          counts, total);
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      above_sum += __shfl_down(above_sum, o);
+      above_cnt += __shfl_down(above_cnt, o);
+    }
+    if (lane == 0) {
+      red_sum[wave] = above_sum;
+      red_cnt[wave] = above_cnt;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const float sm = red_sum[0] + red_sum[1] + red_sum[2] + red_sum[3];
+      const int c = red_cnt[0] + red_cnt[1] + red_cnt[2] + red_cnt[3];
+      if (c > 0) {
+        atomicAdd(summary + 2 * f, (float)c);
+        atomicAdd(summary + 2 * f + 1, sm);
+      }
+    }
+    // the halo tile and red_* are rewritten for the next frame only after everyone is done
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// v3 "stream" (default): candidates are rare in detector frames (synthetic epix10k2M: 0.02 % of
+// pixels above thr_peak, 0.5 % of 64-pixel wave rows contain one), so the LDS halo tile of v2 is
+// overhead: here every pixel is read ONCE with coalesced 16-B loads (4 float4 per lane in flight),
+// thresholded in registers, and only the rare candidates read their neighbourhood directly from
+// global memory (just-touched lines, L1/L2 hits).  No halo over-fetch, no LDS, no barrier except
+// the per-block reduction of the hit statistics.
+// ---------------------------------------------------------------------------------------------
+template <int RAD, int K>
+__global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp, const PfParams pp,
+                                                              float* __restrict__ peaks, int* __restrict__ counts,
+                                                              float* __restrict__ summary,
+                                                              unsigned long long* __restrict__ total) {
+  __shared__ float red_sum[4];
+  __shared__ int red_cnt[4];
+  const int f = blockIdx.y;
+  const PR_GLOBAL float* img = gin<float>(fp.in[f]);
+  const int64_t hw = (int64_t)pp.rows * pp.cols;
+  const int64_t n4 = (int64_t)pp.n_panels * hw / 4;
+  const int64_t q0 = (int64_t)blockIdx.x * 256 * K + threadIdx.x;
+  const float NaN = __int_as_float(0x7fc00000);
+  f32x4_t v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int64_t q = q0 + 256 * k;
+    v[k] = q < n4 ? *(const PR_GLOBAL f32x4_t*)(img + 4 * q) : f32x4_t{NaN, NaN, NaN, NaN};
+  }
+  // pass 1 (unrolled, registers only): hit statistics + a bitmask of the candidates
   float above_sum = 0.0f;
   int above_cnt = 0;
-  if (gx < pp.cols) {
+  uint64_t cand = 0;
 #pragma unroll
-    for (int k = 0; k < kPf2TY / 4; ++k) {
-      const int y = y0 + 4 * k;
-      const float v = t[y + H][x + kPf2HX];   // NaN below the panel edge -> rejected
-      if (!(v > pp.thr_peak)) continue;
-      above_sum += v;
-      ++above_cnt;
-      pf_candidate<RAD>(t, y + H, x + kPf2HX, v, pp, f, panel, ty0 + y, gx, peaks, counts, total);
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float val = v[k][e];
+      const bool hit = val > pp.thr_peak;   // rejects NaN padding too
+      above_sum += hit ? val : 0.0f;
+      above_cnt += hit ? 1 : 0;
+      cand |= (uint64_t)hit << (4 * k + e);
     }
+  }
+  // pass 2 (rare): ONE copy of the candidate test, looped over the set bits; the value is re-read
+  // (an L1 hit) instead of indexing the register array at run time
+  while (cand) {
+    const int b = __builtin_ctzll(cand);
+    cand &= cand - 1;
+    const int64_t p = 4 * (q0 + 256 * (b >> 2)) + (b & 3);
+    const float val = img[p];
+    const int panel = (int)(p / hw);
+    const int64_t rem = p - (int64_t)panel * hw;
+    const int y = (int)(rem / pp.cols), x = (int)(rem - (int64_t)(rem / pp.cols) * pp.cols);
+    const PR_GLOBAL float* pim = img + (int64_t)panel * hw;
+    pf_candidate<RAD>(
+        [&](int dy, int dx) {
+          const int yy = y + dy, xx = x + dx;
+          return (yy >= 0 && yy < pp.rows && xx >= 0 && xx < pp.cols) ? pim[(int64_t)yy * pp.cols + xx] : NaN;
+        },
+        val, pp, f, panel, y, x, peaks, counts, total);
   }
   for (int o = 32; o > 0; o >>= 1) {
     above_sum += __shfl_down(above_sum, o);
@@ -269,18 +384,19 @@ __global__ __launch_bounds__(256) void peakfind_kernel(const FramePtrs fp, const
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float s = red_sum[0] + red_sum[1] + red_sum[2] + red_sum[3];
+    const float sm = red_sum[0] + red_sum[1] + red_sum[2] + red_sum[3];
     const int c = red_cnt[0] + red_cnt[1] + red_cnt[2] + red_cnt[3];
     if (c > 0) {
       atomicAdd(summary + 2 * f, (float)c);
-      atomicAdd(summary + 2 * f + 1, s);
+      atomicAdd(summary + 2 * f + 1, sm);
     }
   }
 }
 
-static bool pf_force_v1() {
-  const char* e = getenv("PSANA_RAY_PF_V1");
-  return e != nullptr && e[0] == '1';
+static int pf_version() {   // PSANA_RAY_PF_VERSION: 1 | 2 (LDS tiles) | 3 (stream, default)
+  if (const char* e = getenv("PSANA_RAY_PF_V1"); e && e[0] == '1') return 1;
+  if (const char* e = getenv("PSANA_RAY_PF_VERSION"); e && *e) return atoi(e);
+  return 3;
 }
 
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
@@ -297,7 +413,23 @@ void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, i
   int* C = reinterpret_cast<int*>(counts);
   float* S = reinterpret_cast<float*>(summary);
   unsigned long long* T = reinterpret_cast<unsigned long long*>(total);
-  if (pf_force_v1()) {
+  const int ver = pf_version();
+  if (ver == 3) {
+    // float4 per lane (PSANA_RAY_PF_K: 4 | 8 | 16, A/B): K=4 2.21, 8 2.22, 16 2.26 us/frame; nontemporal
+    // loads measured no faster (profiles/kernels_r1_peakfind_ab.jsonl)
+    int K = 4;
+    if (const char* e = getenv("PSANA_RAY_PF_K"); e && *e) K = atoi(e);
+    check(K == 4 || K == 8 || K == 16, "peakfind: PSANA_RAY_PF_K must be 4, 8 or 16");
+    const int64_t n4 = (int64_t)n_panels * rows * cols / 4;
+    const dim3 grid((unsigned)((n4 + 256 * K - 1) / (256 * K)), (unsigned)nframes);
+#define PR_PF3(R_, K_) hipLaunchKernelGGL((peakfind_stream_kernel<R_, K_>), grid, dim3(256), 0, s, fp, pp, P, C, S, T)
+    if (radius == 1) {
+      if (K == 4) PR_PF3(1, 4); else if (K == 8) PR_PF3(1, 8); else PR_PF3(1, 16);
+    } else {
+      if (K == 4) PR_PF3(2, 4); else if (K == 8) PR_PF3(2, 8); else PR_PF3(2, 16);
+    }
+#undef PR_PF3
+  } else if (ver == 1) {
     const int tiles = ((cols + kPfTX - 1) / kPfTX) * ((rows + kPfTY - 1) / kPfTY);
     const dim3 grid((unsigned)(tiles * n_panels), (unsigned)nframes);
     if (radius == 1)
@@ -305,12 +437,16 @@ void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, i
     else
       hipLaunchKernelGGL(peakfind_v1_kernel<2>, grid, dim3(256), 0, s, fp, pp, P, C, S, T);
   } else {
-    const int tiles = ((cols + kPf2TX - 1) / kPf2TX) * ((rows + kPf2TY - 1) / kPf2TY);
-    const dim3 grid((unsigned)(tiles * n_panels), (unsigned)nframes);
+    const int tiles = ((cols + kPf2TX - 1) / kPf2TX) * ((rows + kPf2TY - 1) / kPf2TY) * n_panels;
+    // frame groups: enough workgroups to fill the chip (>= ~4096), the rest of the batch is walked
+    // by each workgroup with the next frame prefetched (PSANA_RAY_PF_GROUPS overrides, A/B)
+    int groups = std::max(1, std::min(nframes, (4096 + tiles - 1) / tiles));
+    if (const char* e = getenv("PSANA_RAY_PF_GROUPS"); e && *e) groups = std::max(1, std::min(nframes, atoi(e)));
+    const dim3 grid((unsigned)tiles, (unsigned)groups);
     if (radius == 1)
-      hipLaunchKernelGGL(peakfind_kernel<1>, grid, dim3(256), 0, s, fp, pp, P, C, S, T);
+      hipLaunchKernelGGL(peakfind_kernel<1>, grid, dim3(256), 0, s, fp, nframes, pp, P, C, S, T);
     else
-      hipLaunchKernelGGL(peakfind_kernel<2>, grid, dim3(256), 0, s, fp, pp, P, C, S, T);
+      hipLaunchKernelGGL(peakfind_kernel<2>, grid, dim3(256), 0, s, fp, nframes, pp, P, C, S, T);
   }
   hip_check(hipGetLastError(), "peakfind launch");
 }

@@ -130,11 +130,15 @@ def _sorted_peaks(p):
     return p[torch.argsort(key)]
 
 
-@pytest.mark.parametrize("version", ["v2", "v1"])
+@pytest.mark.parametrize("version", ["stream", "stream_k4", "stream_k16", "tiles", "tiles_walk", "v1"])
 @pytest.mark.parametrize("radius", [1, 2])
 @pytest.mark.parametrize("det", ["tiny_epix", "tiny_plain", "epix10k2M", "jungfrau05M"])
 def test_peakfind_vs_reference(cuda_device, det, radius, version, monkeypatch):
     monkeypatch.setenv("PSANA_RAY_PF_V1", "1" if version == "v1" else "0")
+    monkeypatch.setenv("PSANA_RAY_PF_VERSION", "3" if version.startswith("stream") else "2")
+    monkeypatch.setenv("PSANA_RAY_PF_K", version.split("_k")[1] if "_k" in version else "")
+    # tiles_walk: one frame group -> every workgroup walks all frames with the next one prefetched
+    monkeypatch.setenv("PSANA_RAY_PF_GROUPS", "1" if version == "tiles_walk" else "")
     spec, consts, raw = _setup(det, 3, seed=8, gain_config="AHL")
     frames = reference.calibrate_reference(raw.to(torch.int32), consts, None, None)
     params = PeakFinderParams(thr_peak=15.0, son_min=4.0, radius=radius, max_peaks=4096)
