@@ -117,13 +117,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("peakfind_slots",
         [](uint64_t base, int64_t slot_bytes, const std::vector<int>& slots, int n_panels, int rows, int cols,
            float thr_peak, float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
-           uint64_t summary, uint64_t total, uint64_t stream) {
+           uint64_t summary, uint64_t total, uint64_t stream, uint64_t zero_ptr, int64_t zero_bytes) {
           const int n = (int)slots.size();
           pr::check(n >= 1, "peakfind_slots: no slots");
           pr::check(base != 0 && slot_bytes >= (int64_t)n_panels * rows * cols * 4, "peakfind_slots: bad ring");
           hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-          pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(counts), 0, (size_t)n * 4, s), "zero counts");
-          pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(summary), 0, (size_t)n * 8, s), "zero summary");
+          if (zero_ptr != 0) {   // caller-provided region covering counts + summary: one fill
+            pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(zero_ptr), 0, (size_t)zero_bytes, s), "zero outputs");
+          } else {
+            pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(counts), 0, (size_t)n * 4, s), "zero counts");
+            pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(summary), 0, (size_t)n * 8, s), "zero summary");
+          }
           for (int a = 0; a < n; a += pr::kMaxFrames) {
             const int m = std::min(pr::kMaxFrames, n - a);
             std::vector<uint64_t> in(m);
@@ -139,7 +143,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("base"), py::arg("slot_bytes"), py::arg("slots"), py::arg("n_panels"), py::arg("rows"),
         py::arg("cols"), py::arg("thr_peak"), py::arg("son_min"), py::arg("radius"), py::arg("max_peaks"),
         py::arg("peaks"), py::arg("counts"), py::arg("summary"), py::arg("total"), py::arg("stream"),
-        py::call_guard<py::gil_scoped_release>());
+        py::arg("zero_ptr") = 0, py::arg("zero_bytes") = 0, py::call_guard<py::gil_scoped_release>());
 
   m.def("plan_round", &pr::plan_round_native, py::arg("offers"), py::arg("credits"), py::arg("round_id"),
         py::arg("policy"), "flattened (producer, offer_index, consumer) triples");
@@ -300,6 +304,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_cycled_source", &pr::ProducerEngine::set_cycled_source, py::arg("frames"), py::arg("photon_energy"))
       .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"), py::arg("k0") = 0)
       .def("request_stop", &pr::ProducerEngine::request_stop)
+      .def_property_readonly("device_resident", &pr::ProducerEngine::device_resident)
       .def("join", &pr::ProducerEngine::join, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &pr::ProducerEngine::running)
       .def_property_readonly("frames", &pr::ProducerEngine::frames)

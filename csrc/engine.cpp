@@ -110,6 +110,19 @@ void ProducerEngine::set_cycled_source(const std::vector<uint64_t>& frames, cons
   check(!frames.empty() && frames.size() == pe.size(), "ProducerEngine: bad cycled source");
   src_frames_ = frames;
   src_pe_ = pe;
+  // frames already resident in this GPU's memory are calibrated in place: no staging copy
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  bool all_dev = true;
+  for (uint64_t f : frames) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, reinterpret_cast<const void*>(f)) != hipSuccess ||
+        a.type != hipMemoryTypeDevice || a.device != device_) {
+      (void)hipGetLastError();   // pageable host memory reports an error: clear it
+      all_dev = false;
+      break;
+    }
+  }
+  device_resident_ = all_dev;
 }
 
 void ProducerEngine::start(int64_t n_local_events, int64_t max_steps, int64_t k0) {
@@ -183,7 +196,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
     int64_t k = k0;      // first event of the current chunk
     int64_t chunk_no = 0;
     int n = chunk_len(k0);
-    if (n > 0) {
+    if (n > 0 && !device_resident_) {
       const auto t0 = clk::now();
       stage(k0, n, 0);
       t_stage_ += secs(t0, clk::now());
@@ -194,7 +207,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       const int n_next = chunk_len(k_next);
       trace::Range chunk_range("producer.chunk");
       auto t0 = clk::now();
-      if (n_next > 0) {
+      if (n_next > 0 && !device_resident_) {
         trace::Range r("producer.stage_h2d");
         stage(k_next, n_next, (int)((chunk_no + 1) % n_raw_bufs_));
       }
@@ -214,18 +227,20 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       t_acquire_ += secs(t1, t2);
       if ((int)slots.size() < n) break;   // stopped while waiting
       char* buf = static_cast<char*>(raw_bufs_) + (size_t)b * chunk_ * plan_.raw_frame_bytes;
-      hip_check(hipStreamWaitEvent(compute_, h2d_done_[b], 0), "wait h2d");
       in.resize(n);
       out.resize(n);
-      for (int q = 0; q < n; ++q) {
-        in[q] = reinterpret_cast<uint64_t>(buf) + (uint64_t)q * plan_.raw_frame_bytes;
-        out[q] = ring_base_ + (uint64_t)slots[q] * (uint64_t)slot_bytes_;
+      if (device_resident_) {   // calibrate straight from the resident source frames
+        for (int q = 0; q < n; ++q) in[q] = src_frames_[(size_t)((k + q) % (int64_t)nsrc)];
+      } else {
+        hip_check(hipStreamWaitEvent(compute_, h2d_done_[b], 0), "wait h2d");
+        for (int q = 0; q < n; ++q) in[q] = reinterpret_cast<uint64_t>(buf) + (uint64_t)q * plan_.raw_frame_bytes;
       }
+      for (int q = 0; q < n; ++q) out[q] = ring_base_ + (uint64_t)slots[q] * (uint64_t)slot_bytes_;
       {
         trace::Range r("producer.launch_calib");
         run_calib_plan(plan_, in, out, stream_c);
       }
-      hip_check(hipEventRecord(buf_free_[b], compute_), "record buf free");
+      if (!device_resident_) hip_check(hipEventRecord(buf_free_[b], compute_), "record buf free");
       auto t3 = clk::now();
       t_launch_ += secs(t2, t3);
       hdrs.resize(n);

@@ -65,6 +65,7 @@ class ProducerEngine {
 
   // cycled source: frame k of this rank reads host_frames[k % n] (pinned host or device memory)
   void set_cycled_source(const std::vector<uint64_t>& frames, const std::vector<double>& photon_energy);
+  bool device_resident() const { return device_resident_; }
   // rank-local events [k0, n_local_events) (n_local_events < 0: endless), at most max_steps of them
   void start(int64_t n_local_events, int64_t max_steps, int64_t k0 = 0);
   void request_stop() { stop_.store(true); }
@@ -89,6 +90,7 @@ class ProducerEngine {
   int64_t rank_, size_;
   std::vector<uint64_t> src_frames_;
   std::vector<double> src_pe_;
+  bool device_resident_ = false;   // source frames live in this GPU's HBM: no staging copies
   hipStream_t h2d_ = nullptr, compute_ = nullptr;
   std::vector<hipEvent_t> buf_free_, h2d_done_;
   void* raw_bufs_ = nullptr;

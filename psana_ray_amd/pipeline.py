@@ -241,8 +241,10 @@ class PeakFinderConsumer:
             B = self.batch
             self._nbuf = 3
             self.peaks = torch.empty((self._nbuf, B, self.params.max_peaks, 8), dtype=torch.float32, device=self.device)
-            self.counts = torch.zeros((self._nbuf, B), dtype=torch.int32, device=self.device)
-            self.summary = torch.zeros((self._nbuf, B, 2), dtype=torch.float32, device=self.device)
+            # counts [B] int32 and summary [B, 2] f32 of a batch share ONE row, zeroed by one fill
+            self._meta = torch.zeros((self._nbuf, 3 * B), dtype=torch.int32, device=self.device)
+            self.counts = self._meta[:, :B]
+            self.summary = self._meta[:, B:].view(torch.float32).view(self._nbuf, B, 2)
             self.count_acc = torch.zeros((), dtype=torch.int64, device=self.device)
             self._b = 0
 
@@ -309,7 +311,8 @@ class PeakFinderConsumer:
             C.peakfind_slots(self.ep._base, self.ep._slot_bytes, slots, P, H, W, float(self.params.thr_peak),
                              float(self.params.son_min), int(self.params.radius), int(self.params.max_peaks),
                              int(self.peaks[b].data_ptr()), int(self.counts[b].data_ptr()),
-                             int(self.summary[b].data_ptr()), int(self.count_acc.data_ptr()), sh)
+                             int(self.summary[b].data_ptr()), int(self.count_acc.data_ptr()), sh,
+                             int(self._meta[b].data_ptr()), int(self._meta.shape[1] * 4))
             if self.keep_results:
                 hs = self.ep.pool.headers(slots)
                 with torch.cuda.stream(self.stream):

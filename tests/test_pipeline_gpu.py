@@ -73,3 +73,45 @@ def test_peakfinder_consumer_counts(cuda_device):
     ref_peaks, _ = reference.peakfind_reference(frames, params)
     expect = sum(ref_peaks[i % 4].shape[0] for i in range(40))
     assert total == expect
+
+
+def test_device_resident_source_calibrates_in_place(cuda_device):
+    """Frames already in HBM: the native engine calibrates them in place (no staging copy) and the
+    results are identical to the golden model."""
+    src = SyntheticRun("synthetic", 5, "epix10k2M", n_events=40, pool_frames=8, pinned=False, gen_device="cuda")
+    dev_pool = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(cuda_device)
+
+    class DevSource:
+        spec = src.spec
+        size = 1
+        calibrated = False
+        consts = src.consts
+
+        def cycled_frames(self):
+            return [int(dev_pool[j].data_ptr()) for j in range(dev_pool.shape[0])], [9.5] * dev_pool.shape[0]
+
+        def n_local_events(self):
+            return 40
+
+    cal = Calibrator(src.consts, cuda_device, Mode.calib, common_mode=CommonModeParams())
+    ring = FrameRing(cal.out_shape, cal.out_dtype, cuda_device, 16, 64)
+    ep = QueueEndpoint(ring)
+    prod = ProducerPipeline(DevSource(), cal, ep, chunk=8)
+    assert prod.engine is not None and prod.engine.device_resident
+    prod.run()
+    ref = reference.calibrate_reference(torch.from_numpy(src.pool.astype(np.int32)), src.consts, None, cal.cm)
+    n = 0
+    while True:
+        try:
+            it = ep.get(timeout=0.5)
+        except EndOfStream:
+            break
+        if it is None:
+            continue
+        with it:
+            got = it.data.clone()
+        torch.cuda.synchronize()
+        assert torch.equal(got.cpu(), ref[it.idx % 8]), f"frame {it.idx}"
+        n += 1
+    assert n == 40
+    assert prod.engine.timing()[0] < 1e-3, "no staging copies expected for a device-resident source"

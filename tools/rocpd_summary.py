@@ -41,7 +41,22 @@ def summarize(path):
             mc = [[k, v[0], v[1], v[2] / max(v[1], 1e-9) / 1e3] for k, v in agg.items()]
         except Exception:
             pass
-        out[db] = {"kernels": kern, "copies": mc}
+        marks = []
+        try:   # roctx ranges (--marker-trace): message in regions.extdata
+            agg = {}
+            for ext, st, en in con.execute("select extdata, start, end from regions"):
+                try:
+                    msg = json.loads(ext).get("message", "?")
+                except Exception:
+                    msg = "?"
+                agg.setdefault(msg, []).append((en - st) / 1e3)
+            for k, v in agg.items():
+                v.sort()
+                marks.append([k, len(v), sum(v), sum(v) / len(v), v[len(v) // 2], v[-1]])
+            marks.sort(key=lambda x: -x[2])
+        except Exception:
+            pass
+        out[db] = {"kernels": kern, "copies": mc, "ranges": marks}
     return out
 
 
@@ -58,6 +73,12 @@ def to_markdown(s):
             lines.append("|---|---|---|---|")
             for c in d["copies"]:
                 lines.append(f"| {c[0]} | {c[1]} | {c[2]:.1f} | {c[3]:.1f} |")
+        if d.get("ranges"):
+            lines.append("")
+            lines.append("| roctx range | n | total us | mean us | p50 us | max us |")
+            lines.append("|---|---|---|---|---|---|")
+            for m in d["ranges"]:
+                lines.append(f"| `{m[0]}` | {m[1]} | {m[2]:.1f} | {m[3]:.1f} | {m[4]:.1f} | {m[5]:.1f} |")
     return "\n".join(lines)
 
 
