@@ -121,11 +121,22 @@ def main(argv=None):
         calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
         calmem = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams(flags=0))
         for rnd in range(2):
-            for stripe in ("192", "96", "48"):
-                os.environ["PSANA_RAY_CM_STRIPE"] = stripe
-                report(f"calib_cm(sort networks, stripe={stripe}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
+            for gather in ("0", "1"):
+                os.environ["PSANA_RAY_CM_GATHER"] = gather
+                report(f"calib_cm(default, select-then-load={gather}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
                        F * npix * 6)
+                report(f"calib_cm(memory phases only, select-then-load={gather}) r{rnd}",
+                       timeit(lambda: calmem.run(rl, ol), a.iters), F * npix * 6)
+        os.environ.pop("PSANA_RAY_CM_GATHER", None)
+        for rnd in range(2):
+            for colq in ("2", "4"):
+                for stripe in ("192", "96", "48"):
+                    os.environ["PSANA_RAY_CM_STRIPE"] = stripe
+                    os.environ["PSANA_RAY_CM_COLQ"] = colq
+                    report(f"calib_cm(sort networks, {colq} lanes/column, stripe={stripe}) r{rnd}",
+                           timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
         os.environ.pop("PSANA_RAY_CM_STRIPE", None)
+        os.environ.pop("PSANA_RAY_CM_COLQ", None)
         for rnd in range(2):   # interleaved A/B in one process (methodology rule 24)
             for swz in ("1", "0"):
                 os.environ["PSANA_RAY_CM_SWZ"] = swz

@@ -153,6 +153,7 @@ struct CmParams {
   int npix_min;     // minimum participating pixels for a correction
   int flags;        // bit0: rows by bank, bit1: columns
   int bank_cols;    // columns per bank (<= 64, divides the ASIC width)
+  int gather;       // 1: load only the candidate tables a pixel group uses (net kernels)
 };
 
 struct TileGeom {
@@ -365,8 +366,38 @@ __device__ __forceinline__ void fixed_median_pos(int cnt, int& lo, int& hi) {
   hi = a + (cnt >> 1);
 }
 
-template <int KIND, int L, int M, int BLOCK>
-__global__ __launch_bounds__(BLOCK, 512 / BLOCK) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
+// quad_perm DPP read of a lane of the same quad (CTRL = p0 | p1<<2 | p2<<4 | p3<<6)
+template <int CTRL>
+__device__ __forceinline__ float dpp_quad(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_quad_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+}
+
+// Ascending sort of a V-shaped (non-increasing then non-decreasing) register sequence, virtually
+// padded with +inf to the next power of two: the bitonic half-cleaner network restricted to the
+// comparators between real positions (a comparator against a +inf pad is a no-op).
+template <int N>
+__device__ __forceinline__ void bitonic_merge_vpad(float (&z)[N]) {
+  constexpr int P2 = N <= 1 ? 1 : (N <= 2 ? 2 : (N <= 4 ? 4 : (N <= 8 ? 8 : (N <= 16 ? 16 : (N <= 32 ? 32 : 64)))));
+  static_assert(N <= 64, "bitonic_merge_vpad: at most 64 registers");
+#pragma unroll
+  for (int j = P2 / 2; j >= 1; j >>= 1) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      if ((i & j) == 0 && i + j < N) {
+        const float a = z[i], b = z[i + j];
+        z[i] = fminf(a, b);
+        z[i + j] = fmaxf(a, b);
+      }
+    }
+  }
+}
+
+template <int KIND, int L, int M, int BLOCK, int CQ>
+__global__ __launch_bounds__(BLOCK, CQ == 4 ? 4 : 512 / BLOCK) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
                                                             const float* __restrict__ gf,
                                                             const uint8_t* __restrict__ pflags,
                                                             const TileGeom tg, const CmParams cp) {
@@ -397,11 +428,24 @@ __global__ __launch_bounds__(BLOCK, 512 / BLOCK) void calib_cm_net_kernel(const 
     const uint2 fl = *reinterpret_cast<const uint2*>(pflags + pix);
     const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
     const uint32_t fw[2] = {fl.x, fl.y};
+    // select-then-load: a candidate table is read only by the 8-pixel groups that use it
+    // (gain-switched pixels are rare, so the second/third table's lines are almost never fetched;
+    // memory phases 5.6 -> see profiles/kernels_r1_cm_gather.jsonl)
+    uint32_t need = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bool vd;
+      need |= 1u << decode_cand((w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, KIND, vd);
+    }
+    if (!cp.gather) need = (1u << NT) - 1u;
     float pa[NT][8];
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
-      const float4 a = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix);
-      const float4 b = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix + 4);
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if ((need >> k) & 1u) {
+        a = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix);
+        b = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix + 4);
+      }
       pa[k][0] = a.x; pa[k][1] = a.y; pa[k][2] = a.z; pa[k][3] = a.w;
       pa[k][4] = b.x; pa[k][5] = b.y; pa[k][6] = b.z; pa[k][7] = b.w;
     }
@@ -481,7 +525,95 @@ __global__ __launch_bounds__(BLOCK, 512 / BLOCK) void calib_cm_net_kernel(const 
     __syncthreads();
   }
 
-  // ---- phase 2b: columns, two lanes per column ---------------------------------------------
+  // ---- phase 2b (CQ = 4): columns, FOUR lanes (a quad) per column, M rows each ---------------
+  //  each lane sorts its M values (sort_regs<M>); lanes (q, q^1) merge-split (lower lane keeps
+  //  min(x[i], partner[M-1-i]), upper the max) and sort the resulting bitonic sequences (the
+  //  lower lane negated so both are V-shaped: bitonic_merge_vpad); the two sorted halves of the
+  //  pair (0,1) and of the pair (2,3) are then merged by merge-path for k = 2M-1 and 2M with ONE
+  //  quad_perm(3,2,1,0) fetch per register.  Half the registers and half the serial comparator
+  //  chain of the two-lane path; validated by a numpy emulation of the exact lane algorithm.
+  if constexpr (CQ == 4) {
+    if (cp.flags & 2) {
+      const int nwork = 4 * C;
+      for (int w = tid; w < ((nwork + 63) / 64) * 64; w += blockDim.x) {
+        const bool act = w < nwork;
+        const int c = act ? (w >> 2) : 0;
+        const int q = w & 3;
+        const bool lower = (q & 1) == 0;
+        const uint32_t shift = 4 * (c & 7) + 3;
+        float x[M];
+        int my_cnt = 0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          const int r = q * M + i;
+          const bool in = act && r < R;
+          const float v = in ? tile[r * LD + c] : 0.0f;
+          const bool el = in && ((nib[r * C8 + (c >> 3)] >> shift) & 1u);
+          const bool pt = el && (fabsf(v) < cp.thr);
+          my_cnt += pt ? 1 : 0;
+          x[i] = pt ? v : QNAN;
+          if ((i & 15) == 15) asm volatile("" ::: "memory");
+        }
+        // quad totals + exclusive prefix of the non-participants: balanced +-inf padding
+        const int my_inv = M - my_cnt;
+        const int i0 = dpp_quad_i<0x00>(my_inv), i1 = dpp_quad_i<0x55>(my_inv);
+        const int i2 = dpp_quad_i<0xAA>(my_inv), i3 = dpp_quad_i<0xFF>(my_inv);
+        const int total_inv = i0 + i1 + i2 + i3;
+        const int cnt = 4 * M - total_inv;
+        const int a = total_inv >> 1;
+        const int prefix = (q > 0 ? i0 : 0) + (q > 1 ? i1 : 0) + (q > 2 ? i2 : 0);
+        const int neg_budget = min(my_inv, max(0, a - prefix));
+        int ninv = 0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          const bool inv = x[i] != x[i];
+          x[i] = inv ? (ninv < neg_budget ? -INF : INF) : x[i];
+          ninv += inv ? 1 : 0;
+        }
+        asm volatile("" ::: "memory");
+        sort_regs<M>(x);
+        // level 1: merge-split with lane q^1 (partner read reversed)
+        float z[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          const float pv = dpp_quad<0xB1>(x[M - 1 - i]);
+          const float y = lower ? fminf(x[i], pv) : fmaxf(x[i], pv);
+          z[i] = lower ? -y : y;   // both lanes V-shaped
+        }
+        bitonic_merge_vpad<M>(z);
+#pragma unroll
+        for (int i = 0; i < M; ++i) x[i] = lower ? -z[M - 1 - i] : z[i];   // ascending half of the pair
+        asm volatile("" ::: "memory");
+        // level 2: merge-path of pair (0,1) with pair (2,3); lane 0 reads lane 3, lane 1 lane 2
+        float k88 = INF, k87 = INF, plast = INF;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          const float pj = dpp_quad<0x1B>(x[j]);
+          k88 = fminf(k88, fmaxf(x[M - 1 - j], pj));
+          if (j <= M - 2) k87 = fminf(k87, fmaxf(x[M - 2 - j], pj));
+          if (j == M - 1) plast = pj;
+        }
+        const float e = dpp_quad<0xAA>(x[M - 1]);   // lane 2's last element
+        const float extra = q == 0 ? fminf(plast, fmaxf(x[M - 1], e)) : x[M - 1];
+        k87 = fminf(k87, extra);
+        k87 = fminf(k87, dpp_quad<0xB1>(k87));
+        k88 = fminf(k88, dpp_quad<0xB1>(k88));
+        const float k_lo = dpp_quad<0x00>(k87), k_hi = dpp_quad<0x00>(k88);   // lane 0 has the answer
+        const float med = (k_lo + ((cnt & 1) ? k_lo : k_hi)) * 0.5f;
+        asm volatile("" ::: "memory");
+        if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            const int r = q * M + i;
+            if (r < R && ((nib[r * C8 + (c >> 3)] >> shift) & 1u)) tile[r * LD + c] -= med;
+            if ((i & 15) == 15) asm volatile("" ::: "memory");
+          }
+        }
+      }
+      __syncthreads();
+    }
+  } else
+  // ---- phase 2b (CQ = 2): columns, two lanes per column ------------------------------------
   if (cp.flags & 2) {
     const int nwork = 2 * C;
     for (int w = tid; w < ((nwork + 63) / 64) * 64; w += blockDim.x) {
@@ -546,11 +678,18 @@ __global__ __launch_bounds__(BLOCK, 512 / BLOCK) void calib_cm_net_kernel(const 
     const int r = i / C8, c = (i % C8) * 8;
     const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
     const uint32_t nb = nib[i];
+    uint32_t need = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) need |= 1u << ((nb >> (4 * j)) & 3u);
+    if (!cp.gather) need = (1u << NT) - 1u;
     float ga[NT][8];
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
-      const float4 a = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix);
-      const float4 b = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix + 4);
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if ((need >> k) & 1u) {
+        a = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix);
+        b = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix + 4);
+      }
       ga[k][0] = a.x; ga[k][1] = a.y; ga[k][2] = a.z; ga[k][3] = a.w;
       ga[k][4] = b.x; ga[k][5] = b.y; ga[k][6] = b.z; ga[k][7] = b.w;
     }
@@ -641,7 +780,8 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   tg.asics_per_col = panel_rows / asic_rows;
   tg.asics_per_row = panel_cols / asic_cols;
   tg.npix = (int64_t)n_panels * panel_rows * panel_cols;
-  CmParams cp{thr, maxcorr, npix_min, flags, bank_cols};
+  CmParams cp{thr, maxcorr, npix_min, flags, bank_cols, 1};
+  if (const char* e = getenv("PSANA_RAY_CM_GATHER"); e && *e) cp.gather = atoi(e) != 0;   // A/B
   tg.nframes = nframes;
   {
     // XCD-aware placement is OFF by default: measured slower (sort nets 17.4 vs 15.8 us/frame,
@@ -658,18 +798,27 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   const int M = (asic_rows + 1) / 2;
   bool done = false;
   const bool narrow = asic_cols <= 128;   // 2 lanes per column fit a 256-thread block
-#define PR_CM_NET(KIND_, L_, M_, B_)                                                                  \
-  if (!done && kind == KIND_ && bank_cols == L_ && M == M_ && (B_ == 256) == narrow && !cm_force_generic()) { \
-    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<KIND_, L_, M_, B_>,                 \
+  // lanes per column: 4 (quad merge, <= 128 VGPRs, 4 waves/SIMD) unless PSANA_RAY_CM_COLQ=2 (A/B)
+  int cq_req = 0;
+  if (const char* e = getenv("PSANA_RAY_CM_COLQ"); e && *e) cq_req = atoi(e);
+  const int M2 = (asic_rows + 1) / 2, M4 = (asic_rows + 3) / 4;
+#define PR_CM_NET(KIND_, L_, M_, B_, CQ_)                                                              \
+  if (!done && kind == KIND_ && bank_cols == L_ && (CQ_ == 4 ? M4 : M2) == M_ &&                        \
+      (cq_req == 0 || cq_req == CQ_) && B_ == (narrow ? 256 : 512) * (CQ_ / 2) && !cm_force_generic()) {  \
+    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_>,             \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");   \
-    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_, B_>), grid, dim3(B_), lds, s, fp, P, G, F, tg, cp); \
+    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_>), grid, dim3(B_), lds, s, fp, P, G, F, tg, cp); \
     done = true;                                                                                      \
   }
-  PR_CM_NET(kEpix10ka, 48, 88, 512)
-  PR_CM_NET(kEpix10ka, 48, 88, 256)
-  PR_CM_NET(kEpix10ka, 8, 8, 256)
-  PR_CM_NET(kPlain, 32, 64, 256)
-  PR_CM_NET(kPlain, 8, 4, 256)
+  PR_CM_NET(kEpix10ka, 48, 44, 512, 4)
+  PR_CM_NET(kEpix10ka, 48, 44, 1024, 4)
+  PR_CM_NET(kEpix10ka, 48, 88, 512, 2)
+  PR_CM_NET(kEpix10ka, 48, 88, 256, 2)
+  PR_CM_NET(kEpix10ka, 8, 4, 512, 4)
+  PR_CM_NET(kEpix10ka, 8, 8, 256, 2)
+  PR_CM_NET(kPlain, 32, 32, 512, 4)
+  PR_CM_NET(kPlain, 32, 64, 256, 2)
+  PR_CM_NET(kPlain, 8, 4, 256, 2)
 #undef PR_CM_NET
   if (!done) {
   switch (kind) {

@@ -42,14 +42,19 @@ def test_calib_basic_bitwise(cuda_device, det, masked):
     _assert_equal(out, ref, f"calib {det}")
 
 
-@pytest.mark.parametrize("det,stripe", [("tiny_epix", ""), ("epix10k2M", ""), ("epix10k2M", "0"), ("epix10k2M", "48"),
-                                        ("jungfrau05M", "")])
+@pytest.mark.parametrize("det,stripe,colq,gather", [("tiny_epix", "", "", ""), ("tiny_epix", "", "2", ""),
+                                                    ("epix10k2M", "", "", ""), ("epix10k2M", "", "", "0"),
+                                                    ("epix10k2M", "0", "", ""), ("epix10k2M", "48", "", ""),
+                                                    ("epix10k2M", "", "2", ""), ("epix10k2M", "0", "2", ""),
+                                                    ("jungfrau05M", "", "", "")])
 @pytest.mark.parametrize("flags", [1, 2, 3])
-def test_common_mode_bitwise(cuda_device, det, stripe, flags, monkeypatch):
-    # stripe: PSANA_RAY_CM_STRIPE caps the full-height stripe width ("" default = 96 for epix with
-    # 256-thread blocks, "0" full width with 512-thread blocks, "48" one bank per stripe)
+def test_common_mode_bitwise(cuda_device, det, stripe, colq, gather, flags, monkeypatch):
+    # stripe: PSANA_RAY_CM_STRIPE caps the full-height stripe width ("" default = 96 for epix,
+    # "0" full width, "48" one bank per stripe); colq: lanes per column ("" default = 4-lane quad
+    # merge, "2" two-lane merge-path)
     monkeypatch.setenv("PSANA_RAY_CM_STRIPE", stripe)
-    # jungfrau05M: 256x256 ASICs exceed LDS -> two full-height 256x128 stripes per ASIC
+    monkeypatch.setenv("PSANA_RAY_CM_COLQ", colq)
+    monkeypatch.setenv("PSANA_RAY_CM_GATHER", gather)   # "" = default select-then-load
     n = 2 if det in ("epix10k2M", "jungfrau05M") else 5
     spec, consts, raw = _setup(det, n, seed=11, gain_config="mixed")
     cm = CommonModeParams(flags=flags, thr=30.0, maxcorr=50.0, npix_min=5)
