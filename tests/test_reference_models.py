@@ -149,3 +149,16 @@ def test_tile_map_reproduces_assembly(det, masked):
     ref = reference.assemble_reference(torch.from_numpy(frame)[None], geo.rows, geo.cols, geo.image_shape,
                                        mask)[0, 0].numpy()
     np.testing.assert_array_equal(_emulate_tiles(frame, tm), ref)
+
+
+def test_cm_quad_lane_algorithm_emulation():
+    """The 4-lanes-per-column median of csrc/common_mode.hip (CQ = 4), emulated lane by lane in
+    numpy, equals np.median on random columns (ties, empty / tiny / odd-sized columns)."""
+    import importlib.util
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "cm_quad_emulation.py")
+    spec = importlib.util.spec_from_file_location("cm_quad_emulation", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.run(trials=600, seed=3) == 0

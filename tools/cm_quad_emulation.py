@@ -63,22 +63,27 @@ def quad_median(col, part):
     hi = kth87 if (cnt & 1) else kth88
     return lo, hi, cnt
 
-rng = np.random.default_rng(0)
-bad = 0
-for trial in range(3000):
-    R = int(rng.choice([176, 175, 173, 16, 9, 4, 1, 8, 12]))
-    col = rng.normal(0, 10, R).astype(np.float32)
-    if trial % 7 == 0:
-        col = np.round(col)            # ties
-    part = rng.random(R) < rng.choice([0.0, 0.05, 0.5, 0.9, 1.0])
-    lo, hi, cnt = quad_median(col, part)
-    assert cnt == part.sum()
-    if cnt == 0:
-        continue
-    med = np.float32((np.float32(lo) + np.float32(hi)) * np.float32(0.5))
-    ref = np.float32(np.median(col[part]))
-    if med != ref:
-        bad += 1
-        if bad < 5:
-            print("MISMATCH", R, cnt, med, ref)
-print("mismatches:", bad)
+def run(trials=3000, seed=0):
+  rng = np.random.default_rng(seed)
+  bad = 0
+  for trial in range(trials):
+      R = int(rng.choice([176, 175, 173, 16, 9, 4, 1, 8, 12]))
+      col = rng.normal(0, 10, R).astype(np.float32)
+      if trial % 7 == 0:
+          col = np.round(col)            # ties
+      part = rng.random(R) < rng.choice([0.0, 0.05, 0.5, 0.9, 1.0])
+      lo, hi, cnt = quad_median(col, part)
+      assert cnt == part.sum()
+      if cnt == 0:
+          continue
+      med = np.float32((np.float32(lo) + np.float32(hi)) * np.float32(0.5))
+      ref = np.float32(np.median(col[part]))
+      if med != ref:
+          bad += 1
+          if bad < 5:
+              print("MISMATCH", R, cnt, med, ref)
+  return bad
+
+
+if __name__ == "__main__":
+    print("mismatches:", run())
