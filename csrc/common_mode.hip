@@ -397,7 +397,7 @@ __device__ __forceinline__ void bitonic_merge_vpad(float (&z)[N]) {
 }
 
 template <int KIND, int L, int M, int BLOCK, int CQ>
-__global__ __launch_bounds__(BLOCK, CQ == 4 ? 4 : 512 / BLOCK) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
+__global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
                                                             const float* __restrict__ gf,
                                                             const uint8_t* __restrict__ pflags,
                                                             const TileGeom tg, const CmParams cp) {
@@ -816,6 +816,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   PR_CM_NET(kEpix10ka, 48, 88, 256, 2)
   PR_CM_NET(kEpix10ka, 8, 4, 512, 4)
   PR_CM_NET(kEpix10ka, 8, 8, 256, 2)
+  PR_CM_NET(kJungfrau, 64, 64, 512, 4)
   PR_CM_NET(kPlain, 32, 32, 512, 4)
   PR_CM_NET(kPlain, 32, 64, 256, 2)
   PR_CM_NET(kPlain, 8, 4, 256, 2)

@@ -177,3 +177,17 @@ def test_kernel_rejects_bad_shapes(cuda_device):
         kernels.calib_basic([raw[0].to(cuda_device)], [bad_out], cal.ped, cal.gf, spec.kernel_kind)
     with pytest.raises(ValueError):
         kernels.calib_basic([raw[0]], [torch.empty(spec.npix)], cal.ped, cal.gf, spec.kernel_kind)
+
+
+@pytest.mark.parametrize("det", ["tiny_epix", "epix10k2M", "jungfrau05M"])
+def test_common_mode_generic_kernel_bitwise(cuda_device, det, monkeypatch):
+    """The generic whole-wave bitonic kernel (any tile size) stays exact as well."""
+    monkeypatch.setenv("PSANA_RAY_CM_GENERIC", "1")
+    spec, consts, raw = _setup(det, 2, seed=13, gain_config="mixed")
+    cm = CommonModeParams(flags=3, thr=30.0, maxcorr=50.0, npix_min=5)
+    mask = _mask(spec)
+    cal = Calibrator(consts, cuda_device, Mode.calib, mask=mask, common_mode=cm)
+    out = cal(raw.to(cuda_device))
+    torch.cuda.synchronize()
+    ref = reference.calibrate_reference(raw.to(torch.int32), consts, mask, cal.cm)
+    _assert_equal(out, ref, f"generic cm {det}")
