@@ -8,7 +8,7 @@ timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/full/pytest_gpu.
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke(); print('SMOKE_OK')" > gpurun_out/full/smoke.log 2>&1 || exit $?
 tail -1 gpurun_out/full/smoke.log
 timeout -k 10 600 python bench/kernels.py --json-out gpurun_out/full/kernels.jsonl > gpurun_out/full/kernels.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py --steps 100 --warmup 10 --json-out gpurun_out/full/bench_n1_host.json > gpurun_out/full/bench_host.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --json-out gpurun_out/full/bench_n1_host.json > gpurun_out/full/bench_host.log 2>&1 || exit $?
 tail -1 gpurun_out/full/bench_host.log | cut -c1-200
 timeout -k 10 300 python bench.py --steps 200 --warmup 20 --source device --json-out gpurun_out/full/bench_n1_device.json > gpurun_out/full/bench_dev.log 2>&1 || exit $?
 tail -1 gpurun_out/full/bench_dev.log | cut -c1-200
