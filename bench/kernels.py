@@ -179,11 +179,20 @@ def main(argv=None):
             for ver in ("v1", "tiles"):
                 report(f"calib_image(fused,{ver}) r{rnd}", timeit(lambda: cals[ver].run(rl, il), a.iters),
                        F * (npix * 2 + nout * 4), extra)
-            for grp in (1, 4, 8):
-                os.environ["PSANA_RAY_IMAGE_GROUPS"] = str(grp)
-                report(f"calib_image(fused,tiles,groups={grp}) r{rnd}", timeit(lambda: cali.run(rl, il), a.iters),
-                       F * (npix * 2 + nout * 4))
-            os.environ.pop("PSANA_RAY_IMAGE_GROUPS", None)
+            for blk in ("256", "512"):
+                os.environ["PSANA_RAY_IMAGE_BLOCK"] = blk
+                for grp in (2, 4, 8):
+                    os.environ["PSANA_RAY_IMAGE_GROUPS"] = str(grp)
+                    report(f"calib_image(fused,tiles,block={blk},groups={grp}) r{rnd}",
+                           timeit(lambda: cali.run(rl, il), a.iters), F * (npix * 2 + nout * 4))
+                os.environ.pop("PSANA_RAY_IMAGE_GROUPS", None)
+                report(f"assemble(tiles,block={blk}) r{rnd}",
+                       timeit(lambda: C.image_tiles(op, ip, False, spec.kernel_kind, 0, 0, npix, spec.panel_rows,
+                                                    spec.panel_cols, int(cali._tiles.data_ptr()), tm.n_tiles,
+                                                    tm.tiles_x, int(cali._codes.data_ptr()), tm.image_shape[0],
+                                                    tm.image_shape[1], _ext.stream_handle()), a.iters),
+                       F * (npix * 4 + nout * 4))
+            os.environ.pop("PSANA_RAY_IMAGE_BLOCK", None)
             report(f"assemble(v1) r{rnd}", timeit(lambda: kernels.assemble(ol, il, cali.idx, npix), a.iters),
                    F * (npix * 4 + nout * 4))
             report(f"assemble(tiles) r{rnd}",

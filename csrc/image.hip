@@ -53,16 +53,16 @@ __device__ __forceinline__ float img_pick(const float (&t)[NT], int c) {
 
 // CALIB = true: in = raw u16 frames, calibrate (K-01/02/04) while staging.
 // CALIB = false: in = calibrated f32 frames (after common mode), pure assembly.
-template <int KIND, bool CALIB>
-__global__ __launch_bounds__(256) void image_tile_kernel(const FramePtrs fp, const int f0, const int f1,
+template <int KIND, bool CALIB, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void image_tile_kernel(const FramePtrs fp, const int f0, const int f1,
                                                          const float* __restrict__ ped,
                                                          const float* __restrict__ gf,
                                                          const int32_t* __restrict__ tiles,   // [n][8]
                                                          const int32_t* __restrict__ codes,   // [img_h*img_w]
                                                          const ImgGeom g) {
   constexpr int NT = ImgTraits<KIND>::NT;
-  constexpr int SJ = kImgStage / 256;            // staged pixels per thread
-  constexpr int OK = kImgTH * kImgTW / 256;      // output pixels per thread
+  constexpr int SJ = kImgStage / BLOCK;            // staged pixels per thread
+  constexpr int OK = kImgTH * kImgTW / BLOCK;      // output pixels per thread
   __shared__ float stage[kImgLds];
 
   const int t = blockIdx.x;
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void image_tile_kernel(const FramePtrs fp, con
   float p[SJ][NT], q[SJ][NT];
 #pragma unroll
   for (int j = 0; j < SJ; ++j) {
-    const int i = tid + 256 * j;
+    const int i = tid + BLOCK * j;
     src[j] = -1;
     lds[j] = 0;
     if (panel >= 0 && i < bh * bw) {
@@ -99,12 +99,12 @@ __global__ __launch_bounds__(256) void image_tile_kernel(const FramePtrs fp, con
   // consecutive columns of one row, so stores are 256-B contiguous
   const int oy0 = ty0 + (tid >> 6), ox = tx0 + (tid & 63);
   const int64_t obase = (int64_t)oy0 * g.img_w + ox;
-  const int64_t ostep = (int64_t)(256 / kImgTW) * g.img_w;
+  const int64_t ostep = (int64_t)(BLOCK / kImgTW) * g.img_w;
   int32_t code[OK];
   unsigned valid_mask = 0;
 #pragma unroll
   for (int k = 0; k < OK; ++k) {
-    const bool in = ox < g.img_w && oy0 + (256 / kImgTW) * k < g.img_h;
+    const bool in = ox < g.img_w && oy0 + (BLOCK / kImgTW) * k < g.img_h;
     valid_mask |= (unsigned)in << k;
     code[k] = in ? codes[obase + k * ostep] : -1;
   }
@@ -196,7 +196,17 @@ void launch_image_tiles(const FramePtrs& fp, int nframes, bool calib, int kind, 
   const float* G = reinterpret_cast<const float*>(gf);
   const int32_t* T = reinterpret_cast<const int32_t*>(tiles);
   const int32_t* Cd = reinterpret_cast<const int32_t*>(codes);
-#define PR_IMG(K, CAL) hipLaunchKernelGGL((image_tile_kernel<K, CAL>), grid, dim3(256), 0, s, fp, 0, nframes, P, G, T, Cd, g)
+  // 512-thread blocks: half the per-thread staged pixels / codes (fewer VGPRs, more waves in flight);
+  // PSANA_RAY_IMAGE_BLOCK=256 for A/B
+  int block = 512;
+  if (const char* e = getenv("PSANA_RAY_IMAGE_BLOCK"); e && *e) block = atoi(e) == 256 ? 256 : 512;
+#define PR_IMG(K, CAL)                                                                                         \
+  do {                                                                                                         \
+    if (block == 512)                                                                                          \
+      hipLaunchKernelGGL((image_tile_kernel<K, CAL, 512>), grid, dim3(512), 0, s, fp, 0, nframes, P, G, T, Cd, g); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((image_tile_kernel<K, CAL, 256>), grid, dim3(256), 0, s, fp, 0, nframes, P, G, T, Cd, g); \
+  } while (0)
   if (calib) {
     switch (kind) {
       case kEpix10ka: PR_IMG(kEpix10ka, true); break;

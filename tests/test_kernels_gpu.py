@@ -91,17 +91,18 @@ def test_common_mode_even_odd_and_empty_segments(cuda_device):
     _assert_equal(out, ref, "cm edge cases")
 
 
-@pytest.mark.parametrize("version", ["tiles", "v1"])
+@pytest.mark.parametrize("version", ["tiles", "tiles256", "v1"])
 @pytest.mark.parametrize("det,cm", [("tiny_epix", None), ("tiny_epix", "3,30,50,5"), ("epix10k2M", None),
                                     ("epix10k2M", "default"), ("tiny_jungfrau", None), ("jungfrau05M", None),
                                     ("tiny_plain", None)])
 def test_image_mode_matches_scatter(cuda_device, det, cm, version, monkeypatch):
     monkeypatch.setenv("PSANA_RAY_IMAGE_V1", "1" if version == "v1" else "0")
+    monkeypatch.setenv("PSANA_RAY_IMAGE_BLOCK", "256" if version == "tiles256" else "")
     n = 2 if det in ("epix10k2M", "jungfrau05M") else 37   # 37 > 32: launch chunking
     spec, consts, raw = _setup(det, n, seed=21)
     cmp = CommonModeParams.parse(cm)
     cal = Calibrator(consts, cuda_device, Mode.image, common_mode=cmp)
-    assert (cal.tile_map is not None) == (version == "tiles")
+    assert (cal.tile_map is not None) == (version != "v1")
     out = cal(raw.to(cuda_device))
     torch.cuda.synchronize()
     geo = cal.geometry
