@@ -95,6 +95,10 @@ def main(argv=None):
     comm = None
     coord = None
     if world > 1:
+        # single-node contract (rendezvous on 127.0.0.1): keep gloo's control traffic on loopback
+        # instead of whatever interface the container hostname resolves to (or fails to)
+        if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost") and os.path.isdir("/sys/class/net/lo"):
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         comm = init_groups(rank, world, device)
         coord = dist.new_group(backend="gloo")
     elif args.loopback:
