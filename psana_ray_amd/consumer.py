@@ -86,30 +86,36 @@ def main(argv=None) -> int:
                     items = reader.read_batch(args.batch, timeout=1.0)
                     if not items:
                         continue
-                    shape = tuple(items[0].data.shape)
-                    dev = items[0].data.device
+                    meta_items = [(it.rank, it.idx, it.gevt) for it in items]
+                    if reader.calibrator is not None:    # raw ring (--calibrate_on_read): calibrate here
+                        frames = reader.calibrate(items)
+                    else:
+                        frames = [it.data for it in items]
+                    shape = tuple(frames[0].shape)
+                    dev = frames[0].device
                     F = len(items)
                     if dev.type == "cuda":
                         pk = torch.empty((F, params.max_peaks, 8), dtype=torch.float32, device=dev)
                         cnt = torch.zeros(F, dtype=torch.int32, device=dev)
                         sm = torch.zeros((F, 2), dtype=torch.float32, device=dev)
-                        kernels.peakfind([it.data for it in items], shape, params, pk, cnt, sm)
+                        kernels.peakfind([frames[i] for i in range(F)], shape, params, pk, cnt, sm)
                         cnt_h = cnt.cpu()
                         for i, it in enumerate(items):
                             k = min(int(cnt_h[i]), params.max_peaks)
                             peaks_total += k
                             if args.out:
-                                records.append((it.rank, it.idx, it.gevt, pk[i, :k].cpu().numpy()))
+                                records.append((*meta_items[i], pk[i, :k].cpu().numpy()))
                     else:
                         from .ops import reference
 
-                        pl, _ = reference.peakfind_reference(torch.stack([it.data for it in items]), params)
-                        for it, p in zip(items, pl):
+                        pl, _ = reference.peakfind_reference(torch.stack([frames[i] for i in range(F)]), params)
+                        for m, p in zip(meta_items, pl):
                             peaks_total += p.shape[0]
                             if args.out:
-                                records.append((it.rank, it.idx, it.gevt, p.numpy()))
-                    for it in items:
-                        it.release()
+                                records.append((*m, p.numpy()))
+                    if reader.calibrator is None:
+                        for it in items:
+                            it.release()
                     n += F
                 else:
                     result = reader.read(timeout=1.0)

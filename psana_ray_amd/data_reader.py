@@ -115,9 +115,50 @@ class DataReader:
                            max_offer=int(meta.extra.get("max_offer", 64)), is_producer=False, is_consumer=True)
         ep.start()
         self._sess, self._comm, self._queue = sess, comm, ep
+        recipe = meta.extra.get("calibrate_on_read")
+        if recipe:
+            self._calibrator = self._make_calibrator(recipe, device)
         self.consumer_id = sess.role_index
         log.info("consumer %d joined queue %s/%s as rank %d of %d on %s (%d slots)", sess.role_index,
                  self.ray_namespace, self.queue_name, sess.rank, sess.world, device, slots)
+
+    @staticmethod
+    def _make_calibrator(recipe: dict, device):
+        """Rebuild the producer's calibration from the session recipe (--calibrate_on_read)."""
+        from .config import CommonModeParams
+        from .models.calibrator import Calibrator
+        from .models.detector import Mode
+        from .producer import load_masks
+        from .source import open_source
+
+        src = open_source(recipe["exp"], int(recipe["run"]), recipe["detector_name"], rank=0, size=1, pinned=False,
+                          pool_frames=1, data_dir=recipe.get("data_dir"))
+        if getattr(src, "calibrated", False) or not hasattr(src, "consts"):
+            raise DataReaderError("calibrate_on_read: the producer's source has no calibration constants here")
+        mask = load_masks(src, recipe.get("uses_bad_pixel_mask", False), recipe.get("manual_mask_path"))
+        cm = recipe.get("common_mode")
+        cm = None if cm is None else CommonModeParams(int(cm[0]), float(cm[1]), float(cm[2]), int(cm[3]),
+                                                      None if cm[4] is None else int(cm[4]))
+        return Calibrator(src.consts, device, Mode(recipe["mode"]), mask=mask, common_mode=cm)
+
+    @property
+    def calibrator(self):
+        """The consumer-side Calibrator when the producer used --calibrate_on_read, else None."""
+        return getattr(self, "_calibrator", None)
+
+    def calibrate(self, items: List[FrameItem], release: bool = True, stream=None) -> torch.Tensor:
+        """Calibrate leased RAW items (``--calibrate_on_read`` queues) into a new
+        ``[n, *out_shape]`` tensor on this reader's device; releases the items by default."""
+        cal = self.calibrator
+        if cal is None:
+            raise DataReaderError("calibrate(): the queue carries calibrated frames already")
+        out = torch.empty((len(items), *cal.out_shape), dtype=cal.out_dtype, device=cal.device)
+        if items:
+            cal.run([it.data for it in items], [out[i] for i in range(len(items))], stream)
+            if release:
+                for it in items:
+                    it.release(stream)
+        return out
 
     # ------------------------------------------------------------------------------------
     @property
@@ -133,7 +174,8 @@ class DataReader:
             raise RuntimeError("DataReader is not connected. Call connect() first.")   # data_reader.py:33
 
     def lease(self, timeout: float = 0.0, stream=None) -> Optional[FrameItem]:
-        """Zero-copy: the next frame as a leased HBM slot (release it, or use ``with``)."""
+        """Zero-copy: the next frame as a leased HBM slot (release it, or use ``with``).  With a
+        ``--calibrate_on_read`` producer the slot holds the RAW frame: see :meth:`calibrate`."""
         self._check()
         if self._local is not None:
             raise DataReaderError("lease() needs the distributed HBM queue")
@@ -159,7 +201,11 @@ class DataReader:
         it = self.lease(timeout)
         if it is None:
             return None
-        rank, idx, data, pe = it.to_list(copy=True)
+        if self.calibrator is not None:   # raw ring: calibrate on read (capacity tier)
+            data = self.calibrate([it])[0]
+            rank, idx, pe = it.rank, it.idx, it.photon_energy
+        else:
+            rank, idx, data, pe = it.to_list(copy=True)
         if self.as_numpy:
             data = data.cpu().numpy()
         return [rank, idx, data, pe]

@@ -67,6 +67,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--producer_slots", type=int, default=64, help="calibrated frames a rank may hold un-routed")
     g.add_argument("--hbm_fraction", type=float, default=0.8, help="cap of free HBM used for ring slots")
     g.add_argument("--timeout", type=float, default=300.0, help="rendezvous / peer timeout in seconds")
+    g.add_argument("--calibrate_on_read", action="store_true",
+                   help="capacity tier: the ring holds RAW u16 frames (half the HBM and xGMI bytes of f32); "
+                        "consumers calibrate on read with the same constants / mode / masks / common mode")
     g.add_argument("--start_event", type=int, default=0,
                    help="resume: first global event id to produce (frames carry gevt, so consumers can dedupe)")
     g.add_argument("--metrics_interval", type=float, default=10.0,
@@ -127,6 +130,15 @@ def load_masks(source, uses_bad_pixel_mask: bool, manual_mask_path: Optional[str
     return mask
 
 
+def _read_recipe(args, read_mode, read_cm) -> dict:
+    """What a consumer needs to reproduce this producer's calibration (--calibrate_on_read)."""
+    return {"exp": args.exp, "run": args.run, "detector_name": args.detector_name, "mode": read_mode.value,
+            "common_mode": None if read_cm is None else [read_cm.flags, read_cm.thr, read_cm.maxcorr,
+                                                          read_cm.npix_min, read_cm.bank_cols],
+            "uses_bad_pixel_mask": bool(args.uses_bad_pixel_mask), "manual_mask_path": args.manual_mask_path,
+            "data_dir": args.data_dir}
+
+
 def produce_data(pipeline, max_steps=None, stop=None):
     """Run one rank's producer pipeline (producer.py:78-130); returns frames produced."""
     from .queue.endpoint import QueueClosed, QueuePeerError
@@ -173,6 +185,13 @@ def main(argv=None) -> int:
     signal.signal(signal.SIGINT, signal_handler)
 
     mode = Mode(args.mode) if args.mode else (Mode.calib if args.calib else Mode.image)   # producer.py:156-159
+    read_mode = mode
+    if args.calibrate_on_read:
+        if args.local or args.consumer_task != "none":
+            log.error("--calibrate_on_read needs separate consumers (DataReader); it does not apply to --local "
+                      "or a co-located --consumer_task")
+            return 2
+        mode = Mode.raw   # frames travel raw; DataReader applies read_mode
     source = open_source(args.exp, args.run, args.detector_name, rank=rank, size=size, n_events=args.num_events,
                          pinned=device.type == "cuda", data_dir=args.data_dir)
     if args.start_event:
@@ -183,6 +202,7 @@ def main(argv=None) -> int:
         log.info("Rank %d: resuming at global event %d (local index %d)", rank, args.start_event, k0)
     mask = load_masks(source, args.uses_bad_pixel_mask, args.manual_mask_path)
     cm = CommonModeParams.parse(args.common_mode) if mode != Mode.raw else None
+    read_cm = CommonModeParams.parse(args.common_mode) if (args.calibrate_on_read and read_mode != Mode.raw) else None
     calibrator = Calibrator(source.consts, device, mode, mask=mask, common_mode=cm) \
         if not getattr(source, "calibrated", False) else None
     frame_shape = calibrator.out_shape if calibrator else tuple(source.spec.frame_shape)
@@ -206,7 +226,9 @@ def main(argv=None) -> int:
             n_consumer_ranks = args.num_consumers
             sess = initialize_queue(args.ray_address, args.ray_namespace, args.queue_name, args.queue_size, rank,
                                     size, n_consumer_ranks, frame_shape, dtype, device.type,
-                                    extra={"route": args.route, "co_consumers": co_consumer},
+                                    extra={"route": args.route, "co_consumers": co_consumer,
+                                           "calibrate_on_read": _read_recipe(args, read_mode, read_cm)
+                                           if args.calibrate_on_read else None},
                                     timeout_s=args.timeout)
             if sess is None:
                 return 1

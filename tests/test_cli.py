@@ -113,3 +113,30 @@ def test_cli_end_to_end_cpu(native, tmp_path, n_prod, n_cons):
     assert len(processed) == n_events
     for l in processed:
         assert "shape=(2, 32, 48)" in l
+
+
+def test_calibrate_on_read_cpu(native):
+    """Capacity tier: the producer queues RAW frames (--calibrate_on_read) and the DataReader
+    calibrates them on read with the same constants, mask and common mode."""
+    port = random.randint(30000, 45000)
+    addr = f"127.0.0.1:{port}"
+    n_events = 10
+    prod = subprocess.Popen(
+        [sys.executable, "-m", "psana_ray_amd.producer", "--exp", "synthetic", "--run", "4", "--detector_name",
+         "tiny_epix", "--calib", "--num_events", str(n_events), "--ray_address", addr, "--num_consumers", "1",
+         "--queue_size", "4", "--device", "cpu", "--uses_bad_pixel_mask", "--common_mode", "default",
+         "--calibrate_on_read", "--timeout", "60"],
+        env=_env({"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"}), stdout=subprocess.PIPE,
+        stderr=subprocess.STDOUT, text=True)
+    cons = subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_cor_consumer.py"), addr, "1", "tiny_epix",
+                             "4"], env=_env(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        pout, _ = prod.communicate(timeout=180)
+        cout, _ = cons.communicate(timeout=180)
+    finally:
+        for p in (prod, cons):
+            if p.poll() is None:
+                p.kill()
+    assert prod.returncode == 0, pout[-3000:]
+    assert cons.returncode == 0, cout[-3000:]
+    assert f"COR_OK {n_events}" in cout
