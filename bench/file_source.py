@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Raw-run file source throughput: file (page cache / tmpfs) -> native pread thread pool -> pinned
+staging -> H2D -> calibration + common mode -> shared queue -> on-GPU peak finder, one GPU.
+
+The reference reads XTC2 through psana's C++ reader; here the whole per-chunk loop is the native
+producer engine (csrc/engine.cpp, set_file_source).  Prints one JSON line."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=512)
+    ap.add_argument("--dir", default="/dev/shm/psana_ray_file_bench")
+    ap.add_argument("--detector", default="epix10k2M")
+    ap.add_argument("--threads", type=int, default=8, help="reader pread threads")
+    ap.add_argument("--chunk", type=int, default=32)
+    ap.add_argument("--common-mode", default="default")
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from psana_ray_amd.config import CommonModeParams, PeakFinderParams
+    from psana_ray_amd.models import Calibrator, Mode
+    from psana_ray_amd.pipeline import PeakFinderConsumer, ProducerPipeline
+    from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
+    from psana_ray_amd.source import RawFileRun, make_synthetic_run
+
+    dev = torch.device("cuda:0")
+    shutil.rmtree(a.dir, ignore_errors=True)
+    try:
+        path = make_synthetic_run(a.dir, "bench", 1, a.detector, n_events=a.frames, chunk=32)
+        src = RawFileRun(path, a.detector, exp="bench", run=1, n_threads=a.threads, pinned=False)
+        cal = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams.parse(a.common_mode))
+        ring = FrameRing(cal.out_shape, cal.out_dtype, dev, 4 * a.chunk + 32, 400)
+        ep = QueueEndpoint(ring)
+        prod = ProducerPipeline(src, cal, ep, chunk=a.chunk)
+        cons = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=32)
+        t0 = time.perf_counter()
+        th = threading.Thread(target=prod.run, daemon=True)
+        th.start()
+        n = 0
+        while True:
+            try:
+                n += cons.poll(timeout=0.05)
+            except EndOfStream:
+                break
+        peaks = cons.synchronize()
+        dt = time.perf_counter() - t0
+        th.join()
+        st = prod.engine.timing() if prod.engine is not None else None
+        print(json.dumps({"bench": "raw-run file source, 1 GPU", "detector": a.detector, "frames": n,
+                          "seconds": round(dt, 4), "frames_per_s": round(n / dt, 1),
+                          "GB_per_s_raw": round(n * src.spec.raw_frame_bytes / dt / 1e9, 2),
+                          "native_engine": prod.engine is not None, "reader_threads": a.threads, "peaks": peaks,
+                          "engine_host_s_stage_acquire_launch_commit_total": st}))
+    finally:
+        shutil.rmtree(a.dir, ignore_errors=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -101,6 +101,7 @@ ProducerEngine::~ProducerEngine() {
   for (auto e : buf_free_) (void)hipEventDestroy(e);
   for (auto e : h2d_done_) (void)hipEventDestroy(e);
   if (raw_bufs_) (void)hipFree(raw_bufs_);
+  if (file_staging_) (void)hipHostFree(file_staging_);
   if (h2d_) (void)hipStreamDestroy(h2d_);
   if (compute_) (void)hipStreamDestroy(compute_);
 }
@@ -125,8 +126,24 @@ void ProducerEngine::set_cycled_source(const std::vector<uint64_t>& frames, cons
   device_resident_ = all_dev;
 }
 
+void ProducerEngine::set_file_source(RawRunReader* reader) {
+  check(!running_.load(), "ProducerEngine: cannot change the source while running");
+  check(reader != nullptr, "ProducerEngine: null reader");
+  check(reader->frame_bytes() == plan_.raw_frame_bytes, "ProducerEngine: file frame size != detector raw frame");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  if (file_staging_ == nullptr)
+    hip_check(hipHostMalloc(&file_staging_, (size_t)n_raw_bufs_ * chunk_ * plan_.raw_frame_bytes, hipHostMallocDefault),
+              "hipHostMalloc file staging");
+  file_ = reader;
+  device_resident_ = false;
+  src_frames_.assign(1, 0);     // non-empty marker; the cycled pool is not used
+  src_pe_.assign(1, 0.0);
+  buf_meta_.assign(n_raw_bufs_, {});
+}
+
 void ProducerEngine::start(int64_t n_local_events, int64_t max_steps, int64_t k0) {
-  check(!src_frames_.empty(), "ProducerEngine: no source");
+  check(!src_frames_.empty() || file_ != nullptr, "ProducerEngine: no source");
+  if (file_ != nullptr) check(n_local_events >= 0, "ProducerEngine: a file source needs its event count");
   check(k0 >= 0, "ProducerEngine: negative start event");
   check(!running_.load() && !thread_.joinable(), "ProducerEngine: already started");
   stop_.store(false);
@@ -174,6 +191,28 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
     // chunk c waits for slots / launches, so the copy engine never runs dry behind host work
     auto stage = [&](int64_t k0, int n, int b) {
       char* buf = static_cast<char*>(raw_bufs_) + (size_t)b * chunk_ * plan_.raw_frame_bytes;
+      if (file_ != nullptr) {
+        // staging region b is rewritten only after its previous H2D copy finished (host wait; with
+        // n_raw_bufs regions it is n_raw_bufs chunks old by now)
+        char* stg = static_cast<char*>(file_staging_) + (size_t)b * chunk_ * plan_.raw_frame_bytes;
+        if (used[b]) hip_check(hipEventSynchronize(h2d_done_[b]), "wait staging free");
+        std::vector<int64_t> ev(n);
+        std::vector<uint64_t> dst(n);
+        for (int i = 0; i < n; ++i) {
+          ev[i] = rank_ + (k0 + i) * size_;
+          dst[i] = reinterpret_cast<uint64_t>(stg) + (uint64_t)i * plan_.raw_frame_bytes;
+        }
+        {
+          trace::Range r("producer.file_read");
+          buf_meta_[b] = file_->read(ev, dst);   // native pread thread pool
+        }
+        if (used[b]) hip_check(hipStreamWaitEvent(h2d_, buf_free_[b], 0), "wait buf free");
+        used[b] = 1;
+        hip_check(hipMemcpyAsync(buf, stg, (size_t)n * plan_.raw_frame_bytes, hipMemcpyHostToDevice, h2d_),
+                  "stage copy");
+        hip_check(hipEventRecord(h2d_done_[b], h2d_), "record h2d");
+        return;
+      }
       if (used[b]) hip_check(hipStreamWaitEvent(h2d_, buf_free_[b], 0), "wait buf free");
       used[b] = 1;
       int i = 0;
@@ -247,8 +286,13 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       for (int q = 0; q < n; ++q) {
         hdrs[q].rank = rank_;
         hdrs[q].idx = k + q;
-        hdrs[q].gevt = rank_ + (k + q) * size_;
-        hdrs[q].photon_energy = src_pe_[(k + q) % src_pe_.size()];
+        if (file_ != nullptr) {
+          hdrs[q].gevt = buf_meta_[b][q].first;
+          hdrs[q].photon_energy = buf_meta_[b][q].second;
+        } else {
+          hdrs[q].gevt = rank_ + (k + q) * size_;
+          hdrs[q].photon_energy = src_pe_[(k + q) % src_pe_.size()];
+        }
       }
       pool_->commit_batch(slots, hdrs, stream_c);   // one ready event for the whole chunk
       t_commit_ += secs(t3, clk::now());

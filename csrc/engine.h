@@ -65,6 +65,10 @@ class ProducerEngine {
 
   // cycled source: frame k of this rank reads host_frames[k % n] (pinned host or device memory)
   void set_cycled_source(const std::vector<uint64_t>& frames, const std::vector<double>& photon_energy);
+  // raw-run file source: rank-local event k is file record rank + k*size, read by the native
+  // thread pool into pinned staging (one region per raw buffer) while the previous chunk's
+  // H2D copy runs; (gevt, photon energy) come from the records.  The reader must outlive the run.
+  void set_file_source(RawRunReader* reader);
   bool device_resident() const { return device_resident_; }
   // rank-local events [k0, n_local_events) (n_local_events < 0: endless), at most max_steps of them
   void start(int64_t n_local_events, int64_t max_steps, int64_t k0 = 0);
@@ -91,6 +95,9 @@ class ProducerEngine {
   std::vector<uint64_t> src_frames_;
   std::vector<double> src_pe_;
   bool device_resident_ = false;   // source frames live in this GPU's HBM: no staging copies
+  RawRunReader* file_ = nullptr;   // file source (instead of the cycled pool)
+  void* file_staging_ = nullptr;   // pinned, n_raw_bufs x chunk frames
+  std::vector<std::vector<std::pair<int64_t, double>>> buf_meta_;   // per raw buffer: (gevt, pe)
   hipStream_t h2d_ = nullptr, compute_ = nullptr;
   std::vector<hipEvent_t> buf_free_, h2d_done_;
   void* raw_bufs_ = nullptr;

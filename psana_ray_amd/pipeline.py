@@ -51,7 +51,9 @@ class ProducerPipeline:
         self.t_first = None
         self.calibrated_source = getattr(source, "calibrated", False)
         spec = getattr(source, "spec", None)
-        use_engine = self.gpu and not self.calibrated_source and hasattr(source, "cycled_frames")
+        file_source = getattr(source, "reader", None)   # RawFileRun: native RawRunReader
+        use_engine = self.gpu and not self.calibrated_source and (hasattr(source, "cycled_frames")
+                                                                  or file_source is not None)
         if self.gpu and not self.calibrated_source and not use_engine:
             _ext.load()
             self.h2d = torch.cuda.Stream(device=self.device)
@@ -68,14 +70,17 @@ class ProducerPipeline:
         if use_engine:
             # native hot loop: no Python (and no GIL) per frame or per chunk
             C = _ext.load()
-            ptrs, pe = source.cycled_frames()
             ring = endpoint.ring
             dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
             self.engine = C.ProducerEngine(ring.pool, int(ring.storage.data_ptr()), ring.frame_bytes, dev_index,
                                            calibrator.plan, self.chunk, n_raw_buffers, int(rank),
                                            int(getattr(source, "size", 1)))
-            self.engine.set_cycled_source([int(x) for x in ptrs],
-                                          [float("nan") if v is None else float(v) for v in pe])
+            if file_source is not None:
+                self.engine.set_file_source(file_source)    # file reads + staging in the native loop
+            else:
+                ptrs, pe = source.cycled_frames()
+                self.engine.set_cycled_source([int(x) for x in ptrs],
+                                              [float("nan") if v is None else float(v) for v in pe])
 
     # --------------------------------------------------------------------------------
     def _acquire(self, n: int, stream) -> List[int]:
