@@ -22,9 +22,10 @@ def main(argv=None):
     ap.add_argument("--frames", type=int, default=512)
     ap.add_argument("--dir", default="/dev/shm/psana_ray_file_bench")
     ap.add_argument("--detector", default="epix10k2M")
-    ap.add_argument("--threads", type=int, default=8, help="reader pread threads")
+    ap.add_argument("--threads", type=int, default=16, help="reader pread threads")
     ap.add_argument("--chunk", type=int, default=32)
     ap.add_argument("--common-mode", default="default")
+    ap.add_argument("--no-numa", action="store_true", help="do not bind to the GPU's NUMA node")
     a = ap.parse_args(argv)
 
     import torch
@@ -35,7 +36,10 @@ def main(argv=None):
     from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
     from psana_ray_amd.source import RawFileRun, make_synthetic_run
 
+    from psana_ray_amd.parallel.launch import bind_numa_to_device
+
     dev = torch.device("cuda:0")
+    numa = None if a.no_numa else bind_numa_to_device(dev)
     shutil.rmtree(a.dir, ignore_errors=True)
     try:
         path = make_synthetic_run(a.dir, "bench", 1, a.detector, n_events=a.frames, chunk=32)
@@ -61,7 +65,7 @@ def main(argv=None):
         print(json.dumps({"bench": "raw-run file source, 1 GPU", "detector": a.detector, "frames": n,
                           "seconds": round(dt, 4), "frames_per_s": round(n / dt, 1),
                           "GB_per_s_raw": round(n * src.spec.raw_frame_bytes / dt / 1e9, 2),
-                          "native_engine": prod.engine is not None, "reader_threads": a.threads, "peaks": peaks,
+                          "native_engine": prod.engine is not None, "reader_threads": a.threads, "peaks": peaks, "numa": numa,
                           "engine_host_s_stage_acquire_launch_commit_total": st}))
     finally:
         shutil.rmtree(a.dir, ignore_errors=True)

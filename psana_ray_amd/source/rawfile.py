@@ -67,7 +67,7 @@ class RawFileRun:
     its H2D copy completed -- the producer pipeline waits on the copy event)."""
 
     def __init__(self, path, detector_name: str, exp: str = "file", run: int = 0, rank: int = 0, size: int = 1,
-                 staging: int = 64, n_threads: int = 4, pinned: bool = True, n_events: Optional[int] = None):
+                 staging: int = 64, n_threads: int = 16, pinned: bool = True, n_events: Optional[int] = None):
         from ..ops import _ext
 
         C = _ext.load()
