@@ -38,7 +38,9 @@ def parse(argv=None):
     ap.add_argument("--common-mode", default="default", help="off | default | flags,thr,maxcorr,npix_min[,bank]")
     ap.add_argument("--consumer", default="peakfind", choices=["peakfind", "none"])
     ap.add_argument("--route", default="balanced", choices=["balanced", "local_first", "spread"])
-    ap.add_argument("--queue-size", type=int, default=400, help="logical queue capacity (README.md:20 example)")
+    ap.add_argument("--queue-size", type=int, default=None,
+                    help="logical (global) queue capacity; default 400 per GPU (README.md:20 example, weak scaling: "
+                         "constant queue depth per consumer shard). BASELINE config 3: --gpus 8 --queue-size 400")
     ap.add_argument("--source", default="host", choices=["host", "device"],
                     help="host: pinned host pool + H2D (real pipeline); device: raw frames already in HBM")
     ap.add_argument("--chunk", type=int, default=32,
@@ -125,6 +127,8 @@ def main(argv=None):
                        pool_frames=args.pool_frames if is_prod else 1,
                        pinned=(args.source == "host" and gpu and is_prod), gen_device=str(device))
     cal = Calibrator(src.consts, device, mode, common_mode=cm)
+    if args.queue_size is None:
+        args.queue_size = 400 * world
     share = max(1, math.ceil(args.queue_size / world))
     # slack for frames waiting to be routed / in flight over xGMI (a round can hold max_offer frames)
     producer_slots = (4 * args.chunk + args.batch + (64 if comm is not None else 0)) if is_prod else 1
