@@ -288,6 +288,9 @@ def main(argv=None):
             "producer_host_s_stage_acquire_launch_commit_total": (
                 [round(x, 4) for x in prod.engine.timing()] if prod is not None and prod.engine is not None
                 else None),
+            "producer_gpu_ms_h2d_chunks_calib_chunks": (
+                [round(x, 3) for x in prod.engine.gpu_timing()]
+                if prod is not None and prod.engine is not None and prod.engine.gpu_timing_enabled else None),
         },
     }
     if rank == 0:

@@ -311,7 +311,9 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("frames", &pr::ProducerEngine::frames)
       .def_property_readonly("full_waits", &pr::ProducerEngine::full_waits)
       .def("error", &pr::ProducerEngine::error)
-      .def("timing", &pr::ProducerEngine::timing);
+      .def("timing", &pr::ProducerEngine::timing)
+      .def("gpu_timing", &pr::ProducerEngine::gpu_timing)
+      .def_property_readonly("gpu_timing_enabled", &pr::ProducerEngine::gpu_timing_enabled);
 
   py::class_<pr::RawRunReader>(m, "RawRunReader")
       .def(py::init<const std::string&, int>(), py::arg("path"), py::arg("n_threads") = 4)

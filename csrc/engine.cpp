@@ -82,11 +82,23 @@ ProducerEngine::ProducerEngine(SlotPool* pool, uint64_t ring_base, int64_t slot_
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
   hip_check(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate");
+  if (const char* e = getenv("PSANA_RAY_ENGINE_GPU_TIMING"); e && e[0] == '1') gpu_timing_ = true;
+  const unsigned ev_flags = gpu_timing_ ? hipEventDefault : hipEventDisableTiming;
   buf_free_.resize(n_raw_bufs_);
   h2d_done_.resize(n_raw_bufs_);
   for (int i = 0; i < n_raw_bufs_; ++i) {
-    hip_check(hipEventCreateWithFlags(&buf_free_[i], hipEventDisableTiming), "hipEventCreate");
-    hip_check(hipEventCreateWithFlags(&h2d_done_[i], hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&buf_free_[i], ev_flags), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&h2d_done_[i], ev_flags), "hipEventCreate");
+  }
+  if (gpu_timing_) {
+    h2d_start_.resize(n_raw_bufs_);
+    calib_start_.resize(n_raw_bufs_);
+    for (int i = 0; i < n_raw_bufs_; ++i) {
+      hip_check(hipEventCreate(&h2d_start_[i]), "hipEventCreate");
+      hip_check(hipEventCreate(&calib_start_[i]), "hipEventCreate");
+    }
+    h2d_pending_.assign(n_raw_bufs_, 0);
+    calib_pending_.assign(n_raw_bufs_, 0);
   }
   hip_check(hipMalloc(&raw_bufs_, (size_t)n_raw_bufs_ * chunk_ * plan.raw_frame_bytes), "hipMalloc raw chunks");
 }
@@ -100,6 +112,8 @@ ProducerEngine::~ProducerEngine() {
   if (compute_) (void)hipStreamSynchronize(compute_);
   for (auto e : buf_free_) (void)hipEventDestroy(e);
   for (auto e : h2d_done_) (void)hipEventDestroy(e);
+  for (auto e : h2d_start_) (void)hipEventDestroy(e);
+  for (auto e : calib_start_) (void)hipEventDestroy(e);
   if (raw_bufs_) (void)hipFree(raw_bufs_);
   if (file_staging_) (void)hipHostFree(file_staging_);
   if (h2d_) (void)hipStreamDestroy(h2d_);
@@ -167,6 +181,31 @@ std::vector<double> ProducerEngine::timing() const {
   return {t_stage_, t_acquire_, t_launch_, t_commit_, t_total_};
 }
 
+// Fold the finished measurements of raw buffer b into the totals (block: wait for them).
+void ProducerEngine::harvest(int b, bool block) {
+  if (!gpu_timing_) return;
+  auto take = [&](char& pending, hipEvent_t a, hipEvent_t z, double& tot, int64_t& n) {
+    if (!pending) return;
+    if (block) (void)hipEventSynchronize(z);
+    else if (hipEventQuery(z) != hipSuccess) return;   // keep pending; try again next time
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, z) == hipSuccess) {
+      std::lock_guard<std::mutex> lk(err_mu_);   // gpu_timing() reads these from another thread
+      tot += ms;
+      ++n;
+    }
+    (void)hipGetLastError();
+    pending = 0;
+  };
+  take(h2d_pending_[b], h2d_start_[b], h2d_done_[b], gpu_h2d_ms_, gpu_h2d_n_);
+  take(calib_pending_[b], calib_start_[b], buf_free_[b], gpu_calib_ms_, gpu_calib_n_);
+}
+
+std::vector<double> ProducerEngine::gpu_timing() const {
+  std::lock_guard<std::mutex> lk(err_mu_);
+  return {gpu_h2d_ms_, (double)gpu_h2d_n_, gpu_calib_ms_, (double)gpu_calib_n_};
+}
+
 std::string ProducerEngine::error() const {
   std::lock_guard<std::mutex> lk(err_mu_);
   return error_;
@@ -208,6 +247,11 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
         }
         if (used[b]) hip_check(hipStreamWaitEvent(h2d_, buf_free_[b], 0), "wait buf free");
         used[b] = 1;
+        if (gpu_timing_) {
+          harvest(b, false);
+          hip_check(hipEventRecord(h2d_start_[b], h2d_), "record h2d start");
+          h2d_pending_[b] = 1;
+        }
         hip_check(hipMemcpyAsync(buf, stg, (size_t)n * plan_.raw_frame_bytes, hipMemcpyHostToDevice, h2d_),
                   "stage copy");
         hip_check(hipEventRecord(h2d_done_[b], h2d_), "record h2d");
@@ -215,6 +259,11 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       }
       if (used[b]) hip_check(hipStreamWaitEvent(h2d_, buf_free_[b], 0), "wait buf free");
       used[b] = 1;
+      if (gpu_timing_) {
+        harvest(b, false);
+        hip_check(hipEventRecord(h2d_start_[b], h2d_), "record h2d start");
+        h2d_pending_[b] = 1;
+      }
       int i = 0;
       while (i < n) {   // coalesce host-contiguous runs into single copies
         const uint64_t s0 = src_frames_[(k0 + i) % nsrc];
@@ -275,11 +324,16 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
         for (int q = 0; q < n; ++q) in[q] = reinterpret_cast<uint64_t>(buf) + (uint64_t)q * plan_.raw_frame_bytes;
       }
       for (int q = 0; q < n; ++q) out[q] = ring_base_ + (uint64_t)slots[q] * (uint64_t)slot_bytes_;
+      if (gpu_timing_) {
+        if (device_resident_) harvest(b, false);
+        hip_check(hipEventRecord(calib_start_[b], compute_), "record calib start");
+        calib_pending_[b] = 1;
+      }
       {
         trace::Range r("producer.launch_calib");
         run_calib_plan(plan_, in, out, stream_c);
       }
-      if (!device_resident_) hip_check(hipEventRecord(buf_free_[b], compute_), "record buf free");
+      if (!device_resident_ || gpu_timing_) hip_check(hipEventRecord(buf_free_[b], compute_), "record buf free");
       auto t3 = clk::now();
       t_launch_ += secs(t2, t3);
       hdrs.resize(n);
@@ -303,6 +357,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
     }
     hip_check(hipStreamSynchronize(compute_), "final sync");
     hip_check(hipStreamSynchronize(h2d_), "final sync");
+    for (int b = 0; b < n_raw_bufs_; ++b) harvest(b, true);
   } catch (const std::exception& e) {
     std::lock_guard<std::mutex> lk(err_mu_);
     error_ = e.what();

@@ -80,6 +80,10 @@ class ProducerEngine {
   std::string error() const;
   // host-side time (seconds) spent per loop part: [stage copies, acquire slots, launch kernels, commit, total]
   std::vector<double> timing() const;
+  // GPU-side per-stage time from timing events (PSANA_RAY_ENGINE_GPU_TIMING=1 at construction):
+  // [h2d ms total, h2d chunks measured, calib ms total, calib chunks measured]; zeros when off
+  std::vector<double> gpu_timing() const;
+  bool gpu_timing_enabled() const { return gpu_timing_; }
 
  private:
   void loop(int64_t n_local_events, int64_t max_steps, int64_t k0);
@@ -100,6 +104,14 @@ class ProducerEngine {
   std::vector<std::vector<std::pair<int64_t, double>>> buf_meta_;   // per raw buffer: (gevt, pe)
   hipStream_t h2d_ = nullptr, compute_ = nullptr;
   std::vector<hipEvent_t> buf_free_, h2d_done_;
+  // optional GPU timing: start events per raw buffer, harvested (non-blocking) when the buffer is
+  // reused or at the end of the run
+  bool gpu_timing_ = false;
+  std::vector<hipEvent_t> h2d_start_, calib_start_;
+  std::vector<char> h2d_pending_, calib_pending_;
+  double gpu_h2d_ms_ = 0, gpu_calib_ms_ = 0;
+  int64_t gpu_h2d_n_ = 0, gpu_calib_n_ = 0;
+  void harvest(int b, bool block);
   void* raw_bufs_ = nullptr;
   std::thread thread_;
   std::atomic<bool> stop_{false}, running_{false};

@@ -178,6 +178,10 @@ class ProducerPipeline:
         if self.engine is not None:
             st, acq, launch, commit, total = self.engine.timing()
             d.update(host_stage_s=st, host_acquire_s=acq, host_launch_s=launch, host_commit_s=commit)
+            if self.engine.gpu_timing_enabled:   # PSANA_RAY_ENGINE_GPU_TIMING=1: event-timed GPU stages
+                h2d_ms, h2d_n, cal_ms, cal_n = self.engine.gpu_timing()
+                d.update(gpu_h2d_ms_per_chunk=h2d_ms / max(1.0, h2d_n), gpu_calib_ms_per_chunk=cal_ms / max(1.0, cal_n),
+                         gpu_chunks_timed=cal_n)
         return d
 
     def run(self, max_steps: Optional[int] = None, stop=None) -> int:

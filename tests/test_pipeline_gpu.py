@@ -154,3 +154,20 @@ def test_file_source_native_engine(cuda_device, tmp_path):
         seen[gevt] = seen.get(gevt, 0) + 1
     t.join()
     assert sorted(seen) == list(range(5, 70)) and all(v == 1 for v in seen.values())
+
+
+def test_engine_gpu_stage_timing(cuda_device, monkeypatch):
+    """PSANA_RAY_ENGINE_GPU_TIMING=1: the engine event-times every chunk's H2D copy and calibration."""
+    monkeypatch.setenv("PSANA_RAY_ENGINE_GPU_TIMING", "1")
+    src = SyntheticRun("synthetic", 6, "epix10k2M", n_events=96, pool_frames=8, pinned=True, gen_device="cuda")
+    cal = Calibrator(src.consts, cuda_device, Mode.calib, common_mode=CommonModeParams())
+    ring = FrameRing(cal.out_shape, cal.out_dtype, cuda_device, 64, 128)
+    ep = QueueEndpoint(ring)
+    prod = ProducerPipeline(src, cal, ep, chunk=16)
+    assert prod.engine.gpu_timing_enabled
+    prod.run()
+    h2d_ms, h2d_n, cal_ms, cal_n = prod.engine.gpu_timing()
+    assert h2d_n == 6 and cal_n == 6, (h2d_n, cal_n)
+    assert h2d_ms > 0 and cal_ms > 0
+    m = prod.metrics()
+    assert m["gpu_chunks_timed"] == 6 and m["gpu_h2d_ms_per_chunk"] > 0
