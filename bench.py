@@ -283,6 +283,8 @@ def main(argv=None):
             "queue_full_waits_rank0": prod.full_waits if prod is not None else 0,
             "transport_rounds_rank0": st.get("rounds", 0),
             "transport_round_ms_rank0": round(st.get("round_ms", 0.0), 3),
+            "transport_ctrl_ms_rank0": round(st.get("ctrl_ms", 0.0), 4),
+            "transport_driver": ep.xport,
             "bytes_sent_rank0": st.get("bytes_sent", 0),
             "numa_node": numa,
             "producer_host_s_stage_acquire_launch_commit_total": (
@@ -307,6 +309,7 @@ def main(argv=None):
         wd.daemon = True
         wd.start()
         if clean:
+            ep.close()
             comm.close()
             dist.destroy_process_group()
         else:

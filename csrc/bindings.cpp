@@ -15,6 +15,7 @@ namespace py = pybind11;
 #include "kernels.h"
 #include "trace.h"
 #include "transport.h"
+#include "xport_engine.h"
 
 namespace pr {
 std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers, const std::vector<int64_t>& credits,
@@ -178,6 +179,65 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("bytes_sent", &pr::RcclTransport::bytes_sent)
       .def_property_readonly("bytes_recv", &pr::RcclTransport::bytes_recv)
       .def_property_readonly("groups", &pr::RcclTransport::groups);
+
+
+  py::class_<pr::ShmControl>(m, "ShmControl")
+      .def(py::init<const std::string&, bool, int, int, int, int64_t, double>(), py::arg("name"), py::arg("create"),
+           py::arg("rank"), py::arg("world"), py::arg("vec_words"), py::arg("outbox_bytes"), py::arg("timeout_s"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("unlink", &pr::ShmControl::unlink)
+      .def("allgather",
+           [](pr::ShmControl& c, int64_t round, const std::vector<int64_t>& vec) {
+             pr::check((int)vec.size() == c.vec_words(), "ShmControl.allgather: vector size mismatch");
+             std::vector<int64_t> out((size_t)c.world() * c.vec_words());
+             {
+               py::gil_scoped_release nogil;
+               c.allgather(round, vec.data(), out.data());
+             }
+             return out;
+           },
+           py::arg("round"), py::arg("vec"))
+      .def("set_failed", &pr::ShmControl::set_failed)
+      .def("cancel", &pr::ShmControl::cancel)
+      .def("set_check_pids", &pr::ShmControl::set_check_pids)
+      .def_property_readonly("name", &pr::ShmControl::name)
+      .def_property_readonly("rank", &pr::ShmControl::rank)
+      .def_property_readonly("world", &pr::ShmControl::world)
+      .def_property_readonly("vec_words", &pr::ShmControl::vec_words)
+      .def_property_readonly("outbox_bytes", &pr::ShmControl::outbox_bytes);
+  m.def("xport_vec_words", &pr::TransportEngine::vec_words_for, py::arg("max_offer"));
+
+  py::class_<pr::XportStats>(m, "XportStats")
+      .def_readonly("rounds", &pr::XportStats::rounds)
+      .def_readonly("idle_rounds", &pr::XportStats::idle_rounds)
+      .def_readonly("frames_routed", &pr::XportStats::frames_routed)
+      .def_readonly("frames_sent", &pr::XportStats::frames_sent)
+      .def_readonly("frames_recv", &pr::XportStats::frames_recv)
+      .def_readonly("frames_local", &pr::XportStats::frames_local)
+      .def_readonly("bytes_sent", &pr::XportStats::bytes_sent)
+      .def_readonly("bytes_recv", &pr::XportStats::bytes_recv)
+      .def_readonly("round_s", &pr::XportStats::round_s)
+      .def_readonly("ctrl_s", &pr::XportStats::ctrl_s)
+      .def_readonly("data_s", &pr::XportStats::data_s);
+
+  py::class_<pr::TransportEngine>(m, "TransportEngine")
+      .def(py::init<pr::SlotPool*, pr::ShmControl*, pr::RcclTransport*, uint64_t, int64_t, int, int,
+                    const std::vector<int>&, bool, bool, int, int, bool, uint64_t, int>(),
+           py::arg("pool"), py::arg("ctrl"), py::arg("rccl"), py::arg("ring_base"), py::arg("slot_bytes"),
+           py::arg("rank"), py::arg("world"), py::arg("producer_ranks"), py::arg("is_producer"),
+           py::arg("is_consumer"), py::arg("policy"), py::arg("max_offer"), py::arg("loopback"), py::arg("stream"),
+           py::arg("device"), py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def("start", &pr::TransportEngine::start)
+      .def("join", &pr::TransportEngine::join, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
+      .def("step", &pr::TransportEngine::step, py::call_guard<py::gil_scoped_release>())
+      .def("set_producer_finished", &pr::TransportEngine::set_producer_finished)
+      .def("set_consumer_closed", &pr::TransportEngine::set_consumer_closed)
+      .def("request_stop", &pr::TransportEngine::request_stop)
+      .def_property_readonly("done", &pr::TransportEngine::done)
+      .def_property_readonly("consumers_gone", &pr::TransportEngine::consumers_gone)
+      .def_property_readonly("running", &pr::TransportEngine::running)
+      .def("error", &pr::TransportEngine::error)
+      .def("stats", &pr::TransportEngine::stats);
 
   py::class_<pr::PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())
       .def(py::init<size_t>(), py::arg("bytes"))

@@ -235,6 +235,7 @@ class DataReader:
             if ep.comm is not None:
                 if ep.failed is not None:
                     ep.comm.abort()
+                ep.close()
                 ep.comm.close()
             try:
                 import torch.distributed as dist

@@ -25,9 +25,15 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, rank: int, world: int, ctrl_group, data_group, device: torch.device, rccl=None):
+    def __init__(self, rank: int, world: int, ctrl_group, data_group, device: torch.device, rccl=None,
+                 node_local: bool = False, token: str = ""):
         self.rank = rank
         self.world = world
+        # every rank on this host: the native transport engine (csrc/xport_engine.h) can run the
+        # control plane through shared memory instead of gloo
+        self.node_local = bool(node_local)
+        self.token = token
+        self._n_shm = 0
         self.ctrl_group = ctrl_group
         self.data_group = data_group
         self.device = torch.device(device)
@@ -49,6 +55,12 @@ class Comm:
         """GPU: one fused native transport round (see csrc/transport.h).  Returns the recv slots."""
         return self.rccl.round(pool, ring_base, slot_bytes, send_slots, send_peers, recv_peers, recv_headers,
                                self.stream_handle)
+
+    def shm_name(self) -> str:
+        """A fresh node-local segment name, identical on every rank (endpoints are created in the
+        same order on every rank of a session)."""
+        self._n_shm += 1
+        return f"/psray-{self.token}-{self._n_shm}"
 
     def check_async(self) -> None:
         if self.rccl is not None:
@@ -131,6 +143,16 @@ def init_groups(rank: int, world: int, device, store=None, master_addr: Optional
             kw["init_method"] = f"tcp://{master_addr}:{master_port}"
         dist.init_process_group("gloo", **kw)
     ctrl = dist.new_group(backend="gloo", timeout=tmo)
+    # node locality + a session token for shared-memory names (one small exchange at startup)
+    import socket
+    import uuid
+
+    here = [socket.gethostname(), _boot_id()]
+    hosts = [None] * world
+    dist.all_gather_object(hosts, here, group=ctrl)
+    tok = [uuid.uuid4().hex[:12] if rank == 0 else None]
+    dist.broadcast_object_list(tok, src=0, group=ctrl)
+    node_local = all(h == here for h in hosts)
     rccl = None
     if gpu:
         from ..ops import _ext
@@ -142,4 +164,12 @@ def init_groups(rank: int, world: int, device, store=None, master_addr: Optional
         dist.broadcast(uid, src=0, group=ctrl)
         dev_index = device.index if device.index is not None else torch.cuda.current_device()
         rccl = C.RcclTransport(bytes(uid.numpy().tobytes()), rank, world, dev_index)
-    return Comm(rank, world, ctrl, dist.group.WORLD, device, rccl=rccl)
+    return Comm(rank, world, ctrl, dist.group.WORLD, device, rccl=rccl, node_local=node_local, token=tok[0])
+
+
+def _boot_id() -> str:
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            return f.read().strip()
+    except OSError:
+        return ""

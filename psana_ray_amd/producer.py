@@ -291,8 +291,10 @@ def main(argv=None) -> int:
         if sess is not None:
             finish_session(sess)
         if comm is not None:
-            if 'ep' in locals() and ep.failed is not None:
-                comm.abort()
+            if 'ep' in locals():
+                if ep.failed is not None:
+                    comm.abort()
+                ep.close()
             comm.close()
         try:
             import torch.distributed as dist

@@ -12,15 +12,22 @@ Reference contract being replaced (psana_ray/shared_queue.py, producer.py, data_
   * a dead queue actor raised RayActorError -> DataReaderError (data_reader.py:36-37) -- here a
     failed control/data exchange (peer died) raises :class:`QueuePeerError`.
 
-Transport (world > 1): a progress thread runs rounds -- all-gather (offers, credits, headers) on
-the gloo control group, deterministic routing (parallel.routing), then one grouped RCCL
-send/recv exchange of the frames on a dedicated stream.  World == 1: frames are routed locally
-(zero copy: the calibration kernel already wrote them into the consumer's slot).
+Transport (world > 1, or loopback): rounds of all-gather (offers, credits, headers),
+deterministic routing (parallel.routing), then one grouped RCCL send/recv exchange of the frames
+on a dedicated stream.  Two drivers of those rounds:
+  * ``native`` (default when every rank is on this host): the C++ TransportEngine
+    (csrc/xport_engine.h) -- its own thread, control vectors all-gathered through a node-local
+    shared-memory segment (microseconds instead of a gloo TCP all-gather), routing and the RCCL
+    group issued without Python or the GIL; host pools copy through shared-memory outboxes;
+  * ``python``: a Python thread, gloo all-gather, same routing and data plane (multi-host, A/B).
+Select with ``xport=`` or ``PSANA_RAY_XPORT``.  World == 1: frames are routed locally (zero copy:
+the calibration kernel already wrote them into the consumer's slot).
 """
 from __future__ import annotations
 
 import logging
 import math
+import os
 import struct
 import threading
 import time
@@ -105,7 +112,7 @@ class QueueEndpoint:
     def __init__(self, ring: FrameRing, rank: int = 0, world: int = 1, comm=None,
                  producer_ranks: Optional[Sequence[int]] = None, consumer_ranks: Optional[Sequence[int]] = None,
                  route: str = "balanced", max_offer: int = 64, is_producer: bool = True, is_consumer: bool = True,
-                 loopback: bool = False):
+                 loopback: bool = False, xport: Optional[str] = None):
         self.ring = ring
         self.pool = ring.pool
         self.rank, self.world, self.comm = rank, world, comm
@@ -125,8 +132,8 @@ class QueueEndpoint:
         self._consumer_closed = not is_consumer
         self._eos_from: set = set()
         self._transport_done = comm is None and False
-        self._failed: Optional[BaseException] = None
-        self._consumers_gone = False
+        self._py_failed: Optional[BaseException] = None
+        self._py_consumers_gone = False
         self._round = 0
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
@@ -141,6 +148,59 @@ class QueueEndpoint:
         self._views = list(ring.storage.unbind(0))   # per-slot tensor views, built once
         self._base = int(ring.storage.data_ptr())
         self._slot_bytes = ring.frame_bytes
+        self._engine = None
+        self._engine_exc: Optional[BaseException] = None
+        self.xport = "local" if comm is None else self._pick_xport(xport)
+        if self.xport == "native":
+            self._make_engine()
+
+    # ------------------------------------------------------------------------ native transport
+    def _pick_xport(self, xport: Optional[str]) -> str:
+        x = (xport or os.environ.get("PSANA_RAY_XPORT", "native")).lower()
+        if x not in ("native", "python"):
+            raise ValueError(f"unknown transport driver {x!r} (native | python)")
+        if x == "native" and not getattr(self.comm, "node_local", False):
+            log.info("rank %d: ranks span hosts -> python transport driver", self.rank)
+            x = "python"
+        return x
+
+    def _make_engine(self):
+        C = _ext.load()
+        comm = self.comm
+        rccl = getattr(comm, "rccl", None)
+        tmo = float(os.environ.get("PSANA_RAY_XPORT_TIMEOUT_S", "300"))
+        # host pools move frames through per-rank shared-memory outboxes (max_offer slots each)
+        box = 0 if rccl is not None else self.max_offer * self._slot_bytes
+        name = comm.shm_name()
+        self._ctrl = C.ShmControl(name, self.rank == 0, self.rank, self.world, C.xport_vec_words(self.max_offer),
+                                  box, tmo)
+        dev = self.ring.device.index if self.gpu else -1
+        if self.gpu and dev is None:
+            dev = torch.cuda.current_device()
+        self._engine = C.TransportEngine(self.pool, self._ctrl, rccl, self._base, self._slot_bytes, self.rank,
+                                         self.world, self.producer_ranks, self.is_producer, self.is_consumer,
+                                         _POLICY_CODE[self.route], self.max_offer, self.loopback,
+                                         comm.stream_handle if rccl is not None else 0, dev)
+        if self._producer_finished:
+            self._engine.set_producer_finished()
+        if self._consumer_closed:
+            self._engine.set_consumer_closed()
+
+    @property
+    def _failed(self) -> Optional[BaseException]:
+        if self._py_failed is not None:
+            return self._py_failed
+        if self._engine is not None and self._engine_exc is None:
+            err = self._engine.error()
+            if err:
+                self._engine_exc = RuntimeError(err)
+        return self._engine_exc
+
+    @property
+    def _consumers_gone(self) -> bool:
+        if self._engine is not None:
+            return bool(self._engine.consumers_gone)
+        return self._py_consumers_gone
 
     # ------------------------------------------------------------------------ helpers
     def _stream(self, stream) -> int:
@@ -186,6 +246,8 @@ class QueueEndpoint:
     def finish(self):
         """This rank's producer has no more events (its EOS is advertised once drained)."""
         self._producer_finished = True
+        if self._engine is not None:
+            self._engine.set_producer_finished()
 
     # ------------------------------------------------------------------------ consumer
     def get(self, timeout: float = 0.0, stream=None) -> Optional[FrameItem]:
@@ -222,11 +284,15 @@ class QueueEndpoint:
 
     def close_consumer(self):
         self._consumer_closed = True
+        if self._engine is not None:
+            self._engine.set_consumer_closed()
 
     @property
     def stream_done(self) -> bool:
         if self.comm is None:
             return self._producer_finished and self.pool.n_produced() == 0
+        if self._engine is not None:
+            return bool(self._engine.done)
         return self._transport_done
 
     def size(self) -> int:
@@ -256,6 +322,8 @@ class QueueEndpoint:
 
     def step(self) -> int:
         """Run ONE transport round (collective: every rank must call it).  Returns frames moved."""
+        if self._engine is not None:
+            return int(self._engine.step())
         t0 = time.perf_counter()
         C = _ext.load()
         comm = self.comm
@@ -269,7 +337,7 @@ class QueueEndpoint:
             if flags[r] & F_EOS:
                 self._eos_from.add(r)
         consumers_alive = [r for r in range(self.world) if (flags[r] & F_CONSUMER) and not (flags[r] & F_CLOSED)]
-        self._consumers_gone = len(consumers_alive) == 0
+        self._py_consumers_gone = len(consumers_alive) == 0
         flat = C.plan_round(offer_n, credits, self._round, _POLICY_CODE[self.route])
         me = self.rank
         sh = comm.stream_handle
@@ -331,7 +399,7 @@ class QueueEndpoint:
                 else:
                     idle = 0.0
         except BaseException as e:  # noqa: BLE001 - surfaced to both roles
-            self._failed = e
+            self._py_failed = e
             log.error("rank %d: shared-queue transport failed: %r", self.rank, e)
             try:
                 self.comm.abort()   # RCCL: never leave kernels waiting on a dead peer
@@ -343,22 +411,54 @@ class QueueEndpoint:
     def start(self):
         if self.comm is None or self._thread is not None:
             return self
+        if self._engine is not None:
+            if not self._engine.running and not self._engine.done:
+                self._engine.start()
+            return self
         self._thread = threading.Thread(target=self._loop, name=f"psana-ray-transport-{self.rank}", daemon=True)
         self._thread.start()
         return self
 
     def join(self, timeout: Optional[float] = None) -> bool:
+        if self._engine is not None:
+            return bool(self._engine.join(-1.0 if timeout is None else float(timeout)))
         if self._thread is None:
             return True
         self._thread.join(timeout)
         return not self._thread.is_alive()
 
+    def close(self, timeout: float = 10.0) -> None:
+        """Stop the transport driver and drop the native engine (it holds references to the RCCL
+        communicator and the control segment).  Idempotent; call before ``Comm.close()``."""
+        if self._engine is not None:
+            _ = self._failed                      # cache a late error before the engine goes
+            self._final_counters = self._engine_counters()
+            self._engine.request_stop()
+            if not self._engine.join(timeout):
+                log.warning("rank %d: transport engine did not stop within %.0f s", self.rank, timeout)
+                return
+            self._engine = None
+            self._ctrl = None
+
     @property
     def failed(self) -> Optional[BaseException]:
         return self._failed
 
+    def _engine_counters(self) -> dict:
+        if self._engine is None:
+            return dict(getattr(self, "_final_counters", {}))
+        st = self._engine.stats()
+        return {"rounds": st.rounds, "frames_routed": st.frames_routed, "bytes_sent": st.bytes_sent,
+                "bytes_recv": st.bytes_recv, "round_ms": 1e3 * st.round_s / max(1, st.rounds),
+                "ctrl_ms": 1e3 * st.ctrl_s / max(1, st.rounds), "idle_rounds": st.idle_rounds,
+                "frames_local": st.frames_local}
+
     def metrics(self) -> dict:
         """Gauges + cumulative counters for utils.metrics."""
+        if self._engine is not None or self.xport == "native":
+            d = {"ready": self.pool.n_ready(), "credits": self.pool.credits()}
+            d.update(self._engine_counters())
+            return d
         d = {"ready": self.pool.n_ready(), "credits": self.pool.credits(), "rounds": self.rounds,
              "frames_routed": self.frames_routed if self.comm is not None else self.pool.stats().routed_local}
         if self.comm is not None:
@@ -368,6 +468,10 @@ class QueueEndpoint:
 
     def stats(self) -> dict:
         d = self.ring.stats()
+        if self._engine is not None or self.xport == "native":
+            d.update(self._engine_counters())
+            d["xport"] = "native"
+            return d
         d.update(rounds=self.rounds, frames_routed=self.frames_routed if self.comm is not None else d["routed_local"],
                  round_ms=1e3 * self.round_time_s / max(1, self.rounds))
         if self.comm is not None:

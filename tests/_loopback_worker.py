@@ -61,8 +61,9 @@ def main(device: str, n: int) -> int:
         return 1
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
-    print(f"LOOPBACK_OK {n} {comm.bytes_sent} native={comm.rccl is not None}")
+    print(f"LOOPBACK_OK {n} {comm.bytes_sent} native={comm.rccl is not None} xport={ep.xport}")
     import torch.distributed as dist
+    ep.close()
     comm.close()
     dist.destroy_process_group()
     return 0

@@ -6,8 +6,9 @@ import numpy as np
 import torch
 
 
-def transport_worker(rank, world, port, roles, n_events, policy, out_q, slow_rank=-1, mode="calib"):
+def transport_worker(rank, world, port, roles, n_events, policy, out_q, slow_rank=-1, mode="calib", xport="native"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["PSANA_RAY_XPORT"] = xport
     os.environ["MASTER_PORT"] = str(port)
     try:
         from psana_ray_amd.models import Calibrator, Mode
@@ -65,7 +66,9 @@ def transport_worker(rank, world, port, roles, n_events, policy, out_q, slow_ran
         if th is not None:
             th.join(60)
         ep.join(60)
-        out_q.put((rank, "ok", seen, bad, ep.stats()))
+        st = ep.stats()
+        st["xport_used"] = ep.xport
+        out_q.put((rank, "ok", seen, bad, st))
         import torch.distributed as dist
 
         dist.destroy_process_group()
@@ -75,9 +78,10 @@ def transport_worker(rank, world, port, roles, n_events, policy, out_q, slow_ran
         out_q.put((rank, "err", traceback.format_exc(), 0, {}))
 
 
-def dying_consumer_worker(rank, world, port, out_q):
+def dying_consumer_worker(rank, world, port, out_q, xport="native"):
     """rank 1 (consumer) exits abruptly mid-stream; rank 0 (producer) must fail cleanly."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["PSANA_RAY_XPORT"] = xport
     os.environ["MASTER_PORT"] = str(port)
     from psana_ray_amd.models import Calibrator, Mode
     from psana_ray_amd.parallel.comm import init_groups

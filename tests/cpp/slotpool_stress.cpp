@@ -11,10 +11,18 @@
 //   scenario 2 (auto-route): producer thread + 3 consumer threads on ONE pool in single-process
 //                           mode (routing inside commit/release), batch and single-slot calls mixed.
 //   scenario 3 (routing): random plan_round inputs; every plan respects offers and credits.
+//   scenario 4 (transport engine): 3 ranks in one process (producer / producer+consumer /
+//                           consumer), each with its own pool, its own mapping of ONE shared-memory
+//                           control segment and a TransportEngine thread; host data plane through
+//                           the outboxes; checks payload bytes, exactly-once delivery and EOS.
 #include <stdint.h>
 #include <stdio.h>
 
+#include <unistd.h>
+
 #include <atomic>
+#include <memory>
+#include <string>
 #include <mutex>
 #include <random>
 #include <stdexcept>
@@ -22,6 +30,7 @@
 #include <vector>
 
 #include "runtime.h"
+#include "xport_engine.h"
 
 namespace pr {
 std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers_in, const std::vector<int64_t>& credits_in,
@@ -213,12 +222,96 @@ static void scenario_routing(int iters) {
   printf("routing scenario: %d random rounds x 3 policies OK\n", iters);
 }
 
+static void scenario_engine(int64_t n_per_producer, int policy) {
+  const int world = 3, max_offer = 8;
+  const int64_t slot_bytes = 192;
+  const bool is_p[world] = {true, true, false}, is_c[world] = {false, true, true};
+  const std::vector<int> prods = {0, 1};
+  const std::string name = "/psray-stress-" + std::to_string((long long)getpid()) + "-" + std::to_string(policy);
+  std::vector<std::unique_ptr<SlotPool>> pools;
+  std::vector<std::vector<uint8_t>> rings;
+  std::vector<std::unique_ptr<pr::ShmControl>> ctrls;
+  std::vector<std::unique_ptr<pr::TransportEngine>> engines;
+  for (int r = 0; r < world; ++r) {
+    pools.emplace_back(new SlotPool(is_p[r] ? 12 : 0, is_c[r] ? 10 : 0, -1));
+    rings.emplace_back((size_t)pools[r]->n_slots() * slot_bytes);
+  }
+  for (int r = 0; r < world; ++r)
+    ctrls.emplace_back(new pr::ShmControl(name, r == 0, r, world, pr::TransportEngine::vec_words_for(max_offer),
+                                          max_offer * slot_bytes, 60.0));
+  for (int r = 0; r < world; ++r)
+    engines.emplace_back(new pr::TransportEngine(pools[r].get(), ctrls[r].get(), nullptr,
+                                                 (uint64_t)(uintptr_t)rings[r].data(), slot_bytes, r, world, prods,
+                                                 is_p[r], is_c[r], policy, max_offer, false, 0, -1));
+  for (auto& e : engines) e->start();
+  auto payload = [](int64_t rank, int64_t idx, int64_t j) { return (uint8_t)(rank * 131 + idx * 7 + j * 3); };
+  std::vector<std::thread> th;
+  for (int r = 0; r < world; ++r) {
+    if (!is_p[r]) continue;
+    th.emplace_back([&, r] {
+      for (int64_t k = 0; k < n_per_producer;) {
+        const int s = pools[r]->acquire_produce(0.01);
+        if (s < 0) continue;
+        uint8_t* d = rings[r].data() + (size_t)s * slot_bytes;
+        for (int64_t j = 0; j < slot_bytes; ++j) d[j] = payload(r, k, j);
+        SlotHeader h;
+        h.rank = r;
+        h.idx = k;
+        h.gevt = 1000 * r + k;
+        h.photon_energy = 0.5 * (double)k;
+        pools[r]->commit_produce(s, h, 0);
+        ++k;
+      }
+      engines[r]->set_producer_finished();
+    });
+  }
+  std::vector<std::atomic<int>> seen(2 * n_per_producer);
+  for (auto& x : seen) x.store(0);
+  for (int r = 0; r < world; ++r) {
+    if (!is_c[r]) continue;
+    th.emplace_back([&, r] {
+      int64_t last[2] = {-1, -1};
+      for (;;) {
+        const int s = pools[r]->get(0.005);
+        if (s < 0) {
+          const std::string e = engines[r]->error();
+          require(e.empty(), "transport engine failed");
+          if (engines[r]->done() && pools[r]->n_ready() == 0) return;
+          continue;
+        }
+        const SlotHeader h = pools[r]->header(s);
+        require(h.rank >= 0 && h.rank < 2 && h.idx >= 0 && h.idx < n_per_producer, "engine: header out of range");
+        require(h.gevt == 1000 * h.rank + h.idx && h.photon_energy == 0.5 * (double)h.idx, "engine: header corrupted");
+        require(h.idx > last[h.rank], "engine: per-producer FIFO order violated within a shard");
+        last[h.rank] = h.idx;
+        const uint8_t* d = rings[r].data() + (size_t)s * slot_bytes;
+        for (int64_t j = 0; j < slot_bytes; ++j) {
+          if (d[j] != payload(h.rank, h.idx, j))
+            fprintf(stderr, "consumer %d: frame (%lld,%lld) byte %lld = %d, want %d (slot %d)\n", r, (long long)h.rank,
+                    (long long)h.idx, (long long)j, (int)d[j], (int)payload(h.rank, h.idx, j), s);
+          require(d[j] == payload(h.rank, h.idx, j), "engine: payload corrupted");
+        }
+        seen[h.rank * n_per_producer + h.idx].fetch_add(1);
+        pools[r]->release(s, 0);
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : engines) require(e->join(60.0), "engine did not finish");
+  for (auto& e : engines) require(e->error().empty(), "engine reported an error");
+  for (size_t i = 0; i < seen.size(); ++i) require(seen[i].load() == 1, "engine: event lost or duplicated");
+  const pr::XportStats s1 = engines[1]->stats();
+  printf("engine scenario (policy %d): %lld events OK (%lld rounds, %lld sent by rank 1)\n", policy, (long long)seen.size(),
+         (long long)s1.rounds, (long long)s1.frames_sent);
+}
+
 int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : 20000;
   try {
     scenario_transport(n);
     scenario_auto_route(n);
     scenario_routing(2000);
+    for (int policy = 0; policy < 3; ++policy) scenario_engine(std::max<int64_t>(200, n / 8), policy);
   } catch (const std::exception& e) {
     fprintf(stderr, "FAILED with exception: %s\n", e.what());
     return 1;

@@ -9,11 +9,14 @@ import pytest
 from tests._mp_workers import dying_consumer_worker, transport_worker
 
 
-def _run(world, roles, n_events, policy, slow_rank=-1, mode="calib", timeout=120):
+XPORTS = ["native", "python"]
+
+
+def _run(world, roles, n_events, policy, slow_rank=-1, mode="calib", timeout=120, xport="native"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    ps = [ctx.Process(target=transport_worker, args=(r, world, port, roles, n_events, policy, q, slow_rank, mode))
+    ps = [ctx.Process(target=transport_worker, args=(r, world, port, roles, n_events, policy, q, slow_rank, mode, xport))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -22,6 +25,7 @@ def _run(world, roles, n_events, policy, slow_rank=-1, mode="calib", timeout=120
         for _ in range(world):
             r, status, seen, bad, st = q.get(timeout=timeout)
             assert status == "ok", seen
+            assert st["xport_used"] == xport
             res[r] = (seen, bad, st)
     finally:
         for p in ps:
@@ -31,9 +35,10 @@ def _run(world, roles, n_events, policy, slow_rank=-1, mode="calib", timeout=120
     return res
 
 
+@pytest.mark.parametrize("xport", XPORTS)
 @pytest.mark.parametrize("policy", ["balanced", "spread", "local_first"])
-def test_two_ranks_exactly_once(native, policy):
-    res = _run(2, ["pc", "pc"], 20, policy)
+def test_two_ranks_exactly_once(native, policy, xport):
+    res = _run(2, ["pc", "pc"], 20, policy, xport=xport)
     allseen = [k for r in res for k in res[r][0]]
     assert sorted(allseen) == sorted([(0, i) for i in range(10)] + [(1, i) for i in range(10)])
     assert all(res[r][1] == 0 for r in res), "frame content corrupted in transit"
@@ -45,24 +50,27 @@ def test_two_ranks_exactly_once(native, policy):
         assert res[0][2]["bytes_sent"] > 0 and res[1][2]["bytes_sent"] > 0
 
 
-def test_producer_only_and_consumer_only_ranks(native):
-    res = _run(3, ["p", "p", "c"], 15, "balanced")
+@pytest.mark.parametrize("xport", XPORTS)
+def test_producer_only_and_consumer_only_ranks(native, xport):
+    res = _run(3, ["p", "p", "c"], 15, "balanced", xport=xport)
     assert sorted(res[2][0]) == sorted([(0, i) for i in range(8)] + [(1, i) for i in range(7)])
     assert res[0][0] == [] and res[1][0] == []
 
 
-def test_competing_consumers_slow_one_gets_less(native):
-    res = _run(3, ["p", "c", "c"], 60, "balanced", slow_rank=2)
+@pytest.mark.parametrize("xport", XPORTS)
+def test_competing_consumers_slow_one_gets_less(native, xport):
+    res = _run(3, ["p", "c", "c"], 60, "balanced", slow_rank=2, xport=xport)
     n1, n2 = len(res[1][0]), len(res[2][0])
     assert n1 + n2 == 60
     assert n1 > n2, f"fast consumer got {n1}, slow got {n2}"
 
 
-def test_dead_consumer_makes_producer_fail_cleanly(native):
+@pytest.mark.parametrize("xport", XPORTS)
+def test_dead_consumer_makes_producer_fail_cleanly(native, xport):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    ps = [ctx.Process(target=dying_consumer_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=dying_consumer_worker, args=(r, 2, port, q, xport)) for r in range(2)]
     for p in ps:
         p.start()
     msgs = {}

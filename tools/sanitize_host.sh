@@ -18,5 +18,6 @@ esac
 $CXX -x hip --offload-host-only --offload-arch=gfx950 -fno-gpu-sanitize -std=c++17 -O1 -g $FLAGS \
   -I"$R/csrc" \
   "$R/tests/cpp/slotpool_stress.cpp" "$R/csrc/runtime.cpp" "$R/csrc/routing.cpp" \
-  -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64 -lpthread -o "$OUT"
+  "$R/csrc/xport_engine.cpp" "$R/csrc/transport.cpp" "$R/csrc/trace.cpp" \
+  -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64 -lrccl -lpthread -o "$OUT"
 "$OUT" "$N"
