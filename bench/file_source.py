@@ -26,6 +26,8 @@ def main(argv=None):
     ap.add_argument("--chunk", type=int, default=32)
     ap.add_argument("--common-mode", default="default")
     ap.add_argument("--no-numa", action="store_true", help="do not bind to the GPU's NUMA node")
+    ap.add_argument("--format", choices=["praw", "xtc2"], default="praw",
+                    help="fixed-record raw-run file, or XTC2-style bigdata + smalldata index")
     a = ap.parse_args(argv)
 
     import torch
@@ -34,7 +36,7 @@ def main(argv=None):
     from psana_ray_amd.models import Calibrator, Mode
     from psana_ray_amd.pipeline import PeakFinderConsumer, ProducerPipeline
     from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
-    from psana_ray_amd.source import RawFileRun, make_synthetic_run
+    from psana_ray_amd.source import RawFileRun, make_synthetic_run, make_synthetic_xtc2_run, open_xtc2_run
 
     from psana_ray_amd.parallel.launch import bind_numa_to_device
 
@@ -42,8 +44,15 @@ def main(argv=None):
     numa = None if a.no_numa else bind_numa_to_device(dev)
     shutil.rmtree(a.dir, ignore_errors=True)
     try:
-        path = make_synthetic_run(a.dir, "bench", 1, a.detector, n_events=a.frames, chunk=32)
-        src = RawFileRun(path, a.detector, exp="bench", run=1, n_threads=a.threads, pinned=False)
+        if a.format == "xtc2":
+            make_synthetic_xtc2_run(a.dir, "bench", 1, a.detector, n_events=a.frames, chunk=32)
+            t_scan = time.perf_counter()
+            src = open_xtc2_run(a.dir, "bench", 1, a.detector, n_threads=a.threads, pinned=False)
+            t_scan = time.perf_counter() - t_scan
+        else:
+            path = make_synthetic_run(a.dir, "bench", 1, a.detector, n_events=a.frames, chunk=32)
+            t_scan = 0.0
+            src = RawFileRun(path, a.detector, exp="bench", run=1, n_threads=a.threads, pinned=False)
         cal = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams.parse(a.common_mode))
         ring = FrameRing(cal.out_shape, cal.out_dtype, dev, 4 * a.chunk + 32, 400)
         ep = QueueEndpoint(ring)
@@ -62,7 +71,8 @@ def main(argv=None):
         dt = time.perf_counter() - t0
         th.join()
         st = prod.engine.timing() if prod.engine is not None else None
-        print(json.dumps({"bench": "raw-run file source, 1 GPU", "detector": a.detector, "frames": n,
+        print(json.dumps({"bench": f"{a.format} file source, 1 GPU", "detector": a.detector, "frames": n,
+                          "index_scan_s": round(t_scan, 4),
                           "seconds": round(dt, 4), "frames_per_s": round(n / dt, 1),
                           "GB_per_s_raw": round(n * src.spec.raw_frame_bytes / dt / 1e9, 2),
                           "native_engine": prod.engine is not None, "reader_threads": a.threads, "peaks": peaks, "numa": numa,

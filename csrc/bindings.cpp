@@ -16,6 +16,7 @@ namespace py = pybind11;
 #include "trace.h"
 #include "transport.h"
 #include "xport_engine.h"
+#include "xtc2.h"
 
 namespace pr {
 std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers, const std::vector<int64_t>& credits,
@@ -375,8 +376,27 @@ PYBIND11_MODULE(_C, m) {
       .def("gpu_timing", &pr::ProducerEngine::gpu_timing)
       .def_property_readonly("gpu_timing_enabled", &pr::ProducerEngine::gpu_timing_enabled);
 
+  py::class_<pr::Xtc2Index>(m, "Xtc2Index")
+      .def_readonly("det_type", &pr::Xtc2Index::det_type)
+      .def_readonly("shape", &pr::Xtc2Index::shape)
+      .def_readonly("dtype", &pr::Xtc2Index::dtype)
+      .def_readonly("frame_bytes", &pr::Xtc2Index::frame_bytes)
+      .def_readonly("payload_off", &pr::Xtc2Index::payload_off)
+      .def_readonly("gevt", &pr::Xtc2Index::gevt)
+      .def_readonly("timestamp", &pr::Xtc2Index::timestamp)
+      .def_readonly("photon_energy", &pr::Xtc2Index::photon_energy)
+      .def_readonly("transitions", &pr::Xtc2Index::transitions)
+      .def_readonly("walked", &pr::Xtc2Index::walked);
+  m.def("xtc2_scan", &pr::xtc2_scan, py::arg("smd_path"), py::arg("big_path"), py::arg("det_name"),
+        py::arg("array_name") = "raw", py::call_guard<py::gil_scoped_release>());
+
   py::class_<pr::RawRunReader>(m, "RawRunReader")
       .def(py::init<const std::string&, int>(), py::arg("path"), py::arg("n_threads") = 4)
+      .def(py::init<const std::string&, int, std::vector<int64_t>, std::vector<int64_t>, std::vector<double>,
+                    int64_t>(),
+           py::arg("path"), py::arg("n_threads"), py::arg("payload_off"), py::arg("gevt"), py::arg("photon_energy"),
+           py::arg("frame_bytes"))
+      .def_property_readonly("indexed", &pr::RawRunReader::indexed)
       .def_property_readonly("n_events", &pr::RawRunReader::n_events)
       .def_property_readonly("frame_bytes", &pr::RawRunReader::frame_bytes)
       .def_property_readonly("record_bytes", &pr::RawRunReader::record_bytes)

@@ -615,6 +615,23 @@ RawRunReader::RawRunReader(const std::string& path, int n_threads) : n_threads_(
   check(frame_bytes_ > 0, "RawRunReader: bad record size");
 }
 
+RawRunReader::RawRunReader(const std::string& path, int n_threads, std::vector<int64_t> payload_off,
+                           std::vector<int64_t> gevt, std::vector<double> photon_energy, int64_t frame_bytes)
+    : n_threads_(n_threads < 1 ? 1 : n_threads), off_(std::move(payload_off)), gevt_(std::move(gevt)),
+      pe_(std::move(photon_energy)) {
+  check(!off_.empty(), "RawRunReader: empty event index");
+  check(off_.size() == gevt_.size() && off_.size() == pe_.size(), "RawRunReader: index columns differ in length");
+  check(frame_bytes > 0, "RawRunReader: bad frame size");
+  fd_ = ::open(path.c_str(), O_RDONLY);
+  check(fd_ >= 0, "RawRunReader: cannot open " + path);
+  struct stat sb;
+  check(fstat(fd_, &sb) == 0, "RawRunReader: fstat failed");
+  for (int64_t o : off_)
+    check(o >= 0 && o + frame_bytes <= (int64_t)sb.st_size, "RawRunReader: index points past the end of " + path);
+  n_events_ = (int64_t)off_.size();
+  frame_bytes_ = frame_bytes;
+}
+
 RawRunReader::~RawRunReader() {
   if (fd_ >= 0) ::close(fd_);
 }
@@ -630,6 +647,11 @@ std::vector<std::pair<int64_t, double>> RawRunReader::read(const std::vector<int
       const size_t i = next.fetch_add(1);
       if (i >= n) return;
       check(events[i] >= 0 && events[i] < n_events_, "RawRunReader.read: event index out of range");
+      if (!off_.empty()) {
+        meta[i] = {gevt_[events[i]], pe_[events[i]]};
+        pread_full(fd_, reinterpret_cast<void*>(dst_ptrs[i]), (size_t)frame_bytes_, (off_t)off_[events[i]]);
+        continue;
+      }
       const off_t off = (off_t)(header_bytes_ + events[i] * record_bytes_);
       int64_t rh[4];
       pread_full(fd_, rh, sizeof(rh), off);

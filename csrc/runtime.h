@@ -170,7 +170,12 @@ class SlotPool {
 class RawRunReader {
  public:
   RawRunReader(const std::string& path, int n_threads);
+  // Index mode (variable-size containers, e.g. XTC2 bigdata located through its small-data file):
+  // event i's frame is `frame_bytes` at payload_off[i]; its metadata comes from the index.
+  RawRunReader(const std::string& path, int n_threads, std::vector<int64_t> payload_off, std::vector<int64_t> gevt,
+               std::vector<double> photon_energy, int64_t frame_bytes);
   ~RawRunReader();
+  bool indexed() const { return !off_.empty(); }
   int64_t n_events() const { return n_events_; }
   int64_t frame_bytes() const { return frame_bytes_; }
   int64_t record_bytes() const { return record_bytes_; }
@@ -184,6 +189,8 @@ class RawRunReader {
   int fd_ = -1;
   int n_threads_;
   int64_t n_events_ = 0, frame_bytes_ = 0, record_bytes_ = 0, header_bytes_ = 0;
+  std::vector<int64_t> off_, gevt_;
+  std::vector<double> pe_;
 };
 
 // ---------------------------------------------------------------------------------------

@@ -7,6 +7,7 @@ from typing import Optional
 from .psana_adapter import PsanaWrapperSource, psana_available
 from .rawfile import RawFileRun, make_synthetic_run, run_path, write_run
 from .synthetic import RawEvent, SyntheticRun, generate_raw
+from .xtc2 import find_xtc2_run, make_synthetic_xtc2_run, open_xtc2_run, write_xtc2_run, xtc2_paths
 
 ENV_DATA_DIR = "PSANA_RAY_DATA"
 
@@ -16,11 +17,16 @@ def open_source(exp: str, run: int, detector_name: str, rank: int = 0, size: int
                 data_dir: Optional[str] = None, **kw):
     """Pick the event source for ``(exp, run, detector_name)``:
 
-    1. a raw-run file ``$PSANA_RAY_DATA/<exp>/r<run>/<detector>.praw`` if it exists;
-    2. the synthetic detector for ``--exp synthetic`` (or whenever psana is unavailable);
-    3. the real psana_wrapper otherwise (import-gated).
+    1. an XTC2-style run ``$PSANA_RAY_DATA/<exp>/xtc/<exp>-r<run>-s000-c000.xtc2`` (+ its
+       smalldata index) if it exists;
+    2. a raw-run file ``$PSANA_RAY_DATA/<exp>/r<run>/<detector>.praw`` if it exists;
+    3. the synthetic detector for ``--exp synthetic`` (or whenever psana is unavailable);
+    4. the real psana_wrapper otherwise (import-gated).
     """
     data_dir = data_dir or os.environ.get(ENV_DATA_DIR)
+    if data_dir and find_xtc2_run(data_dir, exp, run) is not None:
+        return open_xtc2_run(data_dir, exp, run, detector_name, rank=rank, size=size, pinned=pinned,
+                             n_events=n_events)
     if data_dir:
         p = run_path(data_dir, exp, run, detector_name)
         if p.exists():
@@ -33,4 +39,5 @@ def open_source(exp: str, run: int, detector_name: str, rank: int = 0, size: int
 
 
 __all__ = ["RawEvent", "SyntheticRun", "RawFileRun", "PsanaWrapperSource", "open_source", "generate_raw",
-           "write_run", "make_synthetic_run", "run_path", "psana_available"]
+           "write_run", "make_synthetic_run", "run_path", "psana_available", "find_xtc2_run", "open_xtc2_run",
+           "write_xtc2_run", "make_synthetic_xtc2_run", "xtc2_paths"]

@@ -67,13 +67,16 @@ class RawFileRun:
     its H2D copy completed -- the producer pipeline waits on the copy event)."""
 
     def __init__(self, path, detector_name: str, exp: str = "file", run: int = 0, rank: int = 0, size: int = 1,
-                 staging: int = 64, n_threads: int = 16, pinned: bool = True, n_events: Optional[int] = None):
+                 staging: int = 64, n_threads: int = 16, pinned: bool = True, n_events: Optional[int] = None,
+                 reader=None):
         from ..ops import _ext
 
         C = _ext.load()
         self.spec = get_detector(detector_name)
         self.exp, self.run = exp, run
-        self.reader = C.RawRunReader(str(path), n_threads)
+        self.path = str(path)
+        # reader: a prebuilt native reader (e.g. index mode over an XTC2 bigdata file)
+        self.reader = C.RawRunReader(str(path), n_threads) if reader is None else reader
         if self.reader.frame_bytes != self.spec.raw_frame_bytes:
             raise ValueError(f"{path}: frame size {self.reader.frame_bytes} != {self.spec.name} raw frame")
         self.rank, self.size = rank, size
