@@ -62,20 +62,26 @@ def main(argv=None):
         th = threading.Thread(target=prod.run, daemon=True)
         th.start()
         n = 0
+        t_first, n_first = None, 0
         while True:
             try:
                 n += cons.poll(timeout=0.05)
             except EndOfStream:
                 break
+            if t_first is None and n > 0:
+                t_first, n_first = time.perf_counter(), n     # steady state: after the pipeline filled
         peaks = cons.synchronize()
         dt = time.perf_counter() - t0
+        steady = (n - n_first) / max(1e-9, time.perf_counter() - t_first) if t_first is not None else 0.0
         th.join()
         st = prod.engine.timing() if prod.engine is not None else None
         print(json.dumps({"bench": f"{a.format} file source, 1 GPU", "detector": a.detector, "frames": n,
                           "index_scan_s": round(t_scan, 4),
                           "seconds": round(dt, 4), "frames_per_s": round(n / dt, 1),
+                          "steady_frames_per_s": round(steady, 1),
                           "GB_per_s_raw": round(n * src.spec.raw_frame_bytes / dt / 1e9, 2),
-                          "native_engine": prod.engine is not None, "reader_threads": a.threads, "peaks": peaks, "numa": numa,
+                          "native_engine": prod.engine is not None, "zero_copy": prod.zero_copy, "reader_threads": a.threads, "peaks": peaks, "numa": numa,
+                          "engine_span_copies_frame_copies": prod.engine.copy_stats(),
                           "engine_host_s_stage_acquire_launch_commit_total": st}))
     finally:
         shutil.rmtree(a.dir, ignore_errors=True)

@@ -374,7 +374,16 @@ PYBIND11_MODULE(_C, m) {
       .def("error", &pr::ProducerEngine::error)
       .def("timing", &pr::ProducerEngine::timing)
       .def("gpu_timing", &pr::ProducerEngine::gpu_timing)
+      .def("copy_stats", &pr::ProducerEngine::copy_stats)
       .def_property_readonly("gpu_timing_enabled", &pr::ProducerEngine::gpu_timing_enabled);
+
+  py::class_<pr::MappedFile>(m, "MappedFile")
+      .def(py::init<const std::string&, bool>(), py::arg("path"), py::arg("register_with_hip") = true,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("ptr", &pr::MappedFile::ptr)
+      .def_property_readonly("nbytes", &pr::MappedFile::bytes)
+      .def_property_readonly("registered", &pr::MappedFile::registered)
+      .def_property_readonly("register_s", &pr::MappedFile::register_s);
 
   py::class_<pr::Xtc2Index>(m, "Xtc2Index")
       .def_readonly("det_type", &pr::Xtc2Index::det_type)

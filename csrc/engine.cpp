@@ -100,7 +100,9 @@ ProducerEngine::ProducerEngine(SlotPool* pool, uint64_t ring_base, int64_t slot_
     h2d_pending_.assign(n_raw_bufs_, 0);
     calib_pending_.assign(n_raw_bufs_, 0);
   }
-  hip_check(hipMalloc(&raw_bufs_, (size_t)n_raw_bufs_ * chunk_ * plan.raw_frame_bytes), "hipMalloc raw chunks");
+  region_bytes_ = (int64_t)chunk_ * (plan.raw_frame_bytes + kCopySlack);
+  hip_check(hipMalloc(&raw_bufs_, (size_t)n_raw_bufs_ * region_bytes_), "hipMalloc raw chunks");
+  dev_in_.assign(n_raw_bufs_, std::vector<uint64_t>(chunk_, 0));
 }
 
 ProducerEngine::~ProducerEngine() {
@@ -228,8 +230,10 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
     const size_t nsrc = src_frames_.size();
     // host-side software pipeline: the copy of chunk c+1 is queued on the side stream BEFORE
     // chunk c waits for slots / launches, so the copy engine never runs dry behind host work
+    const int64_t fb = plan_.raw_frame_bytes;
     auto stage = [&](int64_t k0, int n, int b) {
-      char* buf = static_cast<char*>(raw_bufs_) + (size_t)b * chunk_ * plan_.raw_frame_bytes;
+      char* buf = static_cast<char*>(raw_bufs_) + (size_t)b * region_bytes_;
+      std::vector<uint64_t>& dev = dev_in_[b];
       if (file_ != nullptr) {
         // staging region b is rewritten only after its previous H2D copy finished (host wait; with
         // n_raw_bufs regions it is n_raw_bufs chunks old by now)
@@ -255,6 +259,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
         hip_check(hipMemcpyAsync(buf, stg, (size_t)n * plan_.raw_frame_bytes, hipMemcpyHostToDevice, h2d_),
                   "stage copy");
         hip_check(hipEventRecord(h2d_done_[b], h2d_), "record h2d");
+        for (int q = 0; q < n; ++q) dev[q] = reinterpret_cast<uint64_t>(buf) + (uint64_t)q * fb;
         return;
       }
       if (used[b]) hip_check(hipStreamWaitEvent(h2d_, buf_free_[b], 0), "wait buf free");
@@ -264,14 +269,31 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
         hip_check(hipEventRecord(h2d_start_[b], h2d_), "record h2d start");
         h2d_pending_[b] = 1;
       }
+      // coalesce runs of frames spaced by one constant stride d (fb <= d <= fb + slack, d a
+      // multiple of 16 so every frame lands 16-B aligned) into ONE copy of the whole span: a
+      // pinned pool (d == fb) or the records of a registered run file (d = record size)
       int i = 0;
-      while (i < n) {   // coalesce host-contiguous runs into single copies
+      int64_t pos = 0;
+      while (i < n) {
         const uint64_t s0 = src_frames_[(k0 + i) % nsrc];
         int j = i + 1;
-        while (j < n && src_frames_[(k0 + j) % nsrc] == s0 + (uint64_t)(j - i) * plan_.raw_frame_bytes) ++j;
-        hip_check(hipMemcpyAsync(buf + (size_t)i * plan_.raw_frame_bytes, reinterpret_cast<const void*>(s0),
-                                 (size_t)(j - i) * plan_.raw_frame_bytes, hipMemcpyDefault, h2d_),
+        int64_t d = 0;
+        if (j < n) {
+          d = (int64_t)(src_frames_[(k0 + j) % nsrc] - s0);
+          if (d < fb || d > fb + kCopySlack || d % 16 != 0) d = 0;
+        }
+        if (d > 0)
+          while (j < n && src_frames_[(k0 + j) % nsrc] == s0 + (uint64_t)((j - i) * d)) ++j;
+        else
+          j = i + 1;
+        const int64_t span = (int64_t)(j - i - 1) * d + fb;
+        pos = (pos + 255) & ~int64_t(255);
+        check(pos + span <= region_bytes_, "ProducerEngine: staging region overflow");
+        hip_check(hipMemcpyAsync(buf + pos, reinterpret_cast<const void*>(s0), (size_t)span, hipMemcpyDefault, h2d_),
                   "stage copy");
+        for (int q = i; q < j; ++q) dev[q] = reinterpret_cast<uint64_t>(buf) + (uint64_t)(pos + (q - i) * d);
+        (j - i > 1 ? span_copies_ : frame_copies_).fetch_add(1, std::memory_order_relaxed);
+        pos += span;
         i = j;
       }
       hip_check(hipEventRecord(h2d_done_[b], h2d_), "record h2d");
@@ -314,14 +336,13 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       auto t2 = clk::now();
       t_acquire_ += secs(t1, t2);
       if ((int)slots.size() < n) break;   // stopped while waiting
-      char* buf = static_cast<char*>(raw_bufs_) + (size_t)b * chunk_ * plan_.raw_frame_bytes;
       in.resize(n);
       out.resize(n);
       if (device_resident_) {   // calibrate straight from the resident source frames
         for (int q = 0; q < n; ++q) in[q] = src_frames_[(size_t)((k + q) % (int64_t)nsrc)];
       } else {
         hip_check(hipStreamWaitEvent(compute_, h2d_done_[b], 0), "wait h2d");
-        for (int q = 0; q < n; ++q) in[q] = reinterpret_cast<uint64_t>(buf) + (uint64_t)q * plan_.raw_frame_bytes;
+        for (int q = 0; q < n; ++q) in[q] = dev_in_[b][q];
       }
       for (int q = 0; q < n; ++q) out[q] = ring_base_ + (uint64_t)slots[q] * (uint64_t)slot_bytes_;
       if (gpu_timing_) {

@@ -83,6 +83,8 @@ class ProducerEngine {
   // GPU-side per-stage time from timing events (PSANA_RAY_ENGINE_GPU_TIMING=1 at construction):
   // [h2d ms total, h2d chunks measured, calib ms total, calib chunks measured]; zeros when off
   std::vector<double> gpu_timing() const;
+  // (copies that moved a multi-frame span, copies of a single frame) in cycled-host mode
+  std::vector<int64_t> copy_stats() const { return {span_copies_.load(), frame_copies_.load()}; }
   bool gpu_timing_enabled() const { return gpu_timing_; }
 
  private:
@@ -113,6 +115,13 @@ class ProducerEngine {
   int64_t gpu_h2d_n_ = 0, gpu_calib_n_ = 0;
   void harvest(int b, bool block);
   void* raw_bufs_ = nullptr;
+  // raw chunk region b: chunk x (frame + kCopySlack) bytes.  Host frames spaced by a constant
+  // stride <= frame + kCopySlack (records of a mapped run file: payload + record / datagram
+  // headers) are staged with ONE copy of the whole span; dev_in_[b][q] is frame q's position.
+  static constexpr int64_t kCopySlack = 4096;
+  int64_t region_bytes_ = 0;
+  std::vector<std::vector<uint64_t>> dev_in_;
+  std::atomic<int64_t> span_copies_{0}, frame_copies_{0};
   std::thread thread_;
   std::atomic<bool> stop_{false}, running_{false};
   std::atomic<int64_t> frames_{0}, full_waits_{0};

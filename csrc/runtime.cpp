@@ -1,6 +1,7 @@
 #include "runtime.h"
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -601,6 +602,38 @@ void pread_full(int fd, void* dst, size_t n, off_t off) {
   }
 }
 }  // namespace
+
+MappedFile::MappedFile(const std::string& path, bool register_with_hip) {
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  check(fd >= 0, "MappedFile: cannot open " + path);
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || sb.st_size <= 0) {
+    ::close(fd);
+    throw std::runtime_error("psana_ray_amd: MappedFile: empty or unreadable " + path);
+  }
+  bytes_ = (size_t)sb.st_size;
+  // MAP_POPULATE: fault the pages in now (registration pins them anyway)
+  base_ = mmap(nullptr, bytes_, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, 0);
+  ::close(fd);
+  check(base_ != MAP_FAILED, "MappedFile: mmap failed for " + path);
+  if (register_with_hip) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipError_t e = hipHostRegister(base_, bytes_, hipHostRegisterReadOnly);
+    if (e != hipSuccess) {
+      munmap(base_, bytes_);
+      base_ = nullptr;
+      throw std::runtime_error(std::string("psana_ray_amd: MappedFile: hipHostRegister failed: ") +
+                               hipGetErrorString(e));
+    }
+    registered_ = true;
+    register_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+}
+
+MappedFile::~MappedFile() {
+  if (registered_) (void)hipHostUnregister(base_);
+  if (base_ != nullptr) munmap(base_, bytes_);
+}
 
 RawRunReader::RawRunReader(const std::string& path, int n_threads) : n_threads_(n_threads < 1 ? 1 : n_threads) {
   fd_ = ::open(path.c_str(), O_RDONLY);

@@ -52,6 +52,10 @@ class ProducerPipeline:
         self.calibrated_source = getattr(source, "calibrated", False)
         spec = getattr(source, "spec", None)
         file_source = getattr(source, "reader", None)   # RawFileRun: native RawRunReader
+        # file sources: DMA straight out of the registered file mapping when possible
+        zero_copy = source.zero_copy_frames() if (self.gpu and not self.calibrated_source
+                                                  and hasattr(source, "zero_copy_frames")) else None
+        self.zero_copy = zero_copy is not None
         use_engine = self.gpu and not self.calibrated_source and (hasattr(source, "cycled_frames")
                                                                   or file_source is not None)
         if self.gpu and not self.calibrated_source and not use_engine:
@@ -75,7 +79,11 @@ class ProducerPipeline:
             self.engine = C.ProducerEngine(ring.pool, int(ring.storage.data_ptr()), ring.frame_bytes, dev_index,
                                            calibrator.plan, self.chunk, n_raw_buffers, int(rank),
                                            int(getattr(source, "size", 1)))
-            if file_source is not None:
+            if zero_copy is not None:
+                ptrs, pe = zero_copy
+                self._source_map = source._map       # keep the registered mapping alive
+                self.engine.set_cycled_source(ptrs, [float("nan") if v is None else float(v) for v in pe])
+            elif file_source is not None:
                 self.engine.set_file_source(file_source)    # file reads + staging in the native loop
             else:
                 ptrs, pe = source.cycled_frames()

@@ -10,6 +10,7 @@ records ``[i64 gevt, f64 photon_energy, i64 timestamp, i64 reserved, raw frame b
 """
 from __future__ import annotations
 
+import logging
 import os
 import struct
 from pathlib import Path
@@ -20,6 +21,8 @@ import numpy as np
 from ..models.constants import CalibConstants, run_seed
 from ..models.detector import DetectorSpec, get_detector
 from .synthetic import RawEvent, generate_raw
+
+log = logging.getLogger(__name__)
 
 HEADER_BYTES = 4096
 RECORD_HEADER = 32
@@ -61,6 +64,32 @@ def make_synthetic_run(data_dir: str, exp: str, run: int, detector: str, n_event
     return path
 
 
+ENV_ZEROCOPY = "PSANA_RAY_FILE_ZEROCOPY"
+
+
+def _mem_available() -> int:
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 0
+
+
+def zero_copy_wanted(nbytes: int) -> bool:
+    """``PSANA_RAY_FILE_ZEROCOPY``: 1 = always map + register the run file, 0 = never (pread into
+    pinned staging), auto (default) = when the file fits in min(64 GiB, 25 % of available RAM):
+    registration pins every page of the file for the whole run."""
+    mode = os.environ.get(ENV_ZEROCOPY, "auto").lower()
+    if mode in ("0", "off", "false"):
+        return False
+    if mode in ("1", "on", "true"):
+        return True
+    return nbytes <= min(64 << 30, _mem_available() // 4)
+
+
 class RawFileRun:
     """Event source over a raw-run file, read by the native thread-pool reader into pinned
     staging buffers (ring of ``staging`` frames; callers must not reuse a staged frame before
@@ -92,9 +121,50 @@ class RawFileRun:
         self.n_staging = staging
         self._cursor = 0
         self._slot = 0
+        self._map = None
+        # per-event (payload offset, gevt, photon energy) when the reader is index-based (XTC2)
+        self.index = None
 
     def create_bad_pixel_mask(self) -> np.ndarray:
         return self.consts.create_bad_pixel_mask()
+
+    def _event_table(self):
+        """(payload offsets, gevts, photon energies) of every event in the file."""
+        if self.index is not None:
+            return self.index
+        import ctypes
+
+        r = self.reader
+        n = self.n_events
+        raw = np.ctypeslib.as_array((ctypes.c_uint8 * (r.header_bytes + n * r.record_bytes)).from_address(self._map.ptr))
+        recs = raw[r.header_bytes:].reshape(n, r.record_bytes)[:, :RECORD_HEADER].copy()
+        gevt = recs[:, :8].view(np.int64)[:, 0]
+        pe = recs[:, 8:16].view(np.float64)[:, 0]
+        off = r.header_bytes + np.arange(n, dtype=np.int64) * r.record_bytes + RECORD_HEADER
+        return off, gevt, pe
+
+    def zero_copy_frames(self):
+        """Host pointers (into the registered file mapping) + photon energies of this rank's
+        events, for the producer engine's copy-from-source path: the DMA engines read the payloads
+        straight out of the page cache (no pread into staging).  None when disabled / unsuitable."""
+        from ..ops import _ext
+
+        try:
+            if self._map is None:
+                if not zero_copy_wanted(os.path.getsize(self.path)):
+                    return None
+                self._map = _ext.load().MappedFile(self.path, True)
+            off, gevt, pe = (np.asarray(x) for x in self._event_table())
+        except Exception as e:  # noqa: BLE001 - fall back to the pread path
+            log.warning("zero-copy mapping of %s unavailable (%r): pread staging", self.path, e)
+            self._map = None
+            return None
+        local = np.arange(self.rank, self.n_events, self.size, dtype=np.int64)
+        if not np.array_equal(gevt[local], local):
+            return None      # event ids are not positions: the engine derives gevt from the position
+        ptrs = [int(self._map.ptr + int(o)) for o in off[local]]
+        pes = [None if np.isnan(v) else float(v) for v in pe[local]]
+        return ptrs, pes
 
     def n_local_events(self) -> int:
         return max(0, (self.n_events - self.rank + self.size - 1) // self.size)

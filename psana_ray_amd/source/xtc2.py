@@ -286,6 +286,8 @@ def open_xtc2_run(data_dir, exp: str, run: int, detector_name: str, **kw):
     reader = C.RawRunReader(str(big), n_threads, list(ix.payload_off), list(ix.gevt), list(ix.photon_energy),
                             int(ix.frame_bytes))
     src = RawFileRun(big, detector_name, exp=exp, run=run, reader=reader, **kw)
+    src.index = (np.asarray(ix.payload_off, dtype=np.int64), np.asarray(ix.gevt, dtype=np.int64),
+                 np.asarray(ix.photon_energy, dtype=np.float64))
     src.timestamps = np.asarray(ix.timestamp, dtype=np.int64)
     src.transitions = list(ix.transitions)
     return src

@@ -117,12 +117,15 @@ def test_device_resident_source_calibrates_in_place(cuda_device):
     assert prod.engine.timing()[0] < 1e-3, "no staging copies expected for a device-resident source"
 
 
-def test_file_source_native_engine(cuda_device, tmp_path):
-    """Raw-run file -> native producer engine (pread thread pool into pinned staging, H2D, calib +
-    common mode) -> queue: every event once, exact vs the golden model, gevt / photon energy from
-    the file records, resume cursor honoured."""
+@pytest.mark.parametrize("zero_copy", ["0", "1"])
+def test_file_source_native_engine(cuda_device, tmp_path, monkeypatch, zero_copy):
+    """Raw-run file -> native producer engine (pread thread pool into pinned staging, or DMA
+    straight out of the registered file mapping; H2D, calib + common mode) -> queue: every event
+    once, exact vs the golden model, gevt / photon energy from the file records, resume cursor
+    honoured."""
     from psana_ray_amd.source import RawFileRun, make_synthetic_run
 
+    monkeypatch.setenv("PSANA_RAY_FILE_ZEROCOPY", zero_copy)
     path = make_synthetic_run(str(tmp_path), "exp", 7, "epix10k2M", n_events=70, chunk=16)
     src = RawFileRun(path, "epix10k2M", exp="exp", run=7, rank=0, size=1)
     src.seek(5)
@@ -131,6 +134,7 @@ def test_file_source_native_engine(cuda_device, tmp_path):
     ep = QueueEndpoint(ring)
     prod = ProducerPipeline(src, cal, ep, chunk=8)
     assert prod.engine is not None, "file sources must run on the native engine"
+    assert prod.zero_copy == (zero_copy == "1")
     t = threading.Thread(target=prod.run)
     t.start()
     ref_src = RawFileRun(path, "epix10k2M", exp="exp", run=7, rank=0, size=1, pinned=False)

@@ -130,10 +130,35 @@ def test_mkrun_cli_xtc2(native, tmp_path):
     assert src.n_events == 6
 
 
+def test_zero_copy_event_pointers(native, tmp_path):
+    """The zero-copy file path hands the engine pointers into the file mapping: check they address
+    exactly each local event's raw array (CPU: plain mmap, no HIP registration)."""
+    import ctypes
+
+    from psana_ray_amd.source import RawFileRun, write_run
+
+    spec, frames, pe, big, smd = _run(tmp_path, nan_at=(4,))
+    praw = tmp_path / "r.praw"
+    write_run(praw, spec, frames, pe)
+    for src in (X.open_xtc2_run(str(tmp_path), "expX", 3, spec.name, rank=1, size=2, pinned=False),
+                RawFileRun(praw, spec.name, rank=1, size=2, pinned=False)):
+        src._map = native.MappedFile(src.path, False)
+        ptrs, pes = src.zero_copy_frames()
+        local = list(range(1, len(frames), 2))
+        assert len(ptrs) == len(local) == src.n_local_events()
+        for p, g, v in zip(ptrs, local, pes):
+            got = np.frombuffer((ctypes.c_uint8 * spec.raw_frame_bytes).from_address(p), dtype=np.uint16)
+            np.testing.assert_array_equal(got.reshape(frames[g].shape), frames[g])
+            assert (v is None) == (g == 4) and (v is None or v == pe[g])
+
+
 @pytest.mark.gpu
-def test_xtc2_source_native_engine(cuda_device, tmp_path):
-    """XTC2 run -> native scan -> producer engine (pread pool into pinned staging, H2D, calib +
-    common mode) -> queue: every event once, exact vs the golden model."""
+@pytest.mark.parametrize("zero_copy", ["0", "1"])
+def test_xtc2_source_native_engine(cuda_device, tmp_path, monkeypatch, zero_copy):
+    """XTC2 run -> native scan -> producer engine (pread pool into pinned staging, or DMA out of
+    the registered file mapping; H2D, calib + common mode) -> queue: every event once, exact vs
+    the golden model."""
+    monkeypatch.setenv("PSANA_RAY_FILE_ZEROCOPY", zero_copy)
     from psana_ray_amd.config import CommonModeParams
     from psana_ray_amd.models import Calibrator, Mode
     from psana_ray_amd.ops import reference
@@ -148,6 +173,7 @@ def test_xtc2_source_native_engine(cuda_device, tmp_path):
     ep = QueueEndpoint(ring)
     prod = ProducerPipeline(src, cal, ep, chunk=8)
     assert prod.engine is not None, "XTC2 sources must run on the native engine"
+    assert prod.zero_copy == (zero_copy == "1")
     t = threading.Thread(target=prod.run)
     t.start()
     seen = {}
