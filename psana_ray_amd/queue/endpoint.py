@@ -151,8 +151,8 @@ class QueueEndpoint:
         self._engine = None
         self._engine_exc: Optional[BaseException] = None
         self.xport = "local" if comm is None else self._pick_xport(xport)
-        if self.xport == "native":
-            self._make_engine()
+        if self.xport == "native" and not self._make_engine():
+            self.xport = "python"
 
     # ------------------------------------------------------------------------ native transport
     def _pick_xport(self, xport: Optional[str]) -> str:
@@ -164,7 +164,20 @@ class QueueEndpoint:
             x = "python"
         return x
 
-    def _make_engine(self):
+    def _agree(self, ok: bool) -> bool:
+        """All ranks' verdict (min over ranks, on the gloo control group)."""
+        if self.world == 1:
+            return ok
+        import torch.distributed as dist
+
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.comm.ctrl_group)
+        return bool(t.item())
+
+    def _make_engine(self) -> bool:
+        """Set up the shared-memory control segment and the native engine.  Every rank must pick
+        the same driver, so a segment that cannot be created or attached anywhere (no /dev/shm,
+        size limits, ...) makes ALL ranks fall back to the python driver.  Returns success."""
         C = _ext.load()
         comm = self.comm
         rccl = getattr(comm, "rccl", None)
@@ -172,8 +185,28 @@ class QueueEndpoint:
         # host pools move frames through per-rank shared-memory outboxes (max_offer slots each)
         box = 0 if rccl is not None else self.max_offer * self._slot_bytes
         name = comm.shm_name()
-        self._ctrl = C.ShmControl(name, self.rank == 0, self.rank, self.world, C.xport_vec_words(self.max_offer),
-                                  box, tmo)
+        words = C.xport_vec_words(self.max_offer)
+
+        def open_segment(create: bool):
+            try:
+                if os.environ.get("PSANA_RAY_XPORT_TEST_FAIL_RANK") == str(self.rank):
+                    raise OSError("injected shared-memory failure (test hook)")
+                # attaching happens after rank 0 created the segment: a short wait suffices
+                return C.ShmControl(name, create, self.rank, self.world, words, box, tmo if create else 60.0)
+            except Exception as e:  # noqa: BLE001
+                log.warning("rank %d: shared-memory control segment %s unavailable: %r", self.rank, name, e)
+                return None
+
+        ctrl = open_segment(True) if self.rank == 0 else None
+        if not self._agree(ctrl is not None or self.rank != 0):
+            log.warning("rank %d: native transport unavailable -> python driver", self.rank)
+            return False
+        if self.rank != 0:
+            ctrl = open_segment(False)
+        if not self._agree(ctrl is not None):
+            log.warning("rank %d: native transport unavailable on some rank -> python driver", self.rank)
+            return False
+        self._ctrl = ctrl
         dev = self.ring.device.index if self.gpu else -1
         if self.gpu and dev is None:
             dev = torch.cuda.current_device()
@@ -185,6 +218,7 @@ class QueueEndpoint:
             self._engine.set_producer_finished()
         if self._consumer_closed:
             self._engine.set_consumer_closed()
+        return True
 
     @property
     def _failed(self) -> Optional[BaseException]:

@@ -6,9 +6,12 @@ import numpy as np
 import torch
 
 
-def transport_worker(rank, world, port, roles, n_events, policy, out_q, slow_rank=-1, mode="calib", xport="native"):
+def transport_worker(rank, world, port, roles, n_events, policy, out_q, slow_rank=-1, mode="calib", xport="native",
+                     shm_fail_rank=-1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["PSANA_RAY_XPORT"] = xport
+    if shm_fail_rank >= 0:
+        os.environ["PSANA_RAY_XPORT_TEST_FAIL_RANK"] = str(shm_fail_rank)
     os.environ["MASTER_PORT"] = str(port)
     try:
         from psana_ray_amd.models import Calibrator, Mode

@@ -12,11 +12,13 @@ from tests._mp_workers import dying_consumer_worker, transport_worker
 XPORTS = ["native", "python"]
 
 
-def _run(world, roles, n_events, policy, slow_rank=-1, mode="calib", timeout=120, xport="native"):
+def _run(world, roles, n_events, policy, slow_rank=-1, mode="calib", timeout=120, xport="native", shm_fail_rank=-1,
+         expect_xport=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    ps = [ctx.Process(target=transport_worker, args=(r, world, port, roles, n_events, policy, q, slow_rank, mode, xport))
+    ps = [ctx.Process(target=transport_worker, args=(r, world, port, roles, n_events, policy, q, slow_rank, mode, xport,
+                                                     shm_fail_rank))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -25,7 +27,7 @@ def _run(world, roles, n_events, policy, slow_rank=-1, mode="calib", timeout=120
         for _ in range(world):
             r, status, seen, bad, st = q.get(timeout=timeout)
             assert status == "ok", seen
-            assert st["xport_used"] == xport
+            assert st["xport_used"] == (expect_xport or xport)
             res[r] = (seen, bad, st)
     finally:
         for p in ps:
@@ -48,6 +50,15 @@ def test_two_ranks_exactly_once(native, policy, xport):
             assert idxs == sorted(idxs)
     if policy == "spread":
         assert res[0][2]["bytes_sent"] > 0 and res[1][2]["bytes_sent"] > 0
+
+
+@pytest.mark.parametrize("fail_rank", [0, 2])
+def test_shm_failure_falls_back_to_python_everywhere(native, fail_rank):
+    """The shared-memory segment cannot be created (rank 0) or attached (rank 2): every rank must
+    agree on the python driver and the stream still completes exactly once."""
+    res = _run(3, ["p", "pc", "c"], 12, "balanced", xport="native", shm_fail_rank=fail_rank, expect_xport="python")
+    allseen = [k for r in res for k in res[r][0]]
+    assert sorted(allseen) == sorted([(0, i) for i in range(6)] + [(1, i) for i in range(6)])
 
 
 @pytest.mark.parametrize("xport", XPORTS)
