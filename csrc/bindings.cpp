@@ -87,6 +87,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("roctx_push", [](const std::string& n) { pr::trace::push(n.c_str()); });
   m.def("roctx_pop", &pr::trace::pop);
   m.def("roctx_mark", [](const std::string& n) { pr::trace::mark(n.c_str()); });
+  m.def("gather_frames",
+        [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, int64_t nelem, bool bf16,
+           uint64_t stream) { pr::launch_gather_frames(make_ptrs(in, out), (int)in.size(), nelem, bf16, stream); },
+        py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("nelem"), py::arg("bf16"), py::arg("stream"));
   m.def("convert_u16_f32",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, int64_t npix, uint64_t stream) {
           pr::launch_convert_u16_f32(make_ptrs(in, out), (int)in.size(), npix, stream);

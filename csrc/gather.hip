@@ -1,0 +1,56 @@
+// Batch gather for training consumers: leased ring slots (scattered HBM frames) -> one contiguous
+// [n, *frame] batch tensor, optionally converted to bf16, in ONE launch.
+//
+// Reference parity: the reference's consumer receives one numpy frame per actor RPC
+// (psana_ray/data_reader.py:35) and the architecture figure feeds a "PyTorch Task" (PeakNet,
+// setup.py:11); a training step wants a contiguous batch.  Per-frame hipMemcpyAsync D2D would be
+// n blit launches; here one grid covers (chunks of the frame) x (frames), each lane moving 2 x 16 B
+// (nontemporal reads: the slot is released right after), and the bf16 variant halves the batch
+// bytes (round-to-nearest-even, NaN kept quiet) so the model's first layer reads half as much.
+#include "common.h"
+
+namespace pr {
+
+__device__ __forceinline__ uint32_t f32_to_bf16_bits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;   // NaN: keep it quiet
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void gather_frames_kernel(const FramePtrs fp, const int64_t n4) {
+  const int f = blockIdx.y;
+  const PR_GLOBAL f32x4_t* in = gin<f32x4_t>(fp.in[f]);
+  const int64_t q0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int64_t q = q0 + k;
+    if (q >= n4) return;
+    const f32x4_t v = ld_nt_f4(in + q);
+    if constexpr (BF16) {
+      u32x2_t o;
+      o.x = f32_to_bf16_bits(v.x) | (f32_to_bf16_bits(v.y) << 16);
+      o.y = f32_to_bf16_bits(v.z) | (f32_to_bf16_bits(v.w) << 16);
+      gout<u32x2_t>(fp.out[f])[q] = o;
+    } else {
+      gout<f32x4_t>(fp.out[f])[q] = v;
+    }
+  }
+}
+
+void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool bf16, uint64_t stream) {
+  check(nframes >= 1 && nframes <= kMaxFrames, "gather_frames: 1..32 frames per launch");
+  check(nelem > 0 && nelem % 4 == 0, "gather_frames: frame size must be a multiple of 4 elements");
+  for (int i = 0; i < nframes; ++i)
+    check(aligned16(fp.in[i]) && (fp.out[i] % (bf16 ? 8 : 16)) == 0, "gather_frames: misaligned frame");
+  const int64_t n4 = nelem / 4;
+  const dim3 grid((unsigned)((n4 + 511) / 512), (unsigned)nframes);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (bf16)
+    hipLaunchKernelGGL(gather_frames_kernel<true>, grid, dim3(256), 0, s, fp, n4);
+  else
+    hipLaunchKernelGGL(gather_frames_kernel<false>, grid, dim3(256), 0, s, fp, n4);
+  hip_check(hipGetLastError(), "gather_frames launch");
+}
+
+}  // namespace pr

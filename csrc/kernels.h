@@ -25,6 +25,7 @@ int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols, int max_cols = 0);
 void launch_convert_u16_f32(const FramePtrs& fp, int nframes, int64_t npix, uint64_t stream);
 void launch_read_f32(const FramePtrs& fp, int nframes, int64_t npix, int k, bool nt, uint64_t sums, uint64_t stream);
 void launch_xor_selftest(uint64_t out, uint64_t stream);
+void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool bf16, uint64_t stream);
 void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nout, uint64_t omask,
                      uint64_t stream);
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,

@@ -18,7 +18,8 @@ MI355X-native semantics:
   ``reader.done`` becomes True.
 * a dead peer raises ``DataReaderError("Queue peer is dead.")`` (data_reader.py:36-37).
 * ``close()`` releases only what this reader created (fixes Q-13).
-* ``lease()`` / ``read_batch()`` give zero-copy access to HBM slots for GPU consumers (H-9).
+* ``lease()`` / ``read_batch()`` give zero-copy access to HBM slots for GPU consumers (H-9);
+  ``batches()`` yields contiguous ``[B, *frame]`` tensors for PyTorch steps (``batching.py``).
 
 ``queue_name`` / ``ray_namespace`` may also name an in-process :mod:`cpu queue
 <psana_ray_amd.queue.cpu_queue>` created with ``create_queue`` (BASELINE config 1); it is used
@@ -224,6 +225,58 @@ class DataReader:
                 break
             out.append(it)
         return out
+
+    def batches(self, batch_size: int = 16, dtype: torch.dtype = torch.float32, timeout: float = 1.0,
+                drop_last: bool = False, stream=None):
+        """Yield :class:`~psana_ray_amd.batching.FrameBatch` es of ``batch_size`` frames (the last
+        one partial unless ``drop_last``) until the end of the stream.  HBM queues: the leased
+        slots are gathered into one new ``[n, *frame]`` tensor by a single HIP launch (bf16
+        conversion fused for ``dtype=torch.bfloat16``) and released stream-ordered."""
+        from .batching import collate_items
+
+        self._check()
+        if self._local is not None:
+            # in-process CPU queue (config 1): reference semantics have no end-of-stream marker
+            # (a None get is "empty", Q-2), so the iteration ends after `timeout` s without a frame
+            buf = []
+            while True:
+                item = self.read(timeout)
+                if item is None:
+                    if buf and not drop_last:
+                        yield self._batch_from_lists(buf, dtype)
+                    return
+                buf.append(item)
+                if len(buf) == batch_size:
+                    yield self._batch_from_lists(buf, dtype)
+                    buf = []
+        cal = self.calibrator
+        pending: List[FrameItem] = []
+        while True:
+            try:
+                got = self.read_batch(batch_size - len(pending), timeout)
+            except EndOfStream:
+                if pending and not drop_last:
+                    yield collate_items(pending, dtype, stream,
+                                        calibrate=(lambda its: self.calibrate(its, True, stream)) if cal else None)
+                elif pending:
+                    for it in pending:
+                        it.release(stream)
+                return
+            pending.extend(got)
+            if len(pending) == batch_size:
+                yield collate_items(pending, dtype, stream,
+                                    calibrate=(lambda its: self.calibrate(its, True, stream)) if cal else None)
+                pending = []
+
+    @staticmethod
+    def _batch_from_lists(items, dtype):
+        from .batching import FrameBatch
+
+        data = torch.stack([torch.as_tensor(it[2]) for it in items]).to(dtype)
+        pe = [float("nan") if it[3] is None else float(it[3]) for it in items]
+        r = torch.tensor([it[0] for it in items], dtype=torch.int64)
+        i = torch.tensor([it[1] for it in items], dtype=torch.int64)
+        return FrameBatch(data=data, rank=r, idx=i, gevt=torch.full_like(i, -1), photon_energy=torch.tensor(pe))
 
     def close(self):
         ep = self.endpoint

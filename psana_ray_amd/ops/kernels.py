@@ -143,3 +143,27 @@ def peakfind(frames: Sequence[torch.Tensor], shape, params, peaks: torch.Tensor,
         C.peakfind([_ptr(t) for t in frames[a:b]], P, H, W, float(params.thr_peak), float(params.son_min),
                    int(params.radius), int(params.max_peaks), _ptr(peaks[a]), _ptr(counts[a:]), _ptr(summary[a]), s,
                    0 if total is None else _ptr(total))
+
+
+def gather_frames(frames: Sequence[torch.Tensor], out: torch.Tensor, stream=None):
+    """Copy F leased f32 frames (scattered ring slots) into the contiguous batch ``out`` [F, ...]
+    (float32 or bfloat16: converted on the fly, round-to-nearest-even) with ONE launch per 32
+    frames (csrc/gather.hip)."""
+    C = _ext.load()
+    F = len(frames)
+    if F == 0:
+        return out
+    dev = frames[0].device
+    n = frames[0].numel()
+    _check_frames(frames, torch.float32, n, dev, "gather_frames in")
+    if out.device != dev or out.dtype not in (torch.float32, torch.bfloat16) or not out.is_contiguous():
+        raise ValueError("gather_frames: out must be a contiguous float32/bfloat16 tensor on the frames' device")
+    if out.shape[0] != F or out[0].numel() != n:
+        raise ValueError(f"gather_frames: out shape {tuple(out.shape)} does not hold {F} frames of {n} elements")
+    if n % 4 or out.data_ptr() % 16:
+        raise ValueError("gather_frames: frames must be multiples of 4 elements, out 16-B aligned")
+    bf16 = out.dtype == torch.bfloat16
+    s = _ext.stream_handle(stream)
+    for a, b in _chunks(F):
+        C.gather_frames([_ptr(t) for t in frames[a:b]], [_ptr(out[i]) for i in range(a, b)], n, bf16, s)
+    return out
