@@ -369,6 +369,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_cycled_source", &pr::ProducerEngine::set_cycled_source, py::arg("frames"), py::arg("photon_energy"))
       .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"), py::arg("k0") = 0)
       .def("set_file_source", &pr::ProducerEngine::set_file_source, py::arg("reader"), py::keep_alive<1, 2>())
+      .def("set_header_rank", &pr::ProducerEngine::set_header_rank, py::arg("rank"))
       .def("request_stop", &pr::ProducerEngine::request_stop)
       .def_property_readonly("device_resident", &pr::ProducerEngine::device_resident)
       .def("join", &pr::ProducerEngine::join, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())

@@ -76,7 +76,7 @@ ProducerEngine::ProducerEngine(SlotPool* pool, uint64_t ring_base, int64_t slot_
                                const CalibPlan& plan, int chunk, int n_raw_bufs, int64_t rank, int64_t size)
     : pool_(pool), ring_base_(ring_base), slot_bytes_(slot_bytes), device_(device), plan_(plan),
       chunk_(std::max(1, std::min(chunk, kMaxFrames))), n_raw_bufs_(std::max(2, n_raw_bufs)), rank_(rank),
-      size_(size) {
+      size_(size), hdr_rank_(rank) {
   check(pool != nullptr && device >= 0, "ProducerEngine needs a device SlotPool");
   check(plan.raw_frame_bytes > 0 && plan.raw_frame_bytes % 16 == 0, "ProducerEngine: bad raw frame size");
   hip_check(hipSetDevice(device_), "hipSetDevice");
@@ -359,7 +359,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       t_launch_ += secs(t2, t3);
       hdrs.resize(n);
       for (int q = 0; q < n; ++q) {
-        hdrs[q].rank = rank_;
+        hdrs[q].rank = hdr_rank_;
         hdrs[q].idx = k + q;
         if (file_ != nullptr) {
           hdrs[q].gevt = buf_meta_[b][q].first;

@@ -70,6 +70,10 @@ class ProducerEngine {
   // H2D copy runs; (gevt, photon energy) come from the records.  The reader must outlive the run.
   void set_file_source(RawRunReader* reader);
   bool device_resident() const { return device_resident_; }
+  // the `rank` field written into frame headers (default: the event-sharding rank).  Panel-sharded
+  // producers (SURVEY P-04) shard EVENTS over rank groups but tag frames with their own rank, so a
+  // consumer can tell the panel shard (rank % shards) apart from the event (gevt).
+  void set_header_rank(int64_t r) { hdr_rank_ = r; }
   // rank-local events [k0, n_local_events) (n_local_events < 0: endless), at most max_steps of them
   void start(int64_t n_local_events, int64_t max_steps, int64_t k0 = 0);
   void request_stop() { stop_.store(true); }
@@ -97,7 +101,7 @@ class ProducerEngine {
   CalibPlan plan_;
   int chunk_;
   int n_raw_bufs_;
-  int64_t rank_, size_;
+  int64_t rank_, size_, hdr_rank_;
   std::vector<uint64_t> src_frames_;
   std::vector<double> src_pe_;
   bool device_resident_ = false;   // source frames live in this GPU's HBM: no staging copies

@@ -6,9 +6,11 @@ wants ``[B, *frame]`` on the GPU: :func:`collate_items` gathers B leased HBM slo
 launch (csrc/gather.hip; bf16 conversion fused), then releases the slots stream-ordered, so the
 ring is recycled while the step runs.  :class:`FrameStream` wraps a :class:`DataReader` as a
 ``torch.utils.data.IterableDataset`` (use ``DataLoader(stream, batch_size=None)``).
+:class:`ShardAssembler` regroups the panel shards of ``--panel_shards`` producers into whole frames.
 """
 from __future__ import annotations
 
+import collections
 import math
 from dataclasses import dataclass
 from typing import Callable, Iterator, List, Optional
@@ -90,3 +92,75 @@ class FrameStream(torch.utils.data.IterableDataset):
                 if self.max_batches is not None and k >= self.max_batches:
                     break
                 yield b
+
+
+@dataclass
+class AssembledFrame:
+    gevt: int                     # global event id (shared by every shard of the event)
+    data: torch.Tensor            # [n_panels, H, W]: the whole frame
+    photon_energy: Optional[float]
+
+
+class ShardAssembler:
+    """Regroup panel shards (``--panel_shards G`` producers, source/shard.py) into whole frames.
+
+    Shard ``s = item.rank % G`` of event ``item.gevt`` holds panels ``[s*P/G, (s+1)*P/G)``.  Every
+    :meth:`add` copies its shards into their events' pending frames with ONE gather launch
+    (csrc/gather.hip, destinations = panel ranges of the frames) and releases the ring slots at
+    once, so incomplete events never pin queue slots.  Complete frames are returned in arrival
+    order.  A consumer sees every shard of an event when it is the only consumer (or the shards
+    are routed to it); ``max_pending`` bounds the frames waiting for missing shards."""
+
+    def __init__(self, n_shards: int, shard_shape, device=None, dtype: torch.dtype = torch.float32,
+                 max_pending: int = 256):
+        if n_shards < 1:
+            raise ValueError("n_shards must be >= 1")
+        self.n_shards = int(n_shards)
+        self.shard_shape = tuple(int(x) for x in shard_shape)
+        self.frame_shape = (self.shard_shape[0] * self.n_shards, *self.shard_shape[1:])
+        self.device = None if device is None else torch.device(device)
+        self.dtype = dtype
+        self.max_pending = int(max_pending)
+        self._pending: "collections.OrderedDict[int, list]" = collections.OrderedDict()
+        self._full = (1 << self.n_shards) - 1
+
+    @property
+    def pending(self) -> int:
+        return len(self._pending)
+
+    def add(self, items: List, stream=None) -> List[AssembledFrame]:
+        if not items:
+            return []
+        per = self.shard_shape[0]
+        srcs, dsts = [], []
+        for it in items:
+            if tuple(it.data.shape) != self.shard_shape:
+                raise ValueError(f"shard of shape {tuple(it.data.shape)}, expected {self.shard_shape}")
+            s = int(it.rank) % self.n_shards
+            e = self._pending.get(int(it.gevt))
+            if e is None:
+                if len(self._pending) >= self.max_pending:
+                    raise RuntimeError(f"{len(self._pending)} events wait for missing panel shards: are the "
+                                       f"shards routed to another consumer?")
+                dev = self.device or it.data.device
+                e = [torch.empty(self.frame_shape, dtype=self.dtype, device=dev), 0, it.photon_energy]
+                self._pending[int(it.gevt)] = e
+            if e[1] >> s & 1:
+                raise ValueError(f"duplicate shard {s} of event {it.gevt}")
+            e[1] |= 1 << s
+            srcs.append(it.data)
+            dsts.append(e[0][s * per:(s + 1) * per])
+        if srcs[0].device.type == "cuda" and srcs[0].dtype == torch.float32 and \
+                all(d.device == srcs[0].device for d in dsts):
+            kernels.gather_frames(srcs, dsts, stream)
+        else:
+            for a, d in zip(srcs, dsts):
+                d.copy_(a, non_blocking=True)
+        for it in items:
+            it.release(stream)
+        done = [g for g, e in self._pending.items() if e[1] == self._full]
+        return [AssembledFrame(g, *self._pop(g)) for g in done]
+
+    def _pop(self, g):
+        e = self._pending.pop(g)
+        return e[0], e[2]

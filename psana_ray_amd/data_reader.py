@@ -116,6 +116,7 @@ class DataReader:
                            max_offer=int(meta.extra.get("max_offer", 64)), is_producer=False, is_consumer=True)
         ep.start()
         self._sess, self._comm, self._queue = sess, comm, ep
+        self._panel_shards = meta.extra.get("panel_shards")
         recipe = meta.extra.get("calibrate_on_read")
         if recipe:
             self._calibrator = self._make_calibrator(recipe, device)
@@ -160,6 +161,29 @@ class DataReader:
                 for it in items:
                     it.release(stream)
         return out
+
+    @property
+    def panel_shards(self) -> int:
+        """G when the producers split frames into panel shards (``--panel_shards``), else 1."""
+        ps = getattr(self, "_panel_shards", None)
+        return int(ps["n_shards"]) if ps else 1
+
+    def panel_range(self, item) -> tuple:
+        """Panels ``[lo, hi)`` of the whole detector frame that ``item`` (a FrameItem or a reference
+        ``[rank, idx, data, pe]`` list) carries; the whole frame when frames are not sharded."""
+        rank = item.rank if hasattr(item, "rank") else int(item[0])
+        data = item.data if hasattr(item, "data") else item[2]
+        n = int(data.shape[0])
+        g = self.panel_shards
+        return ((rank % g) * n, (rank % g + 1) * n) if g > 1 else (0, n)
+
+    def shard_assembler(self, dtype: torch.dtype = torch.float32, max_pending: int = 256):
+        """A :class:`~psana_ray_amd.batching.ShardAssembler` for this session's panel shards."""
+        from .batching import ShardAssembler
+
+        self._check()
+        return ShardAssembler(self.panel_shards, self._queue.ring.frame_shape, self._queue.ring.device, dtype,
+                              max_pending)
 
     # ------------------------------------------------------------------------------------
     @property

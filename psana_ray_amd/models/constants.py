@@ -75,6 +75,14 @@ class CalibConstants:
                 cfg = np.full(shape, names.index(gain_config), np.uint8)
         return cls(spec, ped, gains, status, cfg, tuple(cmg))
 
+    def panel_subset(self, lo: int, hi: int) -> "CalibConstants":
+        """Constants of panels ``[lo, hi)`` (views; a panel shard of the frame, SURVEY P-04)."""
+        spec = self.spec.panel_subset(lo, hi)
+        if spec is self.spec:
+            return self
+        return CalibConstants(spec, self.pedestals[:, lo:hi], self.gains[:, lo:hi], self.status[lo:hi],
+                              None if self.gain_config is None else self.gain_config[lo:hi], tuple(self.cm_gains))
+
     # ------------------------------------------------------------------------------------
     def create_bad_pixel_mask(self) -> np.ndarray:
         """psana_wrapper.create_bad_pixel_mask() equivalent (producer.py:81): truthy = good."""

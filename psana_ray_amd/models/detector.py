@@ -80,6 +80,32 @@ class DetectorSpec:
     def n_asics(self) -> int:
         return self.n_panels * (self.panel_rows // self.asic_rows) * (self.panel_cols // self.asic_cols)
 
+    @property
+    def panel_pixels(self) -> int:
+        return self.panel_rows * self.panel_cols
+
+    def panel_subset(self, lo: int, hi: int) -> "DetectorSpec":
+        """The detector made of panels ``[lo, hi)``: same ASIC/bank geometry and gain family, so
+        every per-ASIC kernel (calibration, common mode) runs unchanged on a panel shard."""
+        if not 0 <= lo < hi <= self.n_panels:
+            raise ValueError(f"panel range [{lo}, {hi}) outside the {self.n_panels} panels of {self.name}")
+        if (lo, hi) == (0, self.n_panels):
+            return self
+        return DetectorSpec(f"{self.name}[{lo}:{hi}]", self.kind, hi - lo, self.panel_rows, self.panel_cols,
+                            self.asic_rows, self.asic_cols, self.bank_cols, self.pixel_size_um, self.panel_gap_px)
+
+
+def panel_shard_range(n_panels: int, shard: int, n_shards: int):
+    """Panels ``[lo, hi)`` of shard ``shard`` when a frame is split over ``n_shards`` ranks.  Shards
+    are equal (the queue carries one frame shape per session), so ``n_shards`` must divide the
+    panel count."""
+    if n_shards < 1 or n_panels % n_shards:
+        raise ValueError(f"--panel_shards {n_shards} must divide the detector's {n_panels} panels")
+    if not 0 <= shard < n_shards:
+        raise ValueError(f"panel shard {shard} outside [0, {n_shards})")
+    per = n_panels // n_shards
+    return shard * per, (shard + 1) * per
+
 
 _REGISTRY: Dict[str, DetectorSpec] = {}
 

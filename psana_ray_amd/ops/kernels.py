@@ -145,10 +145,11 @@ def peakfind(frames: Sequence[torch.Tensor], shape, params, peaks: torch.Tensor,
                    0 if total is None else _ptr(total))
 
 
-def gather_frames(frames: Sequence[torch.Tensor], out: torch.Tensor, stream=None):
-    """Copy F leased f32 frames (scattered ring slots) into the contiguous batch ``out`` [F, ...]
-    (float32 or bfloat16: converted on the fly, round-to-nearest-even) with ONE launch per 32
-    frames (csrc/gather.hip)."""
+def gather_frames(frames: Sequence[torch.Tensor], out, stream=None):
+    """Copy F leased f32 frames (scattered ring slots) into ``out``: a contiguous batch [F, ...]
+    or a list of F contiguous destination tensors (e.g. the panel ranges of assembled frames);
+    float32 or bfloat16 (converted on the fly, round-to-nearest-even).  ONE launch per 32 frames
+    (csrc/gather.hip)."""
     C = _ext.load()
     F = len(frames)
     if F == 0:
@@ -156,14 +157,25 @@ def gather_frames(frames: Sequence[torch.Tensor], out: torch.Tensor, stream=None
     dev = frames[0].device
     n = frames[0].numel()
     _check_frames(frames, torch.float32, n, dev, "gather_frames in")
-    if out.device != dev or out.dtype not in (torch.float32, torch.bfloat16) or not out.is_contiguous():
-        raise ValueError("gather_frames: out must be a contiguous float32/bfloat16 tensor on the frames' device")
-    if out.shape[0] != F or out[0].numel() != n:
-        raise ValueError(f"gather_frames: out shape {tuple(out.shape)} does not hold {F} frames of {n} elements")
-    if n % 4 or out.data_ptr() % 16:
-        raise ValueError("gather_frames: frames must be multiples of 4 elements, out 16-B aligned")
-    bf16 = out.dtype == torch.bfloat16
+    outs = list(out) if isinstance(out, (list, tuple)) else None
+    if outs is None:
+        if out.device != dev or out.dtype not in (torch.float32, torch.bfloat16) or not out.is_contiguous():
+            raise ValueError("gather_frames: out must be a contiguous float32/bfloat16 tensor on the frames' device")
+        if out.shape[0] != F or out[0].numel() != n:
+            raise ValueError(f"gather_frames: out shape {tuple(out.shape)} does not hold {F} frames of {n} elements")
+        odt = out.dtype
+        outs = [out[i] for i in range(F)]
+    else:
+        if len(outs) != F:
+            raise ValueError(f"gather_frames: {len(outs)} destinations for {F} frames")
+        odt = outs[0].dtype
+        if odt not in (torch.float32, torch.bfloat16):
+            raise ValueError("gather_frames: destinations must be float32/bfloat16")
+        _check_frames(outs, odt, n, dev, "gather_frames out")
+    if n % 4 or any(o.data_ptr() % 16 for o in outs):
+        raise ValueError("gather_frames: frames must be multiples of 4 elements, destinations 16-B aligned")
+    bf16 = odt == torch.bfloat16
     s = _ext.stream_handle(stream)
     for a, b in _chunks(F):
-        C.gather_frames([_ptr(t) for t in frames[a:b]], [_ptr(out[i]) for i in range(a, b)], n, bf16, s)
+        C.gather_frames([_ptr(t) for t in frames[a:b]], [_ptr(o) for o in outs[a:b]], n, bf16, s)
     return out

@@ -76,9 +76,13 @@ class ProducerPipeline:
             C = _ext.load()
             ring = endpoint.ring
             dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            # gevt = event_rank + k * size; a panel-sharded source (source/shard.py) shards events
+            # over rank GROUPS, while the headers keep this rank (its panel shard)
             self.engine = C.ProducerEngine(ring.pool, int(ring.storage.data_ptr()), ring.frame_bytes, dev_index,
-                                           calibrator.plan, self.chunk, n_raw_buffers, int(rank),
+                                           calibrator.plan, self.chunk, n_raw_buffers,
+                                           int(getattr(source, "event_rank", rank)),
                                            int(getattr(source, "size", 1)))
+            self.engine.set_header_rank(int(rank))
             if zero_copy is not None:
                 ptrs, pe = zero_copy
                 self._source_map = source._map       # keep the registered mapping alive

@@ -76,6 +76,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="seconds between metric summary lines (rates, queue depth); 0 disables")
     g.add_argument("--metrics_json", type=str, default=None, help="append per-interval metrics as JSON lines")
     g.add_argument("--metrics_port", type=int, default=None, help="Prometheus exporter port (if installed)")
+    g.add_argument("--panel_shards", type=int, default=1,
+                   help="split every frame's panels over groups of this many ranks (SP analog for Jungfrau-16M-"
+                        "scale frames): a group walks the same events, each rank stages/calibrates/queues 1/N "
+                        "of the panels; needs --calib or --mode raw (source/shard.py)")
     g.add_argument("--local", action="store_true",
                    help="single-process queue: no rendezvous; requires --consumer_task (no external consumers)")
     return parser
@@ -121,6 +125,9 @@ def load_masks(source, uses_bad_pixel_mask: bool, manual_mask_path: Optional[str
         mask = np.asarray(source.create_bad_pixel_mask()).astype(bool)
     if manual_mask_path is not None:
         manual = np.load(manual_mask_path).astype(bool)   # allow_pickle stays False
+        full = getattr(source, "full_spec", None)        # panel shard: a whole-detector mask is sliced
+        if full is not None and manual.shape == tuple(full.frame_shape):
+            manual = manual[source.lo:source.hi]
         if mask is None:
             mask = manual
         elif manual.shape == mask.shape:
@@ -192,8 +199,23 @@ def main(argv=None) -> int:
                       "or a co-located --consumer_task")
             return 2
         mode = Mode.raw   # frames travel raw; DataReader applies read_mode
-    source = open_source(args.exp, args.run, args.detector_name, rank=rank, size=size, n_events=args.num_events,
-                         pinned=device.type == "cuda", data_dir=args.data_dir)
+    shards = int(args.panel_shards)
+    if shards > 1:
+        from .source.shard import PanelShardSource, shard_layout
+
+        if read_mode == Mode.image or args.calibrate_on_read:
+            log.error("--panel_shards queues per-panel shards: use --calib (or --mode raw), without "
+                      "--calibrate_on_read (image assembly needs every panel of the frame)")
+            return 2
+        group, n_groups, shard = shard_layout(rank, size, shards)   # events over groups, panels within
+        source = open_source(args.exp, args.run, args.detector_name, rank=group, size=n_groups,
+                             n_events=args.num_events, pinned=device.type == "cuda", data_dir=args.data_dir)
+        source = PanelShardSource(source, shard, shards)
+        log.info("Rank %d: panel shard %d/%d (panels %d:%d) of event group %d/%d", rank, shard, shards, source.lo,
+                 source.hi, group, n_groups)
+    else:
+        source = open_source(args.exp, args.run, args.detector_name, rank=rank, size=size, n_events=args.num_events,
+                             pinned=device.type == "cuda", data_dir=args.data_dir)
     if args.start_event:
         if not hasattr(source, "seek"):
             log.error("--start_event: source %s cannot seek", type(source).__name__)
@@ -227,6 +249,10 @@ def main(argv=None) -> int:
             sess = initialize_queue(args.ray_address, args.ray_namespace, args.queue_name, args.queue_size, rank,
                                     size, n_consumer_ranks, frame_shape, dtype, device.type,
                                     extra={"route": args.route, "co_consumers": co_consumer,
+                                           "panel_shards": {"n_shards": shards,
+                                                            "n_panels": source.full_spec.n_panels,
+                                                            "detector_name": args.detector_name}
+                                           if shards > 1 else None,
                                            "calibrate_on_read": _read_recipe(args, read_mode, read_cm)
                                            if args.calibrate_on_read else None},
                                     timeout_s=args.timeout)
