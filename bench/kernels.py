@@ -157,6 +157,22 @@ def main(argv=None):
         report("calib_cm(rows)", timeit(lambda: calr.run(rl, ol), a.iters), F * npix * 6)
         calc = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams(flags=2))
         report("calib_cm(cols)", timeit(lambda: calc.run(rl, ol), a.iters), F * npix * 6)
+    if want("calib_cm_image") and spec.kind != "plain":
+        # image mode with common mode: fused (CM kernel writes the image from LDS + gap fill) vs
+        # two-pass (CM into frame-shaped scratch, then the LDS-tiled assembly); interleaved A/B
+        import os
+        cals = {}
+        for fused in ("1", "0"):
+            os.environ["PSANA_RAY_IMAGE_CM_FUSED"] = fused
+            cals[fused] = Calibrator(src.consts, dev, Mode.image, common_mode=CommonModeParams())
+        os.environ.pop("PSANA_RAY_IMAGE_CM_FUSED", None)
+        img = torch.empty((F, *cals["1"].out_shape), dtype=torch.float32, device=dev)
+        il = [img[i] for i in range(F)]
+        for rnd in range(2):
+            for fused in ("1", "0"):
+                c = cals[fused]
+                report(f"calib_cm_image({'fused' if fused == '1' else 'scratch + assemble'}) r{rnd}",
+                       timeit(lambda: c.run(rl, il), a.iters), F * npix * 6 + img.numel() // F * F * 4)
     if want("calib_image") and spec.kind != "plain":
         import os
         C = _ext.load()

@@ -358,7 +358,10 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("n_tiles", &pr::CalibPlan::n_tiles)
       .def_readwrite("tiles_x", &pr::CalibPlan::tiles_x)
       .def_readwrite("img_h", &pr::CalibPlan::img_h)
-      .def_readwrite("img_w", &pr::CalibPlan::img_w);
+      .def_readwrite("img_w", &pr::CalibPlan::img_w)
+      .def_readwrite("img_desc", &pr::CalibPlan::img_desc)
+      .def_readwrite("gap_runs", &pr::CalibPlan::gap_runs)
+      .def_readwrite("n_gap_runs", &pr::CalibPlan::n_gap_runs);
   m.def("run_calib_plan", &pr::run_calib_plan, py::arg("plan"), py::arg("in_ptrs"), py::arg("out_ptrs"),
         py::arg("stream"));
 

@@ -175,12 +175,95 @@ __device__ __forceinline__ void cm_block_coords(const TileGeom& tg, int& asic, i
   f = id % tg.nframes;
 }
 
+// Fused K-05 output (image mode with common mode).  Every panel is placed by an integer rotation
+// + translation (geometry.py), so pixel (y, x) of panel p lands at image element
+// desc[3p] + y * desc[3p+1] + x * desc[3p+2]; the corrected tile goes from LDS straight into the
+// assembled image instead of a frame-shaped scratch buffer that a second kernel re-reads
+// (saves a 2 x 8.65 MB HBM round trip per epix10k2M frame).  Gap pixels: launch_fill_runs.
+struct ImgOut {
+  const int32_t* desc;    // [n_panels][3] (base, step per panel row, step per panel column); nullptr: frame layout
+  const uint8_t* omask;   // image-shaped output mask (truthy keeps) or nullptr
+};
+
+// Phase 3 of both common-mode kernels: gain factor (+ folded frame mask) applied to the corrected
+// LDS tile; stored in frame layout (16-B stores) or, with io.desc, written into the image.  The
+// image walk keeps consecutive lanes on consecutive image elements: tile rows when the panel's
+// columns run along image rows (|sx| == 1), tile columns otherwise (column reads of the padded
+// tile are LDS-conflict-free: odd pitch).
+template <int NT>
+__device__ __forceinline__ void cm_store(float* tile, const uint32_t* nib, const float* __restrict__ gf,
+                                         const TileGeom& tg, int64_t base, PR_GLOBAL float* out, const ImgOut& io,
+                                         int panel, int y0, int x0, bool gather) {
+  const int R = tg.asic_rows, C = tg.asic_cols, LD = C + 1, C8 = C >> 3;
+  const int tid = threadIdx.x;
+  const bool img = io.desc != nullptr;
+  for (int i = tid; i < R * C8; i += blockDim.x) {
+    const int r = i / C8, c = (i % C8) * 8;
+    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
+    const uint32_t nb = nib[i];
+    uint32_t need = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) need |= 1u << ((nb >> (4 * j)) & 3u);
+    if (!gather) need = (1u << NT) - 1u;
+    float ga[NT][8];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if ((need >> k) & 1u) {
+        a = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix);
+        b = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix + 4);
+      }
+      ga[k][0] = a.x; ga[k][1] = a.y; ga[k][2] = a.z; ga[k][3] = a.w;
+      ga[k][4] = b.x; ga[k][5] = b.y; ga[k][6] = b.z; ga[k][7] = b.w;
+    }
+    float* trow = tile + r * LD + c;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t q = (nb >> (4 * j)) & 0xFu;
+      const int cand = q & 3;
+      float gg;
+      if constexpr (NT == 1) gg = ga[0][j];
+      else if constexpr (NT == 2) gg = bsel(cand != 0, ga[1][j], ga[0][j]);
+      else gg = bsel(cand == 0, ga[0][j], bsel(cand == 1, ga[1][j], ga[2][j]));
+      o[j] = (q & 4u) ? trow[j] * gg : 0.0f;
+    }
+    if (img) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) trow[j] = o[j];
+    } else {
+      PR_GLOBAL float4* op = (PR_GLOBAL float4*)(out + pix);
+      st_f4(op, make_float4(o[0], o[1], o[2], o[3]));
+      st_f4(op + 1, make_float4(o[4], o[5], o[6], o[7]));
+    }
+  }
+  if (!img) return;
+  __syncthreads();
+  const int32_t* d = io.desc + 3 * panel;
+  const int sy = d[1], sx = d[2];
+  const int64_t b0 = (int64_t)d[0] + (int64_t)y0 * sy + (int64_t)x0 * sx;
+  const int n = R * C;
+  const bool rows = sx == 1 || sx == -1;
+  const int inner = rows ? C : R;
+  const float inv = 1.0f / (float)inner;   // e < 2^24: floor((e + 0.5) / inner) is exact in f32
+  for (int e = tid; e < n; e += blockDim.x) {
+    const int a = (int)(((float)e + 0.5f) * inv);
+    const int bb = e - a * inner;
+    const int r = rows ? a : bb, c = rows ? bb : a;
+    const int64_t q = b0 + (int64_t)r * sy + (int64_t)c * sx;
+    float v = tile[r * LD + c];
+    if (io.omask != nullptr && !io.omask[q]) v = 0.0f;
+    out[q] = v;
+  }
+}
+
 // per-pixel nibble in LDS: bits0-1 candidate, bit2 good, bit3 cm-eligible
 template <int KIND>
 __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, const float* __restrict__ ped,
                                                         const float* __restrict__ gf,
                                                         const uint8_t* __restrict__ pflags,
-                                                        const TileGeom tg, const CmParams cp) {
+                                                        const TileGeom tg, const CmParams cp,
+                                                        const ImgOut io) {
   constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int R = tg.asic_rows, C = tg.asic_cols, LD = C + 1;
@@ -309,34 +392,7 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
   }
 
   // ---- phase 3: gain factor + mask, store -------------------------------------------------
-  for (int i = tid; i < R * C8; i += blockDim.x) {
-    const int r = i / C8, c = (i % C8) * 8;
-    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
-    const uint32_t nb = nib[i];
-    float ga[NT][8];
-#pragma unroll
-    for (int k = 0; k < NT; ++k) {
-      const float4 a = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix);
-      const float4 b = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix + 4);
-      ga[k][0] = a.x; ga[k][1] = a.y; ga[k][2] = a.z; ga[k][3] = a.w;
-      ga[k][4] = b.x; ga[k][5] = b.y; ga[k][6] = b.z; ga[k][7] = b.w;
-    }
-    const float* trow = tile + r * LD + c;
-    float o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t q = (nb >> (4 * j)) & 0xFu;
-      const int cand = q & 3;
-      float gg;
-      if constexpr (NT == 1) gg = ga[0][j];
-      else if constexpr (NT == 2) gg = bsel(cand != 0, ga[1][j], ga[0][j]);
-      else gg = bsel(cand == 0, ga[0][j], bsel(cand == 1, ga[1][j], ga[2][j]));
-      o[j] = (q & 4u) ? trow[j] * gg : 0.0f;
-    }
-    PR_GLOBAL float4* op = (PR_GLOBAL float4*)(out + pix);
-    st_f4(op, make_float4(o[0], o[1], o[2], o[3]));
-    st_f4(op + 1, make_float4(o[4], o[5], o[6], o[7]));
-  }
+  cm_store<NT>(tile, nib, gf, tg, base, out, io, panel, ar * R, ac * C, false);
 }
 
 
@@ -400,7 +456,8 @@ template <int KIND, int L, int M, int BLOCK, int CQ>
 __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
                                                             const float* __restrict__ gf,
                                                             const uint8_t* __restrict__ pflags,
-                                                            const TileGeom tg, const CmParams cp) {
+                                                            const TileGeom tg, const CmParams cp,
+                                                            const ImgOut io) {
   constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int R = tg.asic_rows, C = tg.asic_cols, LD = C + 1;
@@ -674,41 +731,7 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
   }
 
   // ---- phase 3: gain factor + mask, store ---------------------------------------------------
-  for (int i = tid; i < R * C8; i += blockDim.x) {
-    const int r = i / C8, c = (i % C8) * 8;
-    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
-    const uint32_t nb = nib[i];
-    uint32_t need = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) need |= 1u << ((nb >> (4 * j)) & 3u);
-    if (!cp.gather) need = (1u << NT) - 1u;
-    float ga[NT][8];
-#pragma unroll
-    for (int k = 0; k < NT; ++k) {
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-      if ((need >> k) & 1u) {
-        a = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix);
-        b = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix + 4);
-      }
-      ga[k][0] = a.x; ga[k][1] = a.y; ga[k][2] = a.z; ga[k][3] = a.w;
-      ga[k][4] = b.x; ga[k][5] = b.y; ga[k][6] = b.z; ga[k][7] = b.w;
-    }
-    const float* trow = tile + r * LD + c;
-    float o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t q = (nb >> (4 * j)) & 0xFu;
-      const int cand = q & 3;
-      float gg;
-      if constexpr (NT == 1) gg = ga[0][j];
-      else if constexpr (NT == 2) gg = bsel(cand != 0, ga[1][j], ga[0][j]);
-      else gg = bsel(cand == 0, ga[0][j], bsel(cand == 1, ga[1][j], ga[2][j]));
-      o[j] = (q & 4u) ? trow[j] * gg : 0.0f;
-    }
-    PR_GLOBAL float4* op = (PR_GLOBAL float4*)(out + pix);
-    st_f4(op, make_float4(o[0], o[1], o[2], o[3]));
-    st_f4(op + 1, make_float4(o[4], o[5], o[6], o[7]));
-  }
+  cm_store<NT>(tile, nib, gf, tg, base, out, io, panel, ar * R, ac * C, cp.gather != 0);
 }
 
 // PSANA_RAY_CM_GENERIC=1 forces the generic wave-bitonic kernel (A/B benchmarking, read per launch)
@@ -737,7 +760,7 @@ int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols, int max_cols) {
 void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t pflags,
                      int kind, int n_panels, int panel_rows, int panel_cols, int asic_rows,
                      int asic_cols, float thr, float maxcorr, int npix_min, int flags,
-                     int bank_cols, uint64_t stream) {
+                     int bank_cols, uint64_t stream, uint64_t img_desc, uint64_t img_omask) {
   check(nframes >= 1 && nframes <= kMaxFrames, "calib_cm: nframes out of range");
   check(asic_rows >= 1 && asic_rows <= 256, "calib_cm: ASIC rows must be in [1, 256]");
   check(asic_cols % 8 == 0 && asic_cols >= 8, "calib_cm: ASIC cols must be a multiple of 8");
@@ -772,6 +795,8 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   check(aligned16(ped) && aligned16(gf) && (pflags & 7) == 0, "calib_cm: misaligned constant tables");
   for (int f = 0; f < nframes; ++f)
     check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_cm: frame buffers must be 16-B aligned");
+  const ImgOut io{reinterpret_cast<const int32_t*>(img_desc), reinterpret_cast<const uint8_t*>(img_omask)};
+  check(img_omask == 0 || img_desc != 0, "calib_cm: an image mask needs the image output map");
   TileGeom tg;
   tg.panel_rows = panel_rows;
   tg.panel_cols = panel_cols;
@@ -807,7 +832,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
       (cq_req == 0 || cq_req == CQ_) && B_ == (narrow ? 256 : 512) * (CQ_ / 2) && !cm_force_generic()) {  \
     hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_>,             \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");   \
-    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_>), grid, dim3(B_), lds, s, fp, P, G, F, tg, cp); \
+    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_>), grid, dim3(B_), lds, s, fp, P, G, F, tg, cp, io); \
     done = true;                                                                                      \
   }
   PR_CM_NET(kEpix10ka, 48, 44, 512, 4)
@@ -826,17 +851,17 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
     case kEpix10ka:
       hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kEpix10ka>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
-      hipLaunchKernelGGL(calib_cm_kernel<kEpix10ka>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp);
+      hipLaunchKernelGGL(calib_cm_kernel<kEpix10ka>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp, io);
       break;
     case kJungfrau:
       hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kJungfrau>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
-      hipLaunchKernelGGL(calib_cm_kernel<kJungfrau>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp);
+      hipLaunchKernelGGL(calib_cm_kernel<kJungfrau>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp, io);
       break;
     case kPlain:
       hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kPlain>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
-      hipLaunchKernelGGL(calib_cm_kernel<kPlain>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp);
+      hipLaunchKernelGGL(calib_cm_kernel<kPlain>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp, io);
       break;
     default: check(false, "calib_cm: unknown gain kind");
   }

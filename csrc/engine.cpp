@@ -47,6 +47,15 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
         else
           launch_calib_image(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.npix, p.kind, p.idx, p.nout, stream);
         break;
+      case kPlanImageCm: {
+        check(p.use_cm && p.img_desc != 0, "run_calib_plan: fused image plan without common mode / placement");
+        const FramePtrs fp = ptrs_of(in, out, a, b);
+        launch_calib_cm(fp, n, p.ped, p.gf, p.pflags, p.kind, p.n_panels, p.panel_rows, p.panel_cols, p.asic_rows,
+                        p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags, p.bank_cols, stream, p.img_desc,
+                        p.omask);
+        launch_fill_runs(fp, n, p.gap_runs, p.n_gap_runs, stream);
+        break;
+      }
       case kPlanImageScratch: {
         check(p.scratch != 0, "run_calib_plan: image plan without scratch");
         std::vector<uint64_t> tmp(n);

@@ -27,7 +27,8 @@ enum PlanMode : int {
   kPlanCalib = 1,       // K-01/02/04
   kPlanCalibCm = 2,     // K-01..K-04 with K-03 common mode
   kPlanImageFused = 3,  // K-01/02/04 evaluated at image positions (no scratch)
-  kPlanImageScratch = 4 // calib (+cm if use_cm) into scratch, then K-05 assemble (+image mask)
+  kPlanImageScratch = 4, // calib (+cm if use_cm) into scratch, then K-05 assemble (+image mask)
+  kPlanImageCm = 5       // common-mode kernel writing the assembled image directly + gap fill
 };
 
 struct CalibPlan {
@@ -47,6 +48,9 @@ struct CalibPlan {
   int use_tiles = 0;
   uint64_t tiles = 0, codes = 0;
   int n_tiles = 0, tiles_x = 0, img_h = 0, img_w = 0;
+  // kPlanImageCm: per-panel (base, row step, col step) image placement + gap runs (int2 start, len)
+  uint64_t img_desc = 0, gap_runs = 0;
+  int n_gap_runs = 0;
   int64_t raw_frame_bytes = 0;
   int64_t out_frame_bytes = 0;
 };

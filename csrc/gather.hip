@@ -53,4 +53,27 @@ void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool 
   hip_check(hipGetLastError(), "gather_frames launch");
 }
 
+// Zero fill of fixed element runs in every output frame (the gaps between panels of an image
+// written by the fused common-mode kernel).  One wave per run (host splits runs to <= 1024
+// elements so the waves are balanced), consecutive lanes on consecutive elements.
+__global__ __launch_bounds__(256) void fill_runs_kernel(const FramePtrs fp, const int2* __restrict__ runs,
+                                                        const int n_runs) {
+  const int w = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= n_runs) return;
+  const int2 rr = runs[w];
+  PR_GLOBAL float* out = gout<float>(fp.out[blockIdx.y]);
+  for (int k = lane; k < rr.y; k += 64) out[(int64_t)rr.x + k] = 0.0f;
+}
+
+void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_runs, uint64_t stream) {
+  check(nframes >= 1 && nframes <= kMaxFrames, "fill_runs: 1..32 frames per launch");
+  if (n_runs <= 0) return;
+  check(runs % 8 == 0, "fill_runs: misaligned run table");
+  const dim3 grid((unsigned)((n_runs + 3) / 4), (unsigned)nframes);
+  hipLaunchKernelGGL(fill_runs_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), fp,
+                     reinterpret_cast<const int2*>(runs), n_runs);
+  hip_check(hipGetLastError(), "fill_runs launch");
+}
+
 }  // namespace pr

@@ -13,7 +13,8 @@ void launch_calib_image(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t
                         uint64_t idx, int64_t nout, uint64_t stream);
 void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t pflags, int kind,
                      int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
-                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream);
+                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream,
+                     uint64_t img_desc = 0, uint64_t img_omask = 0);   // img_desc: fused K-05 (ImgOut)
 size_t cm_lds_bytes(int asic_rows, int asic_cols);
 void launch_image_tiles(const FramePtrs& fp, int nframes, bool calib, int kind, uint64_t ped, uint64_t gf,
                         int64_t npix, int panel_rows, int panel_cols, uint64_t tiles, int n_tiles, int tiles_x,
@@ -25,6 +26,7 @@ int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols, int max_cols = 0);
 void launch_convert_u16_f32(const FramePtrs& fp, int nframes, int64_t npix, uint64_t stream);
 void launch_read_f32(const FramePtrs& fp, int nframes, int64_t npix, int k, bool nt, uint64_t sums, uint64_t stream);
 void launch_xor_selftest(uint64_t out, uint64_t stream);
+void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_runs, uint64_t stream);
 void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool bf16, uint64_t stream);
 void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nout, uint64_t omask,
                      uint64_t stream);

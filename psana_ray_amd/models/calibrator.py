@@ -156,8 +156,18 @@ class Calibrator:
                 p.tiles, p.codes = int(self._tiles.data_ptr()), int(self._codes.data_ptr())
                 p.n_tiles, p.tiles_x = tm.n_tiles, tm.tiles_x
                 p.img_h, p.img_w = tm.image_shape
+            place = self.geometry.panel_placement() if self.cm is not None else None
             if self.cm is None and (self.omask is None or self.tile_map is not None):
                 p.mode = 3
+            elif place is not None and os.environ.get("PSANA_RAY_IMAGE_CM_FUSED", "1") != "0":
+                # common mode writes the assembled image from its LDS tiles (no scratch round trip);
+                # a fill kernel zeroes the gaps between panels
+                p.mode = 5
+                self._img_desc = torch.from_numpy(place.ravel().copy()).to(self.device)
+                self._gap_runs = torch.from_numpy(self.geometry.gap_runs().ravel().copy()).to(self.device)
+                p.img_desc, p.gap_runs = int(self._img_desc.data_ptr()), int(self._gap_runs.data_ptr())
+                p.n_gap_runs = int(self._gap_runs.numel() // 2)
+                p.omask = 0 if self.omask is None else int(self.omask.data_ptr())
             else:
                 p.mode = 4
                 self._scratch = torch.empty((kernels.MAX_FRAMES, *spec.frame_shape), dtype=torch.float32,

@@ -46,6 +46,39 @@ class Geometry:
         idx[dst] = np.arange(self.spec.npix, dtype=np.int32)
         return idx
 
+    def panel_placement(self):
+        """``[P, 3]`` int32 (base, step per panel row, step per panel column) such that pixel
+        ``(y, x)`` of panel ``p`` lands at flat image element ``base + y*sy + x*sx``, or None when a
+        panel is not placed by an integer rotation + translation (then the fused common-mode image
+        kernel does not apply and the two-pass path is used)."""
+        himg, wimg = self.image_shape
+        P, H, W = self.rows.shape
+        out = np.zeros((P, 3), np.int64)
+        yy, xx = np.meshgrid(np.arange(H, dtype=np.int64), np.arange(W, dtype=np.int64), indexing="ij")
+        for p in range(P):
+            idx = self.rows[p].astype(np.int64) * wimg + self.cols[p]
+            b = int(idx[0, 0])
+            sy = int(idx[1, 0] - b) if H > 1 else wimg
+            sx = int(idx[0, 1] - b) if W > 1 else 1
+            if sorted((abs(sy), abs(sx))) != sorted((1, wimg)) or not np.array_equal(idx, b + yy * sy + xx * sx):
+                return None
+            out[p] = (b, sy, sx)
+        if himg * wimg >= 2 ** 31:
+            return None
+        return out.astype(np.int32)
+
+    def gap_runs(self, max_len: int = 1024) -> np.ndarray:
+        """``[n, 2]`` int32 (start, length) runs of flat image elements no panel pixel covers,
+        split to at most ``max_len`` elements (one GPU wave zero-fills one run)."""
+        gap = (self.index_map() < 0).astype(np.int8)
+        d = np.diff(np.concatenate([[0], gap, [0]]))
+        starts, ends = np.where(d == 1)[0], np.where(d == -1)[0]
+        runs = []
+        for a, e in zip(starts.tolist(), ends.tolist()):
+            for s0 in range(a, e, max_len):
+                runs.append((s0, min(max_len, e - s0)))
+        return np.asarray(runs, np.int32).reshape(-1, 2)
+
     def pixel_coords_um(self):
         """(x, y) pixel-centre coordinates in micrometres (psana-style geometry output)."""
         ps = self.spec.pixel_size_um

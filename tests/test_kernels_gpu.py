@@ -91,19 +91,26 @@ def test_common_mode_even_odd_and_empty_segments(cuda_device):
     _assert_equal(out, ref, "cm edge cases")
 
 
-@pytest.mark.parametrize("version", ["tiles", "tiles256", "v1"])
+@pytest.mark.parametrize("version", ["tiles", "tiles256", "v1", "nofuse"])
 @pytest.mark.parametrize("det,cm", [("tiny_epix", None), ("tiny_epix", "3,30,50,5"), ("epix10k2M", None),
-                                    ("epix10k2M", "default"), ("tiny_jungfrau", None), ("jungfrau05M", None),
-                                    ("tiny_plain", None)])
+                                    ("epix10k2M", "default"), ("tiny_jungfrau", None), ("tiny_jungfrau", "default"),
+                                    ("jungfrau05M", None), ("jungfrau05M", "default"), ("tiny_plain", None)])
 def test_image_mode_matches_scatter(cuda_device, det, cm, version, monkeypatch):
+    """With common mode the default plan is the fused kernel (image written from the LDS tiles,
+    gaps zero-filled); "nofuse" is the two-pass scratch path.  Outputs start as NaN so unwritten
+    (gap) pixels show up."""
     monkeypatch.setenv("PSANA_RAY_IMAGE_V1", "1" if version == "v1" else "0")
     monkeypatch.setenv("PSANA_RAY_IMAGE_BLOCK", "256" if version == "tiles256" else "")
+    monkeypatch.setenv("PSANA_RAY_IMAGE_CM_FUSED", "0" if version == "nofuse" else "1")
     n = 2 if det in ("epix10k2M", "jungfrau05M") else 37   # 37 > 32: launch chunking
     spec, consts, raw = _setup(det, n, seed=21)
     cmp = CommonModeParams.parse(cm)
     cal = Calibrator(consts, cuda_device, Mode.image, common_mode=cmp)
     assert (cal.tile_map is not None) == (version != "v1")
-    out = cal(raw.to(cuda_device))
+    assert (cal.plan.mode == 5) == (cm is not None and version != "nofuse")
+    out = torch.full((n, *cal.out_shape), float("nan"), device=cuda_device)
+    raw = raw.to(cuda_device)
+    cal.run([raw[i] for i in range(n)], [out[i] for i in range(n)])
     torch.cuda.synchronize()
     geo = cal.geometry
     calib = reference.calibrate_reference(raw.to(torch.int32), consts, None, cal.cm)
@@ -112,10 +119,11 @@ def test_image_mode_matches_scatter(cuda_device, det, cm, version, monkeypatch):
     _assert_equal(out, ref, f"image {det}")
 
 
-@pytest.mark.parametrize("version", ["tiles", "v1"])
+@pytest.mark.parametrize("version", ["tiles", "v1", "nofuse"])
 @pytest.mark.parametrize("det,cm", [("tiny_epix", None), ("epix10k2M", None), ("epix10k2M", "default")])
 def test_image_mask_applied_after_assembly(cuda_device, det, cm, version, monkeypatch):
     monkeypatch.setenv("PSANA_RAY_IMAGE_V1", "1" if version == "v1" else "0")
+    monkeypatch.setenv("PSANA_RAY_IMAGE_CM_FUSED", "0" if version == "nofuse" else "1")
     spec, consts, raw = _setup(det, 3, seed=4)
     geo = make_geometry(spec)
     imask = (np.random.default_rng(1).random(geo.image_shape) > 0.3).astype(np.uint8)
