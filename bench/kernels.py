@@ -157,6 +157,16 @@ def main(argv=None):
         report("calib_cm(rows)", timeit(lambda: calr.run(rl, ol), a.iters), F * npix * 6)
         calc = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams(flags=2))
         report("calib_cm(cols)", timeit(lambda: calc.run(rl, ol), a.iters), F * npix * 6)
+    if want("calib_cm_constdims"):
+        # compile-time tile shape (immediate LDS offsets, 96 vs 124 VGPRs) vs runtime shape; interleaved
+        import os
+        calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
+        for rnd in range(2):
+            for cd in ("1", "0"):
+                os.environ["PSANA_RAY_CM_CONSTDIMS"] = cd
+                report(f"calib_cm(rows+cols, compile-time tile shape={cd}) r{rnd}",
+                       timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
+        os.environ.pop("PSANA_RAY_CM_CONSTDIMS", None)
     if want("calib_cm_image") and spec.kind != "plain":
         # image mode with common mode: fused (CM kernel writes the image from LDS + gap fill) vs
         # two-pass (CM into frame-shaped scratch, then the LDS-tiled assembly); interleaved A/B

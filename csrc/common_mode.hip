@@ -192,9 +192,10 @@ struct ImgOut {
 // tile are LDS-conflict-free: odd pitch).
 template <int NT>
 __device__ __forceinline__ void cm_store(float* tile, const uint32_t* nib, const float* __restrict__ gf,
-                                         const TileGeom& tg, int64_t base, PR_GLOBAL float* out, const ImgOut& io,
-                                         int panel, int y0, int x0, bool gather) {
-  const int R = tg.asic_rows, C = tg.asic_cols, LD = C + 1, C8 = C >> 3;
+                                         const TileGeom& tg, const int R, const int C, int64_t base,
+                                         PR_GLOBAL float* out, const ImgOut& io, int panel, int y0, int x0,
+                                         bool gather) {
+  const int LD = C + 1, C8 = C >> 3;
   const int tid = threadIdx.x;
   const bool img = io.desc != nullptr;
   for (int i = tid; i < R * C8; i += blockDim.x) {
@@ -392,7 +393,7 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
   }
 
   // ---- phase 3: gain factor + mask, store -------------------------------------------------
-  cm_store<NT>(tile, nib, gf, tg, base, out, io, panel, ar * R, ac * C, false);
+  cm_store<NT>(tile, nib, gf, tg, R, C, base, out, io, panel, ar * R, ac * C, false);
 }
 
 
@@ -452,7 +453,11 @@ __device__ __forceinline__ void bitonic_merge_vpad(float (&z)[N]) {
   }
 }
 
-template <int KIND, int L, int M, int BLOCK, int CQ>
+// TR / TC: the tile (stripe) rows / columns as compile-time constants for the production shapes
+// (0 = read from TileGeom).  With constants every LDS address in the unrolled median loops is a
+// base VGPR + immediate offset; with runtime dims the compiler kept i*LD / i*C8 for all unrolled
+// i as SGPRs, spilled them to VGPR lanes and re-read them with v_readlane + v_mul_lo per access.
+template <int KIND, int L, int M, int BLOCK, int CQ, int TR = 0, int TC = 0>
 __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
                                                             const float* __restrict__ gf,
                                                             const uint8_t* __restrict__ pflags,
@@ -460,7 +465,7 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
                                                             const ImgOut io) {
   constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int R = tg.asic_rows, C = tg.asic_cols, LD = C + 1;
+  const int R = TR ? TR : tg.asic_rows, C = TC ? TC : tg.asic_cols, LD = C + 1;
   float* tile = reinterpret_cast<float*>(smem);
   uint32_t* nib = reinterpret_cast<uint32_t*>(smem + (((size_t)R * LD * 4 + 15) & ~(size_t)15));
   const int C8 = C >> 3;
@@ -538,13 +543,25 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
       const int b = sgi / R, r = sgi % R;           // consecutive lanes -> consecutive rows: no bank conflicts
       float* seg = tile + r * LD + b * L;
       const uint32_t* nrow = nib + r * C8;
+      // L % 8 == 0: the segment's eligibility bits are L/8 whole nibble words, read once and
+      // indexed by compile-time j in both loops below
+      constexpr int NW = (L % 8 == 0) ? L / 8 : 1;
+      uint32_t nw[NW];
+      if constexpr (L % 8 == 0) {
+#pragma unroll
+        for (int k = 0; k < NW; ++k) nw[k] = nrow[(b * L >> 3) + k];
+      }
+      auto elig = [&](int j) -> bool {
+        if constexpr (L % 8 == 0) return (nw[j >> 3] >> (4 * (j & 7) + 3)) & 1u;
+        const int col = b * L + j;
+        return (nrow[col >> 3] >> (4 * (col & 7) + 3)) & 1u;
+      };
       float x[L];
       int cnt = 0;
 #pragma unroll
       for (int j = 0; j < L; ++j) {
-        const int col = b * L + j;
         const float v = seg[j];
-        const bool el = (nrow[col >> 3] >> (4 * (col & 7) + 3)) & 1u;
+        const bool el = elig(j);
         const bool pt = el && (fabsf(v) < cp.thr);
         cnt += pt ? 1 : 0;
         x[j] = pt ? v : QNAN;
@@ -573,10 +590,8 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
       const float med = (s_lo + s_hi) * 0.5f;
       if (cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
 #pragma unroll
-        for (int j = 0; j < L; ++j) {
-          const int col = b * L + j;
-          if ((nrow[col >> 3] >> (4 * (col & 7) + 3)) & 1u) seg[j] -= med;
-        }
+        for (int j = 0; j < L; ++j)
+          if (elig(j)) seg[j] -= med;
       }
     }
     __syncthreads();
@@ -598,14 +613,17 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
         const int q = w & 3;
         const bool lower = (q & 1) == 0;
         const uint32_t shift = 4 * (c & 7) + 3;
+        // per-lane base addresses; the unrolled i then becomes an immediate LDS offset (i * LD,
+        // i * C8 are constants for compile-time tile shapes)
+        float* colp = tile + (q * M) * LD + c;
+        const uint32_t* nibp = nib + (q * M) * C8 + (c >> 3);
         float x[M];
         int my_cnt = 0;
 #pragma unroll
         for (int i = 0; i < M; ++i) {
-          const int r = q * M + i;
-          const bool in = act && r < R;
-          const float v = in ? tile[r * LD + c] : 0.0f;
-          const bool el = in && ((nib[r * C8 + (c >> 3)] >> shift) & 1u);
+          const bool in = act && q * M + i < R;
+          const float v = in ? colp[i * LD] : 0.0f;
+          const bool el = in && ((nibp[i * C8] >> shift) & 1u);
           const bool pt = el && (fabsf(v) < cp.thr);
           my_cnt += pt ? 1 : 0;
           x[i] = pt ? v : QNAN;
@@ -661,8 +679,7 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
         if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
 #pragma unroll
           for (int i = 0; i < M; ++i) {
-            const int r = q * M + i;
-            if (r < R && ((nib[r * C8 + (c >> 3)] >> shift) & 1u)) tile[r * LD + c] -= med;
+            if (q * M + i < R && ((nibp[i * C8] >> shift) & 1u)) colp[i * LD] -= med;
             if ((i & 15) == 15) asm volatile("" ::: "memory");
           }
         }
@@ -731,7 +748,7 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
   }
 
   // ---- phase 3: gain factor + mask, store ---------------------------------------------------
-  cm_store<NT>(tile, nib, gf, tg, base, out, io, panel, ar * R, ac * C, cp.gather != 0);
+  cm_store<NT>(tile, nib, gf, tg, R, C, base, out, io, panel, ar * R, ac * C, cp.gather != 0);
 }
 
 // PSANA_RAY_CM_GENERIC=1 forces the generic wave-bitonic kernel (A/B benchmarking, read per launch)
@@ -827,14 +844,22 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   int cq_req = 0;
   if (const char* e = getenv("PSANA_RAY_CM_COLQ"); e && *e) cq_req = atoi(e);
   const int M2 = (asic_rows + 1) / 2, M4 = (asic_rows + 3) / 4;
-#define PR_CM_NET(KIND_, L_, M_, B_, CQ_)                                                              \
+  // PSANA_RAY_CM_CONSTDIMS=0 skips the compile-time-shape instantiations (A/B)
+  const char* cd = getenv("PSANA_RAY_CM_CONSTDIMS");
+  const bool const_dims = !(cd != nullptr && cd[0] == '0');
+#define PR_CM_NET_T(KIND_, L_, M_, B_, CQ_, TR_, TC_)                                                   \
   if (!done && kind == KIND_ && bank_cols == L_ && (CQ_ == 4 ? M4 : M2) == M_ &&                        \
-      (cq_req == 0 || cq_req == CQ_) && B_ == (narrow ? 256 : 512) * (CQ_ / 2) && !cm_force_generic()) {  \
-    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_>,             \
+      (cq_req == 0 || cq_req == CQ_) && B_ == (narrow ? 256 : 512) * (CQ_ / 2) && !cm_force_generic() && \
+      ((TR_ == 0 && TC_ == 0) || (const_dims && TR_ == asic_rows && TC_ == asic_cols))) {               \
+    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_, TR_, TC_>,   \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");   \
-    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_>), grid, dim3(B_), lds, s, fp, P, G, F, tg, cp, io); \
+    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_, TR_, TC_>), grid, dim3(B_), lds, s, fp, P, G, \
+                       F, tg, cp, io);                                                                \
     done = true;                                                                                      \
   }
+#define PR_CM_NET(KIND_, L_, M_, B_, CQ_) PR_CM_NET_T(KIND_, L_, M_, B_, CQ_, 0, 0)
+  PR_CM_NET_T(kEpix10ka, 48, 44, 512, 4, 176, 96)    // epix10k2M: 176x96 stripes
+  PR_CM_NET_T(kJungfrau, 64, 64, 512, 4, 256, 128)   // Jungfrau: 256x128 stripes
   PR_CM_NET(kEpix10ka, 48, 44, 512, 4)
   PR_CM_NET(kEpix10ka, 48, 44, 1024, 4)
   PR_CM_NET(kEpix10ka, 48, 88, 512, 2)
@@ -846,6 +871,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   PR_CM_NET(kPlain, 32, 64, 256, 2)
   PR_CM_NET(kPlain, 8, 4, 256, 2)
 #undef PR_CM_NET
+#undef PR_CM_NET_T
   if (!done) {
   switch (kind) {
     case kEpix10ka:
