@@ -167,6 +167,15 @@ def main(argv=None):
                 report(f"calib_cm(rows+cols, compile-time tile shape={cd}) r{rnd}",
                        timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
         os.environ.pop("PSANA_RAY_CM_CONSTDIMS", None)
+    if want("calib_cm_stripes"):
+        import os
+        calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
+        for rnd in range(2):
+            for st in ("96", "48"):
+                os.environ["PSANA_RAY_CM_STRIPE"] = st
+                report(f"calib_cm(rows+cols, stripe={st or 'default'}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
+                       F * npix * 6)
+        os.environ.pop("PSANA_RAY_CM_STRIPE", None)
     if want("calib_cm_image") and spec.kind != "plain":
         # image mode with common mode: fused (CM kernel writes the image from LDS + gap fill) vs
         # two-pass (CM into frame-shaped scratch, then the LDS-tiled assembly); interleaved A/B

@@ -803,6 +803,12 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
         break;
       }
   }
+  // PSANA_RAY_CM_CONSTDIMS=0 skips the compile-time-shape instantiations (A/B)
+  const char* cd = getenv("PSANA_RAY_CM_CONSTDIMS");
+  const bool const_dims = !(cd != nullptr && cd[0] == '0');
+  // epix10k2M with the compile-time kernels: one-bank 176x48 stripes on 256-thread blocks, four
+  // per CU (8.78 vs 9.16 us/frame for 176x96; profiles/kernels_r1_cm_stripes48.jsonl)
+  if (const_dims && kind == kEpix10ka && bank_cols == 48 && asic_rows == 176 && asic_cols % 48 == 0) max_w = 48;
   if (const char* e = getenv("PSANA_RAY_CM_STRIPE"); e && *e) max_w = std::max(0, atoi(e));   // 0: full width
   const int full_cols = asic_cols;
   asic_cols = cm_tile_cols(asic_rows, full_cols, bank_cols, max_w);
@@ -844,9 +850,6 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   int cq_req = 0;
   if (const char* e = getenv("PSANA_RAY_CM_COLQ"); e && *e) cq_req = atoi(e);
   const int M2 = (asic_rows + 1) / 2, M4 = (asic_rows + 3) / 4;
-  // PSANA_RAY_CM_CONSTDIMS=0 skips the compile-time-shape instantiations (A/B)
-  const char* cd = getenv("PSANA_RAY_CM_CONSTDIMS");
-  const bool const_dims = !(cd != nullptr && cd[0] == '0');
 #define PR_CM_NET_T(KIND_, L_, M_, B_, CQ_, TR_, TC_)                                                   \
   if (!done && kind == KIND_ && bank_cols == L_ && (CQ_ == 4 ? M4 : M2) == M_ &&                        \
       (cq_req == 0 || cq_req == CQ_) && B_ == (narrow ? 256 : 512) * (CQ_ / 2) && !cm_force_generic() && \
@@ -858,6 +861,16 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
     done = true;                                                                                      \
   }
 #define PR_CM_NET(KIND_, L_, M_, B_, CQ_) PR_CM_NET_T(KIND_, L_, M_, B_, CQ_, 0, 0)
+  // epix10k2M 176x48 stripes (PSANA_RAY_CM_STRIPE=48): 256-thread blocks (176 row segments,
+  // 192 column lanes), 38.7 KB LDS -> four workgroups per CU
+  if (!done && const_dims && !cm_force_generic() && (cq_req == 0 || cq_req == 4) && kind == kEpix10ka &&
+      bank_cols == 48 && asic_rows == 176 && asic_cols == 48) {
+    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<kEpix10ka, 48, 44, 256, 4, 176, 48>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
+    hipLaunchKernelGGL((calib_cm_net_kernel<kEpix10ka, 48, 44, 256, 4, 176, 48>), grid, dim3(256), lds, s, fp, P, G,
+                       F, tg, cp, io);
+    done = true;
+  }
   PR_CM_NET_T(kEpix10ka, 48, 44, 512, 4, 176, 96)    // epix10k2M: 176x96 stripes
   PR_CM_NET_T(kJungfrau, 64, 64, 512, 4, 256, 128)   // Jungfrau: 256x128 stripes
   PR_CM_NET(kEpix10ka, 48, 44, 512, 4)

@@ -42,16 +42,18 @@ def test_calib_basic_bitwise(cuda_device, det, masked):
     _assert_equal(out, ref, f"calib {det}")
 
 
-@pytest.mark.parametrize("det,stripe,colq,gather", [("tiny_epix", "", "", ""), ("tiny_epix", "", "2", ""),
-                                                    ("epix10k2M", "", "", ""), ("epix10k2M", "", "", "0"),
-                                                    ("epix10k2M", "0", "", ""), ("epix10k2M", "48", "", ""),
-                                                    ("epix10k2M", "", "2", ""), ("epix10k2M", "0", "2", ""),
-                                                    ("jungfrau05M", "", "", "")])
+@pytest.mark.parametrize("det,stripe,colq,gather,cdims", [
+    ("tiny_epix", "", "", "", ""), ("tiny_epix", "", "2", "", ""), ("epix10k2M", "", "", "", ""),
+    ("epix10k2M", "", "", "", "0"), ("epix10k2M", "", "", "0", ""), ("epix10k2M", "0", "", "", ""),
+    ("epix10k2M", "96", "", "", ""), ("epix10k2M", "48", "", "", "0"), ("epix10k2M", "", "2", "", ""),
+    ("epix10k2M", "0", "2", "", ""), ("jungfrau05M", "", "", "", ""), ("jungfrau05M", "", "", "", "0")])
 @pytest.mark.parametrize("flags", [1, 2, 3])
-def test_common_mode_bitwise(cuda_device, det, stripe, colq, gather, flags, monkeypatch):
-    # stripe: PSANA_RAY_CM_STRIPE caps the full-height stripe width ("" default = 96 for epix,
-    # "0" full width, "48" one bank per stripe); colq: lanes per column ("" default = 4-lane quad
-    # merge, "2" two-lane merge-path)
+def test_common_mode_bitwise(cuda_device, det, stripe, colq, gather, cdims, flags, monkeypatch):
+    # stripe: PSANA_RAY_CM_STRIPE caps the full-height stripe width ("" default = 48 for epix,
+    # one bank per stripe; "0" full width); colq: lanes per column ("" default = 4-lane quad
+    # merge, "2" two-lane merge-path); cdims "0": runtime tile shape instead of the compile-time
+    # instantiations (epix10k2M 176x96 / 176x48, Jungfrau 256x128)
+    monkeypatch.setenv("PSANA_RAY_CM_CONSTDIMS", cdims)
     monkeypatch.setenv("PSANA_RAY_CM_STRIPE", stripe)
     monkeypatch.setenv("PSANA_RAY_CM_COLQ", colq)
     monkeypatch.setenv("PSANA_RAY_CM_GATHER", gather)   # "" = default select-then-load
