@@ -865,6 +865,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   // 192 column lanes), 38.7 KB LDS -> four workgroups per CU
   if (!done && const_dims && !cm_force_generic() && (cq_req == 0 || cq_req == 4) && kind == kEpix10ka &&
       bank_cols == 48 && asic_rows == 176 && asic_cols == 48) {
+    // (192-thread blocks measured slower: 9.45 vs 8.82 us/frame; profiles/kernels_r1_cm_b48.jsonl)
     hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<kEpix10ka, 48, 44, 256, 4, 176, 48>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
     hipLaunchKernelGGL((calib_cm_net_kernel<kEpix10ka, 48, 44, 256, 4, 176, 48>), grid, dim3(256), lds, s, fp, P, G,
