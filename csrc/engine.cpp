@@ -312,12 +312,31 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       if (limit >= 0) n = (int)std::max<int64_t>(0, std::min<int64_t>(n, limit - k0));
       return n;
     };
+    // Prefetch depth: H2D copies of this many chunks stay queued on the copy stream ahead of the
+    // chunk being calibrated, so a host hiccup (slot wait, descheduling) of up to depth x 2.5 ms
+    // does not idle the PCIe link.  depth < n_raw_bufs: a buffer is re-staged only after the
+    // calibration that read it was launched (its buf_free event recorded; the copy stream waits on
+    // it device-side), and its pointers / file metadata were consumed.
+    int depth = 3;
+    if (const char* e = getenv("PSANA_RAY_STAGE_DEPTH"); e && *e) depth = std::max(1, atoi(e));
+    depth = std::min(depth, n_raw_bufs_ - 1);
+    int64_t st_k = k0;   // first event not staged yet
+    int64_t st_no = 0;   // chunks staged so far
+    auto stage_upto = [&](int64_t last_no) {   // stage chunks st_no .. last_no
+      while (st_no <= last_no) {
+        const int ns = chunk_len(st_k);
+        if (ns <= 0) break;
+        stage(st_k, ns, (int)(st_no % n_raw_bufs_));
+        st_k += ns;
+        ++st_no;
+      }
+    };
     int64_t k = k0;      // first event of the current chunk
     int64_t chunk_no = 0;
     int n = chunk_len(k0);
     if (n > 0 && !device_resident_) {
       const auto t0 = clk::now();
-      stage(k0, n, 0);
+      stage_upto(0);
       t_stage_ += secs(t0, clk::now());
     }
     while (n > 0 && !stop_.load()) {
@@ -328,7 +347,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       auto t0 = clk::now();
       if (n_next > 0 && !device_resident_) {
         trace::Range r("producer.stage_h2d");
-        stage(k_next, n_next, (int)((chunk_no + 1) % n_raw_bufs_));
+        stage_upto(chunk_no + depth);
       }
       auto t1 = clk::now();
       t_stage_ += secs(t0, t1);
