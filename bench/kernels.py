@@ -192,6 +192,17 @@ def main(argv=None):
                 c = cals[fused]
                 report(f"calib_cm_image({'fused' if fused == '1' else 'scratch + assemble'}) r{rnd}",
                        timeit(lambda: c.run(rl, il), a.iters), F * npix * 6 + img.numel() // F * F * 4)
+    if want("image_stripes") and spec.kind != "plain":
+        # image mode without common mode: LDS-tiled gather (image_tile_kernel) vs the stripe kernel
+        # with its median phases off (decode + pedestal into LDS, gain + placement epilogue)
+        import os
+        cal_t = Calibrator(src.consts, dev, Mode.image)
+        cal_s = Calibrator(src.consts, dev, Mode.image, common_mode=CommonModeParams(flags=0))
+        img = torch.empty((F, *cal_t.out_shape), dtype=torch.float32, device=dev)
+        il = [img[i] for i in range(F)]
+        for rnd in range(2):
+            report(f"image(no cm): tiles r{rnd}", timeit(lambda: cal_t.run(rl, il), a.iters), F * npix * 2 + img.numel() * 4)
+            report(f"image(no cm): stripes r{rnd}", timeit(lambda: cal_s.run(rl, il), a.iters), F * npix * 2 + img.numel() * 4)
     if want("calib_image") and spec.kind != "plain":
         import os
         C = _ext.load()
