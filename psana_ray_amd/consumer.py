@@ -30,7 +30,10 @@ def build_parser():
     ap.add_argument("--ray_namespace", type=str, default=DEFAULT_RAY_NAMESPACE)
     ap.add_argument("--queue_name", type=str, default=DEFAULT_QUEUE_NAME)
     ap.add_argument("--device", type=str, default=None)
-    ap.add_argument("--task", type=str, default="print", choices=["print", "peakfind", "none"])
+    ap.add_argument("--task", type=str, default="print", choices=["print", "peakfind", "train", "none"],
+                    help="train: online PeakNetLite training from peak-finder labels (trainer.py)")
+    ap.add_argument("--lr", type=float, default=1e-3, help="--task train: AdamW learning rate")
+    ap.add_argument("--save", type=str, default=None, help="--task train: write the model state_dict here")
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--max_frames", type=int, default=None)
     ap.add_argument("--thr_peak", type=float, default=20.0)
@@ -80,7 +83,32 @@ def main(argv=None) -> int:
             from .ops import kernels
 
             params = PeakFinderParams(thr_peak=args.thr_peak, son_min=args.son_min)
-        while not stop["flag"] and (args.max_frames is None or n < args.max_frames):
+        if args.task == "train":
+            if reader.endpoint is None:
+                log.error("--task train needs the distributed queue (a producer session)")
+                return 2
+            from .trainer import OnlinePeakNetTrainer
+
+            ring = reader.endpoint.ring
+            shape = reader.calibrator.out_shape if reader.calibrator is not None else ring.frame_shape
+            trainer = OnlinePeakNetTrainer(shape, ring.device, lr=args.lr,
+                                           params=PeakFinderParams(thr_peak=args.thr_peak, son_min=args.son_min))
+            registry.register("trainer", lambda: {"steps": trainer.steps, "loss": trainer.last_loss})
+            try:
+                for batch in reader.batches(args.batch, torch.float32, timeout=1.0):
+                    trainer.step(batch.data)
+                    n += len(batch)
+                    peaks_total = trainer.positives
+                    if stop["flag"] or (args.max_frames is not None and n >= args.max_frames):
+                        break
+            except DataReaderError as e:
+                print(f"DataReader error: {e}")
+                return 1
+            log.info("Consumer %s: %d training steps, last loss %.4f", cid, trainer.steps, trainer.last_loss)
+            print(f"Consumer {cid} trained: steps={trainer.steps} frames={n} loss={trainer.last_loss:.4f}")
+            if args.save:
+                torch.save(trainer.model.state_dict(), args.save)
+        while args.task != "train" and not stop["flag"] and (args.max_frames is None or n < args.max_frames):
             try:
                 if args.task == "peakfind" and reader.endpoint is not None:
                     items = reader.read_batch(args.batch, timeout=1.0)

@@ -1,0 +1,104 @@
+"""Online training consumer (trainer.py, models/peaknet.py): peak-finder labels -> PeakNetLite step.
+CPU: label rasterisation, finite steps, the ``psana-ray-consumer --task train`` CLI session.
+GPU: bf16 autocast training on epix10k2M batches gathered from ring slots overfits a batch."""
+import os
+import random
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from psana_ray_amd.config import CommonModeParams
+from psana_ray_amd.models import Calibrator, Mode
+from psana_ray_amd.models.peaknet import PeakNetLite, peak_masks
+from psana_ray_amd.source import SyntheticRun
+from psana_ray_amd.trainer import OnlinePeakNetTrainer
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_peak_masks_rasterise_records():
+    pk = torch.zeros((2, 4, 8))
+    pk[0, 0, :3] = torch.tensor([1.0, 5.0, 7.0])     # frame 0: panel 1, (5, 7)
+    pk[0, 1, :3] = torch.tensor([0.0, 0.0, 0.0])     # frame 0: panel 0, corner (clamped)
+    pk[1, 0, :3] = torch.tensor([0.0, 9.0, 9.0])     # frame 1: beyond counts -> ignored
+    m = peak_masks(pk, torch.tensor([2, 0]), (2, 12, 16))
+    assert m.shape == (4, 1, 12, 16)
+    assert m[1, 0, 4:7, 6:9].sum() == 9 and m[0, 0, :2, :2].sum() == 4
+    assert m.sum() == 13 and m[2:].sum() == 0
+
+
+def test_peaknet_shapes():
+    net = PeakNetLite(8)
+    assert net(torch.randn(3, 1, 32, 48)).shape == (3, 1, 32, 48)
+
+
+def _frames(det, n, device="cpu"):
+    src = SyntheticRun("synthetic", 9, det, n_events=n, pool_frames=n, gen_device="cpu")
+    cal = Calibrator(src.consts, device, Mode.calib, common_mode=CommonModeParams())
+    raw = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(device)
+    return cal(raw)
+
+
+def test_trainer_steps_cpu():
+    fr = _frames("tiny_epix", 4)
+    tr = OnlinePeakNetTrainer(fr.shape[1:], "cpu", width=8)
+    losses = [tr.step(fr) for _ in range(3)]
+    assert all(np.isfinite(losses)) and tr.steps == 3 and tr.frames == 12 and tr.positives > 0
+    p = tr.predict(fr[:1])
+    assert p.shape == (2, 1, 32, 48) and float(p.min()) >= 0 and float(p.max()) <= 1
+
+
+def test_train_consumer_cli_cpu(native):
+    port = random.randint(30000, 45000)
+    addr = f"127.0.0.1:{port}"
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    prod = subprocess.Popen(
+        [sys.executable, "-m", "psana_ray_amd.producer", "--exp", "synthetic", "--run", "3", "--detector_name",
+         "tiny_epix", "--calib", "--common_mode", "default", "--num_events", "12", "--ray_address", addr,
+         "--num_consumers", "1", "--queue_size", "6", "--device", "cpu", "--timeout", "60"],
+        env={**env, "RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"}, stdout=subprocess.PIPE,
+        stderr=subprocess.STDOUT, text=True)
+    cons = subprocess.Popen([sys.executable, "-m", "psana_ray_amd.consumer", "0", "--ray_address", addr, "--device",
+                             "cpu", "--task", "train", "--batch", "4", "--timeout", "60"],
+                            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        pout, _ = prod.communicate(timeout=240)
+        cout, _ = cons.communicate(timeout=240)
+    finally:
+        for p in (prod, cons):
+            if p.poll() is None:
+                p.kill()
+    assert prod.returncode == 0, pout[-3000:]
+    assert cons.returncode == 0, cout[-3000:]
+    assert "trained: steps=3 frames=12" in cout, cout[-2000:]
+
+
+@pytest.mark.gpu
+def test_trainer_gpu_overfits_ring_batch(native, cuda_device):
+    """Frames leased from an HBM ring, gathered by the HIP kernel, labelled by the HIP peak finder;
+    bf16 PeakNetLite steps drive the loss down on a fixed batch."""
+    from psana_ray_amd.batching import collate_items
+    from psana_ray_amd.pipeline import ProducerPipeline
+    from psana_ray_amd.queue import FrameRing, QueueEndpoint
+
+    src = SyntheticRun("synthetic", 9, "epix10k2M", n_events=4, pool_frames=4, pinned=True, gen_device="cuda")
+    cal = Calibrator(src.consts, cuda_device, Mode.calib, common_mode=CommonModeParams())
+    ring = FrameRing(cal.out_shape, cal.out_dtype, cuda_device, 8, 8)
+    ep = QueueEndpoint(ring)
+    assert ProducerPipeline(src, cal, ep, chunk=4).run() == 4
+    items = [ep.get(timeout=5.0) for _ in range(4)]
+    batch = collate_items(items, torch.float32)
+    # miopen=False: MIOpen JIT-compiles every convolution shape on a fresh node (~80 s for this
+    # net); the HIP gather / peak-finder path under test is the same
+    tr = OnlinePeakNetTrainer(cal.out_shape, cuda_device, width=8, lr=3e-3, miopen=False)
+    first = tr.step(batch.data)
+    for _ in range(25):
+        last = tr.step(batch.data)
+    torch.cuda.synchronize()
+    assert tr.positives > 0 and np.isfinite(first) and last < 0.7 * first, (first, last)
