@@ -54,6 +54,9 @@ def parse(argv=None):
     ap.add_argument("--loopback", action="store_true",
                     help="N=1 only: route frames through the multi-GPU transport (gloo control round + RCCL "
                          "send/recv to self) instead of the zero-copy local route; exercises the N>1 data path")
+    ap.add_argument("--transport", action="store_true",
+                    help="N=1 only: run the multi-GPU transport rounds (control all-gather, routing) with frames "
+                         "routed to this rank itself -- the per-rank steady state of N>1 weak scaling")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: protocol rehearsal with gloo and the golden models (tests only; not a benchmark)")
     return ap.parse_args(argv)
@@ -103,7 +106,7 @@ def main(argv=None):
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         comm = init_groups(rank, world, device)
         coord = dist.new_group(backend="gloo")
-    elif args.loopback:
+    elif args.loopback or args.transport:
         import socket
         with socket.socket() as so:
             so.bind(("127.0.0.1", 0))
@@ -269,6 +272,7 @@ def main(argv=None):
             "source": args.source,
             "chunk": args.chunk,
             "loopback": args.loopback,
+            "transport": bool(args.transport or world > 1 or args.loopback),
             "producer_ranks": n_prod,
         },
         "extra": {
