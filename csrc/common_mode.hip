@@ -483,24 +483,20 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
   const float INF = __int_as_float(0x7f800000);
 
   // ---- phase 1: decode + pedestal into LDS (same as the generic kernel) -------------------
-  for (int i = tid; i < R * C8; i += blockDim.x) {
-    const int r = i / C8, c = (i % C8) * 8;
-    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
-    const uint4 rw = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
-    const uint2 fl = *reinterpret_cast<const uint2*>(pflags + pix);
+  // select-then-load: a candidate table is read only by the 8-pixel groups that use it
+  // (gain-switched pixels are rare, so the second/third table's lines are almost never fetched;
+  // memory phases 5.6 -> see profiles/kernels_r1_cm_gather.jsonl)
+  auto p1_need = [&](const uint4 rw) -> uint32_t {
     const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
-    const uint32_t fw[2] = {fl.x, fl.y};
-    // select-then-load: a candidate table is read only by the 8-pixel groups that use it
-    // (gain-switched pixels are rare, so the second/third table's lines are almost never fetched;
-    // memory phases 5.6 -> see profiles/kernels_r1_cm_gather.jsonl)
     uint32_t need = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       bool vd;
       need |= 1u << decode_cand((w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, KIND, vd);
     }
-    if (!cp.gather) need = (1u << NT) - 1u;
-    float pa[NT][8];
+    return cp.gather ? need : (1u << NT) - 1u;
+  };
+  auto p1_ped = [&](int64_t pix, uint32_t need, float (&pa)[NT][8]) {
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
@@ -511,6 +507,11 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
       pa[k][0] = a.x; pa[k][1] = a.y; pa[k][2] = a.z; pa[k][3] = a.w;
       pa[k][4] = b.x; pa[k][5] = b.y; pa[k][6] = b.z; pa[k][7] = b.w;
     }
+  };
+  auto p1_store = [&](int i, const uint4 rw, const uint2 fl, const float (&pa)[NT][8]) {
+    const int r = i / C8, c = (i % C8) * 8;
+    const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
+    const uint32_t fw[2] = {fl.x, fl.y};
     uint32_t nb = 0;
     float* trow = tile + r * LD + c;
 #pragma unroll
@@ -529,6 +530,47 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
       nb |= (uint32_t)(cand | (good ? 4 : 0) | (elig ? 8 : 0)) << (4 * j);
     }
     nib[r * C8 + (c >> 3)] = nb;
+  };
+  auto p1_pix = [&](int i) -> int64_t {
+    const int r = i / C8, c = (i % C8) * 8;
+    return base + (int64_t)r * tg.panel_cols + c;
+  };
+  constexpr int NITEMS = (TR > 0 && TC > 0) ? TR * (TC / 8) : 0;
+  constexpr int NI = NITEMS > 0 ? (NITEMS + BLOCK - 1) / BLOCK : 0;
+  if constexpr (NI > 0 && NI <= 6) {
+    // compile-time shape: all of this lane's raw / flag loads in flight at once, then all of its
+    // pedestal loads (two dependent round trips per workgroup instead of two per item)
+    uint4 rw[NI];
+    uint2 fl[NI];
+    float pa[NI][NT][8];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = tid + u * BLOCK;
+      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
+        const int64_t pix = p1_pix(i);
+        rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
+        fl[u] = *reinterpret_cast<const uint2*>(pflags + pix);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = tid + u * BLOCK;
+      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) p1_ped(p1_pix(i), p1_need(rw[u]), pa[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = tid + u * BLOCK;
+      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) p1_store(i, rw[u], fl[u], pa[u]);
+    }
+  } else {
+    for (int i = tid; i < R * C8; i += blockDim.x) {
+      const int64_t pix = p1_pix(i);
+      const uint4 rw = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
+      const uint2 fl = *reinterpret_cast<const uint2*>(pflags + pix);
+      float pa[NT][8];
+      p1_ped(pix, p1_need(rw), pa);
+      p1_store(i, rw, fl, pa);
+    }
   }
   __syncthreads();
 
