@@ -496,9 +496,9 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
     }
     return cp.gather ? need : (1u << NT) - 1u;
   };
-  auto p1_ped = [&](int64_t pix, uint32_t need, float (&pa)[NT][8]) {
+  auto p1_ped = [&](int64_t pix, uint32_t need, float (&pa)[NT][8], int k0 = 0) {
 #pragma unroll
-    for (int k = 0; k < NT; ++k) {
+    for (int k = k0; k < NT; ++k) {
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
       if ((need >> k) & 1u) {
         a = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix);
@@ -540,6 +540,8 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
   if constexpr (NI > 0 && NI <= 6) {
     // compile-time shape: all of this lane's raw / flag loads in flight at once, then all of its
     // pedestal loads (two dependent round trips per workgroup instead of two per item)
+    // The first candidate table (the unswitched gain: nearly every pixel) is loaded together with
+    // the raw words; only the rare switched candidates wait for the decoded raw (select-then-load).
     uint4 rw[NI];
     uint2 fl[NI];
     float pa[NI][NT][8];
@@ -550,12 +552,13 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
         const int64_t pix = p1_pix(i);
         rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
         fl[u] = *reinterpret_cast<const uint2*>(pflags + pix);
+        p1_ped(pix, 1u, pa[u]);
       }
     }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
       const int i = tid + u * BLOCK;
-      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) p1_ped(p1_pix(i), p1_need(rw[u]), pa[u]);
+      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) p1_ped(p1_pix(i), p1_need(rw[u]), pa[u], 1);
     }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
