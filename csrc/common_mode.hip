@@ -634,9 +634,13 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
       }
       const float med = (s_lo + s_hi) * 0.5f;
       if (cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
+        // branch-free: every element is rewritten (v - 0 == v bitwise, -0 and NaN included), so
+        // the 48 per-element exec-mask branches become selects
 #pragma unroll
-        for (int j = 0; j < L; ++j)
-          if (elig(j)) seg[j] -= med;
+        for (int j = 0; j < L; ++j) {
+          const float v = seg[j];
+          seg[j] = v - (elig(j) ? med : 0.0f);
+        }
       }
     }
     __syncthreads();
@@ -721,10 +725,14 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
         const float k_lo = dpp_quad<0x00>(k87), k_hi = dpp_quad<0x00>(k88);   // lane 0 has the answer
         const float med = (k_lo + ((cnt & 1) ? k_lo : k_hi)) * 0.5f;
         asm volatile("" ::: "memory");
-        if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
+        if (act) {   // branch-free per element (v - 0 == v bitwise), as in the row pass
+          const float m = (cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) ? med : 0.0f;
 #pragma unroll
           for (int i = 0; i < M; ++i) {
-            if (q * M + i < R && ((nibp[i * C8] >> shift) & 1u)) colp[i * LD] -= med;
+            if (q * M + i < R) {
+              const float v = colp[i * LD];
+              colp[i * LD] = v - (((nibp[i * C8] >> shift) & 1u) ? m : 0.0f);
+            }
             if ((i & 15) == 15) asm volatile("" ::: "memory");
           }
         }
