@@ -54,6 +54,10 @@ def parse(argv=None):
     ap.add_argument("--loopback", action="store_true",
                     help="N=1 only: route frames through the multi-GPU transport (gloo control round + RCCL "
                          "send/recv to self) instead of the zero-copy local route; exercises the N>1 data path")
+    ap.add_argument("--copy-engine", default="blit", choices=["blit", "sdma"],
+                    help="host->HBM staging copies: blit kernels (HSA_ENABLE_SDMA=0; 12.7k vs 12.2k fr/s on the same "
+                         "box, profiles/bench_ab_r1.md) or the SDMA engines.  An HSA_ENABLE_SDMA already in the "
+                         "environment wins")
     ap.add_argument("--transport", action="store_true",
                     help="N=1 only: run the multi-GPU transport rounds (control all-gather, routing) with frames "
                          "routed to this rank itself -- the per-rank steady state of N>1 weak scaling")
@@ -64,6 +68,9 @@ def parse(argv=None):
 
 def main(argv=None):
     args = parse(argv)
+    from psana_ray_amd.utils.runtime_env import select_copy_engine
+
+    select_copy_engine(args.copy_engine)   # before the HIP runtime initialises (first torch.cuda call)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -291,6 +298,8 @@ def main(argv=None):
             "transport_driver": ep.xport,
             "bytes_sent_rank0": st.get("bytes_sent", 0),
             "numa_node": numa,
+            "copy_engine": "blit" if os.environ.get("HSA_ENABLE_SDMA") == "0" else "sdma",
+            "cpus_allowed": len(os.sched_getaffinity(0)),
             "producer_host_s_stage_acquire_launch_commit_total": (
                 [round(x, 4) for x in prod.engine.timing()] if prod is not None and prod.engine is not None
                 else None),

@@ -4,8 +4,9 @@
 //
 // Every rank runs this on identical all-gathered inputs, so all ranks derive the same plan and the
 // RCCL sends / receives match without extra messages.  Policies: 0 balanced (water-filling by
-// free slots, ties -> own GPU then cyclic), 1 local_first (own GPU first, overflow water-filled),
-// 2 spread (strict round robin over consumers with credit).
+// free slots, the producer's own shard counting kLocalSlack extra; ties -> own GPU then cyclic),
+// 1 local_first (own GPU first, overflow water-filled), 2 spread (strict round robin over
+// consumers with credit).
 #include <stdint.h>
 
 #include <vector>
@@ -13,6 +14,9 @@
 #include "common.h"
 
 namespace pr {
+
+// balanced: credit bonus of the producer's own consumer shard (routing.py LOCAL_SLACK)
+static constexpr int64_t kLocalSlack = 64;
 
 std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers_in, const std::vector<int64_t>& credits_in,
                                        int64_t round_id, int policy) {
@@ -75,9 +79,10 @@ std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers_in, co
       for (int k = 0; k < world; ++k) {
         const int c = (p + k) % world;
         if (cred[c] <= 0) continue;
-        if (best < 0 || cred[c] > best_cred) {   // most credit first; ties: smallest k (own GPU first)
+        const int64_t eff = cred[c] + ((k == 0 && policy == 0) ? kLocalSlack : 0);
+        if (best < 0 || eff > best_cred) {   // most credit first; ties: smallest k (own GPU first)
           best = c;
-          best_cred = cred[c];
+          best_cred = eff;
           best_k = k;
         }
       }

@@ -75,6 +75,8 @@ def bind_numa_to_device(device) -> Optional[int]:
     allocated node-local to the GPU's PCIe root (host->device copies cross no socket link)."""
     import torch
 
+    if os.environ.get("PSANA_RAY_NUMA_BIND", "1") == "0":
+        return None
     try:
         if torch.device(device).type != "cuda":
             return None

@@ -9,9 +9,12 @@ the RCCL sends/recvs match by construction.
 
 Policies:
   balanced     water-filling: each frame goes to the consumer with the most free slots (ties:
-               the producer's own GPU, then the next ranks cyclically).  Fast consumers
-               accumulate more credits and therefore receive more frames -- the competing-
-               consumer load balancing of the reference, without a central actor.
+               the producer's own GPU, then the next ranks cyclically), where the producer's own
+               shard counts LOCAL_SLACK extra slots: a frame leaves its GPU only when another
+               shard is more than two chunks emptier.  Fast consumers accumulate more credits and
+               therefore receive more frames -- the competing-consumer load balancing of the
+               reference, without a central actor -- while near-balanced ranks (the weak-scaling
+               steady state) keep their frames local instead of trading them over xGMI.
   local_first  a producer's frames stay on its own GPU while that shard has credit (zero-copy),
                the overflow is water-filled to the others.
   spread       strict round robin over consumers with credit (maximises xGMI link use).
@@ -23,6 +26,10 @@ from typing import List, Sequence, Tuple
 POLICIES = ("balanced", "local_first", "spread")
 
 Assignment = Tuple[int, int, int]  # (producer rank, offer index, consumer rank)
+
+# balanced policy: credit bonus of the producer's own consumer shard (two producer chunks); the
+# native plan (csrc/routing.cpp) uses the same constant
+LOCAL_SLACK = 64
 
 
 def plan_round(offers: Sequence[int], credits: Sequence[int], round_id: int, policy: str = "balanced") -> List[Assignment]:
@@ -76,7 +83,8 @@ def plan_round(offers: Sequence[int], credits: Sequence[int], round_id: int, pol
                 c = (p + k) % world
                 if cred[c] <= 0:
                     continue
-                key = (-cred[c], k)          # most credit first, then own GPU (k=0), then cyclic
+                bonus = LOCAL_SLACK if (k == 0 and policy == "balanced") else 0
+                key = (-(cred[c] + bonus), k)   # most credit first, then own GPU (k=0), then cyclic
                 if best_key is None or key < best_key:
                     best, best_key = c, key
             if best < 0:

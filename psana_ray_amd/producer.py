@@ -80,6 +80,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="split every frame's panels over groups of this many ranks (SP analog for Jungfrau-16M-"
                         "scale frames): a group walks the same events, each rank stages/calibrates/queues 1/N "
                         "of the panels; needs --calib or --mode raw (source/shard.py)")
+    g.add_argument("--copy_engine", type=str, default="blit", choices=["blit", "sdma"],
+                   help="host->HBM staging copies: blit kernels (default, measured faster in the pipeline) or "
+                        "the SDMA engines (utils/runtime_env.py)")
     g.add_argument("--local", action="store_true",
                    help="single-process queue: no rendezvous; requires --consumer_task (no external consumers)")
     return parser
@@ -165,6 +168,9 @@ def main(argv=None) -> int:
     args = parse_arguments(argv)
     logging.basicConfig(level=getattr(logging, args.log_level),
                         format="%(asctime)s - %(levelname)s - %(message)s")   # producer.py:135-136
+    from .utils.runtime_env import select_copy_engine
+
+    select_copy_engine(args.copy_engine)   # before the HIP runtime initialises
     import torch
 
     from .models.calibrator import Calibrator

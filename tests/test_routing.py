@@ -48,6 +48,17 @@ def test_balanced_prefers_most_credit_and_spreads():
     assert counts == [8, 8, 8, 8]
 
 
+def test_balanced_keeps_near_balanced_frames_local():
+    from psana_ray_amd.parallel.routing import LOCAL_SLACK
+
+    # the other shard is emptier, but by less than one chunk: frames stay on their GPU
+    plan = plan_round([16, 16], [40, 40 + LOCAL_SLACK - 1], 0, "balanced")
+    assert all(p == c for p, _, c in plan)
+    # a real imbalance (a slow consumer) still moves frames to the emptier shard
+    plan = plan_round([16, 0], [10, 10 + LOCAL_SLACK + 8], 0, "balanced")
+    assert sum(1 for _, _, c in plan if c == 1) == 12 and sum(1 for _, _, c in plan if c == 0) == 4
+
+
 def test_local_first_keeps_frames_local():
     plan = plan_round([4, 4], [10, 10], 0, "local_first")
     assert all(p == c for p, _, c in plan)
