@@ -309,7 +309,9 @@ class DataReader:
             # stay in the collective rounds until the producers' EOS so peers never see a
             # half-finished world; a reader closed early just stops taking frames
             ep.join(timeout=self.timeout_s)
+            owns = False
             if ep.comm is not None:
+                owns = ep.comm.owns_default_group
                 if ep.failed is not None:
                     ep.comm.abort()
                 ep.close()
@@ -317,7 +319,8 @@ class DataReader:
             try:
                 import torch.distributed as dist
 
-                if dist.is_initialized():
+                # close only what connect() opened (Q-13)
+                if owns and dist.is_initialized():
                     dist.destroy_process_group()
             except Exception:  # noqa: BLE001
                 pass

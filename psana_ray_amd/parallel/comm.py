@@ -26,8 +26,12 @@ import torch.distributed as dist
 
 class Comm:
     def __init__(self, rank: int, world: int, ctrl_group, data_group, device: torch.device, rccl=None,
-                 node_local: bool = False, token: str = ""):
+                 node_local: bool = False, token: str = "", owns_default_group: bool = False):
         self.rank = rank
+        # True when init_groups created the default process group: only then may the owner of this
+        # Comm destroy it (reference quirk Q-13: DataReader.close() shut Ray down even when the
+        # caller had initialised it, psana_ray/data_reader.py:26-29)
+        self.owns_default_group = bool(owns_default_group)
         self.world = world
         # every rank on this host: the native transport engine (csrc/xport_engine.h) can run the
         # control plane through shared memory instead of gloo
@@ -135,7 +139,11 @@ def init_groups(rank: int, world: int, device, store=None, master_addr: Optional
     tmo = datetime.timedelta(seconds=timeout_s)
     if gpu:
         torch.cuda.set_device(device)
-    if not dist.is_initialized():
+    owns = not dist.is_initialized()
+    if not owns and (dist.get_rank(), dist.get_world_size()) != (rank, world):
+        raise RuntimeError(f"an existing default process group (rank {dist.get_rank()} of {dist.get_world_size()}) "
+                           f"does not match the queue world (rank {rank} of {world})")
+    if owns:
         kw = dict(rank=rank, world_size=world, timeout=tmo)
         if store is not None:
             kw["store"] = store
@@ -164,7 +172,8 @@ def init_groups(rank: int, world: int, device, store=None, master_addr: Optional
         dist.broadcast(uid, src=0, group=ctrl)
         dev_index = device.index if device.index is not None else torch.cuda.current_device()
         rccl = C.RcclTransport(bytes(uid.numpy().tobytes()), rank, world, dev_index)
-    return Comm(rank, world, ctrl, dist.group.WORLD, device, rccl=rccl, node_local=node_local, token=tok[0])
+    return Comm(rank, world, ctrl, dist.group.WORLD, device, rccl=rccl, node_local=node_local, token=tok[0],
+                owns_default_group=owns)
 
 
 def _boot_id() -> str:

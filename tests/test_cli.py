@@ -140,3 +140,50 @@ def test_calibrate_on_read_cpu(native):
     assert prod.returncode == 0, pout[-3000:]
     assert cons.returncode == 0, cout[-3000:]
     assert f"COR_OK {n_events}" in cout
+
+
+def test_sigint_on_endless_producer_ends_stream_cleanly(native):
+    """R-03 / Q-14: Ctrl+C on an endless producer (no --num_events) stops production, advertises
+    EOS and exits 0; the consumer sees the end of stream (reference: only rank 0 handled SIGINT,
+    with ray.shutdown(); exit(0), psana_ray/producer.py:73-76,142-143, so consumers polled forever)."""
+    import signal
+    import threading
+
+    port = random.randint(30000, 45000)
+    addr = f"127.0.0.1:{port}"
+    prod = subprocess.Popen(
+        [sys.executable, "-m", "psana_ray_amd.producer", "--exp", "synthetic", "--run", "5", "--detector_name",
+         "tiny_epix", "--calib", "--ray_address", addr, "--num_consumers", "1", "--queue_size", "4",
+         "--device", "cpu", "--timeout", "60"],
+        env=_env({"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"}), stdout=subprocess.PIPE,
+        stderr=subprocess.STDOUT, text=True)
+    cons = subprocess.Popen([sys.executable, "-m", "psana_ray_amd.consumer", "0", "--ray_address", addr,
+                             "--device", "cpu", "--timeout", "60"],
+                            env=_env(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    lines, seen = [], threading.Event()
+
+    def pump():
+        for line in cons.stdout:
+            lines.append(line)
+            if sum("processed:" in l for l in lines) >= 5:
+                seen.set()
+
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    try:
+        assert seen.wait(120), "consumer never received frames:\n" + "".join(lines)[-3000:]
+        prod.send_signal(signal.SIGINT)
+        pout, _ = prod.communicate(timeout=120)
+        cons.wait(timeout=120)
+        t.join(timeout=10)
+    finally:
+        for p in (prod, cons):
+            if p.poll() is None:
+                p.kill()
+    assert prod.returncode == 0, pout[-3000:]
+    assert "Ctrl+C pressed" in pout
+    out = "".join(lines)
+    assert cons.returncode == 0, out[-3000:]
+    assert "end of stream" in out, out[-3000:]
+    idx = [int(l.split("idx=")[1].split()[0]) for l in lines if "processed:" in l]
+    assert idx == list(range(len(idx))), "frames lost or duplicated before EOS"

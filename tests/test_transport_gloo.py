@@ -96,3 +96,28 @@ def test_dead_consumer_makes_producer_fail_cleanly(native, xport):
                 p.kill()
     assert msgs[1][1] == "exiting"
     assert msgs[0][1] == "peer-error", msgs[0]
+
+
+def test_init_groups_reuses_but_never_owns_a_callers_process_group():
+    """Q-13 fixed: a caller's own default process group is reused (when it matches the queue world)
+    and marked not-owned, so DataReader.close() leaves it alive; a mismatched one is refused."""
+    import socket
+
+    import torch.distributed as dist
+
+    from psana_ray_amd.parallel.comm import init_groups
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    assert not dist.is_initialized()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        comm = init_groups(0, 1, "cpu")
+        assert not comm.owns_default_group
+        comm.close()
+        assert dist.is_initialized()
+        with pytest.raises(RuntimeError, match="does not match"):
+            init_groups(1, 2, "cpu")
+    finally:
+        dist.destroy_process_group()
