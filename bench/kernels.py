@@ -263,8 +263,11 @@ def main(argv=None):
                     report(f"read_f32 reference (K={k}, nt={int(nt)}) r{rnd}",
                            timeit(lambda: C.read_f32(op, npix, k, nt, int(sums.data_ptr()), _ext.stream_handle()),
                                   a.iters), F * npix * 4)
-            for ver, groups in (("v1", ""), ("tiles, 2 frames/block", str(max(1, F // 2))), ("stream K=4", ""),
+            for ver, groups in (("v1", ""), ("tiles, 2 frames/block", str(max(1, F // 2))),
+                                ("stream K=4 blocks=0", ""), ("stream K=4 blocks=1024", ""),
+                                ("stream K=4", ""), ("stream K=4 blocks=4096", ""),
                                 ("stream K=8", ""), ("stream K=16", "")):
+                os.environ["PSANA_RAY_PF_BLOCKS"] = ver.split("blocks=")[1] if "blocks=" in ver else ""
                 os.environ["PSANA_RAY_PF_V1"] = "1" if ver == "v1" else "0"
                 os.environ["PSANA_RAY_PF_VERSION"] = "3" if ver.startswith("stream") else "2"
                 os.environ["PSANA_RAY_PF_K"] = ver.split("=")[1].split()[0] if "K=" in ver else ""
@@ -276,6 +279,7 @@ def main(argv=None):
         os.environ.pop("PSANA_RAY_PF_GROUPS", None)
         os.environ.pop("PSANA_RAY_PF_VERSION", None)
         os.environ.pop("PSANA_RAY_PF_K", None)
+        os.environ.pop("PSANA_RAY_PF_BLOCKS", None)
     if want("h2d"):
         C = _ext.load()
         hp = src.pool
