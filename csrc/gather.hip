@@ -9,6 +9,8 @@
 // bytes (round-to-nearest-even, NaN kept quiet) so the model's first layer reads half as much.
 #include "common.h"
 
+#include <algorithm>
+
 namespace pr {
 
 __device__ __forceinline__ uint32_t f32_to_bf16_bits(float f) {
@@ -74,6 +76,49 @@ void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_run
   hipLaunchKernelGGL(fill_runs_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), fp,
                      reinterpret_cast<const int2*>(runs), n_runs);
   hip_check(hipGetLastError(), "fill_runs launch");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host -> HBM staging copy as OUR kernel (PSANA_RAY_COPY_KERNEL=<workgroups>): the pinned pool
+// (or registered run file) is read straight over PCIe by a FEW persistent workgroups, each lane
+// keeping 4 x 16 B nontemporal loads in flight (64 workgroups x 256 lanes x 64 B = 1 MiB in flight,
+// ~8x the PCIe Gen5 bandwidth-delay product), instead of the runtime's blit kernel, whose
+// workgroups occupy CUs across the chip while stalled on PCIe latency and stretch the concurrent
+// calibration / peak-finder kernels (profiles/rocprof_bench_n1_host_r1d.md).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void copy_h2d_kernel(const f32x4_t* __restrict__ src, f32x4_t* __restrict__ dst,
+                                                       const int64_t n16) {
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * 256 * U;
+  for (int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x; base < n16; base += stride) {
+    f32x4_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = base + 256 * u;
+      if (q < n16) v[u] = __builtin_nontemporal_load(src + q);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = base + 256 * u;
+      if (q < n16) dst[q] = v[u];
+    }
+  }
+}
+
+bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgroups, uint64_t stream) {
+  if (workgroups <= 0 || bytes <= 0 || (dst | host_src | (uint64_t)bytes) % 16 != 0) return false;
+  void* dsrc = nullptr;
+  if (hipHostGetDevicePointer(&dsrc, reinterpret_cast<void*>(host_src), 0) != hipSuccess || dsrc == nullptr) {
+    (void)hipGetLastError();   // not pinned / not mapped: the caller falls back to hipMemcpyAsync
+    return false;
+  }
+  const int64_t n16 = bytes / 16;
+  const int64_t need = (n16 + 1023) / 1024;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(workgroups, need));
+  hipLaunchKernelGGL(copy_h2d_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const f32x4_t*>(dsrc), reinterpret_cast<f32x4_t*>(dst), n16);
+  hip_check(hipGetLastError(), "copy_h2d launch");
+  return true;
 }
 
 }  // namespace pr

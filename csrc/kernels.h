@@ -28,6 +28,8 @@ void launch_read_f32(const FramePtrs& fp, int nframes, int64_t npix, int k, bool
 void launch_xor_selftest(uint64_t out, uint64_t stream);
 void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_runs, uint64_t stream);
 void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool bf16, uint64_t stream);
+// host (pinned / registered) -> HBM copy by a kernel; false = not applicable, use hipMemcpyAsync
+bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgroups, uint64_t stream);
 void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nout, uint64_t omask,
                      uint64_t stream);
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
