@@ -81,7 +81,7 @@ def main(argv=None):
                           "steady_frames_per_s": round(steady, 1),
                           "GB_per_s_raw": round(n * src.spec.raw_frame_bytes / dt / 1e9, 2),
                           "native_engine": prod.engine is not None, "zero_copy": prod.zero_copy, "reader_threads": a.threads, "peaks": peaks, "numa": numa,
-                          "engine_span_copies_frame_copies": prod.engine.copy_stats(),
+                          "engine_span_frame_kernel_copies": prod.engine.copy_stats(),
                           "engine_host_s_stage_acquire_launch_commit_total": st}))
     finally:
         shutil.rmtree(a.dir, ignore_errors=True)

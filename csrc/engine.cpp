@@ -271,9 +271,11 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
           hip_check(hipEventRecord(h2d_start_[b], h2d_), "record h2d start");
           h2d_pending_[b] = 1;
         }
-        if (!(copy_kernel_wgs > 0 && launch_copy_h2d(reinterpret_cast<uint64_t>(buf), reinterpret_cast<uint64_t>(stg),
-                                                     (int64_t)n * plan_.raw_frame_bytes, copy_kernel_wgs,
-                                                     reinterpret_cast<uint64_t>(h2d_))))
+        if (copy_kernel_wgs > 0 && launch_copy_h2d(reinterpret_cast<uint64_t>(buf), reinterpret_cast<uint64_t>(stg),
+                                                   (int64_t)n * plan_.raw_frame_bytes, copy_kernel_wgs,
+                                                   reinterpret_cast<uint64_t>(h2d_)))
+          kernel_copies_.fetch_add(1, std::memory_order_relaxed);
+        else
           hip_check(hipMemcpyAsync(buf, stg, (size_t)n * plan_.raw_frame_bytes, hipMemcpyHostToDevice, h2d_),
                     "stage copy");
         hip_check(hipEventRecord(h2d_done_[b], h2d_), "record h2d");
@@ -307,9 +309,11 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
         const int64_t span = (int64_t)(j - i - 1) * d + fb;
         pos = (pos + 255) & ~int64_t(255);
         check(pos + span <= region_bytes_, "ProducerEngine: staging region overflow");
-        if (!(copy_kernel_wgs > 0 && !device_resident_ &&
-              launch_copy_h2d(reinterpret_cast<uint64_t>(buf + pos), s0, span, copy_kernel_wgs,
-                              reinterpret_cast<uint64_t>(h2d_))))
+        if (copy_kernel_wgs > 0 && !device_resident_ &&
+            launch_copy_h2d(reinterpret_cast<uint64_t>(buf + pos), s0, span, copy_kernel_wgs,
+                            reinterpret_cast<uint64_t>(h2d_)))
+          kernel_copies_.fetch_add(1, std::memory_order_relaxed);
+        else
           hip_check(hipMemcpyAsync(buf + pos, reinterpret_cast<const void*>(s0), (size_t)span, hipMemcpyDefault, h2d_),
                     "stage copy");
         for (int q = i; q < j; ++q) dev[q] = reinterpret_cast<uint64_t>(buf) + (uint64_t)(pos + (q - i) * d);

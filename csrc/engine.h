@@ -92,7 +92,8 @@ class ProducerEngine {
   // [h2d ms total, h2d chunks measured, calib ms total, calib chunks measured]; zeros when off
   std::vector<double> gpu_timing() const;
   // (copies that moved a multi-frame span, copies of a single frame) in cycled-host mode
-  std::vector<int64_t> copy_stats() const { return {span_copies_.load(), frame_copies_.load()}; }
+  // {span copies, single-frame copies, copies done by copy_h2d_kernel (the rest went through hipMemcpyAsync)}
+  std::vector<int64_t> copy_stats() const { return {span_copies_.load(), frame_copies_.load(), kernel_copies_.load()}; }
   bool gpu_timing_enabled() const { return gpu_timing_; }
 
  private:
@@ -129,7 +130,7 @@ class ProducerEngine {
   static constexpr int64_t kCopySlack = 4096;
   int64_t region_bytes_ = 0;
   std::vector<std::vector<uint64_t>> dev_in_;
-  std::atomic<int64_t> span_copies_{0}, frame_copies_{0};
+  std::atomic<int64_t> span_copies_{0}, frame_copies_{0}, kernel_copies_{0};
   std::thread thread_;
   std::atomic<bool> stop_{false}, running_{false};
   std::atomic<int64_t> frames_{0}, full_waits_{0};

@@ -15,8 +15,11 @@ from psana_ray_amd.source import SyntheticRun
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("cm", [None, "default"])
-def test_local_pipeline_frames_exact(cuda_device, cm):
+@pytest.mark.parametrize("cm,copy_kernel", [(None, "32"), ("default", "32"), ("default", "0")])
+def test_local_pipeline_frames_exact(cuda_device, cm, copy_kernel, monkeypatch):
+    """copy_kernel: staging copies by copy_h2d_kernel (csrc/gather.hip, default 32 workgroups) or
+    by hipMemcpyAsync (0)."""
+    monkeypatch.setenv("PSANA_RAY_COPY_KERNEL", copy_kernel)
     n_events = 50
     src = SyntheticRun("synthetic", 3, "epix10k2M", n_events=n_events, pool_frames=8, pinned=True,
                        gen_device="cuda")
@@ -48,6 +51,10 @@ def test_local_pipeline_frames_exact(cuda_device, cm):
     assert seen == sorted(seen), "FIFO order within a shard"
     st = ep.stats()
     assert st["produce_full"] > 0, "the small ring should have exercised backpressure"
+    assert prod.engine is not None, "the native producer engine must run on a GPU"
+    span, single, by_kernel = prod.engine.copy_stats()
+    assert span + single > 0
+    assert (by_kernel == span + single) if copy_kernel != "0" else by_kernel == 0
 
 
 def test_peakfinder_consumer_counts(cuda_device):
