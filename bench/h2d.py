@@ -43,6 +43,25 @@ def main():
                  "epix_raw_frames_per_s": round(iters * nfr / dt, 1)}
             res.append(r)
             print(json.dumps(r), flush=True)
+    # the producer engine's default staging path: copy_h2d_kernel with a few persistent workgroups
+    s = torch.cuda.Stream(device=dev)
+    for wgs in (16, 32, 64, 128):
+        def runk(iters):
+            for it in range(iters):
+                for c0 in range(0, nfr, 32):
+                    off = c0 * frame
+                    assert C.copy_h2d_kernel(int(dst.data_ptr()) + off, host.ptr + off, 32 * frame, wgs,
+                                             int(s.cuda_stream)), "copy kernel not applicable"
+            s.synchronize()
+        runk(2)
+        t0 = time.perf_counter()
+        iters = 5
+        runk(iters)
+        dt = time.perf_counter() - t0
+        r = {"copy_kernel_workgroups": wgs, "chunk_frames": 32, "GB_per_s": round(iters * nfr * frame / dt / 1e9, 2),
+             "epix_raw_frames_per_s": round(iters * nfr / dt, 1)}
+        print(json.dumps(r), flush=True)
+    assert torch.all(dst[:1 << 20] == 1).item(), "copy kernel wrote wrong bytes"
 
 
 if __name__ == "__main__":

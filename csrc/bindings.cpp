@@ -153,6 +153,12 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("plan_round", &pr::plan_round_native, py::arg("offers"), py::arg("credits"), py::arg("round_id"),
         py::arg("policy"), "flattened (producer, offer_index, consumer) triples");
+  m.def("copy_h2d_kernel",
+        [](uint64_t dst, uint64_t src, int64_t bytes, int workgroups, uint64_t stream) {
+          return pr::launch_copy_h2d(dst, src, bytes, workgroups, stream);
+        },
+        py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("workgroups"), py::arg("stream") = 0,
+        "host (pinned) -> HBM copy by copy_h2d_kernel; False = not applicable (unaligned / unmapped)");
   m.def("memcpy_h2d_async", &pr::memcpy_h2d_async, py::arg("dst"), py::arg("src"), py::arg("bytes"),
         py::arg("stream"));
   m.def("memcpy_h2d_batch", &pr::memcpy_h2d_batch, py::arg("dst"), py::arg("src"), py::arg("bytes"),

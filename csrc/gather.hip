@@ -10,6 +10,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace pr {
 
@@ -86,9 +87,9 @@ void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_run
 // workgroups occupy CUs across the chip while stalled on PCIe latency and stretch the concurrent
 // calibration / peak-finder kernels (profiles/rocprof_bench_n1_host_r1d.md).
 // ---------------------------------------------------------------------------------------------
+template <int U>
 __global__ __launch_bounds__(256) void copy_h2d_kernel(const f32x4_t* __restrict__ src, f32x4_t* __restrict__ dst,
                                                        const int64_t n16) {
-  constexpr int U = 4;
   const int64_t stride = (int64_t)gridDim.x * 256 * U;
   for (int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x; base < n16; base += stride) {
     f32x4_t v[U];
@@ -112,11 +113,21 @@ bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgro
     (void)hipGetLastError();   // not pinned / not mapped: the caller falls back to hipMemcpyAsync
     return false;
   }
+  // PSANA_RAY_COPY_KERNEL_U: 16-B loads in flight per lane (4 default, 8 for A/B)
+  static const int U = [] {
+    const char* e = getenv("PSANA_RAY_COPY_KERNEL_U");
+    return (e && atoi(e) == 8) ? 8 : 4;
+  }();
   const int64_t n16 = bytes / 16;
-  const int64_t need = (n16 + 1023) / 1024;
+  const int64_t need = (n16 + 256 * U - 1) / (256 * U);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(workgroups, need));
-  hipLaunchKernelGGL(copy_h2d_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<const f32x4_t*>(dsrc), reinterpret_cast<f32x4_t*>(dst), n16);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const f32x4_t* sp = reinterpret_cast<const f32x4_t*>(dsrc);
+  f32x4_t* dp = reinterpret_cast<f32x4_t*>(dst);
+  if (U == 8)
+    hipLaunchKernelGGL(copy_h2d_kernel<8>, dim3(grid), dim3(256), 0, s, sp, dp, n16);
+  else
+    hipLaunchKernelGGL(copy_h2d_kernel<4>, dim3(grid), dim3(256), 0, s, sp, dp, n16);
   hip_check(hipGetLastError(), "copy_h2d launch");
   return true;
 }
