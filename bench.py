@@ -3,13 +3,20 @@
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched by
 ``torch.distributed.run`` with one rank per GPU.  One STEP = every rank's consumer takes
-``--batch`` frames out of the sharded shared queue and runs the on-GPU peak finder on them.
-Behind it, every rank's producer streams raw epix10k2M frames from a pinned host pool through
-hipMemcpyAsync (side stream) into HBM, calibrates them with the HIP kernels (pedestal + gain
-switching + common mode + mask) directly into ring slots, and the transport routes them to the
-consumer shards (RCCL send/recv over xGMI for N > 1, balanced routing).  W untimed warmup
-steps, then exactly K timed steps bracketed by a barrier + device synchronisation; the time is
-the MAX over ranks; rank 0 prints ONE JSON line.  ``value`` = total frames/s of the node.
+``--batch`` frames out of its shard of the shared queue and runs the on-GPU peak finder on them.
+Behind it, every producer rank streams raw epix10k2M frames from a pinned host pool into HBM
+(our copy kernel on a side stream), calibrates them with the HIP kernels (pedestal + gain
+switching + common mode + mask) directly into its ring slots, and the queue routes them to the
+consumer shards.  W untimed warmup steps, then exactly K timed steps bracketed by a barrier +
+device synchronisation; the time is the MAX over ranks; rank 0 prints ONE JSON line.  ``value``
+= total frames/s of the node (headline phase: ``--route``, default balanced -- frames stay on the
+GPU that produced them unless another shard is starving).
+
+N > 1: every rank is a member of one queue session on torchrun's store and links to every other
+rank through the elastic fabric (csrc/fabric.h).  After the headline window a SECOND fixed-step
+window runs with ``route=spread`` (each producer deals its frames round-robin over all consumer
+GPUs, so (N-1)/N of them cross xGMI as HIP-IPC peer copies); its frames/s, cross-GPU GB/s and
+bytes per rank are reported under ``extra.xgmi_phase`` (``--cross-steps 0`` skips it).
 
 Synthetic data: random-init calibration constants and a pre-generated pool of raw frames
 (cycled), because no LCLS data / psana exists offline (BASELINE.json).
@@ -37,7 +44,11 @@ def parse(argv=None):
     ap.add_argument("--mode", default="calib", choices=["calib", "image", "raw"])
     ap.add_argument("--common-mode", default="default", help="off | default | flags,thr,maxcorr,npix_min[,bank]")
     ap.add_argument("--consumer", default="peakfind", choices=["peakfind", "none"])
-    ap.add_argument("--route", default="balanced", choices=["balanced", "local_first", "spread"])
+    ap.add_argument("--route", default="balanced", choices=["balanced", "local_first", "spread"],
+                    help="routing policy of the headline window")
+    ap.add_argument("--cross-steps", type=int, default=None,
+                    help="N > 1: steps of the second, route=spread window that pushes frames across GPUs over xGMI "
+                         "(default: --steps; 0 skips it)")
     ap.add_argument("--queue-size", type=int, default=None,
                     help="logical (global) queue capacity; default 400 per GPU (README.md:20 example, weak scaling: "
                          "constant queue depth per consumer shard). BASELINE config 3: --gpus 8 --queue-size 400")
@@ -51,19 +62,29 @@ def parse(argv=None):
                     help="producer ranks P (ranks < P produce, every rank consumes; 0 = all).  BASELINE config 3: "
                          "--gpus 8 --producers 4")
     ap.add_argument("--hbm-fraction", type=float, default=0.8, help="cap of free HBM used for queue slots")
-    ap.add_argument("--loopback", action="store_true",
-                    help="N=1 only: route frames through the multi-GPU transport (gloo control round + RCCL "
-                         "send/recv to self) instead of the zero-copy local route; exercises the N>1 data path")
     ap.add_argument("--copy-engine", default="blit", choices=["blit", "sdma"],
-                    help="host->HBM staging copies: blit kernels (HSA_ENABLE_SDMA=0; 12.7k vs 12.2k fr/s on the same "
-                         "box, profiles/bench_ab_r1.md) or the SDMA engines.  An HSA_ENABLE_SDMA already in the "
-                         "environment wins")
-    ap.add_argument("--transport", action="store_true",
-                    help="N=1 only: run the multi-GPU transport rounds (control all-gather, routing) with frames "
-                         "routed to this rank itself -- the per-rank steady state of N>1 weak scaling")
+                    help="runtime copies (HBM->HBM peer copies of the cross-GPU window): blit kernels "
+                         "(HSA_ENABLE_SDMA=0) or the SDMA engines.  An HSA_ENABLE_SDMA already in the environment wins")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: protocol rehearsal with gloo and the golden models (tests only; not a benchmark)")
     return ap.parse_args(argv)
+
+
+def _wait_links(ep, n_members: int, expect_in: int, expect_out: int, timeout_s: float = 180.0):
+    """Every member registered and every link of this rank attached (or raise)."""
+    t0 = time.time()
+    while True:
+        ls = ep.links()
+        n_in = sum(1 for x in ls if not x.outgoing and x.attached)
+        n_out = sum(1 for x in ls if x.outgoing and x.attached)
+        if len(ep.session.members) == n_members - 1 and n_in >= expect_in and n_out >= expect_out:
+            return
+        if ep.failed is not None:
+            raise RuntimeError(f"queue fabric failed while linking: {ep.failed}")
+        if time.time() - t0 > timeout_s:
+            raise TimeoutError(f"links not attached after {timeout_s:.0f} s: members {len(ep.session.members) + 1}/"
+                               f"{n_members}, in {n_in}/{expect_in}, out {n_out}/{expect_out}")
+        time.sleep(0.01)
 
 
 def main(argv=None):
@@ -77,21 +98,20 @@ def main(argv=None):
 
     from psana_ray_amd.config import CommonModeParams, PeakFinderParams
     from psana_ray_amd.models import Calibrator, Mode
-    from psana_ray_amd.parallel.comm import init_groups
     from psana_ray_amd.parallel.launch import bind_numa_to_device, detect
     from psana_ray_amd.pipeline import PeakFinderConsumer, ProducerPipeline
     from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
     from psana_ray_amd.queue.ring import physical_slots
+    from psana_ray_amd.queue.session import QueueSession, create_or_attach
     from psana_ray_amd.source import SyntheticRun
 
-    sys.setswitchinterval(5e-4)   # short GIL hand-off: transport / consumer threads stay responsive
+    sys.setswitchinterval(5e-4)   # short GIL hand-off: fabric / consumer threads stay responsive
     li = detect()
     world, rank = li.size, li.rank
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} needs a launcher (torch.distributed.run) with one rank per GPU",
-                  file=sys.stderr)
-            return 2
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s); N > 1 needs "
+              f"torch.distributed.run with one rank per GPU", file=sys.stderr)
+        return 2
     if args.device == "cpu":
         device = torch.device("cpu")
         numa = None
@@ -104,21 +124,18 @@ def main(argv=None):
         numa = bind_numa_to_device(device)
     gpu = device.type == "cuda"
 
-    comm = None
     coord = None
+    store = None
     if world > 1:
         # single-node contract (rendezvous on 127.0.0.1): keep gloo's control traffic on loopback
         # instead of whatever interface the container hostname resolves to (or fails to)
         if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost") and os.path.isdir("/sys/class/net/lo"):
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-        comm = init_groups(rank, world, device)
-        coord = dist.new_group(backend="gloo")
-    elif args.loopback or args.transport:
-        import socket
-        with socket.socket() as so:
-            so.bind(("127.0.0.1", 0))
-            port = so.getsockname()[1]
-        comm = init_groups(0, 1, device, master_addr="127.0.0.1", master_port=port)
+        import datetime
+
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
+        coord = dist.group.WORLD
+        store = dist.distributed_c10d._get_default_store()
 
     def barrier():
         if coord is not None:
@@ -140,14 +157,22 @@ def main(argv=None):
     if args.queue_size is None:
         args.queue_size = 400 * world
     share = max(1, math.ceil(args.queue_size / world))
-    # slack for frames waiting to be routed / in flight over xGMI (a round can hold max_offer frames)
-    producer_slots = (4 * args.chunk + args.batch + (64 if comm is not None else 0)) if is_prod else 1
+    # slack for frames waiting to be routed / copied to another GPU
+    producer_slots = (4 * args.chunk + args.batch + (64 if world > 1 else 0)) if is_prod else 0
     # queue_size is the LOGICAL capacity (deque(maxlen), shared_queue.py:7); physical HBM slots are
     # capped by free memory (config 4: Jungfrau-16M x 400000 would need 26.8 TB)
     cslots = physical_slots(share, cal.out_frame_bytes, device, args.hbm_fraction, producer_slots)
-    ring = FrameRing(cal.out_shape, cal.out_dtype, device, producer_slots, cslots)
-    ep = QueueEndpoint(ring, rank, world, comm, producer_ranks=list(range(n_prod)), route=args.route, max_offer=64,
-                       is_producer=is_prod, loopback=args.loopback)
+    sess = None
+    if world > 1:
+        meta = create_or_attach(store, "bench", "queue",
+                                {"queue_size": args.queue_size, "num_consumers": world, "n_producers": n_prod,
+                                 "frame_shape": list(cal.out_shape), "dtype": str(cal.out_dtype).split(".")[-1],
+                                 "device_kind": device.type})
+        sess = QueueSession(store, "bench", "queue", meta, "prosumer" if is_prod else "consumer",
+                            device=device.index if gpu else -1, rank=rank)
+    ring = FrameRing(cal.out_shape, cal.out_dtype, device, producer_slots, cslots,
+                     shm_name=sess.ring_name() if (sess is not None and not gpu) else None)
+    ep = QueueEndpoint(ring, sess, is_producer=is_prod, is_consumer=True, route=args.route)
     if args.source == "device":
         # raw pool resident in HBM: isolates the GPU pipeline from PCIe (secondary number)
         dev_pool = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(device)
@@ -185,6 +210,9 @@ def main(argv=None):
 
     stop = threading.Event()
     ep.start()
+    if sess is not None:
+        _wait_links(ep, world, n_prod - (1 if is_prod else 0), (world - 1) if is_prod else 0)
+        barrier()
     pt = threading.Thread(target=prod.run if prod is not None else ep.finish, kwargs=dict(stop=stop) if prod else {},
                           name="producer", daemon=True)
     pt.start()
@@ -200,34 +228,74 @@ def main(argv=None):
                     it.release()
                     got += 1
             if ep.failed is not None:
-                raise RuntimeError(f"transport failed: {ep.failed!r}")
+                raise RuntimeError(f"queue fabric failed: {ep.failed!r}")
         return got
 
     def sync():
         if gpu:
             torch.cuda.synchronize(device)
 
+    def window(steps):
+        """``steps`` timed steps between barriers: (seconds (max over ranks), frames produced in the
+        window (sum over ranks), fabric counters before and after on this rank)."""
+        sync()
+        barrier()
+        sync()
+        c0 = ep.metrics()
+        t0 = time.perf_counter()
+        p0 = prod.produced if prod is not None else 0
+        consume(steps * B)
+        sync()
+        t1 = time.perf_counter()
+        p1 = prod.produced if prod is not None else 0
+        c1 = ep.metrics()
+        barrier()
+        dt, pw = t1 - t0, p1 - p0
+        if coord is not None:
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=coord)
+            dt = float(t[0])
+            v = torch.tensor([pw], dtype=torch.int64)
+            dist.all_reduce(v, op=dist.ReduceOp.SUM, group=coord)
+            pw = int(v[0])
+        return dt, pw, p1 - p0, c0, c1
+
+    def allsum(x):
+        if coord is None:
+            return [x]
+        out = [None] * world
+        dist.all_gather_object(out, x, group=coord)
+        return out
+
     B = args.batch
+    total = world * args.steps * B
     consume(args.warmup * B)
-    sync()
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    p0 = prod.produced if prod is not None else 0
-    consume(args.steps * B)
-    sync()
-    t1 = time.perf_counter()
-    p1 = prod.produced if prod is not None else 0
-    barrier()
-    dt = t1 - t0
-    produced_window = p1 - p0
-    if coord is not None:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=coord)
-        dt = float(t[0])
-        pw = torch.tensor([produced_window], dtype=torch.int64)
-        dist.all_reduce(pw, op=dist.ReduceOp.SUM, group=coord)
-        produced_window = int(pw[0])
+    dt, produced_window, p_rank0, c0, c1 = window(args.steps)
+    # sustained throughput through the queue: frames can only leave as fast as they enter, so a
+    # ring that was already (partly) full at t0 must not count -- report min(consumed, produced)
+    value = min(total, produced_window) / dt
+
+    cross = None
+    cross_steps = args.steps if args.cross_steps is None else args.cross_steps
+    if world > 1 and cross_steps > 0:
+        ep.set_route("spread")
+        consume(max(2, args.warmup // 2) * B)
+        xdt, xpw, _, x0, x1 = window(cross_steps)
+        xtotal = world * cross_steps * B
+        sent = allsum(int(x1.get("bytes_sent", 0) - x0.get("bytes_sent", 0)))
+        fr_sent = allsum(int(x1.get("frames_sent", 0) - x0.get("frames_sent", 0)))
+        fr_local = allsum(int(x1.get("frames_local", 0) - x0.get("frames_local", 0)))
+        cms = allsum(round(float(x1.get("copy_ms_per_batch", 0.0)), 3))
+        cross = {
+            "route": "spread", "steps": cross_steps, "ms_per_step": round(1e3 * xdt / cross_steps, 4),
+            "frames_per_s": round(min(xtotal, xpw) / xdt, 2),
+            "cross_gpu_GB_per_s": round(sum(sent) / xdt / 1e9, 2),
+            "cross_gpu_fraction": round(sum(fr_sent) / max(1, sum(fr_sent) + sum(fr_local)), 3),
+            "bytes_sent_per_rank": sent, "frames_sent_per_rank": fr_sent, "frames_local_per_rank": fr_local,
+            "copy_ms_per_batch_per_rank": cms,
+            "data_plane": "HIP IPC peer copies (hipMemcpyAsync D2D into the consumer's ring) over xGMI",
+        }
+        ep.set_route(args.route)
     stop.set()
     # drain until every producer's EOS arrived
     while True:
@@ -245,11 +313,17 @@ def main(argv=None):
     pt.join(timeout=60)
     ep.join(timeout=60)
     peaks = consumer.synchronize() if consumer is not None else 0
-    total = world * args.steps * B
-    # sustained throughput through the queue: frames can only leave as fast as they enter, so a
-    # ring that was already (partly) full at t0 must not count -- report min(consumed, produced)
-    value = min(total, produced_window) / dt
     st = ep.stats()
+    copies = prod.engine.copy_stats() if (prod is not None and prod.engine is not None) else None
+    if not gpu:
+        staging = "host memory (CPU rehearsal)"
+    elif args.source == "device":
+        staging = "raw frames resident in HBM (no host staging)"
+    elif copies is not None and copies[2] > 0:
+        staging = "pinned host memory -> HBM by copy_h2d_kernel"
+    else:
+        staging = "pinned host memory -> HBM by hipMemcpyAsync (" + \
+                  ("blit kernels" if os.environ.get("HSA_ENABLE_SDMA") == "0" else "SDMA") + ")"
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -262,9 +336,8 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "float32" if mode != Mode.raw else "uint16",
-        "data": "synthetic (random-init calibration constants, pre-generated raw epix10k2M pool cycled "
-                + ("from pinned host memory via hipMemcpyAsync)" if args.source == "host" and gpu
-                   else "from HBM)" if gpu else "on the CPU; gloo protocol rehearsal, not a benchmark)"),
+        "data": "synthetic (random-init calibration constants, pre-generated raw " + args.detector
+                + " pool cycled; " + staging + ")" + ("" if gpu else "; gloo protocol rehearsal, not a benchmark"),
         "config": {
             "model": args.detector,
             "global_batch": world * B,
@@ -278,34 +351,30 @@ def main(argv=None):
             "queue_size": args.queue_size,
             "source": args.source,
             "chunk": args.chunk,
-            "loopback": args.loopback,
-            "transport": bool(args.transport or world > 1 or args.loopback),
             "producer_ranks": n_prod,
+            "queue": "local (single process)" if sess is None else "elastic fabric session",
         },
         "extra": {
-            "producer_frames_per_s_rank0": round((p1 - p0) / max(dt, 1e-9), 1),
+            "producer_frames_per_s_rank0": round(p_rank0 / max(dt, 1e-9), 1),
             "consumed_frames_per_s": round(total / dt, 1),
             "produced_frames_per_s": round(produced_window / dt, 1),
             "frame_bytes": ring.frame_bytes,
             "queue_slots_physical_rank0": cslots,
-            "ring_GB_rank0": round(ring.storage.numel() * ring.storage.element_size() / 1e9, 1),
+            "ring_GB_rank0": round(ring.nbytes / 1e9, 1),
             "GB_per_s_out": round(value * ring.frame_bytes / 1e9, 2),
             "peaks_found_rank0": peaks,
             "queue_full_waits_rank0": prod.full_waits if prod is not None else 0,
-            "transport_rounds_rank0": st.get("rounds", 0),
-            "transport_round_ms_rank0": round(st.get("round_ms", 0.0), 3),
-            "transport_ctrl_ms_rank0": round(st.get("ctrl_ms", 0.0), 4),
-            "transport_driver": ep.xport,
+            "frames_local_rank0_headline": int(c1.get("frames_local", 0) - c0.get("frames_local", 0)),
+            "frames_sent_rank0_headline": int(c1.get("frames_sent", 0) - c0.get("frames_sent", 0)),
             "bytes_sent_rank0": st.get("bytes_sent", 0),
+            "xgmi_phase": cross,
+            "staging": staging,
+            "staging_copies_span_frame_kernel": copies,
             "numa_node": numa,
-            "copy_engine": "blit" if os.environ.get("HSA_ENABLE_SDMA") == "0" else "sdma",
             "cpus_allowed": len(os.sched_getaffinity(0)),
             "producer_host_s_stage_acquire_launch_commit_total": (
                 [round(x, 4) for x in prod.engine.timing()] if prod is not None and prod.engine is not None
                 else None),
-            "producer_gpu_ms_h2d_chunks_calib_chunks": (
-                [round(x, 3) for x in prod.engine.gpu_timing()]
-                if prod is not None and prod.engine is not None and prod.engine.gpu_timing_enabled else None),
         },
     }
     if rank == 0:
@@ -315,21 +384,24 @@ def main(argv=None):
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     sys.stdout.flush()
-    if comm is not None:
-        # never let a communicator teardown hang the run after the result line
+    if sess is not None:
+        # never let a teardown hang the run after the result line: the watchdog exits NON-zero
         clean = ep.failed is None and not pt.is_alive()
-        wd = threading.Timer(60.0, lambda: os._exit(0 if clean else 3))
+
+        def _teardown_timeout():
+            print(f"bench.py rank {rank}: teardown timed out", file=sys.stderr, flush=True)
+            os._exit(3)
+
+        wd = threading.Timer(60.0, _teardown_timeout)
         wd.daemon = True
         wd.start()
-        if clean:
-            ep.close()
-            comm.close()
-            dist.destroy_process_group()
-        else:
-            comm.abort()
+        ep.close()
+        barrier()
+        dist.destroy_process_group()
         wd.cancel()
         if not clean:
-            os._exit(3)
+            print(f"bench.py rank {rank}: queue fabric reported {ep.failed!r}", file=sys.stderr, flush=True)
+            return 3
     return 0
 
 

@@ -2,6 +2,7 @@
 // integers (tensor.data_ptr(), torch.cuda.current_stream().cuda_stream), so this module does
 // not depend on the torch C++ ABI; the Python layer validates shapes/dtypes/devices first.
 #include <algorithm>
+#include <memory>
 
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -12,18 +13,69 @@
 namespace py = pybind11;
 
 #include "engine.h"
+#include "fabric.h"
 #include "kernels.h"
 #include "trace.h"
-#include "transport.h"
-#include "xport_engine.h"
 #include "xtc2.h"
 
-namespace pr {
-std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers, const std::vector<int64_t>& credits,
-                                       int64_t round_id, int policy);
-}
 
 using pr::FramePtrs;
+
+// Minimal DLPack (v0.8 ABI, unversioned "dltensor" capsule) so HBM ring segments we allocate with
+// hipMalloc become torch tensors (torch.from_dlpack) without any torch C++ dependency.
+namespace dl {
+struct Device {
+  int32_t device_type;  // kDLROCM = 10, kDLCPU = 1
+  int32_t device_id;
+};
+struct DataType {
+  uint8_t code;  // kDLUInt = 1
+  uint8_t bits;
+  uint16_t lanes;
+};
+struct Tensor {
+  void* data;
+  Device device;
+  int32_t ndim;
+  DataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct Managed {
+  Tensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(Managed* self);
+};
+struct Ctx {
+  std::shared_ptr<pr::DeviceBuffer> buf;
+  int64_t shape[1];
+};
+}  // namespace dl
+
+static py::capsule device_buffer_dlpack(std::shared_ptr<pr::DeviceBuffer> buf) {
+  auto* ctx = new dl::Ctx{buf, {buf->bytes()}};
+  auto* m = new dl::Managed{};
+  m->dl_tensor.data = reinterpret_cast<void*>(buf->ptr());
+  m->dl_tensor.device = dl::Device{10, buf->device()};
+  m->dl_tensor.ndim = 1;
+  m->dl_tensor.dtype = dl::DataType{1, 8, 1};
+  m->dl_tensor.shape = ctx->shape;
+  m->dl_tensor.strides = nullptr;
+  m->dl_tensor.byte_offset = 0;
+  m->manager_ctx = ctx;
+  m->deleter = [](dl::Managed* self) {
+    delete static_cast<dl::Ctx*>(self->manager_ctx);
+    delete self;
+  };
+  // a capsule never consumed (renamed "used_dltensor") frees the tensor itself
+  return py::capsule(m, "dltensor", [](PyObject* cap) {
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto* mm = static_cast<dl::Managed*>(PyCapsule_GetPointer(cap, "dltensor"));
+      if (mm != nullptr && mm->deleter != nullptr) mm->deleter(mm);
+    }
+  });
+}
 
 static FramePtrs make_ptrs(const std::vector<uint64_t>& in, const std::vector<uint64_t>& out) {
   pr::check(in.size() == out.size(), "input/output pointer lists differ in length");
@@ -121,12 +173,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("summary"), py::arg("stream"), py::arg("total") = 0);
   // consumer hot path: ring slots -> zeroed per-batch outputs -> peak finder, one native call
   m.def("peakfind_slots",
-        [](uint64_t base, int64_t slot_bytes, const std::vector<int>& slots, int n_panels, int rows, int cols,
-           float thr_peak, float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
+        [](const pr::SlotPool& pool, int64_t slot_bytes, const std::vector<int>& slots, int n_panels, int rows,
+           int cols, float thr_peak, float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
            uint64_t summary, uint64_t total, uint64_t stream, uint64_t zero_ptr, int64_t zero_bytes) {
           const int n = (int)slots.size();
           pr::check(n >= 1, "peakfind_slots: no slots");
-          pr::check(base != 0 && slot_bytes >= (int64_t)n_panels * rows * cols * 4, "peakfind_slots: bad ring");
+          pr::check(slot_bytes >= (int64_t)n_panels * rows * cols * 4, "peakfind_slots: frame larger than a slot");
           hipStream_t s = reinterpret_cast<hipStream_t>(stream);
           if (zero_ptr != 0) {   // caller-provided region covering counts + summary: one fill
             pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(zero_ptr), 0, (size_t)zero_bytes, s), "zero outputs");
@@ -137,22 +189,17 @@ PYBIND11_MODULE(_C, m) {
           for (int a = 0; a < n; a += pr::kMaxFrames) {
             const int m = std::min(pr::kMaxFrames, n - a);
             std::vector<uint64_t> in(m);
-            for (int i = 0; i < m; ++i) {
-              pr::check(slots[a + i] >= 0, "peakfind_slots: negative slot");
-              in[i] = base + (uint64_t)slots[a + i] * (uint64_t)slot_bytes;
-            }
+            for (int i = 0; i < m; ++i) in[i] = pool.slot_ptr(slots[a + i]);
             pr::launch_peakfind(make_ptrs(in, in), m, n_panels, rows, cols, thr_peak, son_min, radius, max_peaks,
                                 peaks + (uint64_t)a * max_peaks * 32, counts + (uint64_t)a * 4,
                                 summary + (uint64_t)a * 8, total, stream);
           }
         },
-        py::arg("base"), py::arg("slot_bytes"), py::arg("slots"), py::arg("n_panels"), py::arg("rows"),
+        py::arg("pool"), py::arg("slot_bytes"), py::arg("slots"), py::arg("n_panels"), py::arg("rows"),
         py::arg("cols"), py::arg("thr_peak"), py::arg("son_min"), py::arg("radius"), py::arg("max_peaks"),
         py::arg("peaks"), py::arg("counts"), py::arg("summary"), py::arg("total"), py::arg("stream"),
         py::arg("zero_ptr") = 0, py::arg("zero_bytes") = 0, py::call_guard<py::gil_scoped_release>());
 
-  m.def("plan_round", &pr::plan_round_native, py::arg("offers"), py::arg("credits"), py::arg("round_id"),
-        py::arg("policy"), "flattened (producer, offer_index, consumer) triples");
   m.def("copy_h2d_kernel",
         [](uint64_t dst, uint64_t src, int64_t bytes, int workgroups, uint64_t stream) {
           return pr::launch_copy_h2d(dst, src, bytes, workgroups, stream);
@@ -164,91 +211,78 @@ PYBIND11_MODULE(_C, m) {
   m.def("memcpy_h2d_batch", &pr::memcpy_h2d_batch, py::arg("dst"), py::arg("src"), py::arg("bytes"),
         py::arg("stream"));
 
-  m.def("rccl_version", &pr::rccl_version);
-  m.def("rccl_unique_id", [] {
-    const auto v = pr::rccl_unique_id();
-    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
-  });
-  py::class_<pr::RcclTransport>(m, "RcclTransport")
-      .def(py::init([](const py::bytes& id, int rank, int world, int device) {
-             const std::string s = id;
-             std::vector<uint8_t> v(s.begin(), s.end());
-             py::gil_scoped_release nogil;   // ncclCommInitRank blocks until every rank joined
-             return new pr::RcclTransport(v, rank, world, device);
-           }),
-           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
-      .def("exchange", &pr::RcclTransport::exchange, py::arg("send_ptrs"), py::arg("send_peers"),
-           py::arg("recv_ptrs"), py::arg("recv_peers"), py::arg("bytes"), py::arg("stream"),
-           py::call_guard<py::gil_scoped_release>())
-      .def("round", &pr::RcclTransport::round, py::arg("pool"), py::arg("ring_base"), py::arg("slot_bytes"),
-           py::arg("send_slots"), py::arg("send_peers"), py::arg("recv_peers"), py::arg("recv_headers"),
-           py::arg("stream"), py::call_guard<py::gil_scoped_release>())
-      .def("async_error", &pr::RcclTransport::async_error)
-      .def("abort", &pr::RcclTransport::abort, py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("rank", &pr::RcclTransport::rank)
-      .def_property_readonly("world", &pr::RcclTransport::world)
-      .def_property_readonly("bytes_sent", &pr::RcclTransport::bytes_sent)
-      .def_property_readonly("bytes_recv", &pr::RcclTransport::bytes_recv)
-      .def_property_readonly("groups", &pr::RcclTransport::groups);
+  py::class_<pr::DeviceBuffer, std::shared_ptr<pr::DeviceBuffer>>(m, "DeviceBuffer")
+      .def(py::init<int64_t, int>(), py::arg("bytes"), py::arg("device"))
+      .def_property_readonly("ptr", &pr::DeviceBuffer::ptr)
+      .def_property_readonly("nbytes", &pr::DeviceBuffer::bytes)
+      .def_property_readonly("device", &pr::DeviceBuffer::device)
+      .def("__dlpack__", [](std::shared_ptr<pr::DeviceBuffer> b, py::kwargs) { return device_buffer_dlpack(b); })
+      .def("__dlpack_device__", [](const pr::DeviceBuffer& b) { return py::make_tuple(10, b.device()); });
 
-
-  py::class_<pr::ShmControl>(m, "ShmControl")
-      .def(py::init<const std::string&, bool, int, int, int, int64_t, double>(), py::arg("name"), py::arg("create"),
-           py::arg("rank"), py::arg("world"), py::arg("vec_words"), py::arg("outbox_bytes"), py::arg("timeout_s"),
-           py::call_guard<py::gil_scoped_release>())
-      .def("unlink", &pr::ShmControl::unlink)
-      .def("allgather",
-           [](pr::ShmControl& c, int64_t round, const std::vector<int64_t>& vec) {
-             pr::check((int)vec.size() == c.vec_words(), "ShmControl.allgather: vector size mismatch");
-             std::vector<int64_t> out((size_t)c.world() * c.vec_words());
-             {
-               py::gil_scoped_release nogil;
-               c.allgather(round, vec.data(), out.data());
-             }
-             return out;
-           },
-           py::arg("round"), py::arg("vec"))
-      .def("set_failed", &pr::ShmControl::set_failed)
-      .def("cancel", &pr::ShmControl::cancel)
-      .def("set_check_pids", &pr::ShmControl::set_check_pids)
-      .def_property_readonly("name", &pr::ShmControl::name)
-      .def_property_readonly("rank", &pr::ShmControl::rank)
-      .def_property_readonly("world", &pr::ShmControl::world)
-      .def_property_readonly("vec_words", &pr::ShmControl::vec_words)
-      .def_property_readonly("outbox_bytes", &pr::ShmControl::outbox_bytes);
-  m.def("xport_vec_words", &pr::TransportEngine::vec_words_for, py::arg("max_offer"));
-
-  py::class_<pr::XportStats>(m, "XportStats")
-      .def_readonly("rounds", &pr::XportStats::rounds)
-      .def_readonly("idle_rounds", &pr::XportStats::idle_rounds)
-      .def_readonly("frames_routed", &pr::XportStats::frames_routed)
-      .def_readonly("frames_sent", &pr::XportStats::frames_sent)
-      .def_readonly("frames_recv", &pr::XportStats::frames_recv)
-      .def_readonly("frames_local", &pr::XportStats::frames_local)
-      .def_readonly("bytes_sent", &pr::XportStats::bytes_sent)
-      .def_readonly("bytes_recv", &pr::XportStats::bytes_recv)
-      .def_readonly("round_s", &pr::XportStats::round_s)
-      .def_readonly("ctrl_s", &pr::XportStats::ctrl_s)
-      .def_readonly("data_s", &pr::XportStats::data_s);
-
-  py::class_<pr::TransportEngine>(m, "TransportEngine")
-      .def(py::init<pr::SlotPool*, pr::ShmControl*, pr::RcclTransport*, uint64_t, int64_t, int, int,
-                    const std::vector<int>&, bool, bool, int, int, bool, uint64_t, int>(),
-           py::arg("pool"), py::arg("ctrl"), py::arg("rccl"), py::arg("ring_base"), py::arg("slot_bytes"),
-           py::arg("rank"), py::arg("world"), py::arg("producer_ranks"), py::arg("is_producer"),
-           py::arg("is_consumer"), py::arg("policy"), py::arg("max_offer"), py::arg("loopback"), py::arg("stream"),
-           py::arg("device"), py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
-      .def("start", &pr::TransportEngine::start)
-      .def("join", &pr::TransportEngine::join, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
-      .def("step", &pr::TransportEngine::step, py::call_guard<py::gil_scoped_release>())
-      .def("set_producer_finished", &pr::TransportEngine::set_producer_finished)
-      .def("set_consumer_closed", &pr::TransportEngine::set_consumer_closed)
-      .def("request_stop", &pr::TransportEngine::request_stop)
-      .def_property_readonly("done", &pr::TransportEngine::done)
-      .def_property_readonly("consumers_gone", &pr::TransportEngine::consumers_gone)
-      .def_property_readonly("running", &pr::TransportEngine::running)
-      .def("error", &pr::TransportEngine::error)
-      .def("stats", &pr::TransportEngine::stats);
+  // ---- elastic queue fabric (fabric.h)
+  m.def("pid_alive", &pr::pid_alive, py::arg("pid"));
+  m.def("shm_remove", &pr::shm_remove, py::arg("name"));
+  py::class_<pr::ShmRegion>(m, "ShmRegion", py::buffer_protocol())
+      .def(py::init<const std::string&, int64_t, bool, double>(), py::arg("name"), py::arg("bytes"),
+           py::arg("create"), py::arg("timeout_s") = 10.0, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("ptr", &pr::ShmRegion::ptr)
+      .def_property_readonly("nbytes", &pr::ShmRegion::bytes)
+      .def_property_readonly("name", &pr::ShmRegion::name)
+      .def("unlink", &pr::ShmRegion::unlink)
+      .def_buffer([](pr::ShmRegion& r) -> py::buffer_info {
+        return py::buffer_info(reinterpret_cast<void*>(r.ptr()), 1, py::format_descriptor<uint8_t>::format(), 1,
+                               {(py::ssize_t)r.bytes()}, {(py::ssize_t)1});
+      });
+  py::class_<pr::FabricStats>(m, "FabricStats")
+      .def_readonly("iterations", &pr::FabricStats::iterations)
+      .def_readonly("idle_iterations", &pr::FabricStats::idle_iterations)
+      .def_readonly("frames_local", &pr::FabricStats::frames_local)
+      .def_readonly("frames_sent", &pr::FabricStats::frames_sent)
+      .def_readonly("frames_recv", &pr::FabricStats::frames_recv)
+      .def_readonly("frames_requeued", &pr::FabricStats::frames_requeued)
+      .def_readonly("grants_given", &pr::FabricStats::grants_given)
+      .def_readonly("grants_returned", &pr::FabricStats::grants_returned)
+      .def_readonly("grants_reclaimed", &pr::FabricStats::grants_reclaimed)
+      .def_readonly("bytes_sent", &pr::FabricStats::bytes_sent)
+      .def_readonly("bytes_recv", &pr::FabricStats::bytes_recv)
+      .def_readonly("batches", &pr::FabricStats::batches)
+      .def_readonly("links_opened", &pr::FabricStats::links_opened)
+      .def_readonly("peers_dead", &pr::FabricStats::peers_dead)
+      .def_readonly("copy_s", &pr::FabricStats::copy_s);
+  py::class_<pr::LinkStatus>(m, "LinkStatus")
+      .def_readonly("peer", &pr::LinkStatus::peer)
+      .def_readonly("outgoing", &pr::LinkStatus::outgoing)
+      .def_readonly("attached", &pr::LinkStatus::attached)
+      .def_readonly("eos", &pr::LinkStatus::eos)
+      .def_readonly("detached", &pr::LinkStatus::detached)
+      .def_readonly("dead", &pr::LinkStatus::dead)
+      .def_readonly("closed", &pr::LinkStatus::closed)
+      .def_readonly("outstanding", &pr::LinkStatus::outstanding)
+      .def_readonly("frames", &pr::LinkStatus::frames);
+  py::class_<pr::QueueFabric>(m, "QueueFabric")
+      .def(py::init<pr::SlotPool*, int64_t, int, bool, bool, int, int64_t>(), py::arg("pool"),
+           py::arg("slot_bytes"), py::arg("device"), py::arg("is_producer"), py::arg("is_consumer"),
+           py::arg("policy"), py::arg("self_mid"), py::keep_alive<1, 2>())
+      .def("export_host_ring", &pr::QueueFabric::export_host_ring, py::arg("shm_name"))
+      .def("export_ipc_ring", &pr::QueueFabric::export_ipc_ring)
+      .def_property_readonly("export_segments", &pr::QueueFabric::export_segments)
+      .def("add_in_link", &pr::QueueFabric::add_in_link, py::arg("producer_mid"), py::arg("name"))
+      .def("add_out_link", &pr::QueueFabric::add_out_link, py::arg("consumer_mid"), py::arg("name"))
+      .def("drop_peer", &pr::QueueFabric::drop_peer, py::arg("mid"))
+      .def("set_policy", &pr::QueueFabric::set_policy, py::arg("policy"))
+      .def("set_producer_finished", &pr::QueueFabric::set_producer_finished)
+      .def("set_consumer_closed", &pr::QueueFabric::set_consumer_closed)
+      .def("start", &pr::QueueFabric::start)
+      .def("request_stop", &pr::QueueFabric::request_stop)
+      .def("join", &pr::QueueFabric::join, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
+      .def("step", &pr::QueueFabric::step, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("running", &pr::QueueFabric::running)
+      .def_property_readonly("producer_drained", &pr::QueueFabric::producer_drained)
+      .def_property_readonly("consumer_quiesced", &pr::QueueFabric::consumer_quiesced)
+      .def_property_readonly("policy", &pr::QueueFabric::policy)
+      .def("error", &pr::QueueFabric::error)
+      .def("stats", &pr::QueueFabric::stats)
+      .def("links", &pr::QueueFabric::links);
 
   py::class_<pr::PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())
       .def(py::init<size_t>(), py::arg("bytes"))
@@ -290,6 +324,8 @@ PYBIND11_MODULE(_C, m) {
   py::class_<SP>(m, "SlotPool")
       .def(py::init<int, int, int>(), py::arg("producer_budget"), py::arg("consumer_budget"), py::arg("device"))
       .def_property_readonly("n_slots", &SP::n_slots)
+      .def("set_slot_ptrs", &SP::set_slot_ptrs, py::arg("ptrs"))
+      .def("slot_ptr", &SP::slot_ptr, py::arg("slot"))
       .def_property_readonly("producer_budget", &SP::producer_budget)
       .def_property_readonly("consumer_budget", &SP::consumer_budget)
       .def("try_acquire_produce", &SP::try_acquire_produce)
@@ -331,6 +367,10 @@ PYBIND11_MODULE(_C, m) {
       .def("begin_recv_batch", &SP::begin_recv_batch, py::arg("n"), py::arg("stream"))
       .def("end_send_batch", &SP::end_send_batch, py::arg("slots"), py::arg("stream"))
       .def("end_recv_batch", &SP::end_recv_batch, py::arg("slots"), py::arg("headers"), py::arg("stream"))
+      .def("grant_batch", &SP::grant_batch, py::arg("max_n"))
+      .def("complete_recv_batch", &SP::complete_recv_batch, py::arg("slots"), py::arg("headers"))
+      .def("cancel_recv_batch", &SP::cancel_recv_batch, py::arg("slots"))
+      .def("unsend_batch", &SP::unsend_batch, py::arg("slots"))
       .def_property_readonly("event_records", &SP::event_records);
 
   py::class_<pr::CalibPlan>(m, "CalibPlan")
@@ -372,8 +412,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream"));
 
   py::class_<pr::ProducerEngine>(m, "ProducerEngine")
-      .def(py::init<pr::SlotPool*, uint64_t, int64_t, int, const pr::CalibPlan&, int, int, int64_t, int64_t>(),
-           py::arg("pool"), py::arg("ring_base"), py::arg("slot_bytes"), py::arg("device"), py::arg("plan"),
+      .def(py::init<pr::SlotPool*, int64_t, int, const pr::CalibPlan&, int, int, int64_t, int64_t>(),
+           py::arg("pool"), py::arg("slot_bytes"), py::arg("device"), py::arg("plan"),
            py::arg("chunk"), py::arg("n_raw_bufs"), py::arg("rank"), py::arg("size"), py::keep_alive<1, 2>())
       .def("set_cycled_source", &pr::ProducerEngine::set_cycled_source, py::arg("frames"), py::arg("photon_energy"))
       .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"), py::arg("k0") = 0)

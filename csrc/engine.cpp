@@ -81,9 +81,9 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
 }
 
 // ---------------------------------------------------------------------------------------
-ProducerEngine::ProducerEngine(SlotPool* pool, uint64_t ring_base, int64_t slot_bytes, int device,
+ProducerEngine::ProducerEngine(SlotPool* pool, int64_t slot_bytes, int device,
                                const CalibPlan& plan, int chunk, int n_raw_bufs, int64_t rank, int64_t size)
-    : pool_(pool), ring_base_(ring_base), slot_bytes_(slot_bytes), device_(device), plan_(plan),
+    : pool_(pool), slot_bytes_(slot_bytes), device_(device), plan_(plan),
       chunk_(std::max(1, std::min(chunk, kMaxFrames))), n_raw_bufs_(std::max(2, n_raw_bufs)), rank_(rank),
       size_(size), hdr_rank_(rank) {
   check(pool != nullptr && device >= 0, "ProducerEngine needs a device SlotPool");
@@ -388,7 +388,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
         hip_check(hipStreamWaitEvent(compute_, h2d_done_[b], 0), "wait h2d");
         for (int q = 0; q < n; ++q) in[q] = dev_in_[b][q];
       }
-      for (int q = 0; q < n; ++q) out[q] = ring_base_ + (uint64_t)slots[q] * (uint64_t)slot_bytes_;
+      for (int q = 0; q < n; ++q) out[q] = pool_->slot_ptr(slots[q]);
       if (gpu_timing_) {
         if (device_resident_) harvest(b, false);
         hip_check(hipEventRecord(calib_start_[b], compute_), "record calib start");

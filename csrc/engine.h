@@ -61,7 +61,7 @@ void run_calib_plan(const CalibPlan& plan, const std::vector<uint64_t>& in, cons
 
 class ProducerEngine {
  public:
-  ProducerEngine(SlotPool* pool, uint64_t ring_base, int64_t slot_bytes, int device, const CalibPlan& plan,
+  ProducerEngine(SlotPool* pool, int64_t slot_bytes, int device, const CalibPlan& plan,
                  int chunk, int n_raw_bufs, int64_t rank, int64_t size);
   ~ProducerEngine();
   ProducerEngine(const ProducerEngine&) = delete;
@@ -100,7 +100,6 @@ class ProducerEngine {
   void loop(int64_t n_local_events, int64_t max_steps, int64_t k0);
 
   SlotPool* pool_;
-  uint64_t ring_base_;
   int64_t slot_bytes_;
   int device_;
   CalibPlan plan_;

@@ -1,0 +1,944 @@
+#include "fabric.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+#include "common.h"
+#include "trace.h"
+
+namespace pr {
+
+namespace {
+
+constexpr uint64_t kLinkMagic = 0x314B4E494C525350ull;  // "PSRLINK1"
+constexpr int32_t kLinkVersion = 1;
+constexpr int32_t kNoticeReturned = 1;   // the grant comes back unused (producer finished / closing)
+constexpr double kPidCheckS = 0.05;
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void nap_ns(long ns) {
+  timespec ts{0, ns};
+  nanosleep(&ts, nullptr);
+}
+
+size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct Notice {
+  int32_t slot;
+  int32_t flags;
+  int64_t rank, idx, gevt;
+  double photon_energy;
+  int64_t aux;
+};
+static_assert(sizeof(Notice) == 48, "Notice layout");
+
+// The mailbox of one link.  Written by the consumer at creation; afterwards every field has ONE
+// writer: grants/g_head/consumer_closed by the consumer, the rest by the producer.  Counters are
+// monotonic; ring entries are written before the counter is released and read after it is
+// acquired.  Occupancy of both rings is bounded by the outstanding grants (<= n_slots): a slot
+// is granted again only after the consumer took its notice and the frame was released.
+struct SegDesc {          // one allocation of an HBM consumer ring
+  uint8_t handle[HIP_IPC_HANDLE_SIZE];
+  int64_t offset;         // of slot `first` inside the allocation
+  int32_t first, n;       // slots [first, first + n) are contiguous in it
+};
+
+struct alignas(64) LinkSeg {
+  uint64_t magic;
+  int32_t version;
+  int32_t n_slots;        // slots of the consumer ring = capacity of the grant / notice rings
+  int64_t slot_bytes;
+  int64_t producer_mid, consumer_mid;
+  int64_t consumer_pid;
+  int32_t kind;           // 0 host shared memory, 1 HIP IPC
+  int32_t consumer_device;
+  int32_t n_segs;
+  int32_t pad_;
+  char ring_name[128];
+  SegDesc segs[QueueFabric::kMaxSegments];
+  std::atomic<uint64_t> ready;
+  alignas(64) std::atomic<int64_t> producer_pid;       // 0 until the producer attached
+  alignas(64) std::atomic<uint64_t> g_head;            // consumer -> producer
+  alignas(64) std::atomic<uint64_t> g_tail;
+  alignas(64) std::atomic<uint64_t> n_head;            // producer -> consumer
+  alignas(64) std::atomic<uint64_t> n_tail;
+  alignas(64) std::atomic<uint32_t> consumer_closed;
+  alignas(64) std::atomic<uint32_t> producer_eos;
+  std::atomic<uint32_t> producer_detached;
+  std::atomic<uint32_t> producer_ack_closed;           // no copy into this ring is in flight any more
+  std::atomic<int64_t> producer_backlog;               // frames waiting at the producer (demand hint)
+};
+static_assert(std::atomic<uint64_t>::is_always_lock_free && std::atomic<int64_t>::is_always_lock_free,
+              "lock-free 64-bit atomics are required in shared memory");
+
+size_t grants_off() { return round_up(sizeof(LinkSeg), 64); }
+size_t notices_off(int n) { return grants_off() + round_up((size_t)n * sizeof(int32_t), 64); }
+size_t seg_bytes(int n) { return round_up(notices_off(n) + (size_t)n * sizeof(Notice), 4096); }
+int32_t* seg_grants(LinkSeg* s) { return reinterpret_cast<int32_t*>(reinterpret_cast<uint8_t*>(s) + grants_off()); }
+Notice* seg_notices(LinkSeg* s) {
+  return reinterpret_cast<Notice*>(reinterpret_cast<uint8_t*>(s) + notices_off(s->n_slots));
+}
+
+}  // namespace
+
+// A peer that exited is either gone (ESRCH) or a zombie its parent has not reaped yet (state Z/X
+// in /proc/<pid>/stat), e.g. under multiprocessing until join().
+bool pid_alive(int64_t pid) {
+  if (pid <= 0) return false;
+  if (kill((pid_t)pid, 0) != 0 && errno == ESRCH) return false;
+  char path[64];
+  snprintf(path, sizeof(path), "/proc/%lld/stat", (long long)pid);
+  FILE* f = fopen(path, "r");
+  if (f == nullptr) return true;  // no procfs view (other pid namespace): trust kill()
+  char buf[512];
+  const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  const char* rp = strrchr(buf, ')');   // comm may contain spaces / parentheses
+  if (rp == nullptr || rp[1] == 0 || rp[2] == 0) return true;
+  return rp[2] != 'Z' && rp[2] != 'X';
+}
+
+bool shm_remove(const std::string& name) { return !name.empty() && shm_unlink(name.c_str()) == 0; }
+
+// ---------------------------------------------------------------------------------------
+ShmRegion::ShmRegion(const std::string& name, int64_t bytes, bool create, double timeout_s)
+    : name_(name), bytes_(bytes) {
+  check(!name.empty() && name[0] == '/' && name.size() < 120, "ShmRegion: name must start with '/' (< 120 chars)");
+  check(bytes > 0, "ShmRegion: size must be > 0");
+  int fd = -1;
+  if (create) {
+    fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    check(fd >= 0, "ShmRegion: shm_open(create " + name + ") failed: " + strerror(errno));
+    if (ftruncate(fd, (off_t)bytes) != 0) {
+      const int e = errno;
+      close(fd);
+      shm_unlink(name.c_str());
+      throw std::runtime_error(std::string("psana_ray_amd: ShmRegion: ftruncate failed: ") + strerror(e));
+    }
+    owner_ = true;
+  } else {
+    const double t0 = now_s();
+    while (true) {
+      fd = shm_open(name.c_str(), O_RDWR, 0600);
+      if (fd >= 0) {
+        struct stat sb;
+        if (fstat(fd, &sb) == 0 && (int64_t)sb.st_size >= bytes) break;
+        close(fd);
+        fd = -1;
+      }
+      check(now_s() - t0 < timeout_s, "ShmRegion: timed out attaching to " + name);
+      nap_ns(1000000);
+    }
+  }
+  void* p = mmap(nullptr, (size_t)bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) {
+    if (owner_) shm_unlink(name.c_str());
+    throw std::runtime_error(std::string("psana_ray_amd: ShmRegion: mmap failed: ") + strerror(errno));
+  }
+  base_ = static_cast<uint8_t*>(p);
+}
+
+ShmRegion::~ShmRegion() {
+  if (base_ != nullptr) munmap(base_, (size_t)bytes_);
+  if (owner_ && !unlinked_) shm_unlink(name_.c_str());
+}
+
+void ShmRegion::unlink() {
+  if (owner_ && !unlinked_) {
+    shm_unlink(name_.c_str());
+    unlinked_ = true;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+struct QueueFabric::Link {
+  int64_t peer = -1;
+  bool outgoing = false;
+  std::string name;
+  LinkSeg* seg = nullptr;
+  size_t map_bytes = 0;
+  int n = 0;
+  bool attached = false, dead = false, closed = false, eos = false, detached = false, named = true;
+  double t_added = 0, last_check = 0;
+  int64_t frames = 0;
+  // producer side (outgoing)
+  std::deque<int> grants;
+  uint64_t g_tail = 0, n_head = 0;
+  std::vector<uint64_t> remote;       // address of every slot of the consumer ring (this process's view)
+  std::vector<void*> ipc_ptrs;        // one mapping per ring segment
+  std::unique_ptr<ShmRegion> remote_ring;
+  int inflight = 0;
+  bool eos_posted = false, acked_close = false;
+  // consumer side (incoming)
+  uint64_t g_head = 0, n_tail = 0;
+  std::vector<uint8_t> owed;  // slot -> granted to this producer and not answered
+  int64_t outstanding = 0;
+
+  ~Link() {
+    if (seg != nullptr) munmap(seg, map_bytes);
+  }
+  LinkStatus status() const {
+    LinkStatus s;
+    s.peer = peer;
+    s.outgoing = outgoing;
+    s.attached = attached;
+    s.eos = eos;
+    s.detached = detached;
+    s.dead = dead;
+    s.closed = closed;
+    s.outstanding = outgoing ? (int64_t)grants.size() : outstanding;
+    s.frames = frames;
+    return s;
+  }
+};
+
+struct QueueFabric::Batch {
+  std::shared_ptr<Link> link;
+  std::vector<int> slots, rslots;
+  std::vector<SlotHeader> hdrs;
+  hipEvent_t ev = nullptr;
+  double t_issue = 0;
+};
+
+QueueFabric::QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is_producer, bool is_consumer,
+                         int policy, int64_t self_mid)
+    : pool_(pool), slot_bytes_(slot_bytes), device_(device), is_producer_(is_producer), is_consumer_(is_consumer),
+      policy_(policy), self_mid_(self_mid) {
+  check(pool != nullptr && slot_bytes > 0, "QueueFabric: empty ring");
+  check((int)pool->slot_ptrs().size() == pool->n_slots(), "QueueFabric: the pool has no slot addresses");
+  check(policy >= 0 && policy <= 2, "QueueFabric: unknown routing policy");
+  check(is_producer || is_consumer, "QueueFabric: a member must produce or consume");
+  if (device_ >= 0) {
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate (fabric)");
+  }
+  if (!is_producer) drained_.store(true);
+}
+
+QueueFabric::~QueueFabric() {
+  stop_.store(true);
+  if (th_.joinable()) th_.join();
+  try {
+    if (device_ >= 0) hip_check(hipSetDevice(device_), "hipSetDevice");
+    // copies still in flight complete into memory we keep mapped until here
+    for (auto& b : inflight_)
+      if (b.ev != nullptr) (void)hipEventSynchronize(b.ev);
+    inflight_.clear();
+    for (auto& l : links_) {
+      if (l->seg == nullptr) continue;
+      if (l->outgoing) {
+        if (l->attached) {
+          l->seg->producer_ack_closed.store(1, std::memory_order_release);
+          l->seg->producer_detached.store(1, std::memory_order_release);
+        }
+        release_out_link(*l);
+      } else {
+        l->seg->consumer_closed.store(1, std::memory_order_release);
+        if (l->named) shm_remove(l->name);
+      }
+    }
+    links_.clear();
+    for (auto e : all_events_) (void)hipEventDestroy(e);
+    if (stream_ != nullptr) (void)hipStreamDestroy(stream_);
+  } catch (...) {
+  }
+}
+
+std::string QueueFabric::error() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return error_;
+}
+
+FabricStats QueueFabric::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return st_;
+}
+
+std::vector<LinkStatus> QueueFabric::links() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<LinkStatus> v = status_;
+  v.insert(v.end(), retired_.begin(), retired_.end());
+  return v;
+}
+
+void QueueFabric::fail(const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (error_.empty()) error_ = msg;
+  }
+  pool_->wake_all();
+}
+
+void QueueFabric::export_host_ring(const std::string& shm_name) {
+  check(is_consumer_, "QueueFabric: only a consumer exports its ring");
+  check(shm_name.size() < 120, "QueueFabric: ring name too long");
+  export_kind_ = 0;
+  export_name_ = shm_name;
+}
+
+void QueueFabric::export_ipc_ring() {
+  check(is_consumer_ && device_ >= 0, "QueueFabric: IPC export needs a GPU consumer");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  segs_.clear();
+  const int n = pool_->n_slots();
+  uint64_t cur_base = 0, cur_first_ptr = 0;
+  for (int s = 0; s < n; ++s) {
+    const uint64_t p = pool_->slot_ptr(s);
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hip_check(hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(p)),
+              "hipMemGetAddressRange (ring segment)");
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    check(p + (uint64_t)slot_bytes_ <= b + (uint64_t)size, "QueueFabric: a ring slot straddles two allocations");
+    if (!segs_.empty() && b == cur_base && p == cur_first_ptr + (uint64_t)segs_.back().n * (uint64_t)slot_bytes_) {
+      ++segs_.back().n;
+      continue;
+    }
+    check((int)segs_.size() < kMaxSegments, "QueueFabric: ring has too many segments to export");
+    check(size <= (size_t(2) << 30), "QueueFabric: ring allocations above 2 GiB cannot be opened over HIP IPC");
+    SegExport e;
+    hipIpcMemHandle_t h;
+    hip_check(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle (ring segment)");
+    e.handle.assign(reinterpret_cast<const uint8_t*>(h.reserved),
+                    reinterpret_cast<const uint8_t*>(h.reserved) + HIP_IPC_HANDLE_SIZE);
+    e.offset = (int64_t)(p - b);
+    e.first = s;
+    e.n = 1;
+    segs_.push_back(std::move(e));
+    cur_base = b;
+    cur_first_ptr = p;
+  }
+  export_kind_ = 1;
+}
+
+void QueueFabric::add_in_link(int64_t producer_mid, const std::string& name) {
+  check(is_consumer_, "QueueFabric.add_in_link: not a consumer");
+  check(export_kind_ >= 0, "QueueFabric.add_in_link: export the ring first");
+  std::lock_guard<std::mutex> lk(ops_mu_);
+  ops_.push_back(Op{0, producer_mid, name});
+}
+
+void QueueFabric::add_out_link(int64_t consumer_mid, const std::string& name) {
+  check(is_producer_, "QueueFabric.add_out_link: not a producer");
+  std::lock_guard<std::mutex> lk(ops_mu_);
+  ops_.push_back(Op{1, consumer_mid, name});
+}
+
+void QueueFabric::drop_peer(int64_t mid) {
+  std::lock_guard<std::mutex> lk(ops_mu_);
+  ops_.push_back(Op{2, mid, ""});
+}
+
+void QueueFabric::set_policy(int policy) {
+  check(policy >= 0 && policy <= 2, "QueueFabric: unknown routing policy");
+  policy_.store(policy);
+}
+
+hipEvent_t QueueFabric::take_event() {
+  if (!free_events_.empty()) {
+    hipEvent_t e = free_events_.back();
+    free_events_.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate (fabric)");
+  all_events_.push_back(e);
+  return e;
+}
+
+void QueueFabric::apply_ops() {
+  std::vector<Op> ops;
+  {
+    std::lock_guard<std::mutex> lk(ops_mu_);
+    ops.swap(ops_);
+  }
+  for (const Op& op : ops) {
+    if (op.kind == 2) {
+      for (auto& l : links_)
+        if (l->peer == op.mid && !l->dead) {
+          l->dead = true;
+          std::lock_guard<std::mutex> lk(mu_);
+          ++st_.peers_dead;
+        }
+      continue;
+    }
+    bool dup = false;
+    for (auto& l : links_) dup |= (l->peer == op.mid && l->outgoing == (op.kind == 1));
+    if (dup) continue;
+    auto l = std::make_shared<Link>();
+    l->peer = op.mid;
+    l->outgoing = op.kind == 1;
+    l->name = op.name;
+    l->t_added = now_s();
+    if (op.kind == 0) {
+      // consumer: create the mailbox (a stale name from a crashed run is replaced)
+      const int n = std::max(1, pool_->n_slots());
+      const size_t bytes = seg_bytes(n);
+      int fd = shm_open(op.name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0 && errno == EEXIST) {
+        shm_unlink(op.name.c_str());
+        fd = shm_open(op.name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+      }
+      check(fd >= 0, "QueueFabric: shm_open(create " + op.name + ") failed: " + strerror(errno));
+      if (ftruncate(fd, (off_t)bytes) != 0) {
+        const int e = errno;
+        close(fd);
+        shm_unlink(op.name.c_str());
+        throw std::runtime_error(std::string("psana_ray_amd: QueueFabric: ftruncate failed: ") + strerror(e));
+      }
+      void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      close(fd);
+      check(p != MAP_FAILED, "QueueFabric: mmap of a link mailbox failed");
+      auto* s = static_cast<LinkSeg*>(p);   // zero-filled by ftruncate
+      s->magic = kLinkMagic;
+      s->version = kLinkVersion;
+      s->n_slots = n;
+      s->slot_bytes = slot_bytes_;
+      s->producer_mid = op.mid;
+      s->consumer_mid = self_mid_;
+      s->consumer_pid = (int64_t)getpid();
+      s->kind = export_kind_;
+      s->consumer_device = device_;
+      snprintf(s->ring_name, sizeof(s->ring_name), "%s", export_name_.c_str());
+      s->n_segs = (int32_t)segs_.size();
+      for (size_t k = 0; k < segs_.size(); ++k) {
+        memcpy(s->segs[k].handle, segs_[k].handle.data(), HIP_IPC_HANDLE_SIZE);
+        s->segs[k].offset = segs_[k].offset;
+        s->segs[k].first = segs_[k].first;
+        s->segs[k].n = segs_[k].n;
+      }
+      s->ready.store(1, std::memory_order_release);
+      l->seg = s;
+      l->map_bytes = bytes;
+      l->n = n;
+      l->owed.assign((size_t)pool_->n_slots(), 0);
+    }
+    links_.push_back(l);
+    std::lock_guard<std::mutex> lk(mu_);
+    ++st_.links_opened;
+  }
+}
+
+bool QueueFabric::try_attach(Link& l, double now) {
+  (void)now;
+  if (l.seg == nullptr) {
+    const int fd = shm_open(l.name.c_str(), O_RDWR, 0600);
+    if (fd < 0) return false;   // the consumer has not created it yet
+    struct stat sb;
+    if (fstat(fd, &sb) != 0 || (size_t)sb.st_size < seg_bytes(1)) {
+      close(fd);
+      return false;
+    }
+    void* p = mmap(nullptr, (size_t)sb.st_size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return false;
+    auto* s = static_cast<LinkSeg*>(p);
+    if (s->ready.load(std::memory_order_acquire) != 1 || (size_t)sb.st_size < seg_bytes(s->n_slots)) {
+      munmap(p, (size_t)sb.st_size);
+      return false;
+    }
+    l.seg = s;
+    l.map_bytes = (size_t)sb.st_size;
+  }
+  LinkSeg* s = l.seg;
+  check(s->magic == kLinkMagic && s->version == kLinkVersion, "QueueFabric: link mailbox " + l.name + " has a foreign layout");
+  check(s->slot_bytes == slot_bytes_, "QueueFabric: consumer " + std::to_string(l.peer) +
+                                          " has a different frame size (" + std::to_string(s->slot_bytes) + " vs " +
+                                          std::to_string(slot_bytes_) + " bytes)");
+  l.n = s->n_slots;
+  l.remote.assign((size_t)l.n, 0);
+  if (s->kind == 0) {
+    l.remote_ring.reset(new ShmRegion(std::string(s->ring_name), (int64_t)l.n * slot_bytes_, false, 5.0));
+    for (int k = 0; k < l.n; ++k) l.remote[k] = l.remote_ring->ptr() + (uint64_t)k * (uint64_t)slot_bytes_;
+  } else {
+    check(device_ >= 0, "QueueFabric: a GPU consumer's ring can only be written by a GPU producer");
+    check(s->n_segs >= 1 && s->n_segs <= kMaxSegments, "QueueFabric: bad segment table in " + l.name);
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    for (int k = 0; k < s->n_segs; ++k) {
+      const SegDesc& d = s->segs[k];
+      check(d.first >= 0 && d.n >= 1 && d.first + d.n <= l.n, "QueueFabric: bad segment in " + l.name);
+      hipIpcMemHandle_t h;
+      memcpy(h.reserved, d.handle, HIP_IPC_HANDLE_SIZE);
+      void* p = nullptr;
+      hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle (consumer ring)");
+      l.ipc_ptrs.push_back(p);
+      for (int j = 0; j < d.n; ++j)
+        l.remote[d.first + j] = reinterpret_cast<uint64_t>(p) + (uint64_t)d.offset + (uint64_t)j * (uint64_t)slot_bytes_;
+    }
+    for (int k = 0; k < l.n; ++k) check(l.remote[k] != 0, "QueueFabric: segment table leaves a slot unmapped");
+  }
+  l.g_tail = s->g_tail.load(std::memory_order_acquire);
+  l.n_head = s->n_head.load(std::memory_order_acquire);
+  s->producer_pid.store((int64_t)getpid(), std::memory_order_release);
+  l.attached = true;
+  return true;
+}
+
+void QueueFabric::release_out_link(Link& l) {
+  if (!l.ipc_ptrs.empty() && device_ >= 0) (void)hipSetDevice(device_);
+  for (void* p : l.ipc_ptrs) (void)hipIpcCloseMemHandle(p);
+  l.ipc_ptrs.clear();
+  l.remote_ring.reset();
+  l.remote.clear();
+}
+
+// ---------------------------------------------------------------------------------------
+int64_t QueueFabric::consumer_pass(double now) {
+  int64_t work = 0;
+  const bool closing = consumer_closed_.load();
+  std::vector<int> done_slots, ret_slots;
+  std::vector<SlotHeader> done_hdr;
+  for (auto& lp : links_) {
+    Link& l = *lp;
+    if (l.outgoing || l.seg == nullptr) continue;
+    LinkSeg* s = l.seg;
+    if (!l.attached && s->producer_pid.load(std::memory_order_acquire) != 0) {
+      l.attached = true;
+      if (l.named) {   // both ends mapped it: nothing may outlive the two processes
+        shm_remove(l.name);
+        l.named = false;
+      }
+    }
+    if (closing) s->consumer_closed.store(1, std::memory_order_release);
+    // EOS / detach flags BEFORE the notice head: a producer releases them after its last notice
+    const bool eos_flag = s->producer_eos.load(std::memory_order_acquire) != 0;
+    const bool det_flag = s->producer_detached.load(std::memory_order_acquire) != 0;
+    const uint64_t h = s->n_head.load(std::memory_order_acquire);
+    if (l.n_tail < h) {
+      Notice* ns = seg_notices(s);
+      done_slots.clear();
+      ret_slots.clear();
+      done_hdr.clear();
+      for (; l.n_tail < h; ++l.n_tail) {
+        const Notice nt = ns[l.n_tail % (uint64_t)l.n];
+        check(nt.slot >= 0 && nt.slot < (int)l.owed.size() && l.owed[nt.slot],
+              "QueueFabric: producer " + std::to_string(l.peer) + " answered a slot it was never granted");
+        l.owed[nt.slot] = 0;
+        --l.outstanding;
+        if (nt.flags & kNoticeReturned) {
+          ret_slots.push_back(nt.slot);
+        } else {
+          SlotHeader hd;
+          hd.rank = nt.rank;
+          hd.idx = nt.idx;
+          hd.gevt = nt.gevt;
+          hd.photon_energy = nt.photon_energy;
+          hd.aux = nt.aux;
+          done_slots.push_back(nt.slot);
+          done_hdr.push_back(hd);
+        }
+      }
+      s->n_tail.store(l.n_tail, std::memory_order_release);
+      pool_->complete_recv_batch(done_slots, done_hdr);
+      pool_->cancel_recv_batch(ret_slots);
+      l.frames += (int64_t)done_slots.size();
+      work += (int64_t)(done_slots.size() + ret_slots.size());
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.frames_recv += (int64_t)done_slots.size();
+      st_.bytes_recv += (int64_t)done_slots.size() * slot_bytes_;
+      st_.grants_returned += (int64_t)ret_slots.size();
+    }
+    if (eos_flag) l.eos = true;
+    if (det_flag) l.detached = true;
+    if (l.attached && !l.dead && now - l.last_check > kPidCheckS) {
+      l.last_check = now;
+      if (!pid_alive(s->producer_pid.load(std::memory_order_acquire))) {
+        l.dead = true;
+        std::lock_guard<std::mutex> lk(mu_);
+        ++st_.peers_dead;
+      }
+    }
+    if ((l.dead || l.detached) && l.outstanding > 0) {
+      // the producer is gone: everything it still owed comes back (a dead process's copies
+      // cannot land any more; a detached one synchronised them before leaving)
+      std::vector<int> back;
+      for (size_t i = 0; i < l.owed.size(); ++i)
+        if (l.owed[i]) {
+          back.push_back((int)i);
+          l.owed[i] = 0;
+        }
+      pool_->cancel_recv_batch(back);
+      l.outstanding = 0;
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.grants_reclaimed += (int64_t)back.size();
+      work += (int64_t)back.size();
+    }
+    if ((l.dead || l.detached) && l.named) {
+      shm_remove(l.name);
+      l.named = false;
+    }
+  }
+  // grants: free slots of this shard to the live producers that may still send
+  if (!closing) {
+    std::vector<Link*> act;
+    for (auto& lp : links_)
+      if (!lp->outgoing && lp->attached && !lp->eos && !lp->dead && !lp->detached) act.push_back(lp.get());
+    if (!act.empty()) {
+      const int cb = pool_->consumer_budget();
+      const int floor_g = std::max(kMinGrants, std::min(64, cb / (2 * (int)act.size())));
+      std::vector<int64_t> want(act.size());
+      int64_t total = 0;
+      for (size_t i = 0; i < act.size(); ++i) {
+        const int64_t backlog = std::max<int64_t>(0, act[i]->seg->producer_backlog.load(std::memory_order_relaxed));
+        want[i] = std::max<int64_t>(0, std::min<int64_t>(cb, floor_g + backlog) - act[i]->outstanding);
+        total += want[i];
+      }
+      if (total > 0) {
+        const std::vector<int> slots = pool_->grant_batch((int)std::min<int64_t>(total, cb));
+        size_t k = 0;
+        std::vector<uint64_t> head(act.size());
+        for (size_t i = 0; i < act.size(); ++i) head[i] = act[i]->g_head;
+        // round-robin so concurrent demand shares the free slots
+        while (k < slots.size()) {
+          bool any = false;
+          for (size_t i = 0; i < act.size() && k < slots.size(); ++i) {
+            if (want[i] <= 0) continue;
+            Link& l = *act[i];
+            seg_grants(l.seg)[head[i] % (uint64_t)l.n] = slots[k];
+            l.owed[slots[k]] = 1;
+            ++l.outstanding;
+            ++head[i];
+            --want[i];
+            ++k;
+            any = true;
+          }
+          if (!any) break;
+        }
+        check(k == slots.size(), "QueueFabric: grant distribution left slots over");
+        for (size_t i = 0; i < act.size(); ++i)
+          if (head[i] != act[i]->g_head) {
+            act[i]->g_head = head[i];
+            act[i]->seg->g_head.store(head[i], std::memory_order_release);
+          }
+        work += (int64_t)slots.size();
+        std::lock_guard<std::mutex> lk(mu_);
+        st_.grants_given += (int64_t)slots.size();
+      }
+    }
+  }
+  // quiesced: no producer can still write into the ring (close() waits for this before freeing)
+  if (closing) {
+    bool q = true;
+    for (auto& lp : links_) {
+      const Link& l = *lp;
+      if (l.outgoing || l.seg == nullptr || !l.attached || l.dead || l.detached) continue;
+      if (l.seg->producer_ack_closed.load(std::memory_order_acquire) == 0) q = false;
+    }
+    quiesced_.store(q);
+  }
+  return work;
+}
+
+int64_t QueueFabric::producer_pass(double now) {
+  int64_t work = 0;
+  const int policy = policy_.load();
+  // 1. attach / liveness / incoming grants
+  for (auto& lp : links_) {
+    Link& l = *lp;
+    if (!l.outgoing || l.dead) continue;
+    if (!l.attached) {
+      if (!try_attach(l, now)) continue;
+      ++work;
+    }
+    LinkSeg* s = l.seg;
+    if (now - l.last_check > kPidCheckS) {
+      l.last_check = now;
+      if (!pid_alive(s->consumer_pid)) {
+        l.dead = true;
+        std::lock_guard<std::mutex> lk(mu_);
+        ++st_.peers_dead;
+      }
+    }
+    if (!l.closed && s->consumer_closed.load(std::memory_order_acquire) != 0) l.closed = true;
+    if (l.dead || l.closed) {
+      l.grants.clear();
+      continue;
+    }
+    const uint64_t h = s->g_head.load(std::memory_order_acquire);
+    if (l.g_tail < h) {
+      const int32_t* gs = seg_grants(s);
+      for (; l.g_tail < h; ++l.g_tail) {
+        const int32_t slot = gs[l.g_tail % (uint64_t)l.n];
+        check(slot >= 0 && slot < (int32_t)l.remote.size(),
+              "QueueFabric: consumer " + std::to_string(l.peer) + " granted a slot outside its ring");
+        l.grants.push_back(slot);
+      }
+      s->g_tail.store(l.g_tail, std::memory_order_release);
+      ++work;
+    }
+  }
+  // 2. completed copies: notice the frames, or requeue them if their consumer left meanwhile
+  while (!inflight_.empty()) {
+    Batch& b = inflight_.front();
+    if (b.ev != nullptr) {
+      const hipError_t q = hipEventQuery(b.ev);
+      if (q == hipErrorNotReady) break;
+      hip_check(q, "hipEventQuery (frame copy)");
+    }
+    Link& l = *b.link;
+    const int n = (int)b.slots.size();
+    l.inflight -= n;
+    if (l.attached && !l.dead && !l.closed) {
+      Notice* ns = seg_notices(l.seg);
+      for (int i = 0; i < n; ++i) {
+        Notice& nt = ns[l.n_head % (uint64_t)l.n];
+        nt.slot = b.rslots[i];
+        nt.flags = 0;
+        nt.rank = b.hdrs[i].rank;
+        nt.idx = b.hdrs[i].idx;
+        nt.gevt = b.hdrs[i].gevt;
+        nt.photon_energy = b.hdrs[i].photon_energy;
+        nt.aux = b.hdrs[i].aux;
+        ++l.n_head;
+      }
+      l.seg->n_head.store(l.n_head, std::memory_order_release);
+      pool_->end_send_batch(b.slots, reinterpret_cast<uint64_t>(stream_));
+      l.frames += n;
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.frames_sent += n;
+      st_.bytes_sent += (int64_t)n * slot_bytes_;
+      st_.copy_s += now - b.t_issue;
+    } else {
+      pool_->unsend_batch(b.slots);
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.frames_requeued += n;
+    }
+    if (b.ev != nullptr) free_events_.push_back(b.ev);
+    inflight_.pop_front();
+    work += n;
+  }
+  // 3. route produced frames (FIFO) to this process's own consumer or to granted remote slots
+  const std::vector<int> offers = pool_->produced(kMaxDispatch);
+  if (!offers.empty()) {
+    std::vector<Link*> cands;
+    for (auto& lp : links_)
+      if (lp->outgoing && lp->attached && !lp->dead && !lp->closed && !lp->eos_posted) cands.push_back(lp.get());
+    std::vector<int64_t> avail(cands.size());
+    for (size_t i = 0; i < cands.size(); ++i) avail[i] = (int64_t)cands[i]->grants.size();
+    int64_t local_credit = (is_consumer_ && !consumer_closed_.load()) ? pool_->credits() : 0;
+    std::vector<std::vector<int>> assign(cands.size());
+    std::vector<int> local;
+    const int K = (int)cands.size() + 1;   // position K-1 = this process's own consumer
+    for (int s : offers) {
+      int pick = -2;   // -2 none, -1 local, >= 0 remote
+      if (policy == 2) {
+        for (int t = 0; t < K && pick == -2; ++t) {
+          const int p = (rr_ + t) % K;
+          if (p == K - 1) {
+            if (local_credit > 0) pick = -1;
+          } else if (avail[p] > 0) {
+            pick = p;
+          }
+          if (pick != -2) rr_ = (p + 1) % K;
+        }
+      } else {
+        int best = -1;
+        for (size_t i = 0; i < cands.size(); ++i)
+          if (avail[i] > 0 && (best < 0 || avail[i] > avail[best])) best = (int)i;
+        const int64_t best_n = best >= 0 ? avail[best] : 0;
+        if (local_credit > 0 && (policy == 1 || local_credit + kLocalSlack >= best_n)) pick = -1;
+        else if (best >= 0) pick = best;
+      }
+      if (pick == -2) break;
+      if (pick == -1) {
+        local.push_back(s);
+        --local_credit;
+      } else {
+        assign[pick].push_back(s);
+        --avail[pick];
+      }
+    }
+    for (int s : local) pool_->route_local(s);
+    if (!local.empty()) {
+      work += (int64_t)local.size();
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.frames_local += (int64_t)local.size();
+    }
+    for (size_t i = 0; i < cands.size(); ++i) {
+      if (assign[i].empty()) continue;
+      Link& l = *cands[i];
+      const std::vector<int>& slots = assign[i];
+      const int n = (int)slots.size();
+      Batch b;
+      for (std::shared_ptr<Link>& lp : links_)
+        if (lp.get() == &l) b.link = lp;
+      b.slots = slots;
+      b.hdrs = pool_->headers(slots);
+      b.rslots.assign(l.grants.begin(), l.grants.begin() + n);
+      l.grants.erase(l.grants.begin(), l.grants.begin() + n);
+      b.t_issue = now;
+      if (device_ >= 0) {
+        trace::Range tr("fabric.copy_batch");
+        pool_->begin_send_batch(slots, reinterpret_cast<uint64_t>(stream_));   // stream waits for the frames
+        int a = 0;
+        const uint64_t sb = (uint64_t)slot_bytes_;
+        while (a < n) {   // coalesce runs contiguous on both sides
+          int e = a + 1;
+          while (e < n && pool_->slot_ptr(slots[e]) == pool_->slot_ptr(slots[e - 1]) + sb &&
+                 l.remote[b.rslots[e]] == l.remote[b.rslots[e - 1]] + sb)
+            ++e;
+          hip_check(hipMemcpyAsync(reinterpret_cast<void*>(l.remote[b.rslots[a]]),
+                                   reinterpret_cast<const void*>(pool_->slot_ptr(slots[a])), (size_t)sb * (size_t)(e - a),
+                                   hipMemcpyDeviceToDevice, stream_),
+                    "hipMemcpyAsync (frame -> consumer ring)");
+          a = e;
+        }
+        b.ev = take_event();
+        hip_check(hipEventRecord(b.ev, stream_), "hipEventRecord (frame copy)");
+      } else {
+        pool_->begin_send_batch(slots, 0);
+        for (int j = 0; j < n; ++j)
+          memcpy(reinterpret_cast<void*>(l.remote[b.rslots[j]]), reinterpret_cast<const void*>(pool_->slot_ptr(slots[j])),
+                 (size_t)slot_bytes_);
+      }
+      l.inflight += n;
+      inflight_.push_back(std::move(b));
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        ++st_.batches;
+      }
+      work += n;
+    }
+  }
+  // 4. demand hint, close acknowledgements, end of stream, retirement of finished links
+  const int64_t backlog = pool_->n_produced();
+  const bool all_routed = finished_.load() && backlog == 0 && inflight_.empty();
+  bool drained = all_routed;
+  for (auto& lp : links_) {
+    Link& l = *lp;
+    if (!l.outgoing || !l.attached) continue;
+    LinkSeg* s = l.seg;
+    if (!l.dead && !l.closed) s->producer_backlog.store(backlog, std::memory_order_relaxed);
+    if ((l.dead || l.closed) && l.inflight == 0 && !l.acked_close) {
+      s->producer_ack_closed.store(1, std::memory_order_release);
+      l.acked_close = true;
+      release_out_link(l);
+      if (l.dead) {   // nobody else will: the consumer died holding these names
+        shm_remove(l.name);
+        if (s->kind == 0) shm_remove(std::string(s->ring_name));
+      }
+      ++work;
+    }
+    if (all_routed && !l.dead && !l.closed && !l.eos_posted) {
+      // give unused grants back, then EOS (released after the last notice)
+      Notice* ns = seg_notices(s);
+      for (int slot : l.grants) {
+        Notice& nt = ns[l.n_head % (uint64_t)l.n];
+        memset(&nt, 0, sizeof(nt));
+        nt.slot = slot;
+        nt.flags = kNoticeReturned;
+        ++l.n_head;
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        st_.grants_returned += (int64_t)l.grants.size();
+      }
+      l.grants.clear();
+      s->n_head.store(l.n_head, std::memory_order_release);
+      s->producer_eos.store(1, std::memory_order_release);
+      l.eos_posted = true;
+      l.eos = true;
+      ++work;
+    }
+  }
+  // links still being created by their consumer do not hold frames: EOS reaches them on attach
+  drained_.store(drained);
+  return work;
+}
+
+void QueueFabric::publish_status() {
+  std::vector<LinkStatus> v;
+  v.reserve(links_.size());
+  std::vector<std::shared_ptr<Link>> keep;
+  std::vector<LinkStatus> gone;
+  for (auto& lp : links_) {
+    Link& l = *lp;
+    // retire links that can never carry anything again
+    const bool out_done = l.outgoing && (l.dead || l.closed) && l.acked_close && l.inflight == 0;
+    const bool out_never = l.outgoing && l.dead && !l.attached;
+    const bool in_done = !l.outgoing && (l.dead || l.detached) && l.outstanding == 0 && !l.named;
+    const bool in_never = !l.outgoing && l.dead && !l.attached;
+    if (out_done || out_never || in_done || in_never) {
+      if (in_never && l.named) {
+        shm_remove(l.name);
+        l.named = false;
+      }
+      gone.push_back(l.status());
+      continue;
+    }
+    keep.push_back(lp);
+    v.push_back(l.status());
+  }
+  links_.swap(keep);
+  std::lock_guard<std::mutex> lk(mu_);
+  status_.swap(v);
+  retired_.insert(retired_.end(), gone.begin(), gone.end());
+}
+
+int64_t QueueFabric::step() {
+  const double now = now_s();
+  apply_ops();
+  int64_t work = 0;
+  if (is_consumer_) work += consumer_pass(now);
+  if (is_producer_) work += producer_pass(now);
+  publish_status();
+  std::lock_guard<std::mutex> lk(mu_);
+  ++st_.iterations;
+  if (work == 0) ++st_.idle_iterations;
+  return work;
+}
+
+void QueueFabric::loop() {
+  try {
+    if (device_ >= 0) hip_check(hipSetDevice(device_), "hipSetDevice");
+    long nap = 0;
+    while (!stop_.load()) {
+      if (step() == 0) {
+        nap = nap > 0 ? std::min(500000L, nap * 2) : 20000L;
+        nap_ns(nap);
+      } else {
+        nap = 0;
+      }
+    }
+  } catch (const std::exception& e) {
+    fail(e.what());
+  } catch (...) {
+    fail("unknown error in the queue fabric");
+  }
+  running_.store(false);
+}
+
+void QueueFabric::start() {
+  check(!th_.joinable(), "QueueFabric: already started");
+  running_.store(true);
+  th_ = std::thread([this] { loop(); });
+}
+
+bool QueueFabric::join(double timeout_s) {
+  if (!th_.joinable()) return true;
+  const double t0 = now_s();
+  while (running_.load()) {
+    if (timeout_s >= 0 && now_s() - t0 > timeout_s) return false;
+    nap_ns(1000000);
+  }
+  th_.join();
+  return true;
+}
+
+}  // namespace pr

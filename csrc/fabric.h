@@ -1,0 +1,201 @@
+// Elastic fabric of the shared queue: independent producer -> consumer LINKS.
+//
+// Reference semantics being provided (SURVEY R-10/R-11, P-02, C-01..C-03, §5 failure handling):
+// psana-ray's queue is ONE named, detached Ray actor (psana_ray/shared_queue.py:4-35).  Producers
+// put as soon as it exists and it buffers up to `maxsize` items with nobody reading
+// (psana_ray/producer.py:98-111); any number of consumers get() from it at any time, from
+// anywhere (shared_queue.py:19-24, README.md:23-35); a consumer that crashes affects nobody else;
+// only the actor's death stops producers (producer.py:112-114).
+//
+// MI355X design: there is no central actor process.  Each producer process keeps the frames it
+// calibrated in its OWN HBM slot pool (its share of queue_size), and each consumer owns an HBM
+// shard.  Every (producer, consumer) pair that is alive at the same time gets a LINK -- a small
+// POSIX shared-memory mailbox created by the consumer:
+//
+//   consumer --grants--> producer : ids of free slots of the consumer's shard (credit; it pulls)
+//   producer --notices-> consumer : "slot s now holds frame (rank, idx, gevt, photon_energy)"
+//                                   or "grant s returned unused"
+//
+// The frame bytes never pass through the mailbox.  A GPU consumer exports its ring allocation as
+// a HIP IPC handle; the producer maps it and writes granted slots directly with a device-to-device
+// copy on its own stream -- over the point-to-point xGMI link when the two processes sit on
+// different GPUs (one hop, no staging, no rendezvous kernel on the receiver).  The notice is
+// posted only after that copy has completed, so the consumer needs no device-side wait.  Host
+// (CPU) consumers keep their ring in a named shared-memory region the producer maps and memcpy's
+// into.  A producer that is also a consumer (co-located consumer, weak-scaling bench) routes to
+// itself with zero copies.
+//
+// Because links are independent, membership is elastic and failures are isolated:
+//   * producers run with no consumer at all (frames wait in their pool, backpressure when full);
+//   * consumers attach at any time and any number of them (a new link per live producer);
+//   * a consumer that dies or closes: its producers stop using its grants, and frames whose copy
+//     was still in flight go back to the FRONT of the producer's FIFO for another consumer; only
+//     frames already noticed to the dead consumer's shard are lost;
+//   * a producer that dies: its consumers take back the slots granted to it;
+//   * a producer that finishes returns unused grants and posts EOS on every link.
+// Liveness is the peer's pid (same host; zombies count as dead), checked every 50 ms.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <atomic>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "runtime.h"
+
+namespace pr {
+
+bool pid_alive(int64_t pid);
+bool shm_remove(const std::string& name);   // shm_unlink, true when the name existed
+
+// ---------------------------------------------------------------------------------------
+// A named POSIX shared-memory region (the ring of a host consumer).
+class ShmRegion {
+ public:
+  ShmRegion(const std::string& name, int64_t bytes, bool create, double timeout_s);
+  ~ShmRegion();
+  ShmRegion(const ShmRegion&) = delete;
+  ShmRegion& operator=(const ShmRegion&) = delete;
+  uint64_t ptr() const { return reinterpret_cast<uint64_t>(base_); }
+  int64_t bytes() const { return bytes_; }
+  const std::string& name() const { return name_; }
+  void unlink();
+
+ private:
+  std::string name_;
+  uint8_t* base_ = nullptr;
+  int64_t bytes_ = 0;
+  bool owner_ = false, unlinked_ = false;
+};
+
+// ---------------------------------------------------------------------------------------
+struct FabricStats {
+  int64_t iterations = 0, idle_iterations = 0;
+  int64_t frames_local = 0;      // producer -> own consumer, zero copy
+  int64_t frames_sent = 0;       // producer -> another process (noticed)
+  int64_t frames_recv = 0;       // consumer <- another process
+  int64_t frames_requeued = 0;   // copy finished after the consumer left: back to the FIFO
+  int64_t grants_given = 0, grants_returned = 0, grants_reclaimed = 0;
+  int64_t bytes_sent = 0, bytes_recv = 0, batches = 0;
+  int64_t links_opened = 0, peers_dead = 0;
+  double copy_s = 0;             // sum over batches of issue -> completion observed
+};
+
+struct LinkStatus {
+  int64_t peer = -1;         // member id of the other end
+  bool outgoing = false;     // true: this process produces into the peer's shard
+  bool attached = false;     // both ends have mapped the mailbox
+  bool eos = false;          // producer posted EOS (incoming: and every notice was taken)
+  bool detached = false;     // producer left after EOS
+  bool dead = false;         // the peer process exited
+  bool closed = false;       // the consumer closed the link
+  int64_t outstanding = 0;   // grants not answered yet
+  int64_t frames = 0;        // frames moved over the link
+};
+
+class QueueFabric {
+ public:
+  // policy: 0 balanced (local unless a remote consumer has kLocalSlack more free slots granted),
+  //         1 local_first, 2 spread (round-robin over every consumer with credit).
+  // slot addresses come from the pool (SlotPool::set_slot_ptrs): rings are built from segments
+  QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is_producer, bool is_consumer, int policy,
+              int64_t self_mid);
+  ~QueueFabric();
+  QueueFabric(const QueueFabric&) = delete;
+  QueueFabric& operator=(const QueueFabric&) = delete;
+
+  // consumer role: how producers reach this ring (written into every link this process creates):
+  // a host ring is one named shared-memory region; an HBM ring is exported as one HIP IPC handle
+  // per allocation (segment) it is made of
+  void export_host_ring(const std::string& shm_name);
+  void export_ipc_ring();
+  int export_segments() const { return (int)segs_.size(); }
+  static constexpr int kMaxSegments = 256;
+  // membership changes (any thread; applied by the engine thread)
+  void add_in_link(int64_t producer_mid, const std::string& name);   // consumer: create mailbox
+  void add_out_link(int64_t consumer_mid, const std::string& name);  // producer: open it
+  void drop_peer(int64_t mid);                                        // peer gone (store view)
+  void set_policy(int policy);
+  void set_producer_finished() { finished_.store(true); }
+  void set_consumer_closed() { consumer_closed_.store(true); }
+  // consumer: true once no live producer can still be writing into this ring (every attached
+  // producer acknowledged the close, detached or died) -- only then may the ring be freed
+  bool consumer_quiesced() const { return quiesced_.load(); }
+
+  void start();
+  void request_stop() { stop_.store(true); }
+  bool join(double timeout_s);
+  int64_t step();  // one engine iteration on the caller's thread (tests); returns work items
+
+  bool running() const { return running_.load(); }
+  bool producer_drained() const { return drained_.load(); }
+  std::string error() const;
+  FabricStats stats() const;
+  std::vector<LinkStatus> links() const;
+  int policy() const { return policy_.load(); }
+
+  static constexpr int kLocalSlack = 64;
+  static constexpr int kMinGrants = 4;      // grants kept at an idle producer (pipeline depth)
+  static constexpr int kMaxDispatch = 64;   // produced frames routed per iteration
+
+ private:
+  struct Link;
+  struct Batch;
+  void loop();
+  void fail(const std::string& msg);
+  void apply_ops();
+  int64_t consumer_pass(double now);
+  int64_t producer_pass(double now);
+  bool try_attach(Link& l, double now);
+  void release_out_link(Link& l);
+  void finish_in_link(Link& l);
+  void publish_status();
+  hipEvent_t take_event();
+
+  SlotPool* pool_;
+  int64_t slot_bytes_;
+  int device_;
+  bool is_producer_, is_consumer_;
+  std::atomic<int> policy_;
+  int64_t self_mid_;
+  // ring export
+  int export_kind_ = -1;  // 0 host shm, 1 ipc
+  std::string export_name_;
+  struct SegExport {
+    std::vector<uint8_t> handle;
+    int64_t offset = 0;
+    int32_t first = 0, n = 0;
+  };
+  std::vector<SegExport> segs_;
+
+  hipStream_t stream_ = nullptr;
+  std::vector<hipEvent_t> free_events_, all_events_;
+  std::vector<std::shared_ptr<Link>> links_;
+  std::deque<Batch> inflight_;
+  int rr_ = 0;
+
+  struct Op {
+    int kind;  // 0 in, 1 out, 2 drop
+    int64_t mid;
+    std::string name;
+  };
+  std::mutex ops_mu_;
+  std::vector<Op> ops_;
+
+  std::atomic<bool> finished_{false}, consumer_closed_{false}, stop_{false}, running_{false}, drained_{false};
+  std::atomic<bool> quiesced_{false};
+  std::vector<LinkStatus> retired_;
+  std::thread th_;
+  mutable std::mutex mu_;  // error_, st_, status_
+  std::string error_;
+  FabricStats st_;
+  std::vector<LinkStatus> status_;
+};
+
+}  // namespace pr

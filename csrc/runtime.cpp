@@ -5,6 +5,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -24,6 +25,20 @@ PinnedBuffer::PinnedBuffer(size_t bytes) : bytes_(bytes) {
 
 PinnedBuffer::~PinnedBuffer() {
   if (ptr_) (void)hipHostFree(ptr_);
+}
+
+// ---------------------------------------------------------------------------------------
+DeviceBuffer::DeviceBuffer(int64_t bytes, int device) : bytes_(bytes), device_(device) {
+  check(bytes > 0 && device >= 0, "DeviceBuffer: size must be > 0 on a device");
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  hip_check(hipMalloc(&ptr_, (size_t)bytes), "hipMalloc (ring segment)");
+}
+
+DeviceBuffer::~DeviceBuffer() {
+  if (ptr_ != nullptr) {
+    (void)hipSetDevice(device_);
+    (void)hipFree(ptr_);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -54,6 +69,13 @@ SlotPool::~SlotPool() {
 
 void SlotPool::set_device() const {
   if (device_ >= 0) hip_check(hipSetDevice(device_), "hipSetDevice");
+}
+
+void SlotPool::set_slot_ptrs(const std::vector<uint64_t>& ptrs) {
+  check((int)ptrs.size() == n_, "SlotPool.set_slot_ptrs: one address per slot");
+  for (uint64_t p : ptrs) check(p != 0, "SlotPool.set_slot_ptrs: null slot address");
+  std::lock_guard<std::mutex> lk(mu_);
+  ptrs_ = ptrs;
 }
 
 void SlotPool::check_slot(int slot) const {
@@ -543,6 +565,78 @@ void SlotPool::release_batch(const std::vector<int>& slots, uint64_t stream) {
   }
   if (auto_route_) route_pending_locked();
   cv_produce_.notify_all();
+}
+
+std::vector<int> SlotPool::grant_batch(int max_n) {
+  std::vector<int> out;
+  std::lock_guard<std::mutex> lk(mu_);
+  const int n = std::min(max_n, cb_ - consumer_held_);
+  if (n <= 0) return out;
+  if (device_ >= 0) set_device();
+  for (auto it = free_list_.begin(); it != free_list_.end() && (int)out.size() < n;) {
+    const int s = *it;
+    const EvRef r = free_ref_[s];
+    if (device_ >= 0 && ref_live_locked(r)) {
+      const hipError_t q = hipEventQuery(ev_[r.idx]);
+      if (q == hipErrorNotReady) {
+        ++it;
+        continue;
+      }
+      hip_check(q, "hipEventQuery (grant)");
+    }
+    it = free_list_.erase(it);
+    state_[s] = kReceiving;
+    ++consumer_held_;
+    out.push_back(s);
+  }
+  return out;
+}
+
+void SlotPool::complete_recv_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs) {
+  check(slots.size() == hdrs.size(), "complete_recv_batch: size mismatch");
+  if (slots.empty()) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kReceiving, state_msg("complete_recv_batch", kReceiving, state_[s]));
+  }
+  for (size_t i = 0; i < slots.size(); ++i) {
+    const int s = slots[i];
+    hdr_[s] = hdrs[i];
+    ready_ref_[s] = EvRef{};   // the writer completed its copy before the notice: nothing to wait on
+    state_[s] = kReady;
+    ready_fifo_.push_back(s);
+    ++st_.received;
+  }
+  cv_ready_.notify_all();
+}
+
+void SlotPool::cancel_recv_batch(const std::vector<int>& slots) {
+  if (slots.empty()) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kReceiving, state_msg("cancel_recv_batch", kReceiving, state_[s]));
+  }
+  for (int s : slots) {
+    state_[s] = kFree;
+    --consumer_held_;
+    free_list_.push_back(s);
+  }
+  cv_produce_.notify_all();
+}
+
+void SlotPool::unsend_batch(const std::vector<int>& slots) {
+  if (slots.empty()) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kSending, state_msg("unsend_batch", kSending, state_[s]));
+  }
+  for (auto it = slots.rbegin(); it != slots.rend(); ++it) {
+    state_[*it] = kProduced;
+    produced_fifo_.push_front(*it);
+  }
 }
 
 std::vector<SlotHeader> SlotPool::headers(const std::vector<int>& slots) const {

@@ -43,6 +43,27 @@ class PinnedBuffer {
 };
 
 // ---------------------------------------------------------------------------------------
+// One hipMalloc allocation of HBM (ring segments).  Ring memory is allocated here, not by the torch
+// caching allocator, so every allocation is exactly one segment: HIP IPC export works per
+// allocation, and opening an IPC handle of an allocation above 2 GiB hangs on this ROCm stack
+// (measured: 2.08 GB attaches in 0.2 ms, 2.16 GB never returns; tools/diag_ipc_attach.py).
+class DeviceBuffer {
+ public:
+  DeviceBuffer(int64_t bytes, int device);
+  ~DeviceBuffer();
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  uint64_t ptr() const { return reinterpret_cast<uint64_t>(ptr_); }
+  int64_t bytes() const { return bytes_; }
+  int device() const { return device_; }
+
+ private:
+  void* ptr_ = nullptr;
+  int64_t bytes_ = 0;
+  int device_ = 0;
+};
+
+// ---------------------------------------------------------------------------------------
 enum SlotState : int {
   kFree = 0,
   kProducing = 1,
@@ -75,6 +96,13 @@ class SlotPool {
   SlotPool& operator=(const SlotPool&) = delete;
 
   int n_slots() const { return n_; }
+  // device (or host) address of every slot: rings are built from several allocations
+  void set_slot_ptrs(const std::vector<uint64_t>& ptrs);
+  uint64_t slot_ptr(int slot) const {
+    check_slot(slot);
+    return ptrs_.empty() ? 0 : ptrs_[(size_t)slot];
+  }
+  const std::vector<uint64_t>& slot_ptrs() const { return ptrs_; }
   int producer_budget() const { return pb_; }
   int consumer_budget() const { return cb_; }
 
@@ -129,6 +157,13 @@ class SlotPool {
   void end_recv_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream);
   int64_t event_records() const { return ev_records_; }
 
+  // elastic fabric (fabric.h): another PROCESS writes granted slots, so a grant needs the slot's
+  // previous readers to have finished on the host's view (event query), not just stream order
+  std::vector<int> grant_batch(int max_n);                                    // FREE -> RECEIVING
+  void complete_recv_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs);  // -> READY
+  void cancel_recv_batch(const std::vector<int>& slots);                      // RECEIVING -> FREE
+  void unsend_batch(const std::vector<int>& slots);  // SENDING -> PRODUCED, back at the FIFO front
+
  private:
   void set_device() const;
   void check_slot(int slot) const;
@@ -146,6 +181,7 @@ class SlotPool {
   int pop_ready_locked();
 
   int pb_, cb_, n_, device_;
+  std::vector<uint64_t> ptrs_;
   mutable std::mutex mu_;
   std::condition_variable cv_produce_, cv_ready_;
   std::vector<int> state_;

@@ -103,7 +103,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     tlib = _torch_lib_dir()
     if tlib:
         link += [f"-L{tlib}", f"-Wl,-rpath,{tlib}"]
-    link += ["-lamdhip64", "-lrccl", "-lpthread", "-ldl"]
+    link += ["-lamdhip64", "-lpthread", "-ldl", "-lrt"]
     if verbose:
         print(" ".join(link), flush=True)
     r = subprocess.run(link, capture_output=True, text=True)

@@ -52,7 +52,8 @@ class EndOfStream(DataReaderError):
 class DataReader:
     def __init__(self, address: str = DEFAULT_RAY_ADDRESS, queue_name: str = DEFAULT_QUEUE_NAME,
                  ray_namespace: str = DEFAULT_RAY_NAMESPACE, consumer_id: Optional[int] = None,
-                 device: Optional[str] = None, as_numpy: bool = False, timeout_s: float = 300.0):
+                 device: Optional[str] = None, as_numpy: bool = False, timeout_s: float = 300.0,
+                 slots: Optional[int] = None):
         self.address = address
         self.queue_name = queue_name
         self.ray_namespace = ray_namespace
@@ -60,10 +61,10 @@ class DataReader:
         self.device_req = device
         self.as_numpy = as_numpy
         self.timeout_s = timeout_s
+        self.slots = slots          # shard size (default: queue_size / --num_consumers of the producer)
         self._queue = None       # the reference's actor handle slot: endpoint or in-process queue
         self._local = None
         self._sess = None
-        self._comm = None
         self._done = False
         self.frames_read = 0
 
@@ -88,41 +89,47 @@ class DataReader:
         return self
 
     def _connect_distributed(self):
-        from .parallel.launch import device_for, detect
-        from .parallel.rendezvous import consumer_join, form_world, open_store
+        from .parallel.rendezvous import open_store
         from .queue.endpoint import QueueEndpoint
         from .queue.ring import FrameRing, physical_slots
+        from .queue.session import QueueSession, wait_meta
 
-        store = open_store(self.address, host_if_absent=False, timeout_s=self.timeout_s)
-        sess = consumer_join(store, self.ray_namespace, self.queue_name, self.consumer_id, self.timeout_s)
-        meta = sess.meta
-        if meta.device_kind == "cuda":
-            if self.device_req:
-                device = torch.device(self.device_req)
+        store = open_store(self.address, spawn_if_absent=False, timeout_s=self.timeout_s)
+        meta = wait_meta(store, self.ray_namespace, self.queue_name, self.timeout_s)
+        sess = QueueSession(store, self.ray_namespace, self.queue_name, meta, "consumer")
+        try:
+            if meta["device_kind"] == "cuda":
+                if self.device_req:
+                    device = torch.device(self.device_req)
+                else:
+                    import os
+
+                    n = max(1, torch.cuda.device_count())
+                    lr = os.environ.get("LOCAL_RANK")
+                    k = int(lr) if lr is not None else int(meta.get("n_producers", 0)) + sess.consumer_seq
+                    device = torch.device(f"cuda:{k % n}")
+                torch.cuda.set_device(device)
             else:
-                n = max(1, torch.cuda.device_count())
-                device = torch.device(f"cuda:{(meta.n_producers + sess.role_index) % n}")
-            torch.cuda.set_device(device)
-        else:
-            device = torch.device("cpu")
-        comm = form_world(sess, device, self.timeout_s)
-        dtype = {"float32": torch.float32, "uint16": torch.uint16}[meta.dtype]
-        frame_bytes = int(np.prod(meta.frame_shape)) * (4 if meta.dtype == "float32" else 2)
-        share = max(1, math.ceil(meta.queue_size / max(1, meta.n_consumers)))
-        slots = physical_slots(share, frame_bytes, device, 0.8)
-        ring = FrameRing(meta.frame_shape, dtype, device, 0, slots)
-        ep = QueueEndpoint(ring, sess.rank, sess.world, comm, producer_ranks=sess.producer_ranks,
-                           consumer_ranks=sess.consumer_ranks, route=meta.extra.get("route", "balanced"),
-                           max_offer=int(meta.extra.get("max_offer", 64)), is_producer=False, is_consumer=True)
-        ep.start()
-        self._sess, self._comm, self._queue = sess, comm, ep
-        self._panel_shards = meta.extra.get("panel_shards")
-        recipe = meta.extra.get("calibrate_on_read")
+                device = torch.device("cpu")
+            dtype = {"float32": torch.float32, "uint16": torch.uint16}[meta["dtype"]]
+            shape = tuple(meta["frame_shape"])
+            frame_bytes = int(np.prod(shape)) * (4 if meta["dtype"] == "float32" else 2)
+            share = self.slots or max(1, math.ceil(int(meta["queue_size"]) / max(1, int(meta.get("num_consumers", 1)))))
+            slots = physical_slots(share, frame_bytes, device, 0.8)
+            ring = FrameRing(shape, dtype, device, 0, slots, shm_name=sess.ring_name() if device.type == "cpu" else None)
+            ep = QueueEndpoint(ring, sess, is_producer=False, is_consumer=True)
+            ep.start()
+        except BaseException:
+            sess.close("failed")
+            raise
+        self._sess, self._queue = sess, ep
+        self._panel_shards = meta.get("panel_shards")
+        recipe = meta.get("calibrate_on_read")
         if recipe:
             self._calibrator = self._make_calibrator(recipe, device)
-        self.consumer_id = sess.role_index
-        log.info("consumer %d joined queue %s/%s as rank %d of %d on %s (%d slots)", sess.role_index,
-                 self.ray_namespace, self.queue_name, sess.rank, sess.world, device, slots)
+        self.consumer_id = sess.consumer_seq
+        log.info("consumer %d joined queue %s/%s as member %d (session %d) on %s (%d slots)", sess.consumer_seq,
+                 self.ray_namespace, self.queue_name, sess.mid, meta["session"], device, slots)
 
     @staticmethod
     def _make_calibrator(recipe: dict, device):
@@ -305,25 +312,9 @@ class DataReader:
     def close(self):
         ep = self.endpoint
         if ep is not None:
-            ep.close_consumer()
-            # stay in the collective rounds until the producers' EOS so peers never see a
-            # half-finished world; a reader closed early just stops taking frames
-            ep.join(timeout=self.timeout_s)
-            owns = False
-            if ep.comm is not None:
-                owns = ep.comm.owns_default_group
-                if ep.failed is not None:
-                    ep.comm.abort()
-                ep.close()
-                ep.comm.close()
-            try:
-                import torch.distributed as dist
-
-                # close only what connect() opened (Q-13)
-                if owns and dist.is_initialized():
-                    dist.destroy_process_group()
-            except Exception:  # noqa: BLE001
-                pass
+            # leave the queue: producers stop writing into this shard (frames still in flight go to
+            # other consumers) before its memory is released; other members are unaffected
+            ep.close(timeout=min(30.0, self.timeout_s))
         self._queue = None
         self._local = None
 

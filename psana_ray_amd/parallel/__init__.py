@@ -1,5 +1,6 @@
-"""Multi-GPU plumbing: launch-env detection, rendezvous, RCCL/gloo comm, routing."""
-from .comm import Comm, init_groups
-from .routing import POLICIES, plan_round
+"""Multi-process plumbing: launch-env detection (mpirun / torchrun / Slurm) and the rendezvous
+store.  Queue membership and links: :mod:`psana_ray_amd.queue.session`, ``csrc/fabric.h``."""
+from .launch import detect, device_for
+from .rendezvous import open_store, port_open
 
-__all__ = ["Comm", "init_groups", "plan_round", "POLICIES"]
+__all__ = ["detect", "device_for", "open_store", "port_open"]

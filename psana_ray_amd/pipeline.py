@@ -78,7 +78,7 @@ class ProducerPipeline:
             dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
             # gevt = event_rank + k * size; a panel-sharded source (source/shard.py) shards events
             # over rank GROUPS, while the headers keep this rank (its panel shard)
-            self.engine = C.ProducerEngine(ring.pool, int(ring.storage.data_ptr()), ring.frame_bytes, dev_index,
+            self.engine = C.ProducerEngine(ring.pool, ring.frame_bytes, dev_index,
                                            calibrator.plan, self.chunk, n_raw_buffers,
                                            int(getattr(source, "event_rank", rank)),
                                            int(getattr(source, "size", 1)))
@@ -221,7 +221,7 @@ class ProducerPipeline:
         self.engine.start(-1 if n_local is None else int(n_local), -1 if max_steps is None else int(max_steps), k0)
         try:
             while not self.engine.join(0.05):
-                if (stop is not None and stop.is_set()) or self.ep.failed is not None or self.ep._consumers_gone:
+                if (stop is not None and stop.is_set()) or self.ep.failed is not None:
                     self.engine.request_stop()
         finally:
             self.engine.request_stop()
@@ -235,10 +235,6 @@ class ProducerPipeline:
         if err:
             raise RuntimeError(f"producer engine failed: {err}")
         self.ep._raise_if_failed()
-        if self.ep._consumers_gone:
-            from .queue.endpoint import QueueClosed
-
-            raise QueueClosed("no consumer is attached to the queue any more")
         return self.frames
 
 
@@ -329,7 +325,7 @@ class PeakFinderConsumer:
         with trace_range("consumer.peakfind_batch"):
             # one native call: zero this batch's outputs, run the peak finder on the ring slots,
             # bump the on-device running peak total (no per-batch torch ops, no host sync)
-            C.peakfind_slots(self.ep._base, self.ep._slot_bytes, slots, P, H, W, float(self.params.thr_peak),
+            C.peakfind_slots(self.ep.pool, self.ep._slot_bytes, slots, P, H, W, float(self.params.thr_peak),
                              float(self.params.son_min), int(self.params.radius), int(self.params.max_peaks),
                              int(self.peaks[b].data_ptr()), int(self.counts[b].data_ptr()),
                              int(self.summary[b].data_ptr()), int(self.count_acc.data_ptr()), sh,

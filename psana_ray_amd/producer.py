@@ -64,7 +64,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--route", type=str, default="balanced", choices=["balanced", "local_first", "spread"])
     g.add_argument("--consumer_task", type=str, default="none", choices=["none", "peakfind"],
                    help="also consume on every producer rank (co-located consumer, BASELINE config 5)")
-    g.add_argument("--producer_slots", type=int, default=64, help="calibrated frames a rank may hold un-routed")
+    g.add_argument("--producer_slots", type=int, default=None,
+                   help="calibrated frames a rank may hold until a consumer takes them (default: its share of "
+                        "--queue_size, at least 2 x --chunk)")
     g.add_argument("--hbm_fraction", type=float, default=0.8, help="cap of free HBM used for ring slots")
     g.add_argument("--timeout", type=float, default=300.0, help="rendezvous / peer timeout in seconds")
     g.add_argument("--calibrate_on_read", action="store_true",
@@ -102,17 +104,21 @@ def backoff_delays(retries: int):
 def initialize_queue(ray_address, ray_namespace, queue_name, queue_size, rank, size, num_consumers, frame_shape,
                      dtype, device_kind, extra=None, max_retries=QUEUE_LOOKUP_RETRIES,
                      retry_delay=QUEUE_LOOKUP_DELAY_S, timeout_s=300.0):
-    """Join (rank 0: create) the queue session; None on failure (producer.py:35-71)."""
-    from .parallel.rendezvous import SessionMeta, open_store, producer_join
+    """Reach the rendezvous store and create -- or attach to (producer.py:43-45) -- the live session
+    of the named queue.  Returns ``(store, meta)``, or None on failure after logging the reason
+    (producer.py:35-71)."""
+    from .parallel.rendezvous import open_store
+    from .queue.session import create_or_attach
 
     try:
-        store = open_store(ray_address, host_if_absent=(rank == 0), timeout_s=timeout_s, retries=max_retries,
+        store = open_store(ray_address, spawn_if_absent=True, timeout_s=timeout_s, retries=max_retries,
                            retry_delay_s=retry_delay)
-        meta = SessionMeta(int(queue_size), int(size), int(num_consumers), tuple(frame_shape), dtype, device_kind,
-                           extra=dict(extra or {}))
-        sess = producer_join(store, ray_namespace, queue_name, rank, size, meta, timeout_s)
+        meta = {"queue_size": int(queue_size), "num_consumers": int(num_consumers), "n_producers": int(size),
+                "frame_shape": list(frame_shape), "dtype": dtype, "device_kind": device_kind}
+        meta.update(extra or {})
+        meta = create_or_attach(store, ray_namespace, queue_name, meta, timeout_s=timeout_s)
         log.info("Rank %d: Successfully connected to shared queue.", rank)
-        return sess
+        return store, meta
     except Exception as e:  # noqa: BLE001 - reference: log + None (producer.py:69-71)
         log.error("Rank %d: Error in initialize_queue: %s", rank, e)
         return None
@@ -151,16 +157,12 @@ def _read_recipe(args, read_mode, read_cm) -> dict:
 
 def produce_data(pipeline, max_steps=None, stop=None):
     """Run one rank's producer pipeline (producer.py:78-130); returns frames produced."""
-    from .queue.endpoint import QueueClosed, QueuePeerError
+    from .queue.endpoint import QueuePeerError
 
     try:
         return pipeline.run(max_steps=max_steps, stop=stop)
     except QueuePeerError:
-        log.error("Rank %d: Queue peer is dead. Exiting...", pipeline.rank)   # producer.py:113
-        return pipeline.frames
-    except QueueClosed:
-        log.error("Rank %d: No consumer attached any more. Exiting...", pipeline.rank)
-        pipeline.ep.finish()
+        log.error("Rank %d: Queue fabric failed. Exiting...", pipeline.rank)   # producer.py:113
         return pipeline.frames
 
 
@@ -176,10 +178,10 @@ def main(argv=None) -> int:
     from .models.calibrator import Calibrator
     from .models.detector import Mode
     from .parallel.launch import bind_numa_to_device, detect, device_for
-    from .parallel.rendezvous import Heartbeat, finish_session, form_world
     from .pipeline import PeakFinderConsumer, ProducerPipeline
     from .queue.endpoint import EndOfStream, QueueEndpoint
     from .queue.ring import FrameRing, physical_slots
+    from .queue.session import QueueSession
     from .source import open_source
     from .utils.metrics import Registry, Reporter
 
@@ -239,45 +241,49 @@ def main(argv=None) -> int:
     frame_bytes = int(np.prod(frame_shape)) * (2 if mode == Mode.raw else 4)
 
     sess = None
-    comm = None
-    hb = None
+    ep = None
+    chunk = max(1, int(args.chunk))
+    share = max(1, math.ceil(args.queue_size / size))
+    pslots = args.producer_slots if args.producer_slots is not None else max(share, 2 * chunk)
     try:
         if args.local or (size == 1 and args.num_consumers == 0):
             if not co_consumer:
                 log.error("--local needs --consumer_task (nobody would read the queue)")
                 return 2
             ring = FrameRing(frame_shape, torch.float32 if dtype == "float32" else torch.uint16, device,
-                             args.producer_slots, physical_slots(args.queue_size, frame_bytes, device,
-                                                                 args.hbm_fraction, args.producer_slots))
+                             pslots, physical_slots(args.queue_size, frame_bytes, device, args.hbm_fraction, pslots))
             ep = QueueEndpoint(ring)
         else:
-            n_consumer_ranks = args.num_consumers
-            sess = initialize_queue(args.ray_address, args.ray_namespace, args.queue_name, args.queue_size, rank,
-                                    size, n_consumer_ranks, frame_shape, dtype, device.type,
-                                    extra={"route": args.route, "co_consumers": co_consumer,
-                                           "panel_shards": {"n_shards": shards,
-                                                            "n_panels": source.full_spec.n_panels,
-                                                            "detector_name": args.detector_name}
-                                           if shards > 1 else None,
-                                           "calibrate_on_read": _read_recipe(args, read_mode, read_cm)
-                                           if args.calibrate_on_read else None},
-                                    timeout_s=args.timeout)
-            if sess is None:
+            got = initialize_queue(args.ray_address, args.ray_namespace, args.queue_name, args.queue_size, rank,
+                                   size, args.num_consumers, frame_shape, dtype, device.type,
+                                   extra={"co_consumers": co_consumer,
+                                          "panel_shards": {"n_shards": shards,
+                                                           "n_panels": source.full_spec.n_panels,
+                                                           "detector_name": args.detector_name}
+                                          if shards > 1 else None,
+                                          "calibrate_on_read": _read_recipe(args, read_mode, read_cm)
+                                          if args.calibrate_on_read else None},
+                                   timeout_s=args.timeout)
+            if got is None:
                 return 1
-            if rank == 0:
-                hb = Heartbeat(sess.store, args.ray_namespace, args.queue_name)
-            comm = form_world(sess, device, args.timeout)
-            consumers = sess.consumer_ranks + (sess.producer_ranks if co_consumer else [])
-            n_cons = max(1, len(consumers))
-            share = max(1, math.ceil(args.queue_size / n_cons)) if co_consumer else 0
-            cslots = physical_slots(share, frame_bytes, device, args.hbm_fraction, args.producer_slots) if share else 0
-            ring = FrameRing(frame_shape, torch.float32 if dtype == "float32" else torch.uint16, device,
-                             args.producer_slots, cslots)
-            ep = QueueEndpoint(ring, sess.rank, sess.world, comm, producer_ranks=sess.producer_ranks,
-                               consumer_ranks=sorted(consumers), route=args.route, is_producer=True,
-                               is_consumer=co_consumer)
+            store, meta = got
+            dev_index = device.index if device.type == "cuda" and device.index is not None else -1
+            sess = QueueSession(store, args.ray_namespace, args.queue_name, meta,
+                                "prosumer" if co_consumer else "producer", device=dev_index,
+                                job=f"{args.exp}/{args.run}", rank=rank)
+            pslots = physical_slots(pslots, frame_bytes, device, args.hbm_fraction)
+            cslots = 0
+            if co_consumer:
+                cshare = max(1, math.ceil(args.queue_size / max(1, size)))
+                cslots = physical_slots(cshare, frame_bytes, device, args.hbm_fraction, pslots)
+            ring = FrameRing(frame_shape, torch.float32 if dtype == "float32" else torch.uint16, device, pslots,
+                             cslots, shm_name=sess.ring_name() if (co_consumer and device.type == "cpu") else None)
+            ep = QueueEndpoint(ring, sess, is_producer=True, is_consumer=co_consumer, route=args.route)
             ep.start()
-        pipe = ProducerPipeline(source, calibrator, ep, rank=rank, chunk=args.chunk,
+            log.info("Rank %d: member %d of queue %s/%s (session %d): %d producer slots%s", rank, sess.mid,
+                     args.ray_namespace, args.queue_name, meta["session"], pslots,
+                     f", {cslots} consumer slots" if co_consumer else "")
+        pipe = ProducerPipeline(source, calibrator, ep, rank=rank, chunk=chunk,
                                 log_every=1 if logging.getLogger().isEnabledFor(logging.DEBUG) else 0)
         cons_thread = None
         stats = {}
@@ -301,40 +307,34 @@ def main(argv=None) -> int:
             cons_thread.start()
         reporter = Reporter(registry, rank=rank, interval=args.metrics_interval, json_path=args.metrics_json,
                             prometheus_port=(args.metrics_port + rank) if args.metrics_port else None).start()
+        rc = 0
         try:
             n = produce_data(pipe, max_steps=args.max_steps, stop=stop)
             log.info("Rank %d: produced %d frames", rank, n)
+            # drain before exit: the frames this rank holds ARE queue items (the reference's detached
+            # actor kept them after the producer left, shared_queue.py:35); wait for consumers
+            if not ep.join(timeout=args.timeout):
+                if ep.failed is not None:
+                    log.error("Rank %d: queue fabric failed: %s", rank, ep.failed)
+                else:
+                    log.error("Rank %d: %d frames were not taken by any consumer within --timeout %.0f s; "
+                              "exiting without them", rank, ep.undelivered(), args.timeout)
+                rc = 1
             if cons_thread is not None:
                 cons_thread.join()
                 log.info("Rank %d: co-located consumer processed %d frames, %d peaks", rank,
                          stats.get("consumed", 0), stats.get("peaks", 0))
-            ep.join(timeout=args.timeout)
         finally:
             reporter.stop(final_sample=args.metrics_interval > 0 or args.metrics_json is not None)
-        return 0
+        return rc
     except Exception as e:
         log.error("Rank %d: Unhandled exception in main: %s", rank, e)   # producer.py:163-166
         log.error("Traceback:")
         log.error(traceback.format_exc())
         raise
     finally:
-        if hb is not None:
-            hb.stop()
-        if sess is not None:
-            finish_session(sess)
-        if comm is not None:
-            if 'ep' in locals():
-                if ep.failed is not None:
-                    comm.abort()
-                ep.close()
-            comm.close()
-        try:
-            import torch.distributed as dist
-
-            if dist.is_initialized():
-                dist.destroy_process_group()
-        except Exception:  # noqa: BLE001
-            pass
+        if ep is not None:
+            ep.close(timeout=min(30.0, args.timeout))
 
 
 if __name__ == "__main__":

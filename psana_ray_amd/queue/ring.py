@@ -39,9 +39,22 @@ def physical_slots(logical_share: int, frame_bytes: int, device: torch.device, h
     return max(1, min(logical_share, fit))
 
 
+SEGMENT_BYTES = 1 << 30   # HBM rings are built from allocations of at most 1 GiB (HIP IPC limit, see below)
+
+
 class FrameRing:
+    """``producer_slots + consumer_slots`` frame slots plus their native :class:`SlotPool`.
+
+    HBM rings are NOT one tensor: they are made of segments of at most ``SEGMENT_BYTES``, each its
+    own ``hipMalloc`` (``_C.DeviceBuffer``, wrapped zero-copy with DLPack).  A consumer exports
+    every segment to producer processes as a HIP IPC handle, and opening the handle of an
+    allocation above 2 GiB hangs on this ROCm stack (tools/diag_ipc_attach.py: 2.08 GB attaches in
+    0.2 ms, 2.16 GB never returns).  The pool knows every slot's address (``slot_ptrs``), so
+    kernels, copies and the fabric never assume one contiguous ring.  Host rings are one region:
+    named shared memory when producer processes must write into them (``shm_name``)."""
+
     def __init__(self, frame_shape: Tuple[int, ...], dtype: torch.dtype, device, producer_slots: int,
-                 consumer_slots: int):
+                 consumer_slots: int, shm_name: Optional[str] = None, segment_bytes: int = SEGMENT_BYTES):
         C = _ext.load()
         self.device = torch.device(device)
         self.frame_shape = tuple(frame_shape)
@@ -49,19 +62,45 @@ class FrameRing:
         n = producer_slots + consumer_slots
         if n <= 0:
             raise ValueError("ring needs at least one slot")
-        self.storage = torch.empty((n, *self.frame_shape), dtype=dtype, device=self.device)
+        esz = torch.empty((), dtype=dtype).element_size()
+        self.frame_bytes = int(math.prod(self.frame_shape)) * esz
+        self.shm_name = shm_name if self.device.type == "cpu" else None
+        self._region = None
+        self._buffers = []
+        self.segments = []     # (tensor [k, *frame_shape], first slot, k)
         dev_index = -1
-        if self.device.type == "cuda":
+        if self.device.type == "cpu":
+            if self.shm_name is not None:
+                # a host consumer's shard lives in named shared memory so producer processes write into it
+                self._region = C.ShmRegion(self.shm_name, n * self.frame_bytes, True)
+                flat = torch.frombuffer(self._region, dtype=torch.uint8)
+            else:
+                flat = torch.empty(n * self.frame_bytes, dtype=torch.uint8)
+            self.segments.append((flat.view(dtype).view(n, *self.frame_shape), 0, n))
+        else:
             dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            per = max(1, int(segment_bytes) // self.frame_bytes)
+            for first in range(0, n, per):
+                k = min(per, n - first)
+                buf = C.DeviceBuffer(k * self.frame_bytes, dev_index)
+                self._buffers.append(buf)
+                t = torch.from_dlpack(buf).view(dtype).view(k, *self.frame_shape)
+                self.segments.append((t, first, k))
+        self.views = [v for t, _, _ in self.segments for v in t.unbind(0)]
+        self.slot_ptrs = [int(v.data_ptr()) for v in self.views]
         self.pool = C.SlotPool(producer_slots, consumer_slots, dev_index)
-        self.frame_bytes = int(math.prod(self.frame_shape)) * self.storage.element_size()
+        self.pool.set_slot_ptrs(self.slot_ptrs)
 
     @property
     def n_slots(self) -> int:
         return self.pool.n_slots
 
+    @property
+    def nbytes(self) -> int:
+        return self.n_slots * self.frame_bytes
+
     def slot(self, i: int) -> torch.Tensor:
-        return self.storage[i]
+        return self.views[i]
 
     def stats(self) -> dict:
         s = self.pool.stats()

@@ -10,17 +10,21 @@
 //                           per-producer FIFO order per consumer.
 //   scenario 2 (auto-route): producer thread + 3 consumer threads on ONE pool in single-process
 //                           mode (routing inside commit/release), batch and single-slot calls mixed.
-//   scenario 3 (routing): random plan_round inputs; every plan respects offers and credits.
-//   scenario 4 (transport engine): 3 ranks in one process (producer / producer+consumer /
-//                           consumer), each with its own pool, its own mapping of ONE shared-memory
-//                           control segment and a TransportEngine thread; host data plane through
-//                           the outboxes; checks payload bytes, exactly-once delivery and EOS.
+//   scenario 3 (fabric): 3 members in one process (producer / producer+consumer / consumer), each
+//                           with its own pool, host ring in named shared memory and a QueueFabric
+//                           thread; links created through the same mailbox protocol separate
+//                           processes use; checks payload bytes, exactly-once delivery, per-producer
+//                           FIFO order within a shard and EOS, for every routing policy.
+//   scenario 4 (fabric, consumer leaves): the consumer-only member closes mid-stream and is
+//                           dropped; producers requeue its in-flight frames; the surviving consumer
+//                           gets every frame the leaver had not taken, and the stream still ends.
 #include <stdint.h>
 #include <stdio.h>
 
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <string>
 #include <mutex>
@@ -30,12 +34,7 @@
 #include <vector>
 
 #include "runtime.h"
-#include "xport_engine.h"
-
-namespace pr {
-std::vector<int32_t> plan_round_native(const std::vector<int64_t>& offers_in, const std::vector<int64_t>& credits_in,
-                                       int64_t round_id, int policy);
-}
+#include "fabric.h"
 
 using pr::SlotHeader;
 using pr::SlotPool;
@@ -189,120 +188,130 @@ static void scenario_auto_route(int64_t n_events) {
   printf("auto-route scenario: %lld events OK\n", (long long)n_events);
 }
 
-static void scenario_routing(int iters) {
-  std::mt19937 rng(3);
-  for (int it = 0; it < iters; ++it) {
-    const int world = 1 + rng() % 8;
-    std::vector<int64_t> offers(world), credits(world);
-    for (int r = 0; r < world; ++r) {
-      offers[r] = (int64_t)(rng() % 70) - 3;    // includes negative garbage
-      credits[r] = (int64_t)(rng() % 70) - 3;
-    }
-    for (int policy = 0; policy < 3; ++policy) {
-      const std::vector<int32_t> flat = pr::plan_round_native(offers, credits, it, policy);
-      require(flat.size() % 3 == 0, "plan is not a list of triples");
-      std::vector<int64_t> used_off(world, 0), used_cred(world, 0);
-      for (size_t k = 0; k < flat.size(); k += 3) {
-        const int p = flat[k], i = flat[k + 1], c = flat[k + 2];
-        require(p >= 0 && p < world && c >= 0 && c < world, "plan rank out of range");
-        require(i == used_off[p], "offers of a producer must be consumed in FIFO order");
-        ++used_off[p];
-        ++used_cred[c];
-      }
-      int64_t tot_off = 0, tot_cred = 0, moved = (int64_t)flat.size() / 3;
-      for (int r = 0; r < world; ++r) {
-        require(used_off[r] <= std::max<int64_t>(0, offers[r]), "plan exceeds offers");
-        require(used_cred[r] <= std::max<int64_t>(0, credits[r]), "plan exceeds credits");
-        tot_off += std::max<int64_t>(0, offers[r]);
-        tot_cred += std::max<int64_t>(0, credits[r]);
-      }
-      require(moved == std::min(tot_off, tot_cred), "plan is not maximal");
-    }
-  }
-  printf("routing scenario: %d random rounds x 3 policies OK\n", iters);
-}
+// Members of one fabric "session" inside this process (the same mailboxes other processes use).
+struct Member {
+  std::unique_ptr<SlotPool> pool;
+  std::unique_ptr<pr::ShmRegion> ring;
+  std::unique_ptr<pr::QueueFabric> fab;
+  bool prod = false, cons = false;
+};
 
-static void scenario_engine(int64_t n_per_producer, int policy) {
-  const int world = 3, max_offer = 8;
+static void scenario_fabric(int64_t n_per_producer, int policy, bool leave) {
+  const int M = 3;
   const int64_t slot_bytes = 192;
-  const bool is_p[world] = {true, true, false}, is_c[world] = {false, true, true};
-  const std::vector<int> prods = {0, 1};
-  const std::string name = "/psray-stress-" + std::to_string((long long)getpid()) + "-" + std::to_string(policy);
-  std::vector<std::unique_ptr<SlotPool>> pools;
-  std::vector<std::vector<uint8_t>> rings;
-  std::vector<std::unique_ptr<pr::ShmControl>> ctrls;
-  std::vector<std::unique_ptr<pr::TransportEngine>> engines;
-  for (int r = 0; r < world; ++r) {
-    pools.emplace_back(new SlotPool(is_p[r] ? 12 : 0, is_c[r] ? 10 : 0, -1));
-    rings.emplace_back((size_t)pools[r]->n_slots() * slot_bytes);
+  const bool is_p[M] = {true, true, false}, is_c[M] = {false, true, true};
+  const std::string tok = "/psq-stress-" + std::to_string((long long)getpid()) + "-" + std::to_string(policy) +
+                          (leave ? "L" : "");
+  std::vector<Member> m(M);
+  for (int r = 0; r < M; ++r) {
+    m[r].prod = is_p[r];
+    m[r].cons = is_c[r];
+    m[r].pool.reset(new SlotPool(is_p[r] ? 12 : 0, is_c[r] ? 10 : 0, -1));
+    m[r].ring.reset(new pr::ShmRegion(tok + "-r" + std::to_string(r), (int64_t)m[r].pool->n_slots() * slot_bytes,
+                                      true, 5.0));
+    std::vector<uint64_t> ptrs((size_t)m[r].pool->n_slots());
+    for (size_t k = 0; k < ptrs.size(); ++k) ptrs[k] = m[r].ring->ptr() + k * (uint64_t)slot_bytes;
+    m[r].pool->set_slot_ptrs(ptrs);
+    m[r].fab.reset(new pr::QueueFabric(m[r].pool.get(), slot_bytes, -1, is_p[r], is_c[r], policy, r));
+    if (is_c[r]) m[r].fab->export_host_ring(m[r].ring->name());
   }
-  for (int r = 0; r < world; ++r)
-    ctrls.emplace_back(new pr::ShmControl(name, r == 0, r, world, pr::TransportEngine::vec_words_for(max_offer),
-                                          max_offer * slot_bytes, 60.0));
-  for (int r = 0; r < world; ++r)
-    engines.emplace_back(new pr::TransportEngine(pools[r].get(), ctrls[r].get(), nullptr,
-                                                 (uint64_t)(uintptr_t)rings[r].data(), slot_bytes, r, world, prods,
-                                                 is_p[r], is_c[r], policy, max_offer, false, 0, -1));
-  for (auto& e : engines) e->start();
+  for (int p = 0; p < M; ++p)
+    for (int c = 0; c < M; ++c) {
+      if (p == c || !is_p[p] || !is_c[c]) continue;
+      const std::string name = tok + "-" + std::to_string(p) + "-" + std::to_string(c);
+      m[c].fab->add_in_link(p, name);
+      m[p].fab->add_out_link(c, name);
+    }
+  for (auto& x : m) x.fab->start();
   auto payload = [](int64_t rank, int64_t idx, int64_t j) { return (uint8_t)(rank * 131 + idx * 7 + j * 3); };
   std::vector<std::thread> th;
-  for (int r = 0; r < world; ++r) {
+  std::atomic<int> finished{0};
+  for (int r = 0; r < M; ++r) {
     if (!is_p[r]) continue;
     th.emplace_back([&, r] {
+      uint8_t* base = reinterpret_cast<uint8_t*>(m[r].ring->ptr());
       for (int64_t k = 0; k < n_per_producer;) {
-        const int s = pools[r]->acquire_produce(0.01);
+        const int s = m[r].pool->acquire_produce(0.01);
         if (s < 0) continue;
-        uint8_t* d = rings[r].data() + (size_t)s * slot_bytes;
+        uint8_t* d = base + (size_t)s * slot_bytes;
         for (int64_t j = 0; j < slot_bytes; ++j) d[j] = payload(r, k, j);
         SlotHeader h;
         h.rank = r;
         h.idx = k;
         h.gevt = 1000 * r + k;
         h.photon_energy = 0.5 * (double)k;
-        pools[r]->commit_produce(s, h, 0);
+        m[r].pool->commit_produce(s, h, 0);
         ++k;
       }
-      engines[r]->set_producer_finished();
+      m[r].fab->set_producer_finished();
+      finished.fetch_add(1);
     });
   }
   std::vector<std::atomic<int>> seen(2 * n_per_producer);
   for (auto& x : seen) x.store(0);
-  for (int r = 0; r < world; ++r) {
+  std::atomic<int64_t> taken_by_leaver{0};
+  auto stream_done = [&](int r) {
+    // every producer drained (posted EOS) and every link into r saw it
+    if (finished.load() < 2) return false;
+    for (int p = 0; p < M; ++p)
+      if (is_p[p] && !m[p].fab->producer_drained()) return false;
+    for (const auto& ls : m[r].fab->links())
+      if (!ls.outgoing && ls.attached && !(ls.eos || ls.dead || ls.detached)) return false;
+    return true;
+  };
+  for (int r = 0; r < M; ++r) {
     if (!is_c[r]) continue;
     th.emplace_back([&, r] {
+      const bool leaver = leave && r == 2;
       int64_t last[2] = {-1, -1};
+      const uint8_t* base = reinterpret_cast<const uint8_t*>(m[r].ring->ptr());
+      int64_t got = 0;
       for (;;) {
-        const int s = pools[r]->get(0.005);
+        if (leaver && got >= n_per_producer / 4) {
+          // close mid-stream: producers stop writing here and requeue what was in flight
+          m[r].fab->set_consumer_closed();
+          while (!m[r].fab->consumer_quiesced()) std::this_thread::sleep_for(std::chrono::microseconds(200));
+          for (int p = 0; p < M; ++p)
+            if (p != r) m[p].fab->drop_peer(r);
+          taken_by_leaver.store(got);
+          return;
+        }
+        const int s = m[r].pool->get(0.005);
         if (s < 0) {
-          const std::string e = engines[r]->error();
-          require(e.empty(), "transport engine failed");
-          if (engines[r]->done() && pools[r]->n_ready() == 0) return;
+          require(m[r].fab->error().empty(), "fabric failed");
+          if (stream_done(r) && m[r].pool->n_ready() == 0) return;
           continue;
         }
-        const SlotHeader h = pools[r]->header(s);
-        require(h.rank >= 0 && h.rank < 2 && h.idx >= 0 && h.idx < n_per_producer, "engine: header out of range");
-        require(h.gevt == 1000 * h.rank + h.idx && h.photon_energy == 0.5 * (double)h.idx, "engine: header corrupted");
-        require(h.idx > last[h.rank], "engine: per-producer FIFO order violated within a shard");
+        const SlotHeader h = m[r].pool->header(s);
+        require(h.rank >= 0 && h.rank < 2 && h.idx >= 0 && h.idx < n_per_producer, "fabric: header out of range");
+        require(h.gevt == 1000 * h.rank + h.idx && h.photon_energy == 0.5 * (double)h.idx, "fabric: header corrupted");
+        if (!leave) require(h.idx > last[h.rank], "fabric: per-producer FIFO order violated within a shard");
         last[h.rank] = h.idx;
-        const uint8_t* d = rings[r].data() + (size_t)s * slot_bytes;
-        for (int64_t j = 0; j < slot_bytes; ++j) {
-          if (d[j] != payload(h.rank, h.idx, j))
-            fprintf(stderr, "consumer %d: frame (%lld,%lld) byte %lld = %d, want %d (slot %d)\n", r, (long long)h.rank,
-                    (long long)h.idx, (long long)j, (int)d[j], (int)payload(h.rank, h.idx, j), s);
-          require(d[j] == payload(h.rank, h.idx, j), "engine: payload corrupted");
-        }
+        const uint8_t* d = base + (size_t)s * slot_bytes;
+        for (int64_t j = 0; j < slot_bytes; ++j) require(d[j] == payload(h.rank, h.idx, j), "fabric: payload corrupted");
         seen[h.rank * n_per_producer + h.idx].fetch_add(1);
-        pools[r]->release(s, 0);
+        ++got;
+        m[r].pool->release(s, 0);
       }
     });
   }
   for (auto& t : th) t.join();
-  for (auto& e : engines) require(e->join(60.0), "engine did not finish");
-  for (auto& e : engines) require(e->error().empty(), "engine reported an error");
-  for (size_t i = 0; i < seen.size(); ++i) require(seen[i].load() == 1, "engine: event lost or duplicated");
-  const pr::XportStats s1 = engines[1]->stats();
-  printf("engine scenario (policy %d): %lld events OK (%lld rounds, %lld sent by rank 1)\n", policy, (long long)seen.size(),
-         (long long)s1.rounds, (long long)s1.frames_sent);
+  for (auto& x : m) require(x.fab->error().empty(), "fabric reported an error");
+  int64_t lost = 0;
+  for (size_t i = 0; i < seen.size(); ++i) {
+    require(seen[i].load() <= 1, "fabric: event duplicated");
+    lost += seen[i].load() == 0;
+  }
+  // only frames that were already READY in the leaver's shard may be lost (<= its 10 slots)
+  require(leave ? lost <= 10 : lost == 0, "fabric: events lost");
+  const pr::FabricStats s1 = m[1].fab->stats();
+  printf("fabric scenario (policy %d%s): %lld events, %lld lost, %lld sent by member 1, %lld requeued\n", policy,
+         leave ? ", consumer leaves" : "", (long long)seen.size(), (long long)lost, (long long)s1.frames_sent,
+         (long long)(m[0].fab->stats().frames_requeued + s1.frames_requeued));
+  for (auto& x : m) {
+    x.fab->request_stop();
+    require(x.fab->join(30.0), "fabric thread did not stop");
+  }
 }
 
 int main(int argc, char** argv) {
@@ -310,8 +319,8 @@ int main(int argc, char** argv) {
   try {
     scenario_transport(n);
     scenario_auto_route(n);
-    scenario_routing(2000);
-    for (int policy = 0; policy < 3; ++policy) scenario_engine(std::max<int64_t>(200, n / 8), policy);
+    for (int policy = 0; policy < 3; ++policy) scenario_fabric(std::max<int64_t>(200, n / 8), policy, false);
+    scenario_fabric(std::max<int64_t>(400, n / 8), 2, true);
   } catch (const std::exception& e) {
     fprintf(stderr, "FAILED with exception: %s\n", e.what());
     return 1;

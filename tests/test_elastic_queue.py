@@ -1,0 +1,164 @@
+"""Elastic, fault-isolated shared queue (reference: one named detached Ray actor,
+psana_ray/shared_queue.py:19-35, producer.py:43-48,98-130, README.md:23-35).
+
+Separate OS processes on the CPU -- the producer CLI and DataReader consumers -- meeting at a
+rendezvous store; frames move through the native fabric's shared-memory links:
+  (a) a producer runs with NO consumer, buffers its frames, a consumer started 10 s later drains
+      all of them plus EOS, and the producer exits 0 (drain before exit);
+  (b) a consumer that joins mid-stream receives frames; delivery stays exactly-once;
+  (c) kill -9 of one of two consumers mid-stream: the survivor gets every frame not already in the
+      dead consumer's shard, plus EOS, and the producer exits 0;
+  (d) a second producer job attaches to the live queue; one consumer receives both jobs' frames
+      exactly once;
+  plus: a producer that nobody drains fails after --timeout with a clear message (rc 1).
+Every frame is checked bit-exactly against the fp32 golden calibration."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV = dict(os.environ, PYTHONPATH=ROOT + (os.pathsep + os.environ["PYTHONPATH"] if os.environ.get("PYTHONPATH") else ""))
+ENV.pop("LOCAL_RANK", None)
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture
+def store_port():
+    port = _port()
+    p = subprocess.Popen([sys.executable, "-m", "psana_ray_amd.server", "--host", "127.0.0.1", "--port", str(port),
+                          "--log_level", "WARNING"], env=ENV, cwd=ROOT)
+    t0 = time.time()
+    while time.time() - t0 < 30:
+        with socket.socket() as s:
+            if s.connect_ex(("127.0.0.1", port)) == 0:
+                break
+        time.sleep(0.1)
+    yield port
+    p.terminate()
+    try:
+        p.wait(10)
+    except subprocess.TimeoutExpired:
+        p.kill()
+
+
+def producer(port, n_events, *extra, queue_size=16, chunk=4, timeout=60):
+    cmd = [sys.executable, "-m", "psana_ray_amd.producer", "--exp", "synthetic", "--run", "2", "--detector_name",
+           "tiny_epix", "--calib", "--device", "cpu", "--ray_address", f"127.0.0.1:{port}", "--num_events",
+           str(n_events), "--queue_size", str(queue_size), "--chunk", str(chunk), "--timeout", str(timeout),
+           "--metrics_interval", "0", "--log_level", "INFO", *extra]
+    return subprocess.Popen(cmd, env=ENV, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+
+def consumer(port, out, *extra):
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "_elastic_consumer.py"), "--address", f"127.0.0.1:{port}",
+           "--out", str(out), *extra]
+    return subprocess.Popen(cmd, env=ENV, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+
+def records(path):
+    if not os.path.exists(path):
+        return []
+    with open(path) as f:
+        return [json.loads(line) for line in f if line.strip()]
+
+
+def frames(recs):
+    fr = [r for r in recs if "gevt" in r]
+    assert all(r["ok"] for r in fr), "frame content differs from the golden calibration"
+    return [r["gevt"] for r in fr]
+
+
+def finish(p, timeout=90):
+    try:
+        out, _ = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        out, _ = p.communicate()
+        raise AssertionError(f"process did not finish:\n{out[-3000:]}")
+    return p.returncode, out
+
+
+def test_producer_first_consumer_ten_seconds_later(store_port, tmp_path):
+    prod = producer(store_port, 24, queue_size=32)
+    time.sleep(10.0)
+    assert prod.poll() is None, "the producer must wait for a consumer to drain its frames"
+    c = consumer(store_port, tmp_path / "c.jsonl")
+    rc_c, out_c = finish(c)
+    rc_p, out_p = finish(prod)
+    assert rc_c == 0, out_c
+    assert rc_p == 0, out_p
+    recs = records(tmp_path / "c.jsonl")
+    assert sorted(frames(recs)) == list(range(24))
+    assert recs[-1].get("eos") is True
+
+
+def test_consumer_joins_mid_stream(store_port, tmp_path):
+    n = 300
+    prod = producer(store_port, n)
+    c1 = consumer(store_port, tmp_path / "c1.jsonl", "--sleep", "0.04", "--slots", "4")
+    c2 = consumer(store_port, tmp_path / "c2.jsonl", "--sleep", "0.04", "--slots", "4")
+    t0 = time.time()
+    while len(frames(records(tmp_path / "c1.jsonl"))) < 10 and time.time() - t0 < 30:
+        time.sleep(0.05)
+    c3 = consumer(store_port, tmp_path / "c3.jsonl", "--sleep", "0.04", "--slots", "4")
+    for c in (c1, c2, c3):
+        rc, out = finish(c)
+        assert rc == 0, out
+    rc_p, out_p = finish(prod)
+    assert rc_p == 0, out_p
+    got = [frames(records(tmp_path / f"c{i}.jsonl")) for i in (1, 2, 3)]
+    assert len(got[2]) > 0, "the late consumer received nothing"
+    allg = got[0] + got[1] + got[2]
+    assert sorted(allg) == list(range(n)), "exactly-once delivery violated"
+    for i in (1, 2, 3):
+        assert records(tmp_path / f"c{i}.jsonl")[-1].get("eos") is True
+
+
+def test_kill9_consumer_survivor_gets_the_rest(store_port, tmp_path):
+    slots_a = 4
+    prod = producer(store_port, 120)
+    a = consumer(store_port, tmp_path / "a.jsonl", "--sleep", "0.01", "--slots", str(slots_a), "--die_after", "12")
+    b = consumer(store_port, tmp_path / "b.jsonl", "--sleep", "0.01", "--slots", "4")
+    rc_a, _ = finish(a)
+    assert rc_a == -9
+    rc_b, out_b = finish(b)
+    rc_p, out_p = finish(prod)
+    assert rc_b == 0, out_b
+    assert rc_p == 0, out_p
+    ga, gb = frames(records(tmp_path / "a.jsonl")), frames(records(tmp_path / "b.jsonl"))
+    assert len(ga) == 12
+    assert not set(ga) & set(gb), "a frame was delivered twice"
+    lost = set(range(120)) - set(ga) - set(gb)
+    assert len(lost) <= slots_a, f"lost {len(lost)} frames, more than the dead consumer's shard ({slots_a})"
+    assert records(tmp_path / "b.jsonl")[-1].get("eos") is True
+    assert "died" in out_p, out_p[-2000:]
+
+
+def test_second_producer_job_attaches(store_port, tmp_path):
+    c = consumer(store_port, tmp_path / "c.jsonl", "--sleep", "0.01", "--slots", "4")
+    p1 = producer(store_port, 80)
+    time.sleep(1.0)
+    p2 = producer(store_port, 1080, "--start_event", "1000")
+    rc_c, out_c = finish(c)
+    rc1, out1 = finish(p1)
+    rc2, out2 = finish(p2)
+    assert (rc1, rc2, rc_c) == (0, 0, 0), (out1[-2000:], out2[-2000:], out_c[-2000:])
+    got = frames(records(tmp_path / "c.jsonl"))
+    assert sorted(got) == list(range(80)) + list(range(1000, 1080))
+
+
+def test_undrained_producer_times_out_with_a_clear_message(store_port):
+    p = producer(store_port, 8, timeout=3)
+    rc, out = finish(p)
+    assert rc == 1
+    assert "were not taken by any consumer within --timeout" in out

@@ -1,8 +1,9 @@
 """Host-side race / memory-safety checks of the native runtime (SURVEY §5 "Race detection").
 
-tools/sanitize_host.sh builds tests/cpp/slotpool_stress.cpp + csrc/runtime.cpp + csrc/routing.cpp
-with ThreadSanitizer or AddressSanitizer+UBSan (host pass only) and runs producer / transport /
-consumer threads against the slot pool state machine plus a randomized routing check."""
+tools/sanitize_host.sh builds tests/cpp/slotpool_stress.cpp + csrc/runtime.cpp + csrc/fabric.cpp
+with ThreadSanitizer or AddressSanitizer+UBSan (host pass only) and runs producer / fabric /
+consumer threads against the slot pool state machine and the link protocol (including a consumer
+that leaves mid-stream)."""
 import os
 import subprocess
 
