@@ -43,7 +43,8 @@ def main(argv=None):
     a = ap.parse_args(argv)
     import torch
 
-    from psana_ray_amd.data_reader import DataReader, EndOfStream
+    from psana_ray_amd.data_reader import DataReader
+    from psana_ray_amd.queue import EndOfStream
 
     port = _port()
     env = dict(os.environ, PYTHONPATH=ROOT)
