@@ -112,18 +112,18 @@ PYBIND11_MODULE(_C, m) {
         py::arg("kind"), py::arg("idx"), py::arg("nout"), py::arg("stream"));
   m.def("calib_cm",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t ped, uint64_t gf,
-           uint64_t pflags, int kind, int n_panels, int panel_rows, int panel_cols, int asic_rows,
+           uint64_t elig, int kind, int n_panels, int panel_rows, int panel_cols, int asic_rows,
            int asic_cols, float thr, float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream) {
-          pr::launch_calib_cm(make_ptrs(in, out), (int)in.size(), ped, gf, pflags, kind, n_panels, panel_rows,
+          pr::launch_calib_cm(make_ptrs(in, out), (int)in.size(), ped, gf, elig, kind, n_panels, panel_rows,
                               panel_cols, asic_rows, asic_cols, thr, maxcorr, npix_min, flags, bank_cols, stream);
         },
-        py::arg("raw_ptrs"), py::arg("out_ptrs"), py::arg("ped"), py::arg("gf"), py::arg("pflags"),
+        py::arg("raw_ptrs"), py::arg("out_ptrs"), py::arg("ped"), py::arg("gf"), py::arg("elig"),
         py::arg("kind"), py::arg("n_panels"), py::arg("panel_rows"), py::arg("panel_cols"),
         py::arg("asic_rows"), py::arg("asic_cols"), py::arg("thr"), py::arg("maxcorr"), py::arg("npix_min"),
         py::arg("flags"), py::arg("bank_cols"), py::arg("stream"));
-  m.def("cm_lds_bytes", &pr::cm_lds_bytes);
+  m.def("cm_lds_bytes", &pr::cm_lds_bytes, py::arg("asic_rows"), py::arg("asic_cols"), py::arg("kind"));
   m.def("cm_tile_cols", &pr::cm_tile_cols, py::arg("asic_rows"), py::arg("asic_cols"), py::arg("bank_cols"),
-        py::arg("max_cols") = 0);
+        py::arg("max_cols") = 0, py::arg("kind") = 0);
   m.def("image_tile_shape", [] { return py::make_tuple(pr::image_tile_h(), pr::image_tile_w(), pr::image_tile_stage()); });
   m.def("image_tiles",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, bool calib, int kind, uint64_t ped,
@@ -380,7 +380,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("npix", &pr::CalibPlan::npix)
       .def_readwrite("ped", &pr::CalibPlan::ped)
       .def_readwrite("gf", &pr::CalibPlan::gf)
-      .def_readwrite("pflags", &pr::CalibPlan::pflags)
+      .def_readwrite("elig", &pr::CalibPlan::elig)
       .def_readwrite("n_panels", &pr::CalibPlan::n_panels)
       .def_readwrite("panel_rows", &pr::CalibPlan::panel_rows)
       .def_readwrite("panel_cols", &pr::CalibPlan::panel_cols)

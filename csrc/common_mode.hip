@@ -12,16 +12,34 @@
 //   out = v * gain_factor   (mask folded into the gain factor -> masked pixels are 0)
 // Median = numpy semantics (mean of the two middle elements for an even count).
 //
-// MI355X design: one 1024-thread workgroup (16 waves) owns one (frame, ASIC) tile.  The
-// whole pre-gain tile lives in LDS (176 x 193 f32 incl. a 1-float row pad that makes column
-// reads bank-conflict free, + 4 bits of per-pixel state = 152.8 KB of the 160 KB), so HBM is
-// touched exactly once: raw u16 in, f32 out.  Medians are exact: every row-bank segment
-// (<= 64 px) is one wave-register bitonic sort, every column (<= 256 px) a 4-register bitonic
-// sort across the wave, with DPP / permlane-swap lane exchanges (VALU only, no LDS round trips).
+// MI355X design.  Round 2 started VALU-bound (4.0M VALU wave-instructions per epix10k2M frame,
+// ~6.6 us at the chip's ~614 G wave-instr/s); this version is at 3.3M and the memory phases now
+// dominate (medians off: ~4.7-5.0 us/frame, vs a measured 3.0 us/frame floor for the same bytes,
+// tools/bw_ceiling.hip; profiles/r2/cm_kernel.md):
+//  * one workgroup owns one (frame, full-height ASIC stripe) tile in LDS: HBM is touched once;
+//  * the tile holds v for CM-eligible pixels and NaN for every other pixel.  The median phases then
+//    need no eligibility lookups at all: |NaN| < thr is false (never participates) and
+//    NaN - median stays NaN (never corrected);
+//  * the raw v of an 8-pixel group that has non-eligible but kept pixels (status-bad or
+//    gain-switched, a few %) is parked in an LDS side slot (per-wave ranges claimed with a ballot,
+//    no atomics) so the store phase never goes back to HBM for it; a full range falls back to a
+//    recompute from raw + pedestal;
+//  * eligibility arrives as per-8-pixel bit-planes (one byte per candidate gain table), selected by
+//    the pixels' candidate bits with one v_bfi per 8 pixels (SWAR) instead of per-pixel shifts;
+//  * row segments: one lane per (row, bank), values in registers, a median-cone-pruned Batcher
+//    network (select_regs: 580 VALU for 48 values instead of a 768-VALU sort), toggle +-inf padding
+//    so the median sits at fixed register positions;
+//  * columns: four lanes (a quad) per column, per-lane sorts + DPP merge-split + merge-path;
+//  * tile rows are 16-B aligned with an odd number of 16-B slots per row (pitch 52 floats for
+//    48-column stripes) so the row phase moves whole segments with conflict-free ds_read_b128; the
+//    candidate bits and side-slot numbers for the store phase live in the row pad;
+//  * compile-time production shapes issue every load of a phase before the first use (phase 1:
+//    raw + planes + first pedestal table, then the rare switched-gain tables; phase 3: first gain
+//    table) -- 125 VGPRs, no scratch, four 256-thread workgroups per CU.
 #include "common.h"
 #include "sortnet.h"
 
-#include <cstdlib>
+#include <algorithm>
 
 namespace pr {
 
@@ -153,27 +171,17 @@ struct CmParams {
   int npix_min;     // minimum participating pixels for a correction
   int flags;        // bit0: rows by bank, bit1: columns
   int bank_cols;    // columns per bank (<= 64, divides the ASIC width)
-  int gather;       // 1: load only the candidate tables a pixel group uses (net kernels)
 };
 
 struct TileGeom {
-  int panel_rows, panel_cols;  // H, W of one panel
-  int asic_rows, asic_cols;    // R, C of one ASIC tile
+  int panel_rows, panel_cols;        // H, W of one panel
+  int asic_rows, asic_cols;          // R, C of one tile (a full-height ASIC stripe)
   int asics_per_col, asics_per_row;  // H / R, W / C
-  int64_t npix;                // pixels per frame
-  int nframes;                 // frames of this launch (grid = n_asics * nframes, 1-D)
-  int swizzle;                 // 1: XCD-aware remap (all frames of an ASIC on one XCD / L2); opt-in
+  int64_t npix;                      // pixels per frame
+  int nframes;                       // frames of this launch (grid = n_tiles * nframes, 1-D)
+  int side_slots;                    // LDS side slots after the tile (SideCtx)
+  int pitch;                         // LDS floats per tile row (values + candidate bits + pad)
 };
-
-// (asic, frame) of this workgroup.  Frame-minor logical order + the XCD remap put the blocks
-// that read the SAME per-ASIC tables (574 KB for epix) on one XCD, so the tables come from its L2
-// instead of HBM for every frame.
-__device__ __forceinline__ void cm_block_coords(const TileGeom& tg, int& asic, int& f) {
-  const int nwg = (int)gridDim.x;
-  const int id = tg.swizzle ? xcd_swizzle((int)blockIdx.x, nwg) : (int)blockIdx.x;
-  asic = id / tg.nframes;
-  f = id % tg.nframes;
-}
 
 // Fused K-05 output (image mode with common mode).  Every panel is placed by an integer rotation
 // + translation (geometry.py), so pixel (y, x) of panel p lands at image element
@@ -185,60 +193,217 @@ struct ImgOut {
   const uint8_t* omask;   // image-shaped output mask (truthy keeps) or nullptr
 };
 
-// Phase 3 of both common-mode kernels: gain factor (+ folded frame mask) applied to the corrected
-// LDS tile; stored in frame layout (16-B stores) or, with io.desc, written into the image.  The
-// image walk keeps consecutive lanes on consecutive image elements: tile rows when the panel's
-// columns run along image rows (|sx| == 1), tile columns otherwise (column reads of the padded
-// tile are LDS-conflict-free: odd pitch).
+// ---- tile layout ------------------------------------------------------------------------
+// Candidate bits per pixel kept for the store phase (which gain-factor table): 1 for 2-table
+// kinds, 2 for Jungfrau's 3 tables.  Eligibility bit-planes per 8-pixel group in global memory:
+// PB bytes, byte k = pixels eligible when they decode to candidate k.
 template <int NT>
-__device__ __forceinline__ void cm_store(float* tile, const uint32_t* nib, const float* __restrict__ gf,
-                                         const TileGeom& tg, const int R, const int C, int64_t base,
-                                         PR_GLOBAL float* out, const ImgOut& io, int panel, int y0, int x0,
-                                         bool gather) {
-  const int LD = C + 1, C8 = C >> 3;
-  const int tid = threadIdx.x;
-  const bool img = io.desc != nullptr;
-  for (int i = tid; i < R * C8; i += blockDim.x) {
-    const int r = i / C8, c = (i % C8) * 8;
-    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
-    const uint32_t nb = nib[i];
-    uint32_t need = 0;
+struct CmLayout {
+  static constexpr int kCandBits = NT == 3 ? 2 : 1;
+  static constexpr int kPlaneBytes = NT == 3 ? 4 : NT;   // stride of the eligibility planes
+};
+
+// Tile row: C values, then the row pad = candidate bits (C * cand_bits / 8 bytes) + one side-slot
+// byte per 8-pixel group (C / 8 bytes); rows are 16-B aligned with an odd number of 16-B slots.
+__host__ __device__ constexpr int cm_pitch(int cols, int cand_bits) {
+  int p = cols + (cols * (cand_bits + 1) + 31) / 32;
+  while (p % 8 != 4) ++p;
+  return p;
+}
+
+// Side slots: the raw values v of the (few) 8-pixel groups holding non-eligible pixels, so the
+// store phase never goes back to HBM for them.  Every wave owns a fixed slot range (no atomics);
+// a group that finds its wave's range full is marked kSideOverflow and recomputed from global
+// memory instead (correct, just slower).
+constexpr uint32_t kNoSide = 0xFF, kSideOverflow = 0xFE, kMaxSideSlots = 254;
+
+struct SideCtx {
+  float* side;    // slot s = 8 floats at side + 8 s
+  int base, end;  // this wave's slots [base, end)
+  int used;       // wave-uniform running count
+};
+
+__device__ __forceinline__ SideCtx side_ctx(float* side, int nslots) {
+  const int wave = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+  const int per = nslots / nw;
+  return SideCtx{side, wave * per, wave * per + per, 0};
+}
+
+// Claims a slot for every lane with `needs` (call convergently: all lanes of the wave) and writes
+// v[8] into it.  Returns the group's slot byte.
+__device__ __forceinline__ uint32_t side_put(SideCtx& sc, bool needs, const float (&v)[8]) {
+  const uint64_t bal = __ballot(needs);
+  const int before =
+      (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+  const int slot = sc.base + sc.used + before;
+  sc.used += __popcll(bal);
+  if (!needs) return kNoSide;
+  if (slot >= sc.end) return kSideOverflow;
+  float* d = sc.side + 8 * slot;
+  *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  return (uint32_t)slot;
+}
+
+// Decode one 8-pixel group: v = ADU - pedestal (0 for Jungfrau's invalid gain code), el = CM
+// eligibility bits, cbits = candidate bits for the store phase.
+//   rw: raw words (2 pixels each), pa: candidate pedestals, ep: eligibility bit-planes
+template <int KIND, int NT>
+__device__ __forceinline__ void cm_decode8(const uint4 rw, const uint32_t ep, const float (&pa)[NT][8], float (&v)[8],
+                                           uint32_t& el, uint32_t& cbits) {
+  const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
+  uint32_t c0 = 0, c1 = 0;   // candidate bit planes (bit j of pixel j): gain bit 14 / 15
 #pragma unroll
-    for (int j = 0; j < 8; ++j) need |= 1u << ((nb >> (4 * j)) & 3u);
-    if (!gather) need = (1u << NT) - 1u;
-    float ga[NT][8];
-#pragma unroll
-    for (int k = 0; k < NT; ++k) {
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-      if ((need >> k) & 1u) {
-        a = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix);
-        b = *reinterpret_cast<const float4*>(gf + k * tg.npix + pix + 4);
-      }
-      ga[k][0] = a.x; ga[k][1] = a.y; ga[k][2] = a.z; ga[k][3] = a.w;
-      ga[k][4] = b.x; ga[k][5] = b.y; ga[k][6] = b.z; ga[k][7] = b.w;
-    }
-    float* trow = tile + r * LD + c;
-    float o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t q = (nb >> (4 * j)) & 0xFu;
-      const int cand = q & 3;
-      float gg;
-      if constexpr (NT == 1) gg = ga[0][j];
-      else if constexpr (NT == 2) gg = bsel(cand != 0, ga[1][j], ga[0][j]);
-      else gg = bsel(cand == 0, ga[0][j], bsel(cand == 1, ga[1][j], ga[2][j]));
-      o[j] = (q & 4u) ? trow[j] * gg : 0.0f;
-    }
-    if (img) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) trow[j] = o[j];
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t wj = w[j >> 1];
+    const int sh = 16 * (j & 1);
+    if constexpr (KIND == kPlain) {
+      v[j] = (float)__builtin_amdgcn_ubfe(wj, sh, 16) - pa[0][j];
     } else {
-      PR_GLOBAL float4* op = (PR_GLOBAL float4*)(out + pix);
-      st_f4(op, make_float4(o[0], o[1], o[2], o[3]));
-      st_f4(op + 1, make_float4(o[4], o[5], o[6], o[7]));
+      const float adu = (float)__builtin_amdgcn_ubfe(wj, sh, 14);
+      const uint32_t g0 = (uint32_t)__builtin_amdgcn_sbfe((int)wj, sh + 14, 1);   // all ones: gain bit 14
+      if constexpr (KIND == kEpix10ka) {
+        v[j] = adu - __uint_as_float((g0 & __float_as_uint(pa[1][j])) | (~g0 & __float_as_uint(pa[0][j])));
+        c0 |= g0 & (1u << j);
+      } else {   // Jungfrau: gain bits 0 -> G0, 1 -> G1, 3 -> G2, 2 -> invalid (never eligible, output 0)
+        const uint32_t g1 = (uint32_t)__builtin_amdgcn_sbfe((int)wj, sh + 15, 1);
+        const uint32_t p01 = (g0 & __float_as_uint(pa[1][j])) | (~g0 & __float_as_uint(pa[0][j]));
+        const uint32_t sel2 = g0 & g1;
+        const float vj = adu - __uint_as_float((sel2 & __float_as_uint(pa[2][j])) | (~sel2 & p01));
+        v[j] = __uint_as_float(__float_as_uint(vj) & ~(~g0 & g1));
+        c0 |= g0 & (1u << j);
+        c1 |= g1 & (1u << j);
+      }
     }
   }
-  if (!img) return;
+  if constexpr (NT == 1) {
+    el = ep & 0xFFu;
+    cbits = 0;
+  } else if constexpr (NT == 2) {
+    el = ((c0 & (ep >> 8)) | (~c0 & ep)) & 0xFFu;   // v_bfi: plane 1 where the pixel switched
+    cbits = c0;
+  } else {
+    // cand 0: !b14 !b15, cand 1: b14 !b15, cand 2: b14 b15, invalid: !b14 b15
+    el = ((~c0 & ~c1 & ep) | (c0 & ~c1 & (ep >> 8)) | (c0 & c1 & (ep >> 16))) & 0xFFu;
+    uint32_t cb = 0;   // 2-bit candidate field per pixel: 0, 1, 2
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cb |= ((((c0 >> j) & 1u) + (((c0 & c1) >> j) & 1u)) << (2 * j));
+    cbits = cb;
+  }
+}
+
+// tile value: v where eligible, NaN elsewhere
+__device__ __forceinline__ void cm_tile_values(const float (&v)[8], uint32_t el, float (&x)[8]) {
+  const uint32_t qnan = 0x7fc00000u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)el, j, 1);
+    x[j] = __uint_as_float((m & __float_as_uint(v[j])) | (~m & qnan));
+  }
+}
+
+// row pad accessors (group k of the row)
+template <int NT>
+__device__ __forceinline__ void cm_put_meta(uint8_t* pad, int C, int k, uint32_t cbits, uint32_t slot) {
+  if constexpr (CmLayout<NT>::kCandBits == 1) pad[k] = (uint8_t)cbits;
+  else reinterpret_cast<uint16_t*>(pad)[k] = (uint16_t)cbits;
+  pad[(C * CmLayout<NT>::kCandBits) / 8 + k] = (uint8_t)slot;
+}
+template <int NT>
+__device__ __forceinline__ void cm_get_meta(const uint8_t* pad, int C, int k, uint32_t& cbits, uint32_t& slot) {
+  if constexpr (CmLayout<NT>::kCandBits == 1) cbits = pad[k];
+  else cbits = reinterpret_cast<const uint16_t*>(pad)[k];
+  slot = pad[(C * CmLayout<NT>::kCandBits) / 8 + k];
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t cm_need(uint32_t cbits) {
+  // which candidate tables an 8-pixel group touches (bit k = table k)
+  if constexpr (NT == 1) return 1u;
+  else if constexpr (NT == 2) return 1u | (cbits ? 2u : 0u);
+  else return 1u | ((cbits & 0x5555u) ? 2u : 0u) | ((cbits & 0xAAAAu) ? 4u : 0u);
+}
+
+template <int NT>
+__device__ __forceinline__ void load8(const float* __restrict__ t, int64_t npix, int64_t pix, uint32_t need,
+                                      float (&a)[NT][8], int k0 = 0) {
+#pragma unroll
+  for (int k = k0; k < NT; ++k) {
+    float4 u = make_float4(0.f, 0.f, 0.f, 0.f), w = u;
+    if ((need >> k) & 1u) {
+      u = *reinterpret_cast<const float4*>(t + k * npix + pix);
+      w = *reinterpret_cast<const float4*>(t + k * npix + pix + 4);
+    }
+    a[k][0] = u.x; a[k][1] = u.y; a[k][2] = u.z; a[k][3] = u.w;
+    a[k][4] = w.x; a[k][5] = w.y; a[k][6] = w.z; a[k][7] = w.w;
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t load_planes(const uint8_t* __restrict__ planes, int64_t pix) {
+  const int64_t g = pix >> 3;
+  if constexpr (NT == 1) return planes[g];
+  else if constexpr (NT == 2) return *reinterpret_cast<const uint16_t*>(planes + 2 * g);
+  else return *reinterpret_cast<const uint32_t*>(planes + 4 * g);
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t need_from_raw(const uint4 rw) {
+  // candidate tables the group's raw gain bits select (select-then-load of the rare tables)
+  const uint32_t b = (rw.x | rw.y | rw.z | rw.w);
+  if constexpr (NT == 1) return 1u;
+  else if constexpr (NT == 2) return 1u | ((b & 0x40004000u) ? 2u : 0u);
+  else return 1u | ((b & 0x40004000u) ? 6u : 0u);
+}
+
+// gain factor of pixel j from the group's candidate bits
+template <int NT>
+__device__ __forceinline__ float cm_gain(const float (&ga)[NT][8], uint32_t cb, int j) {
+  if constexpr (NT == 1) {
+    return ga[0][j];
+  } else if constexpr (NT == 2) {
+    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)cb, j, 1);
+    return __uint_as_float((m & __float_as_uint(ga[1][j])) | (~m & __float_as_uint(ga[0][j])));
+  } else {
+    const uint32_t cj = (cb >> (2 * j)) & 3u;
+    return bsel(cj == 0, ga[0][j], bsel(cj == 1, ga[1][j], ga[2][j]));
+  }
+}
+
+// Store-phase output of one 8-pixel group.  NaN tile entries are pixels that were not CM-eligible:
+// their raw value comes from the group's side slot (or, on slot overflow, is recomputed from raw
+// + pedestal in global memory); masked pixels have a zero gain factor, Jungfrau's invalid gain
+// code a zero value, so both come out 0.
+template <int KIND, int NT>
+__device__ __forceinline__ void cm_out8(const float* tile_row, const float* side, uint32_t cb, uint32_t slot,
+                                        const float (&ga)[NT][8], const PR_GLOBAL uint16_t* raw,
+                                        const float* __restrict__ ped, int64_t npix, int64_t pix, float (&o)[8]) {
+  const float4 t0 = *reinterpret_cast<const float4*>(tile_row);
+  const float4 t1 = *reinterpret_cast<const float4*>(tile_row + 4);
+  float xv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+  if (slot < kSideOverflow) {
+    const float4 s0 = *reinterpret_cast<const float4*>(side + 8 * slot);
+    const float4 s1 = *reinterpret_cast<const float4*>(side + 8 * slot + 4);
+    const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = xv[j] != xv[j] ? sv[j] : xv[j];
+  } else if (slot == kSideOverflow) {
+    const uint4 rw = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
+    float pa[NT][8];
+    load8<NT>(ped, npix, pix, need_from_raw<NT>(rw), pa);
+    float v[8];
+    uint32_t el, cb2;
+    cm_decode8<KIND, NT>(rw, 0u, pa, v, el, cb2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = xv[j] != xv[j] ? v[j] : xv[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = xv[j] * cm_gain<NT>(ga, cb, j);
+}
+
+// Image-mode epilogue of the store phase: the output tile (already in LDS) into the image.
+__device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C, const ImgOut& io, int panel, int y0,
+                                         int x0, PR_GLOBAL float* out) {
   __syncthreads();
   const int32_t* d = io.desc + 3 * panel;
   const int sy = d[1], sx = d[2];
@@ -247,103 +412,146 @@ __device__ __forceinline__ void cm_store(float* tile, const uint32_t* nib, const
   const bool rows = sx == 1 || sx == -1;
   const int inner = rows ? C : R;
   const float inv = 1.0f / (float)inner;   // e < 2^24: floor((e + 0.5) / inner) is exact in f32
-  for (int e = tid; e < n; e += blockDim.x) {
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
     const int a = (int)(((float)e + 0.5f) * inv);
     const int bb = e - a * inner;
     const int r = rows ? a : bb, c = rows ? bb : a;
     const int64_t q = b0 + (int64_t)r * sy + (int64_t)c * sx;
-    float v = tile[r * LD + c];
+    float v = tile[r * P + c];
     if (io.omask != nullptr && !io.omask[q]) v = 0.0f;
     out[q] = v;
   }
 }
 
-// per-pixel nibble in LDS: bits0-1 candidate, bit2 good, bit3 cm-eligible
+__device__ __forceinline__ void cm_emit(float* trow, PR_GLOBAL float* out, int64_t pix, bool img, const float (&o)[8]) {
+  if (img) {
+    *reinterpret_cast<float4*>(trow) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(trow + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  } else {
+    PR_GLOBAL float4* op = (PR_GLOBAL float4*)(out + pix);
+    st_f4(op, make_float4(o[0], o[1], o[2], o[3]));
+    st_f4(op + 1, make_float4(o[4], o[5], o[6], o[7]));
+  }
+}
+
+// Phase 3 (runtime-shape loop form).
+template <int KIND, int NT>
+__device__ __forceinline__ void cm_store(float* tile, const float* side, const int P, const int R, const int C,
+                                         const TileGeom& tg, const PR_GLOBAL uint16_t* raw,
+                                         const float* __restrict__ ped, const float* __restrict__ gf, int64_t base,
+                                         PR_GLOBAL float* out, const ImgOut& io, int panel, int y0, int x0) {
+  const int C8 = C >> 3;
+  const bool img = io.desc != nullptr;
+  for (int i = threadIdx.x; i < R * C8; i += blockDim.x) {
+    const int r = i / C8, k = i - r * C8, c = k * 8;
+    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
+    uint32_t cb, slot;
+    cm_get_meta<NT>(reinterpret_cast<const uint8_t*>(tile + r * P + C), C, k, cb, slot);
+    float ga[NT][8];
+    load8<NT>(gf, tg.npix, pix, cm_need<NT>(cb), ga);
+    float o[8];
+    cm_out8<KIND, NT>(tile + r * P + c, side, cb, slot, ga, raw, ped, tg.npix, pix, o);
+    cm_emit(tile + r * P + c, out, pix, img, o);
+  }
+  if (img) cm_place(tile, P, R, C, io, panel, y0, x0, out);
+}
+
+// (tile, frame) of this workgroup and the tile's first pixel
+struct TileCoord {
+  int f, panel, ar, ac;
+  int64_t base;
+};
+// Table-major order: consecutive workgroups take the same tile of consecutive frames, so the
+// constant tables of a tile are fetched from HBM about once per XCD and then hit in L2.  (A/B on
+// MI355X, 32 epix10k2M frames: frame-major order 5.7 us/frame vs 5.0 table-major with the medians
+// off; an XCD-grouping remap of the table-major order changed nothing, 4.75 vs 4.65.)
+__device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C) {
+  TileCoord t;
+  const int id = (int)blockIdx.x;
+  const int tile = id / tg.nframes;
+  t.f = id - tile * tg.nframes;
+  const int per_panel = tg.asics_per_col * tg.asics_per_row;
+  t.panel = tile / per_panel;
+  t.ar = (tile % per_panel) / tg.asics_per_row;
+  t.ac = (tile % per_panel) % tg.asics_per_row;
+  t.base = (int64_t)t.panel * tg.panel_rows * tg.panel_cols + (int64_t)t.ar * R * tg.panel_cols + (int64_t)t.ac * C;
+  return t;
+}
+
+// Phase 1 (runtime-shape loop form): decode + pedestal into the tile, side slots for groups with
+// non-eligible pixels.  Whole waves iterate together (side_put is a wave-wide ballot).
+template <int KIND, int NT>
+__device__ __forceinline__ void cm_phase1(float* tile, SideCtx& sc, const int P, const int R, const int C,
+                                          const TileGeom& tg, const PR_GLOBAL uint16_t* raw,
+                                          const float* __restrict__ ped, const uint8_t* __restrict__ planes,
+                                          int64_t base) {
+  const int C8 = C >> 3;
+  const int n = R * C8;
+  for (int i0 = threadIdx.x & ~63; i0 < n; i0 += blockDim.x) {
+    const int i = i0 + (threadIdx.x & 63);
+    const bool act = i < n;
+    const int r = act ? i / C8 : 0, k = act ? i - r * C8 : 0, c = k * 8;
+    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
+    float v[8];
+    uint32_t el = 0xFFu, cb = 0;
+    if (act) {
+      const uint4 rw = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
+      const uint32_t ep = load_planes<NT>(planes, pix);
+      float pa[NT][8];
+      load8<NT>(ped, tg.npix, pix, need_from_raw<NT>(rw), pa);
+      cm_decode8<KIND, NT>(rw, ep, pa, v, el, cb);
+      float x[8];
+      cm_tile_values(v, el, x);
+      float* trow = tile + r * P + c;
+      *reinterpret_cast<float4*>(trow) = make_float4(x[0], x[1], x[2], x[3]);
+      *reinterpret_cast<float4*>(trow + 4) = make_float4(x[4], x[5], x[6], x[7]);
+    }
+    const uint32_t slot = side_put(sc, act && el != 0xFFu, v);
+    if (act) cm_put_meta<NT>(reinterpret_cast<uint8_t*>(tile + r * P + C), C, k, cb, slot);
+  }
+}
+
+// ==========================================================================================
+// Generic kernel (any ASIC shape): 1024 threads, one wave per row segment / column with
+// cross-lane bitonic sorts.  Fallback for shapes without a compile-time instantiation below.
+// ==========================================================================================
 template <int KIND>
 __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, const float* __restrict__ ped,
                                                         const float* __restrict__ gf,
-                                                        const uint8_t* __restrict__ pflags,
-                                                        const TileGeom tg, const CmParams cp,
-                                                        const ImgOut io) {
+                                                        const uint8_t* __restrict__ planes, const TileGeom tg,
+                                                        const CmParams cp, const ImgOut io) {
   constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int R = tg.asic_rows, C = tg.asic_cols, LD = C + 1;
+  const int R = tg.asic_rows, C = tg.asic_cols, P = tg.pitch;
   float* tile = reinterpret_cast<float*>(smem);
-  uint32_t* nib = reinterpret_cast<uint32_t*>(smem + (((size_t)R * LD * 4 + 15) & ~(size_t)15));
-  const int C8 = C >> 3;
-
-  int asic, f;
-  cm_block_coords(tg, asic, f);
-  const int per_panel = tg.asics_per_col * tg.asics_per_row;
-  const int panel = asic / per_panel;
-  const int ar = (asic % per_panel) / tg.asics_per_row;
-  const int ac = (asic % per_panel) % tg.asics_per_row;
-  const int64_t base = (int64_t)panel * tg.panel_rows * tg.panel_cols +
-                       (int64_t)ar * R * tg.panel_cols + (int64_t)ac * C;
-  const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[f]);
-  PR_GLOBAL float* out = gout<float>(fp.out[f]);
+  float* side = tile + R * P;
+  SideCtx sc = side_ctx(side, tg.side_slots);
+  const TileCoord t = cm_coords(tg, R, C);
+  const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[t.f]);
+  PR_GLOBAL float* out = gout<float>(fp.out[t.f]);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int nwaves = blockDim.x >> 6;
 
-  // ---- phase 1: decode + pedestal into LDS ---------------------------------------------
-  for (int i = tid; i < R * C8; i += blockDim.x) {
-    const int r = i / C8, c = (i % C8) * 8;
-    const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
-    const uint4 rw = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
-    const uint2 fl = *reinterpret_cast<const uint2*>(pflags + pix);
-    const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
-    const uint32_t fw[2] = {fl.x, fl.y};
-    float pa[NT][8];
-#pragma unroll
-    for (int k = 0; k < NT; ++k) {
-      const float4 a = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix);
-      const float4 b = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix + 4);
-      pa[k][0] = a.x; pa[k][1] = a.y; pa[k][2] = a.z; pa[k][3] = a.w;
-      pa[k][4] = b.x; pa[k][5] = b.y; pa[k][6] = b.z; pa[k][7] = b.w;
-    }
-    uint32_t nb = 0;
-    float* trow = tile + r * LD + c;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t rv = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-      const uint32_t pf = (fw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-      bool valid;
-      const int cand = decode_cand(rv, KIND, valid);
-      float pp;
-      if constexpr (NT == 1) pp = pa[0][j];
-      else if constexpr (NT == 2) pp = bsel(cand != 0, pa[1][j], pa[0][j]);
-      else pp = bsel(cand == 0, pa[0][j], bsel(cand == 1, pa[1][j], pa[2][j]));
-      const bool good = valid && (pf & 1u);
-      const bool elig = good && ((pf >> (1 + cand)) & 1u);
-      trow[j] = decode_adu(rv, KIND) - pp;
-      nb |= (uint32_t)(cand | (good ? 4 : 0) | (elig ? 8 : 0)) << (4 * j);
-    }
-    nib[r * C8 + (c >> 3)] = nb;
-  }
+  cm_phase1<KIND, NT>(tile, sc, P, R, C, tg, raw, ped, planes, t.base);
   __syncthreads();
-
   const float INF = __int_as_float(0x7f800000);
 
-  // ---- phase 2a: row common mode per bank segment ---------------------------------------
+  // ---- rows per bank segment: a wave sorts up to 4 segments (one element per lane) --------
   if (cp.flags & 1) {
     const int L = cp.bank_cols;
     const int nbanks = C / L;
     for (int r = wave; r < R; r += nwaves) {
-      float* trow = tile + r * LD;
+      float* trow = tile + r * P;
       for (int b0 = 0; b0 < nbanks; b0 += 4) {
-        float x[4];
-        float v[4];
-        bool el[4];
+        float x[4], v[4];
         int cnt[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int col = (b0 + j) * L + lane;
           const bool in = (b0 + j < nbanks) && (lane < L);
-          v[j] = in ? trow[col] : 0.0f;
-          el[j] = in && ((nib[r * C8 + (col >> 3)] >> (4 * (col & 7) + 3)) & 1u);
-          const bool part = el[j] && (fabsf(v[j]) < cp.thr);
+          v[j] = in ? trow[(b0 + j) * L + lane] : __int_as_float(0x7fc00000);
+          const bool part = fabsf(v[j]) < cp.thr;   // NaN (not eligible / outside) never participates
           x[j] = part ? v[j] : INF;
           cnt[j] = __popcll(__ballot(part));
         }
@@ -354,7 +562,7 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
             const int i0 = __builtin_amdgcn_readfirstlane((cnt[j] - 1) >> 1);
             const int i1 = __builtin_amdgcn_readfirstlane(cnt[j] >> 1);
             const float med = (lane_value(x[j], i0) + lane_value(x[j], i1)) * 0.5f;
-            if (fabsf(med) <= cp.maxcorr && el[j]) trow[(b0 + j) * L + lane] = v[j] - med;
+            if (fabsf(med) <= cp.maxcorr && (b0 + j < nbanks) && lane < L) trow[(b0 + j) * L + lane] = v[j] - med;
           }
         }
       }
@@ -362,20 +570,16 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
     __syncthreads();
   }
 
-  // ---- phase 2b: column common mode -------------------------------------------------------
+  // ---- columns: one wave per column (<= 256 rows, 4 per lane) --------------------------------
   if (cp.flags & 2) {
     for (int c = wave; c < C; c += nwaves) {
       float x[4], v[4];
-      bool el[4];
       int cnt = 0;
-      const uint32_t shift = 4 * (c & 7) + 3;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int r = k * 64 + lane;
-        const bool in = r < R;
-        v[k] = in ? tile[r * LD + c] : 0.0f;
-        el[k] = in && ((nib[r * C8 + (c >> 3)] >> shift) & 1u);
-        const bool part = el[k] && (fabsf(v[k]) < cp.thr);
+        v[k] = r < R ? tile[r * P + c] : __int_as_float(0x7fc00000);
+        const bool part = fabsf(v[k]) < cp.thr;
         x[k] = part ? v[k] : INF;
         cnt += __popcll(__ballot(part));
       }
@@ -385,45 +589,27 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
         if (fabsf(med) <= cp.maxcorr) {
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            if (el[k]) tile[(k * 64 + lane) * LD + c] = v[k] - med;
+            if (k * 64 + lane < R) tile[(k * 64 + lane) * P + c] = v[k] - med;   // NaN stays NaN
         }
       }
     }
     __syncthreads();
   }
 
-  // ---- phase 3: gain factor + mask, store -------------------------------------------------
-  cm_store<NT>(tile, nib, gf, tg, R, C, base, out, io, panel, ar * R, ac * C, false);
+  cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.panel, t.ar * R, t.ac * C);
 }
 
-
 // ==========================================================================================
-// Fast path: per-lane in-register sorting networks (no cross-lane traffic in the sorts).
+// Production kernel: per-lane in-register selection / sorting networks.
 //
-//  rows:    ONE lane owns one (row, bank) segment of L pixels; the lane sorts its L values with a
-//           pruned Batcher network (L=48: 384 comparators = 768 VALU) -- 64 segments per wave
-//           instruction instead of one.
-//  columns: TWO lanes (an even/odd pair) own one column, M = ceil(R/2) rows each; each sorts its
-//           half in registers (M=88: 957 comparators), then both evaluate the merge-path
-//           identity  kth(A u B) = min_i max(A[i-1], B[k-i])  with the partner's registers
-//           fetched by one DPP quad_perm each (all register indices compile-time).
-//  Balanced +-inf padding: of the u non-participating elements, the first floor(u/2) become
-//           -inf and the rest +inf.  The numpy median of the participating values then sits at
-//           FIXED sorted positions (N/2-1, N/2 for even N), so no runtime register indexing.
+//  rows:    ONE lane owns one (row, bank) segment of L pixels (12 x ds_read_b128 for L = 48),
+//           pads non-participants with alternating -inf/+inf (the first gets -inf), so the numpy
+//           median of the participants is x[L/2] (odd count) or (x[L/2-1] + x[L/2]) / 2 (even)
+//           after the median-cone network select_regs<L, L/2-1, L/2>.
+//  columns: FOUR lanes (a quad) per column, M = ceil(R/4) rows each: per-lane sorts, a DPP
+//           merge-split between lanes (q, q^1), then merge-path between the two pairs for the two
+//           fixed middle positions of the balanced-padded 4M elements.
 // ==========================================================================================
-__device__ __forceinline__ float dpp_xor1(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
-}
-
-template <int N>
-__device__ __forceinline__ void fixed_median_pos(int cnt, int& lo, int& hi) {
-  // positions of the lower/upper numpy-median elements after balanced +-inf padding of N slots
-  const int u = N - cnt, a = u >> 1;
-  lo = a + ((cnt - 1) >> 1);
-  hi = a + (cnt >> 1);
-}
-
-// quad_perm DPP read of a lane of the same quad (CTRL = p0 | p1<<2 | p2<<4 | p3<<6)
 template <int CTRL>
 __device__ __forceinline__ float dpp_quad(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
@@ -453,321 +639,173 @@ __device__ __forceinline__ void bitonic_merge_vpad(float (&z)[N]) {
   }
 }
 
-// TR / TC: the tile (stripe) rows / columns as compile-time constants for the production shapes
-// (0 = read from TileGeom).  With constants every LDS address in the unrolled median loops is a
-// base VGPR + immediate offset; with runtime dims the compiler kept i*LD / i*C8 for all unrolled
-// i as SGPRs, spilled them to VGPR lanes and re-read them with v_readlane + v_mul_lo per access.
-template <int KIND, int L, int M, int BLOCK, int CQ, int TR = 0, int TC = 0>
-__global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) void calib_cm_net_kernel(const FramePtrs fp, const float* __restrict__ ped,
-                                                            const float* __restrict__ gf,
-                                                            const uint8_t* __restrict__ pflags,
-                                                            const TileGeom tg, const CmParams cp,
-                                                            const ImgOut io) {
+// TR / TC: the tile rows / columns as compile-time constants for the production shapes (0 = from
+// TileGeom): every LDS address in the unrolled loops is then a base VGPR + immediate offset.
+template <int KIND, int L, int M, int BLOCK, int TR = 0, int TC = 0>
+__global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
+    const FramePtrs fp, const float* __restrict__ ped, const float* __restrict__ gf,
+    const uint8_t* __restrict__ planes, const TileGeom tg, const CmParams cp, const ImgOut io) {
   constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
+  constexpr int PC = (TC > 0) ? cm_pitch(TC, CmLayout<NT>::kCandBits) : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int R = TR ? TR : tg.asic_rows, C = TC ? TC : tg.asic_cols, LD = C + 1;
+  const int R = TR ? TR : tg.asic_rows, C = TC ? TC : tg.asic_cols;
+  const int P = PC ? PC : tg.pitch;
   float* tile = reinterpret_cast<float*>(smem);
-  uint32_t* nib = reinterpret_cast<uint32_t*>(smem + (((size_t)R * LD * 4 + 15) & ~(size_t)15));
-  const int C8 = C >> 3;
-  int asic, f;
-  cm_block_coords(tg, asic, f);
-  const int per_panel = tg.asics_per_col * tg.asics_per_row;
-  const int panel = asic / per_panel;
-  const int ar = (asic % per_panel) / tg.asics_per_row;
-  const int ac = (asic % per_panel) % tg.asics_per_row;
-  const int64_t base = (int64_t)panel * tg.panel_rows * tg.panel_cols + (int64_t)ar * R * tg.panel_cols +
-                       (int64_t)ac * C;
-  const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[f]);
-  PR_GLOBAL float* out = gout<float>(fp.out[f]);
+  float* side = tile + R * P;
+  SideCtx sc = side_ctx(side, tg.side_slots);
+  const TileCoord t = cm_coords(tg, R, C);
   const int tid = threadIdx.x;
   const float INF = __int_as_float(0x7f800000);
+  const float QNAN = __int_as_float(0x7fc00000);
+  const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[t.f]);
+  PR_GLOBAL float* out = gout<float>(fp.out[t.f]);
 
-  // ---- phase 1: decode + pedestal into LDS (same as the generic kernel) -------------------
-  // select-then-load: a candidate table is read only by the 8-pixel groups that use it
-  // (gain-switched pixels are rare, so the second/third table's lines are almost never fetched;
-  // memory phases 5.6 -> see profiles/kernels_r1_cm_gather.jsonl)
-  auto p1_need = [&](const uint4 rw) -> uint32_t {
-    const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
-    uint32_t need = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bool vd;
-      need |= 1u << decode_cand((w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, KIND, vd);
-    }
-    return cp.gather ? need : (1u << NT) - 1u;
-  };
-  auto p1_ped = [&](int64_t pix, uint32_t need, float (&pa)[NT][8], int k0 = 0) {
-#pragma unroll
-    for (int k = k0; k < NT; ++k) {
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-      if ((need >> k) & 1u) {
-        a = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix);
-        b = *reinterpret_cast<const float4*>(ped + k * tg.npix + pix + 4);
-      }
-      pa[k][0] = a.x; pa[k][1] = a.y; pa[k][2] = a.z; pa[k][3] = a.w;
-      pa[k][4] = b.x; pa[k][5] = b.y; pa[k][6] = b.z; pa[k][7] = b.w;
-    }
-  };
-  auto p1_store = [&](int i, const uint4 rw, const uint2 fl, const float (&pa)[NT][8]) {
-    const int r = i / C8, c = (i % C8) * 8;
-    const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
-    const uint32_t fw[2] = {fl.x, fl.y};
-    uint32_t nb = 0;
-    float* trow = tile + r * LD + c;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t rv = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-      const uint32_t pf = (fw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-      bool valid;
-      const int cand = decode_cand(rv, KIND, valid);
-      float pp;
-      if constexpr (NT == 1) pp = pa[0][j];
-      else if constexpr (NT == 2) pp = bsel(cand != 0, pa[1][j], pa[0][j]);
-      else pp = bsel(cand == 0, pa[0][j], bsel(cand == 1, pa[1][j], pa[2][j]));
-      const bool good = valid && (pf & 1u);
-      const bool elig = good && ((pf >> (1 + cand)) & 1u);
-      trow[j] = decode_adu(rv, KIND) - pp;
-      nb |= (uint32_t)(cand | (good ? 4 : 0) | (elig ? 8 : 0)) << (4 * j);
-    }
-    nib[r * C8 + (c >> 3)] = nb;
-  };
-  auto p1_pix = [&](int i) -> int64_t {
-    const int r = i / C8, c = (i % C8) * 8;
-    return base + (int64_t)r * tg.panel_cols + c;
-  };
+  // ---- phase 1: decode + pedestal into LDS ------------------------------------------------
   constexpr int NITEMS = (TR > 0 && TC > 0) ? TR * (TC / 8) : 0;
   constexpr int NI = NITEMS > 0 ? (NITEMS + BLOCK - 1) / BLOCK : 0;
   if constexpr (NI > 0 && NI <= 6) {
-    // compile-time shape: all of this lane's raw / flag loads in flight at once, then all of its
-    // pedestal loads (two dependent round trips per workgroup instead of two per item)
-    // The first candidate table (the unswitched gain: nearly every pixel) is loaded together with
-    // the raw words; only the rare switched candidates wait for the decoded raw (select-then-load).
+    // compile-time shape: all of this lane's raw / plane / first-table loads in flight at once,
+    // then the rare switched-candidate tables (select-then-load), then decode
+    constexpr int C8 = TC / 8;
     uint4 rw[NI];
-    uint2 fl[NI];
+    uint32_t ep[NI];
     float pa[NI][NT][8];
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
       const int i = tid + u * BLOCK;
       if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
-        const int64_t pix = p1_pix(i);
+        const int r = i / C8, c = (i % C8) * 8;
+        const int64_t pix = t.base + (int64_t)r * tg.panel_cols + c;
         rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
-        fl[u] = *reinterpret_cast<const uint2*>(pflags + pix);
-        p1_ped(pix, 1u, pa[u]);
+        ep[u] = load_planes<NT>(planes, pix);
+        load8<NT>(ped, tg.npix, pix, 1u, pa[u]);
       }
     }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
       const int i = tid + u * BLOCK;
-      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) p1_ped(p1_pix(i), p1_need(rw[u]), pa[u], 1);
+      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
+        const int r = i / C8, c = (i % C8) * 8;
+        load8<NT>(ped, tg.npix, t.base + (int64_t)r * tg.panel_cols + c, need_from_raw<NT>(rw[u]), pa[u], 1);
+      }
     }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
       const int i = tid + u * BLOCK;
-      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) p1_store(i, rw[u], fl[u], pa[u]);
+      const bool act = (u + 1) * BLOCK <= NITEMS || i < NITEMS;
+      const int r = act ? i / C8 : 0, k = act ? i % C8 : 0, c = k * 8;
+      float v[8];
+      uint32_t el = 0xFFu, cb = 0;
+      if (act) {
+        cm_decode8<KIND, NT>(rw[u], ep[u], pa[u], v, el, cb);
+        float x[8];
+        cm_tile_values(v, el, x);
+        float* trow = tile + r * P + c;
+        *reinterpret_cast<float4*>(trow) = make_float4(x[0], x[1], x[2], x[3]);
+        *reinterpret_cast<float4*>(trow + 4) = make_float4(x[4], x[5], x[6], x[7]);
+      }
+      const uint32_t slot = side_put(sc, act && el != 0xFFu, v);   // convergent: whole wave
+      if (act) cm_put_meta<NT>(reinterpret_cast<uint8_t*>(tile + r * P + C), C, k, cb, slot);
     }
   } else {
-    for (int i = tid; i < R * C8; i += blockDim.x) {
-      const int64_t pix = p1_pix(i);
-      const uint4 rw = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
-      const uint2 fl = *reinterpret_cast<const uint2*>(pflags + pix);
-      float pa[NT][8];
-      p1_ped(pix, p1_need(rw), pa);
-      p1_store(i, rw, fl, pa);
-    }
+    cm_phase1<KIND, NT>(tile, sc, P, R, C, tg, raw, ped, planes, t.base);
   }
   __syncthreads();
 
   // ---- phase 2a: rows by bank, one lane per segment ----------------------------------------
-  // Non-participating elements are first marked NaN (a per-element select, no bit masks: 64-bit
-  // mask extraction per element pushed the sorts into scratch), then turned into the balanced
-  // -inf / +inf padding by a running counter.
-  const float QNAN = __int_as_float(0x7fc00000);
   if (cp.flags & 1) {
     const int nbank = C / L;
     for (int sgi = tid; sgi < R * nbank; sgi += blockDim.x) {
-      const int b = sgi / R, r = sgi % R;           // consecutive lanes -> consecutive rows: no bank conflicts
-      float* seg = tile + r * LD + b * L;
-      const uint32_t* nrow = nib + r * C8;
-      // L % 8 == 0: the segment's eligibility bits are L/8 whole nibble words, read once and
-      // indexed by compile-time j in both loops below
-      constexpr int NW = (L % 8 == 0) ? L / 8 : 1;
-      uint32_t nw[NW];
-      if constexpr (L % 8 == 0) {
-#pragma unroll
-        for (int k = 0; k < NW; ++k) nw[k] = nrow[(b * L >> 3) + k];
-      }
-      auto elig = [&](int j) -> bool {
-        if constexpr (L % 8 == 0) return (nw[j >> 3] >> (4 * (j & 7) + 3)) & 1u;
-        const int col = b * L + j;
-        return (nrow[col >> 3] >> (4 * (col & 7) + 3)) & 1u;
-      };
+      const int b = sgi / R, r = sgi % R;           // consecutive lanes -> consecutive rows
+      float* seg = tile + r * P + b * L;
       float x[L];
       int cnt = 0;
+      float pad = -INF;
+      if constexpr (L % 4 == 0) {
 #pragma unroll
-      for (int j = 0; j < L; ++j) {
-        const float v = seg[j];
-        const bool el = elig(j);
-        const bool pt = el && (fabsf(v) < cp.thr);
-        cnt += pt ? 1 : 0;
-        x[j] = pt ? v : QNAN;
-      }
-      const int a = (L - cnt) >> 1;
-      int ninv = 0;
+        for (int j = 0; j < L; j += 4) {
+          const float4 q = *reinterpret_cast<const float4*>(seg + j);
+          const float e[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-      for (int j = 0; j < L; ++j) {
-        const bool inv = x[j] != x[j];
-        x[j] = inv ? (ninv < a ? -INF : INF) : x[j];
-        ninv += inv ? 1 : 0;
-      }
-      asm volatile("" ::: "memory");   // keep the write-back's LDS reads below the sort (VGPR pressure)
-      sort_regs<L>(x);
-      asm volatile("" ::: "memory");
-      // numpy median at fixed positions: lower = a + (cnt-1)/2, upper = a + cnt/2, which only
-      // depend on the parity of cnt (L even: L/2-1 | L/2; L odd: (L-1)/2 | (L-3)/2,(L-1)/2)
-      float s_lo, s_hi;
-      if constexpr ((L & 1) == 0) {
-        s_lo = x[L / 2 - 1];
-        s_hi = (cnt & 1) ? x[L / 2 - 1] : x[L / 2];
+          for (int u = 0; u < 4; ++u) {
+            const bool pt = fabsf(e[u]) < cp.thr;
+            cnt += pt ? 1 : 0;
+            x[j + u] = pt ? e[u] : pad;
+            pad = pt ? pad : -pad;
+          }
+        }
       } else {
-        s_lo = (cnt & 1) ? x[(L - 1) / 2] : x[(L - 3) / 2];
-        s_hi = x[(L - 1) / 2];
-      }
-      const float med = (s_lo + s_hi) * 0.5f;
-      if (cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
-        // branch-free: every element is rewritten (v - 0 == v bitwise, -0 and NaN included), so
-        // the 48 per-element exec-mask branches become selects
 #pragma unroll
         for (int j = 0; j < L; ++j) {
-          const float v = seg[j];
-          seg[j] = v - (elig(j) ? med : 0.0f);
+          const float e = seg[j];
+          const bool pt = fabsf(e) < cp.thr;
+          cnt += pt ? 1 : 0;
+          x[j] = pt ? e : pad;
+          pad = pt ? pad : -pad;
+        }
+      }
+      asm volatile("" ::: "memory");   // keep the write-back's LDS reads below the network
+      constexpr int PA = (L & 1) ? (L - 1) / 2 : L / 2 - 1;
+      constexpr int PB = PA + 1;
+      select_regs<L, PA, PB>(x);
+      asm volatile("" ::: "memory");
+      // toggle padding: L even -> odd count: x[L/2], even: mean of x[L/2-1], x[L/2];
+      //                 L odd  -> odd count: x[(L-1)/2], even: mean of x[(L-1)/2], x[(L+1)/2]
+      float med;
+      if constexpr ((L & 1) == 0) med = (cnt & 1) ? x[PB] : (x[PA] + x[PB]) * 0.5f;
+      else med = (cnt & 1) ? x[PA] : (x[PA] + x[PB]) * 0.5f;
+      if (cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
+        // every element minus the median: NaN (non-eligible) stays NaN
+        if constexpr (L % 4 == 0) {
+#pragma unroll
+          for (int j = 0; j < L; j += 4) {
+            float4 q = *reinterpret_cast<const float4*>(seg + j);
+            q.x -= med; q.y -= med; q.z -= med; q.w -= med;
+            *reinterpret_cast<float4*>(seg + j) = q;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < L; ++j) seg[j] -= med;
         }
       }
     }
     __syncthreads();
   }
 
-  // ---- phase 2b (CQ = 4): columns, FOUR lanes (a quad) per column, M rows each ---------------
+  // ---- phase 2b: columns, FOUR lanes (a quad) per column, M rows each ------------------------
   //  each lane sorts its M values (sort_regs<M>); lanes (q, q^1) merge-split (lower lane keeps
   //  min(x[i], partner[M-1-i]), upper the max) and sort the resulting bitonic sequences (the
   //  lower lane negated so both are V-shaped: bitonic_merge_vpad); the two sorted halves of the
   //  pair (0,1) and of the pair (2,3) are then merged by merge-path for k = 2M-1 and 2M with ONE
-  //  quad_perm(3,2,1,0) fetch per register.  Half the registers and half the serial comparator
-  //  chain of the two-lane path; validated by a numpy emulation of the exact lane algorithm.
-  if constexpr (CQ == 4) {
-    if (cp.flags & 2) {
-      const int nwork = 4 * C;
-      for (int w = tid; w < ((nwork + 63) / 64) * 64; w += blockDim.x) {
-        const bool act = w < nwork;
-        const int c = act ? (w >> 2) : 0;
-        const int q = w & 3;
-        const bool lower = (q & 1) == 0;
-        const uint32_t shift = 4 * (c & 7) + 3;
-        // per-lane base addresses; the unrolled i then becomes an immediate LDS offset (i * LD,
-        // i * C8 are constants for compile-time tile shapes)
-        float* colp = tile + (q * M) * LD + c;
-        const uint32_t* nibp = nib + (q * M) * C8 + (c >> 3);
-        float x[M];
-        int my_cnt = 0;
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          const bool in = act && q * M + i < R;
-          const float v = in ? colp[i * LD] : 0.0f;
-          const bool el = in && ((nibp[i * C8] >> shift) & 1u);
-          const bool pt = el && (fabsf(v) < cp.thr);
-          my_cnt += pt ? 1 : 0;
-          x[i] = pt ? v : QNAN;
-          if ((i & 15) == 15) asm volatile("" ::: "memory");
-        }
-        // quad totals + exclusive prefix of the non-participants: balanced +-inf padding
-        const int my_inv = M - my_cnt;
-        const int i0 = dpp_quad_i<0x00>(my_inv), i1 = dpp_quad_i<0x55>(my_inv);
-        const int i2 = dpp_quad_i<0xAA>(my_inv), i3 = dpp_quad_i<0xFF>(my_inv);
-        const int total_inv = i0 + i1 + i2 + i3;
-        const int cnt = 4 * M - total_inv;
-        const int a = total_inv >> 1;
-        const int prefix = (q > 0 ? i0 : 0) + (q > 1 ? i1 : 0) + (q > 2 ? i2 : 0);
-        const int neg_budget = min(my_inv, max(0, a - prefix));
-        int ninv = 0;
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          const bool inv = x[i] != x[i];
-          x[i] = inv ? (ninv < neg_budget ? -INF : INF) : x[i];
-          ninv += inv ? 1 : 0;
-        }
-        asm volatile("" ::: "memory");
-        sort_regs<M>(x);
-        // level 1: merge-split with lane q^1 (partner read reversed)
-        float z[M];
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          const float pv = dpp_quad<0xB1>(x[M - 1 - i]);
-          const float y = lower ? fminf(x[i], pv) : fmaxf(x[i], pv);
-          z[i] = lower ? -y : y;   // both lanes V-shaped
-        }
-        bitonic_merge_vpad<M>(z);
-#pragma unroll
-        for (int i = 0; i < M; ++i) x[i] = lower ? -z[M - 1 - i] : z[i];   // ascending half of the pair
-        asm volatile("" ::: "memory");
-        // level 2: merge-path of pair (0,1) with pair (2,3); lane 0 reads lane 3, lane 1 lane 2
-        float k88 = INF, k87 = INF, plast = INF;
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-          const float pj = dpp_quad<0x1B>(x[j]);
-          k88 = fminf(k88, fmaxf(x[M - 1 - j], pj));
-          if (j <= M - 2) k87 = fminf(k87, fmaxf(x[M - 2 - j], pj));
-          if (j == M - 1) plast = pj;
-        }
-        const float e = dpp_quad<0xAA>(x[M - 1]);   // lane 2's last element
-        const float extra = q == 0 ? fminf(plast, fmaxf(x[M - 1], e)) : x[M - 1];
-        k87 = fminf(k87, extra);
-        k87 = fminf(k87, dpp_quad<0xB1>(k87));
-        k88 = fminf(k88, dpp_quad<0xB1>(k88));
-        const float k_lo = dpp_quad<0x00>(k87), k_hi = dpp_quad<0x00>(k88);   // lane 0 has the answer
-        const float med = (k_lo + ((cnt & 1) ? k_lo : k_hi)) * 0.5f;
-        asm volatile("" ::: "memory");
-        if (act) {   // branch-free per element (v - 0 == v bitwise), as in the row pass
-          const float m = (cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) ? med : 0.0f;
-#pragma unroll
-          for (int i = 0; i < M; ++i) {
-            if (q * M + i < R) {
-              const float v = colp[i * LD];
-              colp[i * LD] = v - (((nibp[i * C8] >> shift) & 1u) ? m : 0.0f);
-            }
-            if ((i & 15) == 15) asm volatile("" ::: "memory");
-          }
-        }
-      }
-      __syncthreads();
-    }
-  } else
-  // ---- phase 2b (CQ = 2): columns, two lanes per column ------------------------------------
+  //  quad_perm(3,2,1,0) fetch per register.
   if (cp.flags & 2) {
-    const int nwork = 2 * C;
+    const int nwork = 4 * C;
     for (int w = tid; w < ((nwork + 63) / 64) * 64; w += blockDim.x) {
-      // whole waves iterate together (the DPP exchange needs both lanes of a pair)
       const bool act = w < nwork;
-      const int c = act ? (w >> 1) : 0;
-      const int h = w & 1;
-      const uint32_t shift = 4 * (c & 7) + 3;
+      const int c = act ? (w >> 2) : 0;
+      const int q = w & 3;
+      const bool lower = (q & 1) == 0;
+      float* colp = tile + (q * M) * P + c;
       float x[M];
       int my_cnt = 0;
 #pragma unroll
       for (int i = 0; i < M; ++i) {
-        const int r = h * M + i;
-        const bool in = act && r < R;
-        const float v = in ? tile[r * LD + c] : 0.0f;
-        const bool el = in && ((nib[r * C8 + (c >> 3)] >> shift) & 1u);
-        const bool pt = el && (fabsf(v) < cp.thr);
+        const bool in = act && q * M + i < R;
+        const float v = in ? colp[i * P] : QNAN;
+        const bool pt = fabsf(v) < cp.thr;
         my_cnt += pt ? 1 : 0;
         x[i] = pt ? v : QNAN;
-        if ((i & 15) == 15) asm volatile("" ::: "memory");   // cap loads in flight (VGPR pressure)
+        if ((i & 15) == 15) asm volatile("" ::: "memory");
       }
-      const int other_cnt = __builtin_amdgcn_update_dpp(0, my_cnt, 0xB1, 0xF, 0xF, false);
-      const int cnt = my_cnt + other_cnt;
-      const int a = (2 * M - cnt) >> 1;
-      const int my_inv = M - my_cnt, other_inv = M - other_cnt;
-      // the even lane owns the first non-participating elements of the column
-      const int neg_budget = h == 0 ? min(my_inv, a) : max(0, a - other_inv);
+      // quad totals + exclusive prefix of the non-participants: balanced +-inf padding
+      const int my_inv = M - my_cnt;
+      const int i0 = dpp_quad_i<0x00>(my_inv), i1 = dpp_quad_i<0x55>(my_inv);
+      const int i2 = dpp_quad_i<0xAA>(my_inv), i3 = dpp_quad_i<0xFF>(my_inv);
+      const int total_inv = i0 + i1 + i2 + i3;
+      const int cnt = 4 * M - total_inv;
+      const int a = total_inv >> 1;
+      const int prefix = (q > 0 ? i0 : 0) + (q > 1 ? i1 : 0) + (q > 2 ? i2 : 0);
+      const int neg_budget = min(my_inv, max(0, a - prefix));
       int ninv = 0;
 #pragma unroll
       for (int i = 0; i < M; ++i) {
@@ -777,22 +815,39 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
       }
       asm volatile("" ::: "memory");
       sort_regs<M>(x);
+      // level 1: merge-split with lane q^1 (partner read reversed)
+      float z[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const float pv = dpp_quad<0xB1>(x[M - 1 - i]);
+        const float y = lower ? fminf(x[i], pv) : fmaxf(x[i], pv);
+        z[i] = lower ? -y : y;   // both lanes V-shaped
+      }
+      bitonic_merge_vpad<M>(z);
+#pragma unroll
+      for (int i = 0; i < M; ++i) x[i] = lower ? -z[M - 1 - i] : z[i];   // ascending half of the pair
       asm volatile("" ::: "memory");
-      // merge-path k-th of the union for k = M-1 and k = M (both lanes compute both)
-      float k_lo = fminf(x[M - 1], dpp_xor1(x[M - 1]));   // i = M and i = 0 terms
-      float k_hi = __int_as_float(0x7f800000);
+      // level 2: merge-path of pair (0,1) with pair (2,3); lane 0 reads lane 3, lane 1 lane 2
+      float kh = INF, kl = INF, plast = INF;
 #pragma unroll
-      for (int i = 1; i < M; ++i) k_lo = fminf(k_lo, fmaxf(x[i - 1], dpp_xor1(x[M - 1 - i])));
-#pragma unroll
-      for (int i = 1; i <= M; ++i) k_hi = fminf(k_hi, fmaxf(x[i - 1], dpp_xor1(x[M - i])));
-      // 2M slots: lower median at M-1; upper at M (even count) or M-1 (odd count)
+      for (int j = 0; j < M; ++j) {
+        const float pj = dpp_quad<0x1B>(x[j]);
+        kh = fminf(kh, fmaxf(x[M - 1 - j], pj));
+        if (j <= M - 2) kl = fminf(kl, fmaxf(x[M - 2 - j], pj));
+        if (j == M - 1) plast = pj;
+      }
+      const float e = dpp_quad<0xAA>(x[M - 1]);   // lane 2's last element
+      const float extra = q == 0 ? fminf(plast, fmaxf(x[M - 1], e)) : x[M - 1];
+      kl = fminf(kl, extra);
+      kl = fminf(kl, dpp_quad<0xB1>(kl));
+      kh = fminf(kh, dpp_quad<0xB1>(kh));
+      const float k_lo = dpp_quad<0x00>(kl), k_hi = dpp_quad<0x00>(kh);   // lane 0 has the answer
       const float med = (k_lo + ((cnt & 1) ? k_lo : k_hi)) * 0.5f;
       asm volatile("" ::: "memory");
       if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
 #pragma unroll
         for (int i = 0; i < M; ++i) {
-          const int r = h * M + i;
-          if (r < R && ((nib[r * C8 + (c >> 3)] >> shift) & 1u)) tile[r * LD + c] -= med;
+          if (q * M + i < R) colp[i * P] -= med;   // NaN (non-eligible) stays NaN
           if ((i & 15) == 15) asm volatile("" ::: "memory");
         }
       }
@@ -801,36 +856,74 @@ __global__ __launch_bounds__(BLOCK, CQ == 4 ? (M <= 48 ? 4 : 2) : 512 / BLOCK) v
   }
 
   // ---- phase 3: gain factor + mask, store ---------------------------------------------------
-  cm_store<NT>(tile, nib, gf, tg, R, C, base, out, io, panel, ar * R, ac * C, cp.gather != 0);
+  if constexpr (NI > 0 && NI <= 6) {
+    // compile-time shape: every gain-factor load of this lane in flight before the first use
+    constexpr int C8 = TC / 8;
+    const bool img = io.desc != nullptr;
+    // (the first gain table of every item up front; the switched-gain tables are rare and are
+    // loaded per item, which keeps the production kernel within 128 VGPRs)
+    uint32_t cbs[NI], slots[NI];
+    float g0[NI][1][8];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = tid + u * BLOCK;
+      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
+        const int r = i / C8, k = i % C8, c = k * 8;
+        cm_get_meta<NT>(reinterpret_cast<const uint8_t*>(tile + r * P + C), C, k, cbs[u], slots[u]);
+        load8<1>(gf, tg.npix, t.base + (int64_t)r * tg.panel_cols + c, 1u, g0[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = tid + u * BLOCK;
+      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
+        const int r = i / C8, c = (i % C8) * 8;
+        const int64_t pix = t.base + (int64_t)r * tg.panel_cols + c;
+        float ga[NT][8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ga[0][j] = g0[u][0][j];
+        if constexpr (NT > 1) load8<NT>(gf, tg.npix, pix, cm_need<NT>(cbs[u]), ga, 1);
+        float o[8];
+        cm_out8<KIND, NT>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, ped, tg.npix, pix, o);
+        cm_emit(tile + r * P + c, out, pix, img, o);
+      }
+    }
+    if (img) cm_place(tile, P, R, C, io, t.panel, t.ar * R, t.ac * C, out);
+  } else {
+    cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.panel, t.ar * R, t.ac * C);
+  }
 }
 
-// PSANA_RAY_CM_GENERIC=1 forces the generic wave-bitonic kernel (A/B benchmarking, read per launch)
-static bool cm_force_generic() {
-  const char* e = getenv("PSANA_RAY_CM_GENERIC");
-  return e != nullptr && e[0] == '1';
-}
-
-size_t cm_lds_bytes(int asic_rows, int asic_cols) {
-  const size_t tile = (((size_t)asic_rows * (asic_cols + 1) * 4) + 15) & ~(size_t)15;
-  return tile + (size_t)asic_rows * (asic_cols / 8) * 4;
+size_t cm_lds_bytes(int asic_rows, int asic_cols, int kind) {
+  const int cand_bits = kind == kJungfrau ? 2 : 1;
+  return (size_t)asic_rows * cm_pitch(asic_cols, cand_bits) * 4;
 }
 
 // Width of the LDS tile a workgroup owns.  Row medians are per bank segment and column medians
 // need whole columns, so an ASIC may be cut into full-height stripes whose width is a multiple
-// of the bank width without changing any median (Jungfrau: 256x256 ASIC = 289 KB > 160 KiB ->
-// two 256x128 stripes of 145 KB).  0 = no stripe fits.
-int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols, int max_cols) {
+// of the bank width without changing any median (Jungfrau: 256x256 ASIC -> two 256x128 stripes).
+// 0 = no stripe fits.
+int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols, int max_cols, int kind) {
   for (int w = std::min(asic_cols, max_cols > 0 ? max_cols : asic_cols); w >= bank_cols; --w) {
     if (asic_cols % w || w % bank_cols || w % 8) continue;
-    if (cm_lds_bytes(asic_rows, w) <= 160 * 1024) return w;
+    if (cm_lds_bytes(asic_rows, w, kind) <= 160 * 1024) return w;
   }
   return 0;
 }
 
-void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t pflags,
-                     int kind, int n_panels, int panel_rows, int panel_cols, int asic_rows,
-                     int asic_cols, float thr, float maxcorr, int npix_min, int flags,
-                     int bank_cols, uint64_t stream, uint64_t img_desc, uint64_t img_omask) {
+template <typename K>
+static void cm_launch(K kernel, dim3 grid, int block, size_t lds, hipStream_t s, const FramePtrs& fp,
+                      const float* P, const float* G, const uint8_t* F, const TileGeom& tg, const CmParams& cp,
+                      const ImgOut& io) {
+  hip_check(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+            "cm attr");
+  hipLaunchKernelGGL(kernel, grid, dim3(block), lds, s, fp, P, G, F, tg, cp, io);
+}
+
+void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t planes, int kind,
+                     int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
+                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream, uint64_t img_desc,
+                     uint64_t img_omask) {
   check(nframes >= 1 && nframes <= kMaxFrames, "calib_cm: nframes out of range");
   check(asic_rows >= 1 && asic_rows <= 256, "calib_cm: ASIC rows must be in [1, 256]");
   check(asic_cols % 8 == 0 && asic_cols >= 8, "calib_cm: ASIC cols must be a multiple of 8");
@@ -838,41 +931,45 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   check(bank_cols >= 1 && bank_cols <= 64 && asic_cols % bank_cols == 0,
         "calib_cm: bank_cols must be <= 64 and divide the ASIC width");
   check(panel_cols % 8 == 0, "calib_cm: panel cols must be a multiple of 8");
-  // stripe width: PSANA_RAY_CM_STRIPE caps it (A/B); a stripe of <= 128 columns runs 256-thread
-  // workgroups, two of which fit one CU (LDS <= 80 KB each), so one block's HBM phases overlap
-  // the other's sorts (one 512-thread block per CU cannot overlap anything)
-  // Default: the widest stripe <= 128 columns whose tile fits half the LDS, when a sort-network
-  // instantiation exists for it (epix10k2M: 176x96 stripes, 15.29 vs 15.82 us/frame full width,
-  // 48 columns 22.8; profiles/kernels_r1_cm_stripes.jsonl).
-  const int Mh = (asic_rows + 1) / 2;
-  const bool net256 = !cm_force_generic() &&
-      ((kind == kEpix10ka && bank_cols == 48 && Mh == 88) || (kind == kEpix10ka && bank_cols == 8 && Mh == 8) ||
-       (kind == kPlain && bank_cols == 32 && Mh == 64) || (kind == kPlain && bank_cols == 8 && Mh == 4));
+  check(kind == kEpix10ka || kind == kJungfrau || kind == kPlain, "calib_cm: unknown gain kind");
+  // Tile shape (one decision per shape, no run-time knobs):
+  //  * epix10k2M (176-row ASICs, 48-column banks): one-bank 176x48 stripes on 256-thread blocks,
+  //    four workgroups per CU (round 1: 8.8 us/frame vs 9.2 for 176x96, 15.8 full width);
+  //  * Jungfrau (256x256 ASICs, 64-column banks): 256x128 stripes, 512-thread blocks;
+  //  * otherwise: the widest stripe <= 128 columns whose tile fits half the LDS (two blocks per CU)
+  //    when a compile-time network exists for the shape, else the widest that fits at all.
+  const int M4 = (asic_rows + 3) / 4;
+  const bool epix_prod = kind == kEpix10ka && bank_cols == 48 && asic_rows == 176 && asic_cols % 48 == 0;
+  const bool jf_prod = kind == kJungfrau && bank_cols == 64 && asic_rows == 256 && asic_cols % 128 == 0;
+  const bool net = epix_prod || jf_prod || (kind == kEpix10ka && bank_cols == 48 && M4 == 44) ||
+                   (kind == kEpix10ka && bank_cols == 8 && M4 == 4);
   int max_w = 0;
-  if (net256) {
+  if (epix_prod) {
+    max_w = 48;
+  } else if (jf_prod) {
+    max_w = 128;
+  } else if (net) {
     for (int w = std::min(asic_cols, 128); w >= bank_cols; --w)
-      if (asic_cols % w == 0 && w % bank_cols == 0 && w % 8 == 0 && cm_lds_bytes(asic_rows, w) <= 80 * 1024) {
+      if (asic_cols % w == 0 && w % bank_cols == 0 && w % 8 == 0 && cm_lds_bytes(asic_rows, w, kind) <= 80 * 1024) {
         max_w = w;
         break;
       }
   }
-  // PSANA_RAY_CM_CONSTDIMS=0 skips the compile-time-shape instantiations (A/B)
-  const char* cd = getenv("PSANA_RAY_CM_CONSTDIMS");
-  const bool const_dims = !(cd != nullptr && cd[0] == '0');
-  // epix10k2M with the compile-time kernels: one-bank 176x48 stripes on 256-thread blocks, four
-  // per CU (8.78 vs 9.16 us/frame for 176x96; profiles/kernels_r1_cm_stripes48.jsonl)
-  if (const_dims && kind == kEpix10ka && bank_cols == 48 && asic_rows == 176 && asic_cols % 48 == 0) max_w = 48;
-  if (const char* e = getenv("PSANA_RAY_CM_STRIPE"); e && *e) max_w = std::max(0, atoi(e));   // 0: full width
   const int full_cols = asic_cols;
-  asic_cols = cm_tile_cols(asic_rows, full_cols, bank_cols, max_w);
-  if (asic_cols == 0) asic_cols = cm_tile_cols(asic_rows, full_cols, bank_cols, 0);
+  asic_cols = cm_tile_cols(asic_rows, full_cols, bank_cols, max_w, kind);
+  if (asic_cols == 0) asic_cols = cm_tile_cols(asic_rows, full_cols, bank_cols, 0, kind);
   check(asic_cols > 0, "calib_cm: no full-height ASIC stripe fits in 160 KiB of LDS");
-  const size_t lds = cm_lds_bytes(asic_rows, asic_cols);
-  check(aligned16(ped) && aligned16(gf) && (pflags & 7) == 0, "calib_cm: misaligned constant tables");
+  const size_t lds = cm_lds_bytes(asic_rows, asic_cols, kind);
+  check(aligned16(ped) && aligned16(gf) && (planes & 3) == 0, "calib_cm: misaligned constant tables");
   for (int f = 0; f < nframes; ++f)
     check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_cm: frame buffers must be 16-B aligned");
   const ImgOut io{reinterpret_cast<const int32_t*>(img_desc), reinterpret_cast<const uint8_t*>(img_omask)};
   check(img_omask == 0 || img_desc != 0, "calib_cm: an image mask needs the image output map");
+  // LDS budget of one workgroup: the epix10k2M 176x48 stripe runs four workgroups per CU, the
+  // narrow compile-time kernels two, everything else one; what the tile leaves is side slots
+  const size_t budget = (epix_prod && asic_cols == 48) ? 40 * 1024 : (net && !jf_prod && asic_cols <= 128) ? 80 * 1024
+                                                                                                              : 160 * 1024;
+  const int side_slots = (int)std::min<size_t>(kMaxSideSlots, lds < budget ? (budget - lds) / 32 : 0);
   TileGeom tg;
   tg.panel_rows = panel_rows;
   tg.panel_cols = panel_cols;
@@ -881,83 +978,32 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   tg.asics_per_col = panel_rows / asic_rows;
   tg.asics_per_row = panel_cols / asic_cols;
   tg.npix = (int64_t)n_panels * panel_rows * panel_cols;
-  CmParams cp{thr, maxcorr, npix_min, flags, bank_cols, 1};
-  if (const char* e = getenv("PSANA_RAY_CM_GATHER"); e && *e) cp.gather = atoi(e) != 0;   // A/B
   tg.nframes = nframes;
-  {
-    // XCD-aware placement is OFF by default: measured slower (sort nets 17.4 vs 15.8 us/frame,
-    // memory phases alone 6.5 vs 4.9; profiles/kernels_r1_cm_swizzle.jsonl) -- the per-ASIC tables
-    // are already cache-served under round-robin placement.  PSANA_RAY_CM_SWZ=1 turns it on (A/B).
-    const char* e = getenv("PSANA_RAY_CM_SWZ");
-    tg.swizzle = (e != nullptr && e[0] == '1') ? 1 : 0;
-  }
+  tg.side_slots = side_slots;
+  tg.pitch = cm_pitch(asic_cols, kind == kJungfrau ? 2 : 1);
+  const CmParams cp{thr, maxcorr, npix_min, flags, bank_cols};
   const dim3 grid((unsigned)(n_panels * tg.asics_per_col * tg.asics_per_row * nframes));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float* P = reinterpret_cast<const float*>(ped);
   const float* G = reinterpret_cast<const float*>(gf);
-  const uint8_t* F = reinterpret_cast<const uint8_t*>(pflags);
-  const int M = (asic_rows + 1) / 2;
-  bool done = false;
-  const bool narrow = asic_cols <= 128;   // 2 lanes per column fit a 256-thread block
-  // lanes per column: 4 (quad merge, <= 128 VGPRs, 4 waves/SIMD) unless PSANA_RAY_CM_COLQ=2 (A/B)
-  int cq_req = 0;
-  if (const char* e = getenv("PSANA_RAY_CM_COLQ"); e && *e) cq_req = atoi(e);
-  const int M2 = (asic_rows + 1) / 2, M4 = (asic_rows + 3) / 4;
-#define PR_CM_NET_T(KIND_, L_, M_, B_, CQ_, TR_, TC_)                                                   \
-  if (!done && kind == KIND_ && bank_cols == L_ && (CQ_ == 4 ? M4 : M2) == M_ &&                        \
-      (cq_req == 0 || cq_req == CQ_) && B_ == (narrow ? 256 : 512) * (CQ_ / 2) && !cm_force_generic() && \
-      ((TR_ == 0 && TC_ == 0) || (const_dims && TR_ == asic_rows && TC_ == asic_cols))) {               \
-    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_, TR_, TC_>,   \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");   \
-    hipLaunchKernelGGL((calib_cm_net_kernel<KIND_, L_, M_, B_, CQ_, TR_, TC_>), grid, dim3(B_), lds, s, fp, P, G, \
-                       F, tg, cp, io);                                                                \
-    done = true;                                                                                      \
-  }
-#define PR_CM_NET(KIND_, L_, M_, B_, CQ_) PR_CM_NET_T(KIND_, L_, M_, B_, CQ_, 0, 0)
-  // epix10k2M 176x48 stripes (PSANA_RAY_CM_STRIPE=48): 256-thread blocks (176 row segments,
-  // 192 column lanes), 38.7 KB LDS -> four workgroups per CU
-  if (!done && const_dims && !cm_force_generic() && (cq_req == 0 || cq_req == 4) && kind == kEpix10ka &&
-      bank_cols == 48 && asic_rows == 176 && asic_cols == 48) {
-    // (192-thread blocks measured slower: 9.45 vs 8.82 us/frame; profiles/kernels_r1_cm_b48.jsonl)
-    hip_check(hipFuncSetAttribute((const void*)calib_cm_net_kernel<kEpix10ka, 48, 44, 256, 4, 176, 48>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
-    hipLaunchKernelGGL((calib_cm_net_kernel<kEpix10ka, 48, 44, 256, 4, 176, 48>), grid, dim3(256), lds, s, fp, P, G,
-                       F, tg, cp, io);
-    done = true;
-  }
-  PR_CM_NET_T(kEpix10ka, 48, 44, 512, 4, 176, 96)    // epix10k2M: 176x96 stripes
-  PR_CM_NET_T(kJungfrau, 64, 64, 512, 4, 256, 128)   // Jungfrau: 256x128 stripes
-  PR_CM_NET(kEpix10ka, 48, 44, 512, 4)
-  PR_CM_NET(kEpix10ka, 48, 44, 1024, 4)
-  PR_CM_NET(kEpix10ka, 48, 88, 512, 2)
-  PR_CM_NET(kEpix10ka, 48, 88, 256, 2)
-  PR_CM_NET(kEpix10ka, 8, 4, 512, 4)
-  PR_CM_NET(kEpix10ka, 8, 8, 256, 2)
-  PR_CM_NET(kJungfrau, 64, 64, 512, 4)
-  PR_CM_NET(kPlain, 32, 32, 512, 4)
-  PR_CM_NET(kPlain, 32, 64, 256, 2)
-  PR_CM_NET(kPlain, 8, 4, 256, 2)
-#undef PR_CM_NET
-#undef PR_CM_NET_T
-  if (!done) {
-  switch (kind) {
-    case kEpix10ka:
-      hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kEpix10ka>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
-      hipLaunchKernelGGL(calib_cm_kernel<kEpix10ka>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp, io);
-      break;
-    case kJungfrau:
-      hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kJungfrau>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
-      hipLaunchKernelGGL(calib_cm_kernel<kJungfrau>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp, io);
-      break;
-    case kPlain:
-      hip_check(hipFuncSetAttribute((const void*)calib_cm_kernel<kPlain>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "cm attr");
-      hipLaunchKernelGGL(calib_cm_kernel<kPlain>, grid, dim3(1024), lds, s, fp, P, G, F, tg, cp, io);
-      break;
-    default: check(false, "calib_cm: unknown gain kind");
-  }
+  const uint8_t* F = reinterpret_cast<const uint8_t*>(planes);
+  const bool narrow = asic_cols <= 128;
+  const size_t lds_all = lds + 32 * (size_t)side_slots;
+  if (epix_prod && asic_cols == 48) {
+    cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, 256, 176, 48>, grid, 256, lds_all, s, fp, P, G, F, tg, cp, io);
+  } else if (jf_prod && asic_cols == 128) {
+    cm_launch(calib_cm_net_kernel<kJungfrau, 64, 64, 512, 256, 128>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
+  } else if (kind == kEpix10ka && bank_cols == 48 && M4 == 44) {
+    if (narrow) cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, 512>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
+    else cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, 1024>, grid, 1024, lds_all, s, fp, P, G, F, tg, cp, io);
+  } else if (kind == kEpix10ka && bank_cols == 8 && M4 == 4 && narrow) {
+    cm_launch(calib_cm_net_kernel<kEpix10ka, 8, 4, 512>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
+  } else if (kind == kEpix10ka) {
+    cm_launch(calib_cm_kernel<kEpix10ka>, grid, 1024, lds_all, s, fp, P, G, F, tg, cp, io);
+  } else if (kind == kJungfrau) {
+    cm_launch(calib_cm_kernel<kJungfrau>, grid, 1024, lds_all, s, fp, P, G, F, tg, cp, io);
+  } else {
+    cm_launch(calib_cm_kernel<kPlain>, grid, 1024, lds_all, s, fp, P, G, F, tg, cp, io);
   }
   hip_check(hipGetLastError(), "calib_cm launch");
 }

@@ -36,7 +36,7 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
         launch_calib_basic(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.npix, p.kind, stream);
         break;
       case kPlanCalibCm:
-        launch_calib_cm(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.pflags, p.kind, p.n_panels, p.panel_rows,
+        launch_calib_cm(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.elig, p.kind, p.n_panels, p.panel_rows,
                         p.panel_cols, p.asic_rows, p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags,
                         p.bank_cols, stream);
         break;
@@ -50,7 +50,7 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
       case kPlanImageCm: {
         check(p.use_cm && p.img_desc != 0, "run_calib_plan: fused image plan without common mode / placement");
         const FramePtrs fp = ptrs_of(in, out, a, b);
-        launch_calib_cm(fp, n, p.ped, p.gf, p.pflags, p.kind, p.n_panels, p.panel_rows, p.panel_cols, p.asic_rows,
+        launch_calib_cm(fp, n, p.ped, p.gf, p.elig, p.kind, p.n_panels, p.panel_rows, p.panel_cols, p.asic_rows,
                         p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags, p.bank_cols, stream, p.img_desc,
                         p.omask);
         launch_fill_runs(fp, n, p.gap_runs, p.n_gap_runs, stream);
@@ -62,7 +62,7 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
         for (int i = 0; i < n; ++i) tmp[i] = p.scratch + (uint64_t)i * (uint64_t)p.npix * 4u;
         std::vector<uint64_t> ina(in.begin() + a, in.begin() + b), outa(out.begin() + a, out.begin() + b);
         if (p.use_cm)
-          launch_calib_cm(ptrs_of(ina, tmp, 0, n), n, p.ped, p.gf, p.pflags, p.kind, p.n_panels, p.panel_rows,
+          launch_calib_cm(ptrs_of(ina, tmp, 0, n), n, p.ped, p.gf, p.elig, p.kind, p.n_panels, p.panel_rows,
                           p.panel_cols, p.asic_rows, p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags,
                           p.bank_cols, stream);
         else

@@ -35,7 +35,7 @@ struct CalibPlan {
   int mode = kPlanCalib;
   int kind = 0;
   int64_t npix = 0;
-  uint64_t ped = 0, gf = 0, pflags = 0;
+  uint64_t ped = 0, gf = 0, elig = 0;
   int n_panels = 0, panel_rows = 0, panel_cols = 0, asic_rows = 0, asic_cols = 0;
   float thr = 0, maxcorr = 0;
   int npix_min = 0, cm_flags = 0, bank_cols = 0;

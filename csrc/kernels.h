@@ -11,18 +11,18 @@ void launch_calib_basic(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t
                         uint64_t stream);
 void launch_calib_image(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, int64_t npix, int kind,
                         uint64_t idx, int64_t nout, uint64_t stream);
-void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t pflags, int kind,
+void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t elig, int kind,
                      int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
                      float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream,
                      uint64_t img_desc = 0, uint64_t img_omask = 0);   // img_desc: fused K-05 (ImgOut)
-size_t cm_lds_bytes(int asic_rows, int asic_cols);
+size_t cm_lds_bytes(int asic_rows, int asic_cols, int kind);
 void launch_image_tiles(const FramePtrs& fp, int nframes, bool calib, int kind, uint64_t ped, uint64_t gf,
                         int64_t npix, int panel_rows, int panel_cols, uint64_t tiles, int n_tiles, int tiles_x,
                         uint64_t codes, int img_h, int img_w, uint64_t stream);
 int image_tile_h();
 int image_tile_w();
 int image_tile_stage();
-int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols, int max_cols = 0);
+int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols, int max_cols, int kind);
 void launch_convert_u16_f32(const FramePtrs& fp, int nframes, int64_t npix, uint64_t stream);
 void launch_read_f32(const FramePtrs& fp, int nframes, int64_t npix, int k, bool nt, uint64_t sums, uint64_t stream);
 void launch_xor_selftest(uint64_t out, uint64_t stream);

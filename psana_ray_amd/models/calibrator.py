@@ -59,13 +59,13 @@ class Calibrator:
         self.image_mask = image_mask
 
         self._gpu = self.device.type == "cuda"
-        ped, gf, pflags = consts.device_tables(frame_mask)
+        ped, gf, elig = consts.device_tables(frame_mask)
         self.plan = None
         if self._gpu:
             C = kernels._ext.load()  # fail loudly on a GPU box without the extension
             self.ped = torch.from_numpy(ped).to(self.device)
             self.gf = torch.from_numpy(gf).to(self.device)
-            self.pflags = torch.from_numpy(pflags).to(self.device)
+            self.elig = torch.from_numpy(elig).to(self.device)
             self.idx = None
             self.omask = None
             self.tile_map = None
@@ -82,7 +82,7 @@ class Calibrator:
                 self.omask = None if image_mask is None else \
                     torch.from_numpy(np.asarray(image_mask).astype(np.uint8).ravel()).to(self.device)
             if self.cm is not None:
-                if C.cm_tile_cols(spec.asic_rows, spec.asic_cols, int(self.cm.bank_cols)) == 0:
+                if C.cm_tile_cols(spec.asic_rows, spec.asic_cols, int(self.cm.bank_cols), 0, spec.kernel_kind) == 0:
                     raise ValueError(f"common mode: no full-height stripe of the {spec.asic_rows}x{spec.asic_cols} "
                                      f"ASIC (bank {self.cm.bank_cols}) fits in 160 KiB of LDS")
             self.plan = self._make_plan(C)
@@ -135,7 +135,7 @@ class Calibrator:
         p = C.CalibPlan()
         p.kind = spec.kernel_kind
         p.npix = spec.npix
-        p.ped, p.gf, p.pflags = int(self.ped.data_ptr()), int(self.gf.data_ptr()), int(self.pflags.data_ptr())
+        p.ped, p.gf, p.elig = int(self.ped.data_ptr()), int(self.gf.data_ptr()), int(self.elig.data_ptr())
         p.n_panels, p.panel_rows, p.panel_cols = spec.n_panels, spec.panel_rows, spec.panel_cols
         p.asic_rows, p.asic_cols = spec.asic_rows, spec.asic_cols
         p.raw_frame_bytes = spec.raw_frame_bytes

@@ -100,7 +100,10 @@ class CalibConstants:
         return np.zeros((1, *s.frame_shape), np.int64)
 
     def device_tables(self, mask: Optional[np.ndarray] = None):
-        """Kernel tables: ``ped [NC, npix]``, ``gf [NC, npix]`` (mask folded), ``pflags [npix]``.
+        """Kernel tables: ``ped [NC, npix]``, ``gf [NC, npix]`` (mask folded) and the common-mode
+        eligibility bit-planes ``elig [npix / 8, S]`` (uint8, S = 1, 2 or 4 for 1, 2 or 3 candidate
+        tables): bit j of byte k of group g is set when pixel 8g + j is CM-eligible (kept, status
+        good, gain in the CM set) if it decodes to candidate k (csrc/common_mode.hip cm_decode8).
 
         ``mask`` is the combined output mask (bad-pixel & manual, truthy = keep) in frame shape;
         None keeps every pixel (the reference applies masks only when asked, producer.py:92-95).
@@ -113,13 +116,18 @@ class CalibConstants:
         keep = np.broadcast_to(keep, s.frame_shape)
         gf = np.where(keep[None], np.float32(1.0) / gain, np.float32(0.0)).astype(np.float32)
         status_good = self.status == 0
-        flags = keep.astype(np.uint8).copy()
         cm_set = np.zeros(max(s.n_gains, 1), bool)
         cm_set[list(self.cm_gains)] = True
-        for c in range(cand.shape[0]):
-            elig = keep & status_good & cm_set[cand[c]]
-            flags |= (elig.astype(np.uint8) << (1 + c))
         npix = s.npix
+        if npix % 8:
+            raise ValueError("common-mode tables need a multiple of 8 pixels per frame")
+        nc = cand.shape[0]
+        stride = {1: 1, 2: 2, 3: 4}[nc]
+        planes = np.zeros((npix // 8, stride), np.uint8)
+        weights = (1 << np.arange(8)).astype(np.uint16)
+        for c in range(nc):
+            elig = (keep & status_good & cm_set[cand[c]]).reshape(npix // 8, 8)
+            planes[:, c] = (elig.astype(np.uint16) * weights).sum(axis=1).astype(np.uint8)
         return (np.ascontiguousarray(ped.reshape(-1, npix)),
                 np.ascontiguousarray(gf.reshape(-1, npix)),
-                np.ascontiguousarray(flags.reshape(npix)))
+                np.ascontiguousarray(planes.reshape(-1)))

@@ -79,21 +79,23 @@ def calib_image(raw, out, ped, gf, kind, idx: torch.Tensor, stream=None):
                       _ptr(idx), nout, s)
 
 
-def calib_cm(raw, out, ped, gf, pflags, kind, spec, cm, stream=None):
+def calib_cm(raw, out, ped, gf, elig, kind, spec, cm, stream=None):
     C = _ext.load()
     npix = ped.shape[1]
     dev = ped.device
     _check_frames(raw, torch.uint16, npix, dev, "calib_cm raw")
     _check_frames(out, torch.float32, npix, dev, "calib_cm out")
-    if pflags.dtype != torch.uint8 or pflags.numel() != npix:
-        raise ValueError("calib_cm: pflags must be uint8[npix]")
+    stride = {1: 1, 2: 2, 3: 4}[ped.shape[0]]
+    if elig.dtype != torch.uint8 or elig.numel() != (npix // 8) * stride:
+        raise ValueError("calib_cm: elig must be the uint8 eligibility bit-planes [npix / 8, stride] "
+                         "(CalibConstants.device_tables)")
     bank = cm.bank_cols or spec.bank_cols
-    if C.cm_tile_cols(spec.asic_rows, spec.asic_cols, int(bank)) == 0:
+    if C.cm_tile_cols(spec.asic_rows, spec.asic_cols, int(bank), 0, int(kind)) == 0:
         raise ValueError(f"common mode: no full-height stripe of the {spec.asic_rows}x{spec.asic_cols} ASIC "
                          f"(bank {bank}) fits in 160 KiB of LDS")
     s = _ext.stream_handle(stream)
     for a, b in _chunks(len(raw)):
-        C.calib_cm([_ptr(t) for t in raw[a:b]], [_ptr(t) for t in out[a:b]], _ptr(ped), _ptr(gf), _ptr(pflags), kind,
+        C.calib_cm([_ptr(t) for t in raw[a:b]], [_ptr(t) for t in out[a:b]], _ptr(ped), _ptr(gf), _ptr(elig), kind,
                    spec.n_panels, spec.panel_rows, spec.panel_cols, spec.asic_rows, spec.asic_cols,
                    float(cm.thr), float(cm.maxcorr), int(cm.npix_min), int(cm.flags), int(bank), s)
 
