@@ -100,186 +100,56 @@ def main(argv=None):
     cal = Calibrator(src.consts, dev, Mode.calib)
     if want("calib_basic"):
         report("calib_basic", timeit(lambda: cal.run(rl, ol), a.iters), F * npix * 6)
-    if want("calib_basic_ab"):
-        import os
+    if want("calib_basic"):
         C = _ext.load()
         rp = [int(t.data_ptr()) for t in rl]
         op = [int(t.data_ptr()) for t in ol]
-        for rnd in range(2):
-            report(f"convert_u16_f32 (bandwidth reference) r{rnd}",
-                   timeit(lambda: C.convert_u16_f32(rp, op, npix, _ext.stream_handle()), a.iters), F * npix * 6)
-            for lay in ("8", "4"):
-                for fpb in (32, 8):
-                    os.environ["PSANA_RAY_CALIB_FPB"] = str(fpb)
-                    os.environ["PSANA_RAY_CALIB_LAYOUT"] = lay
-                    report(f"calib_basic(layout={lay}px,fpb={fpb}) r{rnd}", timeit(lambda: cal.run(rl, ol), a.iters),
-                           F * npix * 6)
-        os.environ.pop("PSANA_RAY_CALIB_FPB", None)
-        os.environ.pop("PSANA_RAY_CALIB_LAYOUT", None)
-    if want("calib_cm_ab"):
-        import os
-        calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
-        calmem = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams(flags=0))
-        for rnd in range(2):
-            for gather in ("0", "1"):
-                os.environ["PSANA_RAY_CM_GATHER"] = gather
-                report(f"calib_cm(default, select-then-load={gather}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
-                       F * npix * 6)
-                report(f"calib_cm(memory phases only, select-then-load={gather}) r{rnd}",
-                       timeit(lambda: calmem.run(rl, ol), a.iters), F * npix * 6)
-        os.environ.pop("PSANA_RAY_CM_GATHER", None)
-        for rnd in range(2):
-            for colq in ("2", "4"):
-                for stripe in ("192", "96", "48"):
-                    os.environ["PSANA_RAY_CM_STRIPE"] = stripe
-                    os.environ["PSANA_RAY_CM_COLQ"] = colq
-                    report(f"calib_cm(sort networks, {colq} lanes/column, stripe={stripe}) r{rnd}",
-                           timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
-        os.environ.pop("PSANA_RAY_CM_STRIPE", None)
-        os.environ.pop("PSANA_RAY_CM_COLQ", None)
-        for rnd in range(2):   # interleaved A/B in one process (methodology rule 24)
-            for swz in ("1", "0"):
-                os.environ["PSANA_RAY_CM_SWZ"] = swz
-                os.environ["PSANA_RAY_CM_GENERIC"] = "0"
-                report(f"calib_cm(sort networks, xcd_swizzle={swz}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
-                       F * npix * 6)
-                report(f"calib_cm(memory phases only: flags=0, xcd_swizzle={swz}) r{rnd}",
-                       timeit(lambda: calmem.run(rl, ol), a.iters), F * npix * 6)
-                os.environ["PSANA_RAY_CM_GENERIC"] = "1"
-                report(f"calib_cm(generic bitonic, xcd_swizzle={swz}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
-                       F * npix * 6)
-        os.environ.pop("PSANA_RAY_CM_GENERIC", None)
-        os.environ.pop("PSANA_RAY_CM_SWZ", None)
-    if want("calib_cm"):
-        calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
-        report("calib_cm(rows+cols)", timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
-        calr = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams(flags=1))
-        report("calib_cm(rows)", timeit(lambda: calr.run(rl, ol), a.iters), F * npix * 6)
-        calc = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams(flags=2))
-        report("calib_cm(cols)", timeit(lambda: calc.run(rl, ol), a.iters), F * npix * 6)
-    if want("calib_cm_constdims"):
-        # compile-time tile shape (immediate LDS offsets, 96 vs 124 VGPRs) vs runtime shape; interleaved
-        import os
-        calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
-        for rnd in range(2):
-            for cd in ("1", "0"):
-                os.environ["PSANA_RAY_CM_CONSTDIMS"] = cd
-                report(f"calib_cm(rows+cols, compile-time tile shape={cd}) r{rnd}",
-                       timeit(lambda: calcm.run(rl, ol), a.iters), F * npix * 6)
-        os.environ.pop("PSANA_RAY_CM_CONSTDIMS", None)
-    if want("calib_cm_stripes"):
-        import os
-        calcm = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
-        for rnd in range(2):
-            for st in ("96", "48"):
-                os.environ["PSANA_RAY_CM_STRIPE"] = st
-                report(f"calib_cm(rows+cols, stripe={st or 'default'}) r{rnd}", timeit(lambda: calcm.run(rl, ol), a.iters),
-                       F * npix * 6)
-        os.environ.pop("PSANA_RAY_CM_STRIPE", None)
+        report("convert_u16_f32 (bandwidth reference)",
+               timeit(lambda: C.convert_u16_f32(rp, op, npix, _ext.stream_handle()), a.iters), F * npix * 6)
+    if want("calib_cm") and spec.kind != "plain":
+        for name, flags in (("rows+cols", 3), ("rows", 1), ("cols", 2), ("memory phases only", 0)):
+            c = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams(flags=flags))
+            report(f"calib_cm({name})", timeit(lambda: c.run(rl, ol), a.iters), F * npix * 6)
     if want("calib_cm_image") and spec.kind != "plain":
-        # image mode with common mode: fused (CM kernel writes the image from LDS + gap fill) vs
-        # two-pass (CM into frame-shaped scratch, then the LDS-tiled assembly); interleaved A/B
-        import os
-        cals = {}
-        for fused in ("1", "0"):
-            os.environ["PSANA_RAY_IMAGE_CM_FUSED"] = fused
-            cals[fused] = Calibrator(src.consts, dev, Mode.image, common_mode=CommonModeParams())
-        os.environ.pop("PSANA_RAY_IMAGE_CM_FUSED", None)
-        img = torch.empty((F, *cals["1"].out_shape), dtype=torch.float32, device=dev)
+        # image mode with common mode: the CM kernel writes the assembled image from LDS + gap fill
+        c = Calibrator(src.consts, dev, Mode.image, common_mode=CommonModeParams())
+        img = torch.empty((F, *c.out_shape), dtype=torch.float32, device=dev)
         il = [img[i] for i in range(F)]
-        for rnd in range(2):
-            for fused in ("1", "0"):
-                c = cals[fused]
-                report(f"calib_cm_image({'fused' if fused == '1' else 'scratch + assemble'}) r{rnd}",
-                       timeit(lambda: c.run(rl, il), a.iters), F * npix * 6 + img.numel() // F * F * 4)
-    if want("image_stripes") and spec.kind != "plain":
-        # image mode without common mode: LDS-tiled gather (image_tile_kernel) vs the stripe kernel
-        # with its median phases off (decode + pedestal into LDS, gain + placement epilogue)
-        import os
-        cal_t = Calibrator(src.consts, dev, Mode.image)
-        cal_s = Calibrator(src.consts, dev, Mode.image, common_mode=CommonModeParams(flags=0))
-        img = torch.empty((F, *cal_t.out_shape), dtype=torch.float32, device=dev)
-        il = [img[i] for i in range(F)]
-        for rnd in range(2):
-            report(f"image(no cm): tiles r{rnd}", timeit(lambda: cal_t.run(rl, il), a.iters), F * npix * 2 + img.numel() * 4)
-            report(f"image(no cm): stripes r{rnd}", timeit(lambda: cal_s.run(rl, il), a.iters), F * npix * 2 + img.numel() * 4)
+        report("calib_cm_image(fused)", timeit(lambda: c.run(rl, il), a.iters), F * npix * 2 + img.numel() * 4)
     if want("calib_image") and spec.kind != "plain":
-        import os
         C = _ext.load()
-        cals = {}
-        for ver in ("v1", "tiles"):
-            os.environ["PSANA_RAY_IMAGE_V1"] = "1" if ver == "v1" else "0"
-            cals[ver] = Calibrator(src.consts, dev, Mode.image)
-        os.environ.pop("PSANA_RAY_IMAGE_V1", None)
-        cali = cals["tiles"]
+        cali = Calibrator(src.consts, dev, Mode.image)
         tm = cali.tile_map
         img = torch.empty((F, *cali.out_shape), dtype=torch.float32, device=dev)
         il = [img[i] for i in range(F)]
         nout = int(np.prod(cali.out_shape))
-        rp = [int(t.data_ptr()) for t in rl]
         op = [int(t.data_ptr()) for t in ol]
         ip = [int(t.data_ptr()) for t in il]
-        extra = {"image_shape": list(cali.out_shape), "tile_direct_frac": round(tm.direct_px / max(1, tm.staged_px
-                                                                                                    + tm.direct_px), 4)}
-        for rnd in range(2):
-            for ver in ("v1", "tiles"):
-                report(f"calib_image(fused,{ver}) r{rnd}", timeit(lambda: cals[ver].run(rl, il), a.iters),
-                       F * (npix * 2 + nout * 4), extra)
-            for blk in ("256", "512"):
-                os.environ["PSANA_RAY_IMAGE_BLOCK"] = blk
-                for grp in (2, 4, 8):
-                    os.environ["PSANA_RAY_IMAGE_GROUPS"] = str(grp)
-                    report(f"calib_image(fused,tiles,block={blk},groups={grp}) r{rnd}",
-                           timeit(lambda: cali.run(rl, il), a.iters), F * (npix * 2 + nout * 4))
-                os.environ.pop("PSANA_RAY_IMAGE_GROUPS", None)
-                report(f"assemble(tiles,block={blk}) r{rnd}",
-                       timeit(lambda: C.image_tiles(op, ip, False, spec.kernel_kind, 0, 0, npix, spec.panel_rows,
-                                                    spec.panel_cols, int(cali._tiles.data_ptr()), tm.n_tiles,
-                                                    tm.tiles_x, int(cali._codes.data_ptr()), tm.image_shape[0],
-                                                    tm.image_shape[1], _ext.stream_handle()), a.iters),
-                       F * (npix * 4 + nout * 4))
-            os.environ.pop("PSANA_RAY_IMAGE_BLOCK", None)
-            report(f"assemble(v1) r{rnd}", timeit(lambda: kernels.assemble(ol, il, cali.idx, npix), a.iters),
-                   F * (npix * 4 + nout * 4))
-            report(f"assemble(tiles) r{rnd}",
-                   timeit(lambda: C.image_tiles(op, ip, False, spec.kernel_kind, 0, 0, npix, spec.panel_rows,
-                                                spec.panel_cols, int(cali._tiles.data_ptr()), tm.n_tiles, tm.tiles_x,
-                                                int(cali._codes.data_ptr()), tm.image_shape[0], tm.image_shape[1],
-                                                _ext.stream_handle()), a.iters),
-                   F * (npix * 4 + nout * 4))
+        extra = {"image_shape": list(cali.out_shape),
+                 "tile_direct_frac": round(tm.direct_px / max(1, tm.staged_px + tm.direct_px), 4)}
+        report("calib_image(fused, tiles)", timeit(lambda: cali.run(rl, il), a.iters), F * (npix * 2 + nout * 4), extra)
+        report("assemble(index map)", timeit(lambda: kernels.assemble(ol, il, cali.idx, npix), a.iters),
+               F * (npix * 4 + nout * 4))
+        report("assemble(tiles)",
+               timeit(lambda: C.image_tiles(op, ip, False, spec.kernel_kind, 0, 0, npix, spec.panel_rows,
+                                            spec.panel_cols, int(cali._tiles.data_ptr()), tm.n_tiles, tm.tiles_x,
+                                            int(cali._codes.data_ptr()), tm.image_shape[0], tm.image_shape[1],
+                                            _ext.stream_handle()), a.iters),
+               F * (npix * 4 + nout * 4))
     if want("peakfind"):
-        import os
         cal.run(rl, ol)
         p = PeakFinderParams()
         peaks = torch.empty((F, p.max_peaks, 8), dtype=torch.float32, device=dev)
         counts = torch.zeros(F, dtype=torch.int32, device=dev)
         summ = torch.zeros((F, 2), dtype=torch.float32, device=dev)
-        for rnd in range(2):   # interleaved A/B in one process
-            C = _ext.load()
-            sums = torch.zeros(F, dtype=torch.float32, device=dev)
-            op = [int(t.data_ptr()) for t in ol]
-            for k in (8, 16):
-                for nt in (False, True):
-                    report(f"read_f32 reference (K={k}, nt={int(nt)}) r{rnd}",
-                           timeit(lambda: C.read_f32(op, npix, k, nt, int(sums.data_ptr()), _ext.stream_handle()),
-                                  a.iters), F * npix * 4)
-            for ver, groups in (("v1", ""), ("tiles, 2 frames/block", str(max(1, F // 2))),
-                                ("stream K=4 blocks=0", ""), ("stream K=4 blocks=1024", ""),
-                                ("stream K=4", ""), ("stream K=4 blocks=4096", ""),
-                                ("stream K=8", ""), ("stream K=16", "")):
-                os.environ["PSANA_RAY_PF_BLOCKS"] = ver.split("blocks=")[1] if "blocks=" in ver else ""
-                os.environ["PSANA_RAY_PF_V1"] = "1" if ver == "v1" else "0"
-                os.environ["PSANA_RAY_PF_VERSION"] = "3" if ver.startswith("stream") else "2"
-                os.environ["PSANA_RAY_PF_K"] = ver.split("=")[1].split()[0] if "K=" in ver else ""
-                os.environ["PSANA_RAY_PF_GROUPS"] = groups
-                report(f"peakfind({ver}) r{rnd}",
-                       timeit(lambda: kernels.peakfind(ol, spec.frame_shape, p, peaks, counts, summ), a.iters),
-                       F * npix * 4, {"peaks_per_frame": float(counts.float().mean())})
-        os.environ.pop("PSANA_RAY_PF_V1", None)
-        os.environ.pop("PSANA_RAY_PF_GROUPS", None)
-        os.environ.pop("PSANA_RAY_PF_VERSION", None)
-        os.environ.pop("PSANA_RAY_PF_K", None)
-        os.environ.pop("PSANA_RAY_PF_BLOCKS", None)
+        C = _ext.load()
+        sums = torch.zeros(F, dtype=torch.float32, device=dev)
+        op = [int(t.data_ptr()) for t in ol]
+        report("read_f32 reference (K=16)",
+               timeit(lambda: C.read_f32(op, npix, 16, False, int(sums.data_ptr()), _ext.stream_handle()), a.iters),
+               F * npix * 4)
+        report("peakfind", timeit(lambda: kernels.peakfind(ol, spec.frame_shape, p, peaks, counts, summ), a.iters),
+               F * npix * 4, {"peaks_per_frame": float(counts.float().mean())})
     if want("h2d"):
         C = _ext.load()
         hp = src.pool

@@ -412,9 +412,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream"));
 
   py::class_<pr::ProducerEngine>(m, "ProducerEngine")
-      .def(py::init<pr::SlotPool*, int64_t, int, const pr::CalibPlan&, int, int, int64_t, int64_t>(),
+      .def(py::init<pr::SlotPool*, int64_t, int, const pr::CalibPlan&, int, int, int64_t, int64_t, int, bool>(),
            py::arg("pool"), py::arg("slot_bytes"), py::arg("device"), py::arg("plan"),
-           py::arg("chunk"), py::arg("n_raw_bufs"), py::arg("rank"), py::arg("size"), py::keep_alive<1, 2>())
+           py::arg("chunk"), py::arg("n_raw_bufs"), py::arg("rank"), py::arg("size"),
+           py::arg("copy_workgroups") = 32, py::arg("gpu_timing") = false, py::keep_alive<1, 2>())
       .def("set_cycled_source", &pr::ProducerEngine::set_cycled_source, py::arg("frames"), py::arg("photon_energy"))
       .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"), py::arg("k0") = 0)
       .def("set_file_source", &pr::ProducerEngine::set_file_source, py::arg("reader"), py::keep_alive<1, 2>())

@@ -7,8 +7,8 @@
 // memory-bound streaming pass on the GPU.
 //
 // Design (MI355X):
-//  * one thread owns 8 consecutive pixels: one 16-B raw load + two 16-B f32 stores per frame
-//    (Guideline 13: 16 B / lane).
+//  * one thread owns 4 consecutive pixels: one 8-B raw load + one 16-B f32 store per frame, so
+//    consecutive lanes write consecutive 16 B (whole 128-B lines per store instruction).
 //  * the per-pixel constants (pedestal and gain-factor for every candidate gain, the mask
 //    folded into the gain factor) are loaded ONCE per thread and reused for every frame of the
 //    batch (up to kMaxFrames per launch), so constant traffic is amortised over the batch and
@@ -18,7 +18,6 @@
 #include "common.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace pr {
 
@@ -30,99 +29,6 @@ template <>
 struct KindTraits<kJungfrau> { static constexpr int NT = 3; };
 template <>
 struct KindTraits<kPlain> { static constexpr int NT = 1; };
-
-template <int NT>
-__device__ __forceinline__ float pick(const float (&t)[NT][8], int i, int c) {
-  if constexpr (NT == 1) {
-    return t[0][i];
-  } else if constexpr (NT == 2) {
-    return bsel(c != 0, t[1][i], t[0][i]);
-  } else {
-    return bsel(c == 0, t[0][i], bsel(c == 1, t[1][i], t[2][i]));
-  }
-}
-
-template <int KIND, int NT>
-__device__ __forceinline__ void calib8(const uint4 r, const float (&p)[NT][8],
-                                       const float (&g)[NT][8], float4& o0, float4& o1) {
-  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-  float o[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t raw = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-    bool valid;
-    const int c = decode_cand(raw, KIND, valid);
-    const float adu = decode_adu(raw, KIND);
-    const float v = (adu - pick<NT>(p, i, c)) * pick<NT>(g, i, c);
-    o[i] = valid ? v : 0.0f;
-  }
-  o0 = make_float4(o[0], o[1], o[2], o[3]);
-  o1 = make_float4(o[4], o[5], o[6], o[7]);
-}
-
-template <int NT>
-__device__ __forceinline__ void load_tab8(const float* __restrict__ tab, int64_t npix, int64_t pix0,
-                                          float (&t)[NT][8]) {
-#pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    const float4 a = *reinterpret_cast<const float4*>(tab + k * npix + pix0);
-    const float4 b = *reinterpret_cast<const float4*>(tab + k * npix + pix0 + 4);
-    t[k][0] = a.x; t[k][1] = a.y; t[k][2] = a.z; t[k][3] = a.w;
-    t[k][4] = b.x; t[k][5] = b.y; t[k][6] = b.z; t[k][7] = b.w;
-  }
-}
-
-// raw frames: u16 [npix] each (fp.in[f]); outputs: f32 [npix] each (fp.out[f]).
-//
-// Frames are processed in groups of 4 with the NEXT group's raw loads issued before the current
-// group's stores (register double buffer): on CDNA4 `vmcnt` counts stores too, so without this
-// every group's load wait also drained the previous group's stores (store + load latency in
-// series).  blockIdx.y splits the frame batch into groups of FPB frames for more waves in flight
-// (the constants are then re-read once per group, from L2 / Infinity Cache).
-template <int KIND>
-__global__ __launch_bounds__(256) void calib_basic_kernel(const FramePtrs fp, const int nframes,
-                                                          const float* __restrict__ ped,
-                                                          const float* __restrict__ gf,
-                                                          const int64_t npix, const int fpb) {
-  constexpr int NT = KindTraits<KIND>::NT;
-  const int64_t nvec = npix >> 3;
-  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (v >= nvec) return;
-  const int f_begin = blockIdx.y * fpb;
-  const int f_end = min(nframes, f_begin + fpb);
-  const int64_t pix0 = v * 8;
-  float p[NT][8], g[NT][8];
-  load_tab8<NT>(ped, npix, pix0, p);
-  load_tab8<NT>(gf, npix, pix0, g);
-
-  uint4 cur[4], nxt[4];
-  int f = f_begin;
-  const int n0 = min(4, f_end - f);
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (k < n0) cur[k] = ld_nt_u4(gin<uint4>(fp.in[f + k]) + v);
-  while (f < f_end) {
-    const int n = min(4, f_end - f);
-    const int fn = f + 4;
-    const int nn = min(4, f_end - fn);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)   // prefetch the next group before this group's stores
-      if (k < nn) nxt[k] = ld_nt_u4(gin<uint4>(fp.in[fn + k]) + v);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (k < n) {
-        float4 o0, o1;
-        calib8<KIND, NT>(cur[k], p, g, o0, o1);
-        PR_GLOBAL float4* out = gout<float4>(fp.out[f + k]) + 2 * v;
-        st_f4(out, o0);
-        st_f4(out + 1, o1);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-    f = fn;
-  }
-}
 
 // 4-pixel-per-lane layout: 8-B raw loads and 16-B stores, consecutive lanes on consecutive
 // 16-B output chunks, so every store instruction writes 1 KB contiguous (whole 128-B lines).
@@ -324,32 +230,19 @@ void launch_calib_basic(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t
   check(aligned16(ped) && aligned16(gf), "calib_basic: constant tables must be 16-B aligned");
   for (int f = 0; f < nframes; ++f)
     check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_basic: frame buffers must be 16-B aligned");
-  const int64_t nvec = npix / 8;
-  const char* lay = getenv("PSANA_RAY_CALIB_LAYOUT");
-  const bool layout8 = lay && lay[0] == '8';
-  // frames per block-group: the 4-px layout streams a whole batch per block (tables loaded once;
-  // 2.42 vs 2.72 us/frame at 8, profiles/kernels_r1.jsonl). PSANA_RAY_CALIB_FPB overrides (A/B).
-  int fpb = layout8 ? 8 : kMaxFrames;
-  if (const char* e = getenv("PSANA_RAY_CALIB_FPB")) fpb = std::max(1, atoi(e));
-  const dim3 grid((unsigned)((nvec + 255) / 256), (unsigned)((nframes + fpb - 1) / fpb));
+  // 4 pixels per lane (8-B raw loads, 16-B stores, every store instruction writes 1 KiB
+  // contiguous) and the whole batch per block: the tables are loaded once per lane and reused for
+  // every frame (round 1 A/B: 2.42 us/frame vs 2.72 for 8 px per lane in groups of 8 frames,
+  // profiles/kernels_r1.jsonl)
+  const int fpb = kMaxFrames;
+  const dim3 g4((unsigned)((npix / 4 + 255) / 256), (unsigned)((nframes + fpb - 1) / fpb));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float* P = reinterpret_cast<const float*>(ped);
   const float* G = reinterpret_cast<const float*>(gf);
-  if (!layout8) {   // default: 4-pixel-per-lane layout
-    const dim3 g4((unsigned)((npix / 4 + 255) / 256), (unsigned)((nframes + fpb - 1) / fpb));
-    switch (kind) {
-      case kEpix10ka: hipLaunchKernelGGL(calib_basic4_kernel<kEpix10ka>, g4, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
-      case kJungfrau: hipLaunchKernelGGL(calib_basic4_kernel<kJungfrau>, g4, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
-      case kPlain: hipLaunchKernelGGL(calib_basic4_kernel<kPlain>, g4, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
-      default: check(false, "calib_basic: unknown gain kind");
-    }
-    hip_check(hipGetLastError(), "calib_basic launch");
-    return;
-  }
   switch (kind) {
-    case kEpix10ka: hipLaunchKernelGGL(calib_basic_kernel<kEpix10ka>, grid, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
-    case kJungfrau: hipLaunchKernelGGL(calib_basic_kernel<kJungfrau>, grid, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
-    case kPlain: hipLaunchKernelGGL(calib_basic_kernel<kPlain>, grid, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
+    case kEpix10ka: hipLaunchKernelGGL(calib_basic4_kernel<kEpix10ka>, g4, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
+    case kJungfrau: hipLaunchKernelGGL(calib_basic4_kernel<kJungfrau>, g4, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
+    case kPlain: hipLaunchKernelGGL(calib_basic4_kernel<kPlain>, g4, dim3(256), 0, s, fp, nframes, P, G, npix, fpb); break;
     default: check(false, "calib_basic: unknown gain kind");
   }
   hip_check(hipGetLastError(), "calib_basic launch");

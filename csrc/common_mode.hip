@@ -190,7 +190,6 @@ struct TileGeom {
 // (saves a 2 x 8.65 MB HBM round trip per epix10k2M frame).  Gap pixels: launch_fill_runs.
 struct ImgOut {
   const int32_t* desc;    // [n_panels][3] (base, step per panel row, step per panel column); nullptr: frame layout
-  const uint8_t* omask;   // image-shaped output mask (truthy keeps) or nullptr
 };
 
 // ---- tile layout ------------------------------------------------------------------------
@@ -401,37 +400,69 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
   for (int j = 0; j < 8; ++j) o[j] = xv[j] * cm_gain<NT>(ga, cb, j);
 }
 
-// Image-mode epilogue of the store phase: the output tile (already in LDS) into the image.
-__device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C, const ImgOut& io, int panel, int y0,
-                                         int x0, PR_GLOBAL float* out) {
-  __syncthreads();
-  const int32_t* d = io.desc + 3 * panel;
-  const int sy = d[1], sx = d[2];
-  const int64_t b0 = (int64_t)d[0] + (int64_t)y0 * sy + (int64_t)x0 * sx;
-  const int n = R * C;
-  const bool rows = sx == 1 || sx == -1;
-  const int inner = rows ? C : R;
-  const float inv = 1.0f / (float)inner;   // e < 2^24: floor((e + 0.5) / inner) is exact in f32
-  for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    const int a = (int)(((float)e + 0.5f) * inv);
-    const int bb = e - a * inner;
-    const int r = rows ? a : bb, c = rows ? bb : a;
-    const int64_t q = b0 + (int64_t)r * sy + (int64_t)c * sx;
-    float v = tile[r * P + c];
-    if (io.omask != nullptr && !io.omask[q]) v = 0.0f;
-    out[q] = v;
+// Store phase, part 2.  Part 1 leaves the finished output tile in LDS; part 2 only reads LDS
+// and writes global memory.  On CDNA the vector-memory counter counts stores as well as loads,
+// so a load between two stores would make the wave wait for the earlier stores to retire; with
+// no loads in this loop every store is fire-and-forget (the round-1 form that interleaved the
+// gain-factor loads with the stores serialised one store round trip per 8-pixel group).
+// Frame layout: 16 B per lane, consecutive lanes along tile rows.
+__device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C, PR_GLOBAL float* out, int64_t base,
+                                         int panel_cols) {
+  const int C4 = C >> 2;
+  for (int e = threadIdx.x; e < R * C4; e += blockDim.x) {
+    const int r = e / C4, j = e - r * C4;
+    const float4 v = *reinterpret_cast<const float4*>(tile + r * P + 4 * j);
+    st_f4((PR_GLOBAL float4*)(out + base + (int64_t)r * panel_cols + 4 * j), v);
   }
 }
 
-__device__ __forceinline__ void cm_emit(float* trow, PR_GLOBAL float* out, int64_t pix, bool img, const float (&o)[8]) {
-  if (img) {
-    *reinterpret_cast<float4*>(trow) = make_float4(o[0], o[1], o[2], o[3]);
-    *reinterpret_cast<float4*>(trow + 4) = make_float4(o[4], o[5], o[6], o[7]);
-  } else {
-    PR_GLOBAL float4* op = (PR_GLOBAL float4*)(out + pix);
-    st_f4(op, make_float4(o[0], o[1], o[2], o[3]));
-    st_f4(op + 1, make_float4(o[4], o[5], o[6], o[7]));
+// Image layout (fused K-05): every panel sits in the image by an integer rotation + translation,
+// so either tile rows or tile columns are contiguous image runs (step +-1).  16-B stores when the
+// runs are 16-B aligned, 4-B stores otherwise.  The image mask is folded into the gain factors
+// of this plan (Calibrator), so no mask loads sit between the stores.
+__device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C, const ImgOut& io, int panel, int y0,
+                                         int x0, PR_GLOBAL float* out) {
+  const int32_t* d = io.desc + 3 * panel;
+  const int sy = d[1], sx = d[2];
+  const int64_t b0 = (int64_t)d[0] + (int64_t)y0 * sy + (int64_t)x0 * sx;
+  const bool rows = sx == 1 || sx == -1;           // image runs along tile rows (else along columns)
+  const int inner = rows ? C : R;                   // run length
+  const int step = rows ? sx : sy;                  // +-1 along the run
+  const int64_t outer_stride = rows ? sy : sx;      // image step between runs
+  const int64_t lo0 = step > 0 ? b0 : b0 - 3;       // lowest address of a run's first 4 elements
+  if ((inner & 3) == 0 && (lo0 & 3) == 0 && (outer_stride & 3) == 0) {
+    const int n4 = inner >> 2;
+    for (int e = threadIdx.x; e < (rows ? R : C) * n4; e += blockDim.x) {
+      const int a = e / n4, j = e - a * n4;       // run a, elements 4j..4j+3 of it
+      float v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = rows ? tile[a * P + 4 * j + k] : tile[(4 * j + k) * P + a];
+      const int64_t q = b0 + (int64_t)a * outer_stride + (step > 0 ? 4 * j : -4 * j - 3);
+      st_f4((PR_GLOBAL float4*)(out + q),
+            step > 0 ? make_float4(v[0], v[1], v[2], v[3]) : make_float4(v[3], v[2], v[1], v[0]));
+    }
+    return;
   }
+  const float inv = 1.0f / (float)inner;   // e < 2^24: floor((e + 0.5) / inner) is exact in f32
+  for (int e = threadIdx.x; e < R * C; e += blockDim.x) {
+    const int a = (int)(((float)e + 0.5f) * inv);
+    const int bb = e - a * inner;
+    const int r = rows ? a : bb, c = rows ? bb : a;
+    out[b0 + (int64_t)r * sy + (int64_t)c * sx] = tile[r * P + c];
+  }
+}
+
+__device__ __forceinline__ void cm_put8(float* trow, const float (&o)[8]) {
+  *reinterpret_cast<float4*>(trow) = make_float4(o[0], o[1], o[2], o[3]);
+  *reinterpret_cast<float4*>(trow + 4) = make_float4(o[4], o[5], o[6], o[7]);
+}
+
+__device__ __forceinline__ void cm_write_out(const float* tile, int P, int R, int C, const TileGeom& tg,
+                                             const ImgOut& io, int panel, int y0, int x0, int64_t base,
+                                             PR_GLOBAL float* out) {
+  __syncthreads();
+  if (io.desc != nullptr) cm_place(tile, P, R, C, io, panel, y0, x0, out);
+  else cm_flush(tile, P, R, C, out, base, tg.panel_cols);
 }
 
 // Phase 3 (runtime-shape loop form).
@@ -441,7 +472,6 @@ __device__ __forceinline__ void cm_store(float* tile, const float* side, const i
                                          const float* __restrict__ ped, const float* __restrict__ gf, int64_t base,
                                          PR_GLOBAL float* out, const ImgOut& io, int panel, int y0, int x0) {
   const int C8 = C >> 3;
-  const bool img = io.desc != nullptr;
   for (int i = threadIdx.x; i < R * C8; i += blockDim.x) {
     const int r = i / C8, k = i - r * C8, c = k * 8;
     const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
@@ -451,9 +481,9 @@ __device__ __forceinline__ void cm_store(float* tile, const float* side, const i
     load8<NT>(gf, tg.npix, pix, cm_need<NT>(cb), ga);
     float o[8];
     cm_out8<KIND, NT>(tile + r * P + c, side, cb, slot, ga, raw, ped, tg.npix, pix, o);
-    cm_emit(tile + r * P + c, out, pix, img, o);
+    cm_put8(tile + r * P + c, o);
   }
-  if (img) cm_place(tile, P, R, C, io, panel, y0, x0, out);
+  cm_write_out(tile, P, R, C, tg, io, panel, y0, x0, base, out);
 }
 
 // (tile, frame) of this workgroup and the tile's first pixel
@@ -464,7 +494,8 @@ struct TileCoord {
 // Table-major order: consecutive workgroups take the same tile of consecutive frames, so the
 // constant tables of a tile are fetched from HBM about once per XCD and then hit in L2.  (A/B on
 // MI355X, 32 epix10k2M frames: frame-major order 5.7 us/frame vs 5.0 table-major with the medians
-// off; an XCD-grouping remap of the table-major order changed nothing, 4.75 vs 4.65.)
+// off; an XCD-grouping remap of the table-major order changed nothing, 4.75 vs 4.65, and an
+// XCD-local frame-major order lost, 5.29 vs 4.90.)
 __device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C) {
   TileCoord t;
   const int id = (int)blockIdx.x;
@@ -859,7 +890,6 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
   if constexpr (NI > 0 && NI <= 6) {
     // compile-time shape: every gain-factor load of this lane in flight before the first use
     constexpr int C8 = TC / 8;
-    const bool img = io.desc != nullptr;
     // (the first gain table of every item up front; the switched-gain tables are rare and are
     // loaded per item, which keeps the production kernel within 128 VGPRs)
     uint32_t cbs[NI], slots[NI];
@@ -885,10 +915,10 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
         if constexpr (NT > 1) load8<NT>(gf, tg.npix, pix, cm_need<NT>(cbs[u]), ga, 1);
         float o[8];
         cm_out8<KIND, NT>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, ped, tg.npix, pix, o);
-        cm_emit(tile + r * P + c, out, pix, img, o);
+        cm_put8(tile + r * P + c, o);
       }
     }
-    if (img) cm_place(tile, P, R, C, io, t.panel, t.ar * R, t.ac * C, out);
+    cm_write_out(tile, P, R, C, tg, io, t.panel, t.ar * R, t.ac * C, t.base, out);
   } else {
     cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.panel, t.ar * R, t.ac * C);
   }
@@ -922,8 +952,7 @@ static void cm_launch(K kernel, dim3 grid, int block, size_t lds, hipStream_t s,
 
 void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t planes, int kind,
                      int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
-                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream, uint64_t img_desc,
-                     uint64_t img_omask) {
+                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream, uint64_t img_desc) {
   check(nframes >= 1 && nframes <= kMaxFrames, "calib_cm: nframes out of range");
   check(asic_rows >= 1 && asic_rows <= 256, "calib_cm: ASIC rows must be in [1, 256]");
   check(asic_cols % 8 == 0 && asic_cols >= 8, "calib_cm: ASIC cols must be a multiple of 8");
@@ -932,6 +961,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
         "calib_cm: bank_cols must be <= 64 and divide the ASIC width");
   check(panel_cols % 8 == 0, "calib_cm: panel cols must be a multiple of 8");
   check(kind == kEpix10ka || kind == kJungfrau || kind == kPlain, "calib_cm: unknown gain kind");
+  check(flags >= 0 && flags <= 3, "calib_cm: flags must be in [0, 3] (bit0 rows, bit1 columns)");
   // Tile shape (one decision per shape, no run-time knobs):
   //  * epix10k2M (176-row ASICs, 48-column banks): one-bank 176x48 stripes on 256-thread blocks,
   //    four workgroups per CU (round 1: 8.8 us/frame vs 9.2 for 176x96, 15.8 full width);
@@ -963,8 +993,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   check(aligned16(ped) && aligned16(gf) && (planes & 3) == 0, "calib_cm: misaligned constant tables");
   for (int f = 0; f < nframes; ++f)
     check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_cm: frame buffers must be 16-B aligned");
-  const ImgOut io{reinterpret_cast<const int32_t*>(img_desc), reinterpret_cast<const uint8_t*>(img_omask)};
-  check(img_omask == 0 || img_desc != 0, "calib_cm: an image mask needs the image output map");
+  const ImgOut io{reinterpret_cast<const int32_t*>(img_desc)};
   // LDS budget of one workgroup: the epix10k2M 176x48 stripe runs four workgroups per CU, the
   // narrow compile-time kernels two, everything else one; what the tile leaves is side slots
   const size_t budget = (epix_prod && asic_cols == 48) ? 40 * 1024 : (net && !jf_prod && asic_cols <= 128) ? 80 * 1024
@@ -993,9 +1022,8 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
     cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, 256, 176, 48>, grid, 256, lds_all, s, fp, P, G, F, tg, cp, io);
   } else if (jf_prod && asic_cols == 128) {
     cm_launch(calib_cm_net_kernel<kJungfrau, 64, 64, 512, 256, 128>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
-  } else if (kind == kEpix10ka && bank_cols == 48 && M4 == 44) {
-    if (narrow) cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, 512>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
-    else cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, 1024>, grid, 1024, lds_all, s, fp, P, G, F, tg, cp, io);
+  } else if (kind == kEpix10ka && bank_cols == 48 && M4 == 44 && narrow) {
+    cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, 512>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
   } else if (kind == kEpix10ka && bank_cols == 8 && M4 == 4 && narrow) {
     cm_launch(calib_cm_net_kernel<kEpix10ka, 8, 4, 512>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
   } else if (kind == kEpix10ka) {

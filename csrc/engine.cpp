@@ -51,8 +51,7 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
         check(p.use_cm && p.img_desc != 0, "run_calib_plan: fused image plan without common mode / placement");
         const FramePtrs fp = ptrs_of(in, out, a, b);
         launch_calib_cm(fp, n, p.ped, p.gf, p.elig, p.kind, p.n_panels, p.panel_rows, p.panel_cols, p.asic_rows,
-                        p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags, p.bank_cols, stream, p.img_desc,
-                        p.omask);
+                        p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags, p.bank_cols, stream, p.img_desc);
         launch_fill_runs(fp, n, p.gap_runs, p.n_gap_runs, stream);
         break;
       }
@@ -82,16 +81,16 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
 
 // ---------------------------------------------------------------------------------------
 ProducerEngine::ProducerEngine(SlotPool* pool, int64_t slot_bytes, int device,
-                               const CalibPlan& plan, int chunk, int n_raw_bufs, int64_t rank, int64_t size)
+                               const CalibPlan& plan, int chunk, int n_raw_bufs, int64_t rank, int64_t size,
+                               int copy_workgroups, bool gpu_timing)
     : pool_(pool), slot_bytes_(slot_bytes), device_(device), plan_(plan),
       chunk_(std::max(1, std::min(chunk, kMaxFrames))), n_raw_bufs_(std::max(2, n_raw_bufs)), rank_(rank),
-      size_(size), hdr_rank_(rank) {
+      size_(size), hdr_rank_(rank), gpu_timing_(gpu_timing), copy_workgroups_(std::max(0, copy_workgroups)) {
   check(pool != nullptr && device >= 0, "ProducerEngine needs a device SlotPool");
   check(plan.raw_frame_bytes > 0 && plan.raw_frame_bytes % 16 == 0, "ProducerEngine: bad raw frame size");
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
   hip_check(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate");
-  if (const char* e = getenv("PSANA_RAY_ENGINE_GPU_TIMING"); e && e[0] == '1') gpu_timing_ = true;
   const unsigned ev_flags = gpu_timing_ ? hipEventDefault : hipEventDisableTiming;
   buf_free_.resize(n_raw_bufs_);
   h2d_done_.resize(n_raw_bufs_);
@@ -240,12 +239,11 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
     // host-side software pipeline: the copy of chunk c+1 is queued on the side stream BEFORE
     // chunk c waits for slots / launches, so the copy engine never runs dry behind host work
     const int64_t fb = plan_.raw_frame_bytes;
-    // host->HBM staging copies by our own kernel with PSANA_RAY_COPY_KERNEL workgroups (default 32;
+    // host->HBM staging copies by our own kernel with copy_workgroups_ workgroups (default 32;
     // 0 = hipMemcpyAsync, i.e. the runtime's blit / SDMA copies).  Measured in the pipeline:
     // 12.98-12.99k fr/s with 32 workgroups vs 12.53-12.77k with blit copies on the same box
     // (profiles/bench_r1/copy_kernel/)
-    int copy_kernel_wgs = 32;
-    if (const char* e = getenv("PSANA_RAY_COPY_KERNEL"); e && *e) copy_kernel_wgs = atoi(e);
+    const int copy_kernel_wgs = copy_workgroups_;
     auto stage = [&](int64_t k0, int n, int b) {
       char* buf = static_cast<char*>(raw_bufs_) + (size_t)b * region_bytes_;
       std::vector<uint64_t>& dev = dev_in_[b];
@@ -333,9 +331,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
     // does not idle the PCIe link.  depth < n_raw_bufs: a buffer is re-staged only after the
     // calibration that read it was launched (its buf_free event recorded; the copy stream waits on
     // it device-side), and its pointers / file metadata were consumed.
-    int depth = 3;
-    if (const char* e = getenv("PSANA_RAY_STAGE_DEPTH"); e && *e) depth = std::max(1, atoi(e));
-    depth = std::min(depth, n_raw_bufs_ - 1);
+    const int depth = std::min(3, n_raw_bufs_ - 1);
     int64_t st_k = k0;   // first event not staged yet
     int64_t st_no = 0;   // chunks staged so far
     auto stage_upto = [&](int64_t last_no) {   // stage chunks st_no .. last_no

@@ -61,8 +61,12 @@ void run_calib_plan(const CalibPlan& plan, const std::vector<uint64_t>& in, cons
 
 class ProducerEngine {
  public:
+  // copy_workgroups: host->HBM staging copies by copy_h2d_kernel with this many workgroups
+  // (0 = hipMemcpyAsync, the runtime's blit / SDMA path); gpu_timing: event-time every chunk's
+  // H2D copy and calibration (diagnostics)
   ProducerEngine(SlotPool* pool, int64_t slot_bytes, int device, const CalibPlan& plan,
-                 int chunk, int n_raw_bufs, int64_t rank, int64_t size);
+                 int chunk, int n_raw_bufs, int64_t rank, int64_t size, int copy_workgroups = 32,
+                 bool gpu_timing = false);
   ~ProducerEngine();
   ProducerEngine(const ProducerEngine&) = delete;
   ProducerEngine& operator=(const ProducerEngine&) = delete;
@@ -88,7 +92,7 @@ class ProducerEngine {
   std::string error() const;
   // host-side time (seconds) spent per loop part: [stage copies, acquire slots, launch kernels, commit, total]
   std::vector<double> timing() const;
-  // GPU-side per-stage time from timing events (PSANA_RAY_ENGINE_GPU_TIMING=1 at construction):
+  // GPU-side per-stage time from timing events (gpu_timing=true at construction):
   // [h2d ms total, h2d chunks measured, calib ms total, calib chunks measured]; zeros when off
   std::vector<double> gpu_timing() const;
   // (copies that moved a multi-frame span, copies of a single frame) in cycled-host mode
@@ -117,6 +121,7 @@ class ProducerEngine {
   // optional GPU timing: start events per raw buffer, harvested (non-blocking) when the buffer is
   // reused or at the end of the run
   bool gpu_timing_ = false;
+  int copy_workgroups_ = 32;
   std::vector<hipEvent_t> h2d_start_, calib_start_;
   std::vector<char> h2d_pending_, calib_pending_;
   double gpu_h2d_ms_ = 0, gpu_calib_ms_ = 0;

@@ -80,7 +80,7 @@ void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_run
 }
 
 // ---------------------------------------------------------------------------------------------
-// Host -> HBM staging copy as OUR kernel (PSANA_RAY_COPY_KERNEL=<workgroups>): the pinned pool
+// Host -> HBM staging copy as OUR kernel: the pinned pool
 // (or registered run file) is read straight over PCIe by a FEW persistent workgroups, each lane
 // keeping 4 x 16 B nontemporal loads in flight (64 workgroups x 256 lanes x 64 B = 1 MiB in flight,
 // ~8x the PCIe Gen5 bandwidth-delay product), instead of the runtime's blit kernel, whose
@@ -113,21 +113,14 @@ bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgro
     (void)hipGetLastError();   // not pinned / not mapped: the caller falls back to hipMemcpyAsync
     return false;
   }
-  // PSANA_RAY_COPY_KERNEL_U: 16-B loads in flight per lane (4 default, 8 for A/B)
-  static const int U = [] {
-    const char* e = getenv("PSANA_RAY_COPY_KERNEL_U");
-    return (e && atoi(e) == 8) ? 8 : 4;
-  }();
+  constexpr int U = 4;   // 16-B loads in flight per lane (round-1 A/B: 8 no faster)
   const int64_t n16 = bytes / 16;
   const int64_t need = (n16 + 256 * U - 1) / (256 * U);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(workgroups, need));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const f32x4_t* sp = reinterpret_cast<const f32x4_t*>(dsrc);
   f32x4_t* dp = reinterpret_cast<f32x4_t*>(dst);
-  if (U == 8)
-    hipLaunchKernelGGL(copy_h2d_kernel<8>, dim3(grid), dim3(256), 0, s, sp, dp, n16);
-  else
-    hipLaunchKernelGGL(copy_h2d_kernel<4>, dim3(grid), dim3(256), 0, s, sp, dp, n16);
+  hipLaunchKernelGGL(copy_h2d_kernel<U>, dim3(grid), dim3(256), 0, s, sp, dp, n16);
   hip_check(hipGetLastError(), "copy_h2d launch");
   return true;
 }

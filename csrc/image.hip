@@ -187,26 +187,17 @@ void launch_image_tiles(const FramePtrs& fp, int nframes, bool calib, int kind, 
   // frame groups: tables are loaded once per block and reused over its frames, but a block walks
   // its frames serially, so more groups = more blocks in flight (epix10k2M, 1250 tiles, 32 frames:
   // 1 group 7.98, 2: 6.45, 4: 5.94, 8: 6.42 us/frame; profiles/kernels_r1_image.jsonl)
-  int groups = n_tiles >= 8192 ? 1 : (n_tiles >= 4096 ? 2 : 4);
-  if (const char* e = getenv("PSANA_RAY_IMAGE_GROUPS")) groups = std::max(1, atoi(e));
-  groups = std::min(groups, nframes);
+  const int groups = std::min(n_tiles >= 8192 ? 1 : (n_tiles >= 4096 ? 2 : 4), nframes);
   const dim3 grid((unsigned)n_tiles, (unsigned)groups);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float* P = reinterpret_cast<const float*>(ped);
   const float* G = reinterpret_cast<const float*>(gf);
   const int32_t* T = reinterpret_cast<const int32_t*>(tiles);
   const int32_t* Cd = reinterpret_cast<const int32_t*>(codes);
-  // 512-thread blocks: half the per-thread staged pixels / codes (fewer VGPRs, more waves in flight);
-  // PSANA_RAY_IMAGE_BLOCK=256 for A/B
-  int block = 512;
-  if (const char* e = getenv("PSANA_RAY_IMAGE_BLOCK"); e && *e) block = atoi(e) == 256 ? 256 : 512;
-#define PR_IMG(K, CAL)                                                                                         \
-  do {                                                                                                         \
-    if (block == 512)                                                                                          \
-      hipLaunchKernelGGL((image_tile_kernel<K, CAL, 512>), grid, dim3(512), 0, s, fp, 0, nframes, P, G, T, Cd, g); \
-    else                                                                                                       \
-      hipLaunchKernelGGL((image_tile_kernel<K, CAL, 256>), grid, dim3(256), 0, s, fp, 0, nframes, P, G, T, Cd, g); \
-  } while (0)
+  // 512-thread blocks: half the per-thread staged pixels / codes of 256 (fewer VGPRs, more waves
+  // in flight; round-1 A/B)
+#define PR_IMG(K, CAL) \
+  hipLaunchKernelGGL((image_tile_kernel<K, CAL, 512>), grid, dim3(512), 0, s, fp, 0, nframes, P, G, T, Cd, g)
   if (calib) {
     switch (kind) {
       case kEpix10ka: PR_IMG(kEpix10ka, true); break;

@@ -16,17 +16,15 @@
 // pixel once with coalesced 16-B loads, thresholds in registers, and sends only the rare
 // candidates through the neighbourhood test (direct, cache-hit reads); one atomic per accepted
 // peak reserves its record slot (and bumps an optional 64-bit running total, so consumers never
-// read counts back per batch).  Versions kept for A/B: PSANA_RAY_PF_VERSION=2 (64x32 LDS halo
-// tiles, frames walked with prefetch), PSANA_RAY_PF_V1=1 (64x16 tiles, scalar loads).
-// epix10k2M: v3 2.21, v2 2.76-2.86, v1 5.88 us/frame (profiles/kernels_r1_peakfind_ab.jsonl).
+// read counts back per batch).  Round-1 A/B, epix10k2M: this stream form 2.21 us/frame, 64x32 LDS
+// halo tiles 2.76-2.86, 64x16 tiles with scalar loads 5.88 (profiles/kernels_r1_peakfind_ab.jsonl;
+// the losing variants are retired).
 #include "common.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace pr {
 
-constexpr int kPfTX = 64, kPfTY = 16;
 
 struct PfParams {
   float thr_peak;
@@ -34,128 +32,6 @@ struct PfParams {
   int max_peaks;
   int n_panels, rows, cols;
 };
-
-template <int RAD>
-__global__ __launch_bounds__(256) void peakfind_v1_kernel(const FramePtrs fp, const PfParams pp,
-                                                       float* __restrict__ peaks,     // [F][max][8]
-                                                       int* __restrict__ counts,      // [F]
-                                                       float* __restrict__ summary,   // [F][2]
-                                                       unsigned long long* __restrict__ total) {
-  constexpr int H = RAD + 2;
-  constexpr int LW = kPfTX + 2 * H, LH = kPfTY + 2 * H;
-  __shared__ float t[LH][LW + 1];
-  __shared__ float red_sum[4];
-  __shared__ int red_cnt[4];
-
-  const int f = blockIdx.y;
-  const int tiles_x = (pp.cols + kPfTX - 1) / kPfTX;
-  const int tiles_y = (pp.rows + kPfTY - 1) / kPfTY;
-  const int panel = blockIdx.x / (tiles_x * tiles_y);
-  const int trem = blockIdx.x % (tiles_x * tiles_y);
-  const int ty0 = (trem / tiles_x) * kPfTY, tx0 = (trem % tiles_x) * kPfTX;
-  const PR_GLOBAL float* img = gin<float>(fp.in[f]) + (int64_t)panel * pp.rows * pp.cols;
-  const float NaN = __int_as_float(0x7fc00000);
-
-  for (int i = threadIdx.x; i < LH * LW; i += 256) {
-    const int ly = i / LW, lx = i % LW;
-    const int gy = ty0 + ly - H, gx = tx0 + lx - H;
-    t[ly][lx] = (gy >= 0 && gy < pp.rows && gx >= 0 && gx < pp.cols) ? img[(int64_t)gy * pp.cols + gx] : NaN;
-  }
-  __syncthreads();
-
-  const int ly = threadIdx.x / (kPfTX / 4);
-  const int lx0 = (threadIdx.x % (kPfTX / 4)) * 4;
-  float above_sum = 0.0f;
-  int above_cnt = 0;
-  for (int k = 0; k < 4; ++k) {
-    const int cy = ly + H, cx = lx0 + k + H;
-    const float v = t[cy][cx];
-    if (!(v > pp.thr_peak)) continue;  // also rejects NaN (outside the panel)
-    above_sum += v;
-    ++above_cnt;
-    bool is_max = true;
-#pragma unroll
-    for (int dy = -RAD; dy <= RAD; ++dy)
-#pragma unroll
-      for (int dx = -RAD; dx <= RAD; ++dx) {
-        if (dy == 0 && dx == 0) continue;
-        const float n = t[cy + dy][cx + dx];
-        if (n != n) continue;
-        const bool before = (dy < 0) || (dy == 0 && dx < 0);
-        if (before ? !(v > n) : !(v >= n)) is_max = false;
-      }
-    if (!is_max) continue;
-    float s = 0.0f, s2 = 0.0f;
-    int nr = 0;
-#pragma unroll
-    for (int dy = -H; dy <= H; ++dy)
-#pragma unroll
-      for (int dx = -H; dx <= H; ++dx) {
-        const int d = max(abs(dy), abs(dx));
-        if (d <= RAD) continue;
-        const float n = t[cy + dy][cx + dx];
-        if (n != n) continue;
-        s += n;
-        s2 += n * n;
-        ++nr;
-      }
-    const float bkg = nr > 0 ? s / nr : 0.0f;
-    const float var = nr > 0 ? fmaxf(s2 / nr - bkg * bkg, 0.0f) : 0.0f;
-    const float noise = sqrtf(var);
-    const float snr = (v - bkg) / fmaxf(noise, 1e-6f);
-    if (snr < pp.son_min) continue;
-    float inten = 0.0f;
-#pragma unroll
-    for (int dy = -RAD; dy <= RAD; ++dy)
-#pragma unroll
-      for (int dx = -RAD; dx <= RAD; ++dx) {
-        const float n = t[cy + dy][cx + dx];
-        if (n == n) inten += n - bkg;
-      }
-    const int slot = atomicAdd(counts + f, 1);
-    if (slot < pp.max_peaks) {
-      if (total != nullptr) atomicAdd(total, 1ull);
-      float* rec = peaks + ((int64_t)f * pp.max_peaks + slot) * 8;
-      rec[0] = (float)panel;
-      rec[1] = (float)(ty0 + ly);
-      rec[2] = (float)(tx0 + lx0 + k);
-      rec[3] = v;
-      rec[4] = inten;
-      rec[5] = bkg;
-      rec[6] = noise;
-      rec[7] = snr;
-    }
-  }
-  // block reduction of the hit statistics: wave shuffle -> LDS -> one atomic per block
-  for (int o = 32; o > 0; o >>= 1) {
-    above_sum += __shfl_down(above_sum, o);
-    above_cnt += __shfl_down(above_cnt, o);
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    red_sum[wave] = above_sum;
-    red_cnt[wave] = above_cnt;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float s = red_sum[0] + red_sum[1] + red_sum[2] + red_sum[3];
-    const int c = red_cnt[0] + red_cnt[1] + red_cnt[2] + red_cnt[3];
-    if (c > 0) {
-      atomicAdd(summary + 2 * f, (float)c);
-      atomicAdd(summary + 2 * f + 1, s);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// v2 (default): 64x32 output tile per 256-thread workgroup.  The halo tile is loaded with 16-B
-// aligned float4 loads (x halo rounded up to 4 columns; panels are a multiple of 4 wide, so a
-// float4 is entirely inside or outside the panel) and stored with ds_write_b128; every lane owns
-// ONE column x = lane and 8 rows, so a wave's neighbourhood reads t[y+dy][x+dx] hit 64
-// consecutive words: bank-conflict free.  Half the workgroups of v1 for the same frame, 1.2x halo
-// over-fetch instead of 1.5x.
-// ---------------------------------------------------------------------------------------------
-constexpr int kPf2TX = 64, kPf2TY = 32, kPf2HX = 4;
 
 // at(dy, dx): neighbour value, NaN outside the panel
 template <int RAD, typename At>
@@ -215,115 +91,16 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
   }
 }
 
-template <int RAD>
-__global__ __launch_bounds__(256) void peakfind_kernel(const FramePtrs fp, const int nframes, const PfParams pp,
-                                                       float* __restrict__ peaks, int* __restrict__ counts,
-                                                       float* __restrict__ summary,
-                                                       unsigned long long* __restrict__ total) {
-  constexpr int H = RAD + 2;
-  static_assert(H <= kPf2HX, "x halo must cover the background ring");
-  constexpr int LW = kPf2TX + 2 * kPf2HX;   // 72 floats = 18 float4 per row
-  constexpr int LH = kPf2TY + 2 * H;
-  constexpr int Q = LW / 4;
-  constexpr int NLD = (LH * Q + 255) / 256;  // float4 halo loads per thread
-  __shared__ __attribute__((aligned(16))) float t[LH][LW];
-  __shared__ float red_sum[4];
-  __shared__ int red_cnt[4];
-
-  // this workgroup walks frames [fa, fb) of ONE tile; frame f+1's halo is loaded into registers
-  // while frame f is processed from LDS (plain loads stay in flight across the barriers)
-  const int per = (nframes + (int)gridDim.y - 1) / (int)gridDim.y;
-  const int fa = (int)blockIdx.y * per, fb = min(nframes, fa + per);
-  const int tiles_x = (pp.cols + kPf2TX - 1) / kPf2TX;
-  const int tiles_y = (pp.rows + kPf2TY - 1) / kPf2TY;
-  const int panel = blockIdx.x / (tiles_x * tiles_y);
-  const int trem = blockIdx.x % (tiles_x * tiles_y);
-  const int ty0 = (trem / tiles_x) * kPf2TY, tx0 = (trem % tiles_x) * kPf2TX;
-  const int64_t pbase = (int64_t)panel * pp.rows * pp.cols;
-  const float NaN = __int_as_float(0x7fc00000);
-  const int tid = threadIdx.x;
-
-  int64_t goff[NLD];   // -1: outside the panel (NaN) or beyond the halo tile
-  int lofs[NLD];
-#pragma unroll
-  for (int j = 0; j < NLD; ++j) {
-    const int i = tid + 256 * j;
-    const int ly = i / Q, q = i % Q;
-    const int gy = ty0 + ly - H, gx = tx0 - kPf2HX + 4 * q;
-    lofs[j] = i < LH * Q ? ly * LW + 4 * q : -1;
-    goff[j] = (i < LH * Q && gy >= 0 && gy < pp.rows && gx >= 0 && gx < pp.cols)
-                  ? pbase + (int64_t)gy * pp.cols + gx : -1;
-  }
-  f32x4_t pre[NLD];
-  auto load = [&](int f) {
-    const PR_GLOBAL float* img = gin<float>(fp.in[f]);
-#pragma unroll
-    for (int j = 0; j < NLD; ++j) {
-      f32x4_t v = {NaN, NaN, NaN, NaN};
-      if (goff[j] >= 0) v = *(const PR_GLOBAL f32x4_t*)(img + goff[j]);
-      pre[j] = v;
-    }
-  };
-
-  const int x = tid & 63;
-  const int y0 = tid >> 6;
-  const int gx = tx0 + x;
-  const int lane = tid & 63, wave = tid >> 6;
-  if (fa < fb) load(fa);
-  for (int f = fa; f < fb; ++f) {
-#pragma unroll
-    for (int j = 0; j < NLD; ++j)
-      if (lofs[j] >= 0) *reinterpret_cast<f32x4_t*>(&t[0][0] + lofs[j]) = pre[j];
-    __syncthreads();
-    if (f + 1 < fb) load(f + 1);
-    float above_sum = 0.0f;
-    int above_cnt = 0;
-    if (gx < pp.cols) {
-#pragma unroll
-      for (int k = 0; k < kPf2TY / 4; ++k) {
-        const int y = y0 + 4 * k;
-        const float v = t[y + H][x + kPf2HX];   // NaN below the panel edge -> rejected
-        if (!(v > pp.thr_peak)) continue;
-        above_sum += v;
-        ++above_cnt;
-        const int cy = y + H, cx = x + kPf2HX;
-        pf_candidate<RAD>([&](int dy, int dx) { return t[cy + dy][cx + dx]; }, v, pp, f, panel, ty0 + y, gx, peaks,
-                          counts, total);
-      }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      above_sum += __shfl_down(above_sum, o);
-      above_cnt += __shfl_down(above_cnt, o);
-    }
-    if (lane == 0) {
-      red_sum[wave] = above_sum;
-      red_cnt[wave] = above_cnt;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      const float sm = red_sum[0] + red_sum[1] + red_sum[2] + red_sum[3];
-      const int c = red_cnt[0] + red_cnt[1] + red_cnt[2] + red_cnt[3];
-      if (c > 0) {
-        atomicAdd(summary + 2 * f, (float)c);
-        atomicAdd(summary + 2 * f + 1, sm);
-      }
-    }
-    // the halo tile and red_* are rewritten for the next frame only after everyone is done
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
 // v3 "stream" (default): candidates are rare in detector frames (synthetic epix10k2M: 0.02 % of
-// pixels above thr_peak, 0.5 % of 64-pixel wave rows contain one), so the LDS halo tile of v2 is
+// pixels above thr_peak, 0.5 % of 64-pixel wave rows contain one), so an LDS halo tile is
 // overhead: here every pixel is read ONCE with coalesced 16-B loads (4 float4 per lane in flight),
 // thresholded in registers, and only the rare candidates read their neighbourhood directly from
 // global memory (just-touched lines, L1/L2 hits).  No halo over-fetch, no LDS, no barrier except
 // the per-block reduction of the hit statistics.
 // ---------------------------------------------------------------------------------------------
-// Grid-stride over 16-KB chunks (PSANA_RAY_PF_BLOCKS workgroups for the whole batch, default 2048
-// = 8 per CU): the per-frame hit statistics are device-scope atomics to ONE address pair per frame,
-// and same-address atomics serialise (~3 ns each, measured: read_f32 with one atomic per 8-KB
+// Grid-stride over 16-KB chunks (~2048 workgroups for the whole batch = 8 per CU): the per-frame
+// hit statistics are device-scope atomics to ONE address pair per frame, and same-address atomics serialise (~3 ns each, measured: read_f32 with one atomic per 8-KB
 // block 3.09 us/frame vs 1.81 with one per 16 KB), so a workgroup owns many chunks and issues its
 // two atomics once.  The next chunk's loads are issued before the current chunk's rare candidate
 // tests so the memory pipe stays busy.
@@ -408,12 +185,6 @@ __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp
   }
 }
 
-static int pf_version() {   // PSANA_RAY_PF_VERSION: 1 | 2 (LDS tiles) | 3 (stream, default)
-  if (const char* e = getenv("PSANA_RAY_PF_V1"); e && e[0] == '1') return 1;
-  if (const char* e = getenv("PSANA_RAY_PF_VERSION"); e && *e) return atoi(e);
-  return 3;
-}
-
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
                      float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
                      uint64_t summary, uint64_t total, uint64_t stream) {
@@ -428,47 +199,18 @@ void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, i
   int* C = reinterpret_cast<int*>(counts);
   float* S = reinterpret_cast<float*>(summary);
   unsigned long long* T = reinterpret_cast<unsigned long long*>(total);
-  const int ver = pf_version();
-  if (ver == 3) {
-    // float4 per lane (PSANA_RAY_PF_K: 4 | 8 | 16, A/B): K=4 2.21, 8 2.22, 16 2.26 us/frame; nontemporal
-    // loads measured no faster (profiles/kernels_r1_peakfind_ab.jsonl)
-    int K = 4;
-    if (const char* e = getenv("PSANA_RAY_PF_K"); e && *e) K = atoi(e);
-    check(K == 4 || K == 8 || K == 16, "peakfind: PSANA_RAY_PF_K must be 4, 8 or 16");
-    const int64_t n4 = (int64_t)n_panels * rows * cols / 4;
-    const int64_t nchunks = (n4 + 256 * K - 1) / (256 * K);
-    // workgroups per frame: ~PSANA_RAY_PF_BLOCKS for the whole batch (default 2048 = 8 per CU);
-    // 0 = one workgroup per chunk (the previous grid, A/B)
-    int64_t target = 2048;
-    if (const char* e = getenv("PSANA_RAY_PF_BLOCKS"); e && *e) target = atoll(e);
-    const int64_t per_frame = target <= 0 ? nchunks : std::min(nchunks, std::max<int64_t>(4, (target + nframes - 1) / nframes));
-    const dim3 grid((unsigned)per_frame, (unsigned)nframes);
-#define PR_PF3(R_, K_) hipLaunchKernelGGL((peakfind_stream_kernel<R_, K_>), grid, dim3(256), 0, s, fp, pp, P, C, S, T)
-    if (radius == 1) {
-      if (K == 4) PR_PF3(1, 4); else if (K == 8) PR_PF3(1, 8); else PR_PF3(1, 16);
-    } else {
-      if (K == 4) PR_PF3(2, 4); else if (K == 8) PR_PF3(2, 8); else PR_PF3(2, 16);
-    }
-#undef PR_PF3
-  } else if (ver == 1) {
-    const int tiles = ((cols + kPfTX - 1) / kPfTX) * ((rows + kPfTY - 1) / kPfTY);
-    const dim3 grid((unsigned)(tiles * n_panels), (unsigned)nframes);
-    if (radius == 1)
-      hipLaunchKernelGGL(peakfind_v1_kernel<1>, grid, dim3(256), 0, s, fp, pp, P, C, S, T);
-    else
-      hipLaunchKernelGGL(peakfind_v1_kernel<2>, grid, dim3(256), 0, s, fp, pp, P, C, S, T);
-  } else {
-    const int tiles = ((cols + kPf2TX - 1) / kPf2TX) * ((rows + kPf2TY - 1) / kPf2TY) * n_panels;
-    // frame groups: enough workgroups to fill the chip (>= ~4096), the rest of the batch is walked
-    // by each workgroup with the next frame prefetched (PSANA_RAY_PF_GROUPS overrides, A/B)
-    int groups = std::max(1, std::min(nframes, (4096 + tiles - 1) / tiles));
-    if (const char* e = getenv("PSANA_RAY_PF_GROUPS"); e && *e) groups = std::max(1, std::min(nframes, atoi(e)));
-    const dim3 grid((unsigned)tiles, (unsigned)groups);
-    if (radius == 1)
-      hipLaunchKernelGGL(peakfind_kernel<1>, grid, dim3(256), 0, s, fp, nframes, pp, P, C, S, T);
-    else
-      hipLaunchKernelGGL(peakfind_kernel<2>, grid, dim3(256), 0, s, fp, nframes, pp, P, C, S, T);
-  }
+  // 4 float4 per lane (round-1 A/B: K=4 2.21, 8 2.22, 16 2.26 us/frame; nontemporal loads no
+  // faster; profiles/kernels_r1_peakfind_ab.jsonl); ~2048 workgroups for the whole batch (8 per CU)
+  constexpr int K = 4;
+  const int64_t n4 = (int64_t)n_panels * rows * cols / 4;
+  const int64_t nchunks = (n4 + 256 * K - 1) / (256 * K);
+  const int64_t target = 2048;
+  const int64_t per_frame = std::min(nchunks, std::max<int64_t>(4, (target + nframes - 1) / nframes));
+  const dim3 grid((unsigned)per_frame, (unsigned)nframes);
+  if (radius == 1)
+    hipLaunchKernelGGL((peakfind_stream_kernel<1, K>), grid, dim3(256), 0, s, fp, pp, P, C, S, T);
+  else
+    hipLaunchKernelGGL((peakfind_stream_kernel<2, K>), grid, dim3(256), 0, s, fp, pp, P, C, S, T);
   hip_check(hipGetLastError(), "peakfind launch");
 }
 

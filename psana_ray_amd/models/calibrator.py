@@ -14,7 +14,6 @@ On a CUDA(HIP) device the HIP kernels are mandatory (no silent PyTorch fallback)
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -73,12 +72,11 @@ class Calibrator:
                 imap = self.geometry.index_map()
                 self.idx = torch.from_numpy(imap).to(self.device)
                 kernels._validate_index_map(self.idx, spec.npix, "Calibrator")
-                if os.environ.get("PSANA_RAY_IMAGE_V1") != "1":
-                    # LDS-tiled assembly (csrc/image.hip); the image mask folds into its codes
-                    tm = build_tile_map(imap, spec, self.geometry.image_shape, image_mask)
-                    self.tile_map = tm
-                    self._tiles = torch.from_numpy(tm.tiles).to(self.device)
-                    self._codes = torch.from_numpy(tm.codes).to(self.device)
+                # LDS-tiled assembly (csrc/image.hip); the image mask folds into its codes
+                tm = build_tile_map(imap, spec, self.geometry.image_shape, image_mask)
+                self.tile_map = tm
+                self._tiles = torch.from_numpy(tm.tiles).to(self.device)
+                self._codes = torch.from_numpy(tm.codes).to(self.device)
                 self.omask = None if image_mask is None else \
                     torch.from_numpy(np.asarray(image_mask).astype(np.uint8).ravel()).to(self.device)
             if self.cm is not None:
@@ -159,15 +157,23 @@ class Calibrator:
             place = self.geometry.panel_placement() if self.cm is not None else None
             if self.cm is None and (self.omask is None or self.tile_map is not None):
                 p.mode = 3
-            elif place is not None and os.environ.get("PSANA_RAY_IMAGE_CM_FUSED", "1") != "0":
+            elif place is not None:
                 # common mode writes the assembled image from its LDS tiles (no scratch round trip);
-                # a fill kernel zeroes the gaps between panels
+                # a fill kernel zeroes the gaps between panels.  Every panel pixel lands on exactly
+                # one image pixel, so the image mask folds into this plan's gain factors (the
+                # common-mode eligibility is unchanged: the reference masks after assembly)
                 p.mode = 5
                 self._img_desc = torch.from_numpy(place.ravel().copy()).to(self.device)
                 self._gap_runs = torch.from_numpy(self.geometry.gap_runs().ravel().copy()).to(self.device)
                 p.img_desc, p.gap_runs = int(self._img_desc.data_ptr()), int(self._gap_runs.data_ptr())
                 p.n_gap_runs = int(self._gap_runs.numel() // 2)
-                p.omask = 0 if self.omask is None else int(self.omask.data_ptr())
+                if self.image_mask is not None:
+                    imap = self.geometry.index_map().ravel()
+                    keep = np.ones(spec.npix, dtype=np.float32)
+                    hit = imap >= 0
+                    keep[imap[hit]] = (np.asarray(self.image_mask).ravel()[hit] != 0).astype(np.float32)
+                    self._gf_img = (self.gf.view(-1, spec.npix) * torch.from_numpy(keep).to(self.device)).contiguous()
+                    p.gf = int(self._gf_img.data_ptr())
             else:
                 p.mode = 4
                 self._scratch = torch.empty((kernels.MAX_FRAMES, *spec.frame_shape), dtype=torch.float32,

@@ -36,7 +36,9 @@ log = logging.getLogger(__name__)
 class ProducerPipeline:
     def __init__(self, source, calibrator: Optional[Calibrator], endpoint: QueueEndpoint, rank: int = 0,
                  chunk: int = 32, n_raw_buffers: int = 6, acquire_timeout_s: float = 1.0,
-                 log_every: int = 0):
+                 log_every: int = 0, copy_workgroups: int = 32, gpu_timing: bool = False):
+        """copy_workgroups: host->HBM staging by copy_h2d_kernel with that many workgroups (0 = the
+        runtime's hipMemcpyAsync); gpu_timing: event-time each chunk's copy and calibration."""
         self.source = source
         self.cal = calibrator
         self.ep = endpoint
@@ -81,7 +83,8 @@ class ProducerPipeline:
             self.engine = C.ProducerEngine(ring.pool, ring.frame_bytes, dev_index,
                                            calibrator.plan, self.chunk, n_raw_buffers,
                                            int(getattr(source, "event_rank", rank)),
-                                           int(getattr(source, "size", 1)))
+                                           int(getattr(source, "size", 1)),
+                                           copy_workgroups=int(copy_workgroups), gpu_timing=bool(gpu_timing))
             self.engine.set_header_rank(int(rank))
             if zero_copy is not None:
                 ptrs, pe = zero_copy
@@ -190,7 +193,7 @@ class ProducerPipeline:
         if self.engine is not None:
             st, acq, launch, commit, total = self.engine.timing()
             d.update(host_stage_s=st, host_acquire_s=acq, host_launch_s=launch, host_commit_s=commit)
-            if self.engine.gpu_timing_enabled:   # PSANA_RAY_ENGINE_GPU_TIMING=1: event-timed GPU stages
+            if self.engine.gpu_timing_enabled:   # gpu_timing=True: event-timed GPU stages
                 h2d_ms, h2d_n, cal_ms, cal_n = self.engine.gpu_timing()
                 d.update(gpu_h2d_ms_per_chunk=h2d_ms / max(1.0, h2d_n), gpu_calib_ms_per_chunk=cal_ms / max(1.0, cal_n),
                          gpu_chunks_timed=cal_n)

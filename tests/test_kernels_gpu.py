@@ -5,10 +5,19 @@ import torch
 
 from psana_ray_amd.config import CommonModeParams, PeakFinderParams
 from psana_ray_amd.models import CalibConstants, Calibrator, Mode, get_detector, make_geometry
+from psana_ray_amd.models.detector import DetectorSpec, register
 from psana_ray_amd.ops import kernels, reference
 from psana_ray_amd.source import generate_raw
 
 pytestmark = pytest.mark.gpu
+
+# ASIC shapes that route the common-mode launcher (csrc/common_mode.hip, launch_calib_cm) to each
+# of its kernels: epix10k2M -> 176x48 compile-time net kernel, jungfrau -> 256x128 compile-time
+# net kernel, tiny_epix -> 8-column-bank net kernel (runtime shape), cm_epix174 -> 48-column-bank
+# net kernel (runtime shape), cm_epix44 / cm_jf64 / tiny_jungfrau -> generic bitonic kernel
+register(DetectorSpec("cm_epix174", "epix10ka", 2, 174, 96, 174, 96, 48, 100.0, panel_gap_px=2))
+register(DetectorSpec("cm_epix44", "epix10ka", 2, 88, 96, 44, 48, 16, 100.0, panel_gap_px=2))
+register(DetectorSpec("cm_jf64", "jungfrau", 1, 128, 128, 64, 64, 32, 75.0, panel_gap_px=2))
 
 
 def _setup(det, n, seed=0, gain_config="mixed"):
@@ -42,21 +51,10 @@ def test_calib_basic_bitwise(cuda_device, det, masked):
     _assert_equal(out, ref, f"calib {det}")
 
 
-@pytest.mark.parametrize("det,stripe,colq,gather,cdims", [
-    ("tiny_epix", "", "", "", ""), ("tiny_epix", "", "2", "", ""), ("epix10k2M", "", "", "", ""),
-    ("epix10k2M", "", "", "", "0"), ("epix10k2M", "", "", "0", ""), ("epix10k2M", "0", "", "", ""),
-    ("epix10k2M", "96", "", "", ""), ("epix10k2M", "48", "", "", "0"), ("epix10k2M", "", "2", "", ""),
-    ("epix10k2M", "0", "2", "", ""), ("jungfrau05M", "", "", "", ""), ("jungfrau05M", "", "", "", "0")])
+@pytest.mark.parametrize("det", ["tiny_epix", "epix10k2M", "jungfrau05M", "cm_epix174", "cm_epix44", "cm_jf64",
+                                 "tiny_jungfrau"])
 @pytest.mark.parametrize("flags", [1, 2, 3])
-def test_common_mode_bitwise(cuda_device, det, stripe, colq, gather, cdims, flags, monkeypatch):
-    # stripe: PSANA_RAY_CM_STRIPE caps the full-height stripe width ("" default = 48 for epix,
-    # one bank per stripe; "0" full width); colq: lanes per column ("" default = 4-lane quad
-    # merge, "2" two-lane merge-path); cdims "0": runtime tile shape instead of the compile-time
-    # instantiations (epix10k2M 176x96 / 176x48, Jungfrau 256x128)
-    monkeypatch.setenv("PSANA_RAY_CM_CONSTDIMS", cdims)
-    monkeypatch.setenv("PSANA_RAY_CM_STRIPE", stripe)
-    monkeypatch.setenv("PSANA_RAY_CM_COLQ", colq)
-    monkeypatch.setenv("PSANA_RAY_CM_GATHER", gather)   # "" = default select-then-load
+def test_common_mode_bitwise(cuda_device, det, flags):
     n = 2 if det in ("epix10k2M", "jungfrau05M") else 5
     spec, consts, raw = _setup(det, n, seed=11, gain_config="mixed")
     cm = CommonModeParams(flags=flags, thr=30.0, maxcorr=50.0, npix_min=5)
@@ -93,23 +91,19 @@ def test_common_mode_even_odd_and_empty_segments(cuda_device):
     _assert_equal(out, ref, "cm edge cases")
 
 
-@pytest.mark.parametrize("version", ["tiles", "tiles256", "v1", "nofuse"])
 @pytest.mark.parametrize("det,cm", [("tiny_epix", None), ("tiny_epix", "3,30,50,5"), ("epix10k2M", None),
                                     ("epix10k2M", "default"), ("tiny_jungfrau", None), ("tiny_jungfrau", "default"),
                                     ("jungfrau05M", None), ("jungfrau05M", "default"), ("tiny_plain", None)])
-def test_image_mode_matches_scatter(cuda_device, det, cm, version, monkeypatch):
-    """With common mode the default plan is the fused kernel (image written from the LDS tiles,
-    gaps zero-filled); "nofuse" is the two-pass scratch path.  Outputs start as NaN so unwritten
-    (gap) pixels show up."""
-    monkeypatch.setenv("PSANA_RAY_IMAGE_V1", "1" if version == "v1" else "0")
-    monkeypatch.setenv("PSANA_RAY_IMAGE_BLOCK", "256" if version == "tiles256" else "")
-    monkeypatch.setenv("PSANA_RAY_IMAGE_CM_FUSED", "0" if version == "nofuse" else "1")
+def test_image_mode_matches_scatter(cuda_device, det, cm):
+    """Without common mode: the LDS-tiled fused calibration + assembly; with common mode the CM
+    kernel writes the image from its LDS tiles (gaps zero-filled).  Outputs start as NaN so
+    unwritten (gap) pixels show up."""
     n = 2 if det in ("epix10k2M", "jungfrau05M") else 37   # 37 > 32: launch chunking
     spec, consts, raw = _setup(det, n, seed=21)
     cmp = CommonModeParams.parse(cm)
     cal = Calibrator(consts, cuda_device, Mode.image, common_mode=cmp)
-    assert (cal.tile_map is not None) == (version != "v1")
-    assert (cal.plan.mode == 5) == (cm is not None and version != "nofuse")
+    assert cal.tile_map is not None
+    assert (cal.plan.mode == 5) == (cm is not None)
     out = torch.full((n, *cal.out_shape), float("nan"), device=cuda_device)
     raw = raw.to(cuda_device)
     cal.run([raw[i] for i in range(n)], [out[i] for i in range(n)])
@@ -121,11 +115,11 @@ def test_image_mode_matches_scatter(cuda_device, det, cm, version, monkeypatch):
     _assert_equal(out, ref, f"image {det}")
 
 
-@pytest.mark.parametrize("version", ["tiles", "v1", "nofuse"])
-@pytest.mark.parametrize("det,cm", [("tiny_epix", None), ("epix10k2M", None), ("epix10k2M", "default")])
-def test_image_mask_applied_after_assembly(cuda_device, det, cm, version, monkeypatch):
-    monkeypatch.setenv("PSANA_RAY_IMAGE_V1", "1" if version == "v1" else "0")
-    monkeypatch.setenv("PSANA_RAY_IMAGE_CM_FUSED", "0" if version == "nofuse" else "1")
+@pytest.mark.parametrize("det,cm", [("tiny_epix", None), ("tiny_epix", "3,30,50,5"), ("epix10k2M", None),
+                                    ("epix10k2M", "default")])
+def test_image_mask_applied_after_assembly(cuda_device, det, cm):
+    """Image-shaped masks: folded into the tile codes (no common mode) or into the fused plan's
+    gain factors (common mode; eligibility unchanged, the reference masks after assembly)."""
     spec, consts, raw = _setup(det, 3, seed=4)
     geo = make_geometry(spec)
     imask = (np.random.default_rng(1).random(geo.image_shape) > 0.3).astype(np.uint8)
@@ -146,15 +140,9 @@ def _sorted_peaks(p):
     return p[torch.argsort(key)]
 
 
-@pytest.mark.parametrize("version", ["stream", "stream_k4", "stream_k16", "tiles", "tiles_walk", "v1"])
 @pytest.mark.parametrize("radius", [1, 2])
 @pytest.mark.parametrize("det", ["tiny_epix", "tiny_plain", "epix10k2M", "jungfrau05M"])
-def test_peakfind_vs_reference(cuda_device, det, radius, version, monkeypatch):
-    monkeypatch.setenv("PSANA_RAY_PF_V1", "1" if version == "v1" else "0")
-    monkeypatch.setenv("PSANA_RAY_PF_VERSION", "3" if version.startswith("stream") else "2")
-    monkeypatch.setenv("PSANA_RAY_PF_K", version.split("_k")[1] if "_k" in version else "")
-    # tiles_walk: one frame group -> every workgroup walks all frames with the next one prefetched
-    monkeypatch.setenv("PSANA_RAY_PF_GROUPS", "1" if version == "tiles_walk" else "")
+def test_peakfind_vs_reference(cuda_device, det, radius):
     spec, consts, raw = _setup(det, 3, seed=8, gain_config="AHL")
     frames = reference.calibrate_reference(raw.to(torch.int32), consts, None, None)
     params = PeakFinderParams(thr_peak=15.0, son_min=4.0, radius=radius, max_peaks=4096)
@@ -190,10 +178,10 @@ def test_kernel_rejects_bad_shapes(cuda_device):
         kernels.calib_basic([raw[0]], [torch.empty(spec.npix)], cal.ped, cal.gf, spec.kernel_kind)
 
 
-@pytest.mark.parametrize("det", ["tiny_epix", "epix10k2M", "jungfrau05M"])
-def test_common_mode_generic_kernel_bitwise(cuda_device, det, monkeypatch):
-    """The generic whole-wave bitonic kernel (any tile size) stays exact as well."""
-    monkeypatch.setenv("PSANA_RAY_CM_GENERIC", "1")
+@pytest.mark.parametrize("det", ["cm_epix44", "cm_jf64", "tiny_jungfrau"])
+def test_common_mode_generic_kernel_bitwise(cuda_device, det):
+    """Shapes without a compile-time network run the generic whole-wave bitonic kernel (any tile
+    size): exact as well, with a frame mask and mixed gain configuration."""
     spec, consts, raw = _setup(det, 2, seed=13, gain_config="mixed")
     cm = CommonModeParams(flags=3, thr=30.0, maxcorr=50.0, npix_min=5)
     mask = _mask(spec)

@@ -15,11 +15,10 @@ from psana_ray_amd.source import SyntheticRun
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("cm,copy_kernel", [(None, "32"), ("default", "32"), ("default", "0")])
-def test_local_pipeline_frames_exact(cuda_device, cm, copy_kernel, monkeypatch):
+@pytest.mark.parametrize("cm,copy_kernel", [(None, 32), ("default", 32), ("default", 0)])
+def test_local_pipeline_frames_exact(cuda_device, cm, copy_kernel):
     """copy_kernel: staging copies by copy_h2d_kernel (csrc/gather.hip, default 32 workgroups) or
     by hipMemcpyAsync (0)."""
-    monkeypatch.setenv("PSANA_RAY_COPY_KERNEL", copy_kernel)
     n_events = 50
     src = SyntheticRun("synthetic", 3, "epix10k2M", n_events=n_events, pool_frames=8, pinned=True,
                        gen_device="cuda")
@@ -27,7 +26,7 @@ def test_local_pipeline_frames_exact(cuda_device, cm, copy_kernel, monkeypatch):
     cal = Calibrator(src.consts, cuda_device, Mode.calib, common_mode=cmp)
     ring = FrameRing(cal.out_shape, cal.out_dtype, cuda_device, 16, 12)   # small ring: backpressure
     ep = QueueEndpoint(ring)
-    prod = ProducerPipeline(src, cal, ep, chunk=8)
+    prod = ProducerPipeline(src, cal, ep, chunk=8, copy_workgroups=copy_kernel)
     t = threading.Thread(target=prod.run)
     t.start()
     ref = reference.calibrate_reference(torch.from_numpy(src.pool.astype(np.int32)), src.consts, None, cal.cm)
@@ -54,7 +53,7 @@ def test_local_pipeline_frames_exact(cuda_device, cm, copy_kernel, monkeypatch):
     assert prod.engine is not None, "the native producer engine must run on a GPU"
     span, single, by_kernel = prod.engine.copy_stats()
     assert span + single > 0
-    assert (by_kernel == span + single) if copy_kernel != "0" else by_kernel == 0
+    assert (by_kernel == span + single) if copy_kernel != 0 else by_kernel == 0
 
 
 def test_peakfinder_consumer_counts(cuda_device):
@@ -167,14 +166,13 @@ def test_file_source_native_engine(cuda_device, tmp_path, monkeypatch, zero_copy
     assert sorted(seen) == list(range(5, 70)) and all(v == 1 for v in seen.values())
 
 
-def test_engine_gpu_stage_timing(cuda_device, monkeypatch):
-    """PSANA_RAY_ENGINE_GPU_TIMING=1: the engine event-times every chunk's H2D copy and calibration."""
-    monkeypatch.setenv("PSANA_RAY_ENGINE_GPU_TIMING", "1")
+def test_engine_gpu_stage_timing(cuda_device):
+    """gpu_timing=True: the engine event-times every chunk's H2D copy and calibration."""
     src = SyntheticRun("synthetic", 6, "epix10k2M", n_events=96, pool_frames=8, pinned=True, gen_device="cuda")
     cal = Calibrator(src.consts, cuda_device, Mode.calib, common_mode=CommonModeParams())
     ring = FrameRing(cal.out_shape, cal.out_dtype, cuda_device, 64, 128)
     ep = QueueEndpoint(ring)
-    prod = ProducerPipeline(src, cal, ep, chunk=16)
+    prod = ProducerPipeline(src, cal, ep, chunk=16, gpu_timing=True)
     assert prod.engine.gpu_timing_enabled
     prod.run()
     h2d_ms, h2d_n, cal_ms, cal_n = prod.engine.gpu_timing()
