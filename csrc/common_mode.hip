@@ -187,9 +187,13 @@ struct TileGeom {
 // + translation (geometry.py), so pixel (y, x) of panel p lands at image element
 // desc[3p] + y * desc[3p+1] + x * desc[3p+2]; the corrected tile goes from LDS straight into the
 // assembled image instead of a frame-shaped scratch buffer that a second kernel re-reads
-// (saves a 2 x 8.65 MB HBM round trip per epix10k2M frame).  Gap pixels: launch_fill_runs.
+// (saves a 2 x 8.65 MB HBM round trip per epix10k2M frame).  The gap pixels between panels are
+// zeroed by the same kernel: workgroup (tile t, frame f) takes its 1/n_tiles share of the gap
+// runs, read with scalar loads so no vector load sits between its stores.
 struct ImgOut {
   const int32_t* desc;    // [n_panels][3] (base, step per panel row, step per panel column); nullptr: frame layout
+  const int2* gaps;       // [n_gaps] (start, length) image runs no panel covers: zeroed by the kernel
+  int n_gaps;
 };
 
 // ---- tile layout ------------------------------------------------------------------------
@@ -222,10 +226,12 @@ struct SideCtx {
   int used;       // wave-uniform running count
 };
 
-__device__ __forceinline__ SideCtx side_ctx(float* side, int nslots) {
-  const int wave = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+__device__ __forceinline__ SideCtx side_ctx(float* side, int nslots, int wave, int nw) {
   const int per = nslots / nw;
   return SideCtx{side, wave * per, wave * per + per, 0};
+}
+__device__ __forceinline__ SideCtx side_ctx(float* side, int nslots) {
+  return side_ctx(side, nslots, (int)threadIdx.x >> 6, (int)(blockDim.x >> 6));
 }
 
 // Claims a slot for every lane with `needs` (call convergently: all lanes of the wave) and writes
@@ -417,38 +423,82 @@ __device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C,
 }
 
 // Image layout (fused K-05): every panel sits in the image by an integer rotation + translation,
-// so either tile rows or tile columns are contiguous image runs (step +-1).  16-B stores when the
-// runs are 16-B aligned, 4-B stores otherwise.  The image mask is folded into the gain factors
-// of this plan (Calibrator), so no mask loads sit between the stores.
+// so either tile rows or tile columns are contiguous image runs (step +-1).  Each run is cut into
+// 16-B aligned image chunks: whole chunks are 16-B stores, the (at most two) partial chunks at the
+// ends of a run 4-B stores.  The image mask is folded into the gain factors of this plan
+// (Calibrator), so no mask loads sit between the stores.
+__device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, int tile, int ntiles, PR_GLOBAL float* out) {
+  if (io.n_gaps <= 0) return;
+  const int r0 = (int)((int64_t)io.n_gaps * tile / ntiles), r1 = (int)((int64_t)io.n_gaps * (tile + 1) / ntiles);
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), nw = (int)blockDim.x >> 6;
+  const int lane = (int)threadIdx.x & 63;
+  for (int j = r0 + wave; j < r1; j += nw) {
+    const int2 rr = io.gaps[j];   // wave-uniform address: scalar load
+    for (int k = lane; k < rr.y; k += 64) out[(int64_t)rr.x + k] = 0.0f;
+  }
+}
+
 __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C, const ImgOut& io, int panel, int y0,
                                          int x0, PR_GLOBAL float* out) {
   const int32_t* d = io.desc + 3 * panel;
   const int sy = d[1], sx = d[2];
   const int64_t b0 = (int64_t)d[0] + (int64_t)y0 * sy + (int64_t)x0 * sx;
   const bool rows = sx == 1 || sx == -1;           // image runs along tile rows (else along columns)
-  const int inner = rows ? C : R;                   // run length
+  const int len = rows ? C : R;                     // run length
+  const int nruns = rows ? R : C;
   const int step = rows ? sx : sy;                  // +-1 along the run
-  const int64_t outer_stride = rows ? sy : sx;      // image step between runs
-  const int64_t lo0 = step > 0 ? b0 : b0 - 3;       // lowest address of a run's first 4 elements
-  if ((inner & 3) == 0 && (lo0 & 3) == 0 && (outer_stride & 3) == 0) {
-    const int n4 = inner >> 2;
-    for (int e = threadIdx.x; e < (rows ? R : C) * n4; e += blockDim.x) {
-      const int a = e / n4, j = e - a * n4;       // run a, elements 4j..4j+3 of it
-      float v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = rows ? tile[a * P + 4 * j + k] : tile[(4 * j + k) * P + a];
-      const int64_t q = b0 + (int64_t)a * outer_stride + (step > 0 ? 4 * j : -4 * j - 3);
-      st_f4((PR_GLOBAL float4*)(out + q),
-            step > 0 ? make_float4(v[0], v[1], v[2], v[3]) : make_float4(v[3], v[2], v[1], v[0]));
+  const int64_t outer = rows ? sy : sx;             // image step between runs
+  if ((outer & 3) != 0) {                           // runs not equally aligned: 4-B stores
+    for (int e = threadIdx.x; e < R * C; e += blockDim.x) {
+      const int a = e / len, t = e - a * len;
+      const int r = rows ? a : t, c = rows ? t : a;
+      out[b0 + (int64_t)r * sy + (int64_t)c * sx] = tile[r * P + c];
     }
     return;
   }
-  const float inv = 1.0f / (float)inner;   // e < 2^24: floor((e + 0.5) / inner) is exact in f32
-  for (int e = threadIdx.x; e < R * C; e += blockDim.x) {
-    const int a = (int)(((float)e + 0.5f) * inv);
-    const int bb = e - a * inner;
-    const int r = rows ? a : bb, c = rows ? bb : a;
-    out[b0 + (int64_t)r * sy + (int64_t)c * sx] = tile[r * P + c];
+  const int64_t lo = step > 0 ? b0 : b0 - (len - 1);   // lowest image address of run 0
+  const int head = (int)(lo & 3);                       // the same for every run
+  const int nch = (head + len + 3) >> 2;                // aligned chunks per run
+  // lanes -> (run, chunk): rows-case runs are tile rows (contiguous in LDS too), so consecutive
+  // lanes take consecutive chunks of one run; column-case runs are tile columns, so a wave takes 4
+  // chunks (64 B of image) of 16 neighbouring columns -- LDS reads 2-way instead of 32-way
+  // bank-conflicted, global stores 16 segments of 64 B.  The (run, chunk) walk is incremental (one
+  // integer division per thread, not per chunk).
+  const int span = rows ? nch : ((nch + 3) >> 2) * 4;   // work items per run (column case: padded)
+  const int nb = (int)blockDim.x;
+  int a = (int)threadIdx.x / (rows ? nch : 4 * nruns), w = (int)threadIdx.x - a * (rows ? nch : 4 * nruns);
+  // rows: (a, w = chunk); columns: (a = chunk quad, w = 4 * run + chunk within the quad)
+  const int per = rows ? nch : 4 * nruns;
+  const int da = nb / per, dw = nb - da * per;
+  const int outer_n = rows ? nruns : (span >> 2);
+  for (; a < outer_n;) {
+    const int run = rows ? a : (w >> 2);
+    const int ch = rows ? w : 4 * a + (w & 3);
+    if (ch < nch) {
+      const int64_t sb = lo + (int64_t)run * outer;      // this run's lowest address
+      const int64_t base = (sb & ~(int64_t)3) + 4 * ch;
+      const int t0 = 4 * ch - head;                      // position of base in lowest-address order
+      const int rb = rows ? run * P : run;               // tile address of element i: rb + i * ie
+      const int ie = rows ? 1 : P;
+      if (t0 >= 0 && t0 + 3 < len) {
+        const int i0 = step > 0 ? t0 : len - 1 - t0;
+        const int di = step > 0 ? ie : -ie;
+        const float* tp = tile + rb + i0 * ie;
+        st_f4((PR_GLOBAL float4*)(out + base), make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int t = t0 + k;
+          if (t >= 0 && t < len) out[base + k] = tile[rb + (step > 0 ? t : len - 1 - t) * ie];
+        }
+      }
+    }
+    a += da;
+    w += dw;
+    if (w >= per) {
+      w -= per;
+      ++a;
+    }
   }
 }
 
@@ -458,11 +508,15 @@ __device__ __forceinline__ void cm_put8(float* trow, const float (&o)[8]) {
 }
 
 __device__ __forceinline__ void cm_write_out(const float* tile, int P, int R, int C, const TileGeom& tg,
-                                             const ImgOut& io, int panel, int y0, int x0, int64_t base,
+                                             const ImgOut& io, int tile_id, int panel, int y0, int x0, int64_t base,
                                              PR_GLOBAL float* out) {
   __syncthreads();
-  if (io.desc != nullptr) cm_place(tile, P, R, C, io, panel, y0, x0, out);
-  else cm_flush(tile, P, R, C, out, base, tg.panel_cols);
+  if (io.desc != nullptr) {
+    cm_place(tile, P, R, C, io, panel, y0, x0, out);
+    cm_fill_gaps(io, tile_id, (int)gridDim.x / tg.nframes, out);
+  } else {
+    cm_flush(tile, P, R, C, out, base, tg.panel_cols);
+  }
 }
 
 // Phase 3 (runtime-shape loop form).
@@ -470,7 +524,8 @@ template <int KIND, int NT>
 __device__ __forceinline__ void cm_store(float* tile, const float* side, const int P, const int R, const int C,
                                          const TileGeom& tg, const PR_GLOBAL uint16_t* raw,
                                          const float* __restrict__ ped, const float* __restrict__ gf, int64_t base,
-                                         PR_GLOBAL float* out, const ImgOut& io, int panel, int y0, int x0) {
+                                         PR_GLOBAL float* out, const ImgOut& io, int tile_id, int panel, int y0,
+                                         int x0) {
   const int C8 = C >> 3;
   for (int i = threadIdx.x; i < R * C8; i += blockDim.x) {
     const int r = i / C8, k = i - r * C8, c = k * 8;
@@ -483,12 +538,12 @@ __device__ __forceinline__ void cm_store(float* tile, const float* side, const i
     cm_out8<KIND, NT>(tile + r * P + c, side, cb, slot, ga, raw, ped, tg.npix, pix, o);
     cm_put8(tile + r * P + c, o);
   }
-  cm_write_out(tile, P, R, C, tg, io, panel, y0, x0, base, out);
+  cm_write_out(tile, P, R, C, tg, io, tile_id, panel, y0, x0, base, out);
 }
 
 // (tile, frame) of this workgroup and the tile's first pixel
 struct TileCoord {
-  int f, panel, ar, ac;
+  int f, tile, panel, ar, ac;
   int64_t base;
 };
 // Table-major order: consecutive workgroups take the same tile of consecutive frames, so the
@@ -501,6 +556,7 @@ __device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C)
   const int id = (int)blockIdx.x;
   const int tile = id / tg.nframes;
   t.f = id - tile * tg.nframes;
+  t.tile = tile;
   const int per_panel = tg.asics_per_col * tg.asics_per_row;
   t.panel = tile / per_panel;
   t.ar = (tile % per_panel) / tg.asics_per_row;
@@ -627,7 +683,7 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
     __syncthreads();
   }
 
-  cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.panel, t.ar * R, t.ac * C);
+  cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.tile, t.panel, t.ar * R, t.ac * C);
 }
 
 // ==========================================================================================
@@ -672,6 +728,206 @@ __device__ __forceinline__ void bitonic_merge_vpad(float (&z)[N]) {
 
 // TR / TC: the tile rows / columns as compile-time constants for the production shapes (0 = from
 // TileGeom): every LDS address in the unrolled loops is then a base VGPR + immediate offset.
+// Phase 1, compile-time tile shape: decode + pedestal of the tile into LDS by BLOCK threads
+// (thread index tid in [0, BLOCK)).
+template <int KIND, int NT, int BLOCK, int TR, int TC>
+__device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int P, const TileGeom& tg,
+                                            const PR_GLOBAL uint16_t* raw, const float* __restrict__ ped,
+                                            const uint8_t* __restrict__ planes, const int64_t base, const int tid) {
+  constexpr int C = TC;
+  constexpr int NITEMS = TR * (TC / 8);
+  constexpr int NI = (NITEMS + BLOCK - 1) / BLOCK;
+  // all of this lane's raw / plane / first-table loads in flight at once; the rare switched-gain
+  // tables are loaded per group while decoding (select-then-load, the wave waits only when one of
+  // its lanes needs them), which keeps the live registers at raw + planes + one table
+  constexpr int C8 = TC / 8;
+  uint4 rw[NI];
+  uint32_t ep[NI];
+  float pa0[NI][1][8];
+#pragma unroll
+  for (int u = 0; u < NI; ++u) {
+    const int i = tid + u * BLOCK;
+    if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
+      const int r = i / C8, c = (i % C8) * 8;
+      const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
+      rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
+      ep[u] = load_planes<NT>(planes, pix);
+      load8<1>(ped, tg.npix, pix, 1u, pa0[u]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NI; ++u) {
+    const int i = tid + u * BLOCK;
+    const bool act = (u + 1) * BLOCK <= NITEMS || i < NITEMS;
+    const int r = act ? i / C8 : 0, k = act ? i % C8 : 0, c = k * 8;
+    float v[8];
+    uint32_t el = 0xFFu, cb = 0;
+    if (act) {
+      float pa[NT][8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pa[0][j] = pa0[u][0][j];
+      if constexpr (NT > 1)
+        load8<NT>(ped, tg.npix, base + (int64_t)r * tg.panel_cols + c, need_from_raw<NT>(rw[u]), pa, 1);
+      cm_decode8<KIND, NT>(rw[u], ep[u], pa, v, el, cb);
+      float x[8];
+      cm_tile_values(v, el, x);
+      float* trow = tile + r * P + c;
+      *reinterpret_cast<float4*>(trow) = make_float4(x[0], x[1], x[2], x[3]);
+      *reinterpret_cast<float4*>(trow + 4) = make_float4(x[4], x[5], x[6], x[7]);
+    }
+    const uint32_t slot = side_put(sc, act && el != 0xFFu, v);   // convergent: whole wave
+    if (act) cm_put_meta<NT>(reinterpret_cast<uint8_t*>(tile + r * P + C), C, k, cb, slot);
+  }
+}
+
+// Row-segment medians (one lane per (row, bank) segment), threads t0, t0 + nt, ... of the workgroup.
+template <int L>
+__device__ __forceinline__ void cm_rows(float* tile, const int P, const int R, const int C, const CmParams& cp,
+                                        const int t0, const int nt) {
+  const float INF = __int_as_float(0x7f800000);
+  const int nbank = C / L;
+  for (int sgi = t0; sgi < R * nbank; sgi += nt) {
+    const int b = sgi / R, r = sgi % R;           // consecutive lanes -> consecutive rows
+    float* seg = tile + r * P + b * L;
+    float x[L];
+    int cnt = 0;
+    float pad = -INF;
+    if constexpr (L % 4 == 0) {
+#pragma unroll
+      for (int j = 0; j < L; j += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(seg + j);
+        const float e[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool pt = fabsf(e[u]) < cp.thr;
+          cnt += pt ? 1 : 0;
+          x[j + u] = pt ? e[u] : pad;
+          pad = pt ? pad : -pad;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const float e = seg[j];
+        const bool pt = fabsf(e) < cp.thr;
+        cnt += pt ? 1 : 0;
+        x[j] = pt ? e : pad;
+        pad = pt ? pad : -pad;
+      }
+    }
+    asm volatile("" ::: "memory");   // keep the write-back's LDS reads below the network
+    constexpr int PA = (L & 1) ? (L - 1) / 2 : L / 2 - 1;
+    constexpr int PB = PA + 1;
+    select_regs<L, PA, PB>(x);
+    asm volatile("" ::: "memory");
+    // toggle padding: L even -> odd count: x[L/2], even: mean of x[L/2-1], x[L/2];
+    //                 L odd  -> odd count: x[(L-1)/2], even: mean of x[(L-1)/2], x[(L+1)/2]
+    float med;
+    if constexpr ((L & 1) == 0) med = (cnt & 1) ? x[PB] : (x[PA] + x[PB]) * 0.5f;
+    else med = (cnt & 1) ? x[PA] : (x[PA] + x[PB]) * 0.5f;
+    if (cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
+      // every element minus the median: NaN (non-eligible) stays NaN
+      if constexpr (L % 4 == 0) {
+#pragma unroll
+        for (int j = 0; j < L; j += 4) {
+          float4 q = *reinterpret_cast<const float4*>(seg + j);
+          q.x -= med; q.y -= med; q.z -= med; q.w -= med;
+          *reinterpret_cast<float4*>(seg + j) = q;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < L; ++j) seg[j] -= med;
+      }
+    }
+  }
+}
+
+// Column medians, FOUR lanes (a quad) per column, M rows each (t0 a multiple of 4):
+//  each lane sorts its M values (sort_regs<M>); lanes (q, q^1) merge-split (lower lane keeps
+//  min(x[i], partner[M-1-i]), upper the max) and sort the resulting bitonic sequences (the
+//  lower lane negated so both are V-shaped: bitonic_merge_vpad); the two sorted halves of the
+//  pair (0,1) and of the pair (2,3) are then merged by merge-path for k = 2M-1 and 2M with ONE
+//  quad_perm(3,2,1,0) fetch per register.
+template <int M>
+__device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, const int C, const CmParams& cp,
+                                        const int t0, const int nt) {
+  const float INF = __int_as_float(0x7f800000);
+  const float QNAN = __int_as_float(0x7fc00000);
+  const int nwork = 4 * C;
+  for (int w = t0; w < ((nwork + 63) / 64) * 64; w += nt) {
+    const bool act = w < nwork;
+    const int c = act ? (w >> 2) : 0;
+    const int q = w & 3;
+    const bool lower = (q & 1) == 0;
+    float* colp = tile + (q * M) * P + c;
+    float x[M];
+    int my_cnt = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const bool in = act && q * M + i < R;
+      const float v = in ? colp[i * P] : QNAN;
+      const bool pt = fabsf(v) < cp.thr;
+      my_cnt += pt ? 1 : 0;
+      x[i] = pt ? v : QNAN;
+      if ((i & 15) == 15) asm volatile("" ::: "memory");
+    }
+    // quad totals + exclusive prefix of the non-participants: balanced +-inf padding
+    const int my_inv = M - my_cnt;
+    const int i0 = dpp_quad_i<0x00>(my_inv), i1 = dpp_quad_i<0x55>(my_inv);
+    const int i2 = dpp_quad_i<0xAA>(my_inv), i3 = dpp_quad_i<0xFF>(my_inv);
+    const int total_inv = i0 + i1 + i2 + i3;
+    const int cnt = 4 * M - total_inv;
+    const int a = total_inv >> 1;
+    const int prefix = (q > 0 ? i0 : 0) + (q > 1 ? i1 : 0) + (q > 2 ? i2 : 0);
+    const int neg_budget = min(my_inv, max(0, a - prefix));
+    int ninv = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const bool inv = x[i] != x[i];
+      x[i] = inv ? (ninv < neg_budget ? -INF : INF) : x[i];
+      ninv += inv ? 1 : 0;
+    }
+    asm volatile("" ::: "memory");
+    sort_regs<M>(x);
+    // level 1: merge-split with lane q^1 (partner read reversed)
+    float z[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const float pv = dpp_quad<0xB1>(x[M - 1 - i]);
+      const float y = lower ? fminf(x[i], pv) : fmaxf(x[i], pv);
+      z[i] = lower ? -y : y;   // both lanes V-shaped
+    }
+    bitonic_merge_vpad<M>(z);
+#pragma unroll
+    for (int i = 0; i < M; ++i) x[i] = lower ? -z[M - 1 - i] : z[i];   // ascending half of the pair
+    asm volatile("" ::: "memory");
+    // level 2: merge-path of pair (0,1) with pair (2,3); lane 0 reads lane 3, lane 1 lane 2
+    float kh = INF, kl = INF, plast = INF;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const float pj = dpp_quad<0x1B>(x[j]);
+      kh = fminf(kh, fmaxf(x[M - 1 - j], pj));
+      if (j <= M - 2) kl = fminf(kl, fmaxf(x[M - 2 - j], pj));
+      if (j == M - 1) plast = pj;
+    }
+    const float e = dpp_quad<0xAA>(x[M - 1]);   // lane 2's last element
+    const float extra = q == 0 ? fminf(plast, fmaxf(x[M - 1], e)) : x[M - 1];
+    kl = fminf(kl, extra);
+    kl = fminf(kl, dpp_quad<0xB1>(kl));
+    kh = fminf(kh, dpp_quad<0xB1>(kh));
+    const float k_lo = dpp_quad<0x00>(kl), k_hi = dpp_quad<0x00>(kh);   // lane 0 has the answer
+    const float med = (k_lo + ((cnt & 1) ? k_lo : k_hi)) * 0.5f;
+    asm volatile("" ::: "memory");
+    if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        if (q * M + i < R) colp[i * P] -= med;   // NaN (non-eligible) stays NaN
+        if ((i & 15) == 15) asm volatile("" ::: "memory");
+      }
+    }
+  }
+}
+
 template <int KIND, int L, int M, int BLOCK, int TR = 0, int TC = 0>
 __global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
     const FramePtrs fp, const float* __restrict__ ped, const float* __restrict__ gf,
@@ -686,8 +942,6 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
   SideCtx sc = side_ctx(side, tg.side_slots);
   const TileCoord t = cm_coords(tg, R, C);
   const int tid = threadIdx.x;
-  const float INF = __int_as_float(0x7f800000);
-  const float QNAN = __int_as_float(0x7fc00000);
   const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[t.f]);
   PR_GLOBAL float* out = gout<float>(fp.out[t.f]);
 
@@ -695,49 +949,7 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
   constexpr int NITEMS = (TR > 0 && TC > 0) ? TR * (TC / 8) : 0;
   constexpr int NI = NITEMS > 0 ? (NITEMS + BLOCK - 1) / BLOCK : 0;
   if constexpr (NI > 0 && NI <= 6) {
-    // compile-time shape: all of this lane's raw / plane / first-table loads in flight at once,
-    // then the rare switched-candidate tables (select-then-load), then decode
-    constexpr int C8 = TC / 8;
-    uint4 rw[NI];
-    uint32_t ep[NI];
-    float pa[NI][NT][8];
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      const int i = tid + u * BLOCK;
-      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
-        const int r = i / C8, c = (i % C8) * 8;
-        const int64_t pix = t.base + (int64_t)r * tg.panel_cols + c;
-        rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
-        ep[u] = load_planes<NT>(planes, pix);
-        load8<NT>(ped, tg.npix, pix, 1u, pa[u]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      const int i = tid + u * BLOCK;
-      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
-        const int r = i / C8, c = (i % C8) * 8;
-        load8<NT>(ped, tg.npix, t.base + (int64_t)r * tg.panel_cols + c, need_from_raw<NT>(rw[u]), pa[u], 1);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      const int i = tid + u * BLOCK;
-      const bool act = (u + 1) * BLOCK <= NITEMS || i < NITEMS;
-      const int r = act ? i / C8 : 0, k = act ? i % C8 : 0, c = k * 8;
-      float v[8];
-      uint32_t el = 0xFFu, cb = 0;
-      if (act) {
-        cm_decode8<KIND, NT>(rw[u], ep[u], pa[u], v, el, cb);
-        float x[8];
-        cm_tile_values(v, el, x);
-        float* trow = tile + r * P + c;
-        *reinterpret_cast<float4*>(trow) = make_float4(x[0], x[1], x[2], x[3]);
-        *reinterpret_cast<float4*>(trow + 4) = make_float4(x[4], x[5], x[6], x[7]);
-      }
-      const uint32_t slot = side_put(sc, act && el != 0xFFu, v);   // convergent: whole wave
-      if (act) cm_put_meta<NT>(reinterpret_cast<uint8_t*>(tile + r * P + C), C, k, cb, slot);
-    }
+    cm_load_net<KIND, NT, BLOCK, TR, TC>(tile, sc, P, tg, raw, ped, planes, t.base, tid);
   } else {
     cm_phase1<KIND, NT>(tile, sc, P, R, C, tg, raw, ped, planes, t.base);
   }
@@ -745,144 +957,13 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
 
   // ---- phase 2a: rows by bank, one lane per segment ----------------------------------------
   if (cp.flags & 1) {
-    const int nbank = C / L;
-    for (int sgi = tid; sgi < R * nbank; sgi += blockDim.x) {
-      const int b = sgi / R, r = sgi % R;           // consecutive lanes -> consecutive rows
-      float* seg = tile + r * P + b * L;
-      float x[L];
-      int cnt = 0;
-      float pad = -INF;
-      if constexpr (L % 4 == 0) {
-#pragma unroll
-        for (int j = 0; j < L; j += 4) {
-          const float4 q = *reinterpret_cast<const float4*>(seg + j);
-          const float e[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const bool pt = fabsf(e[u]) < cp.thr;
-            cnt += pt ? 1 : 0;
-            x[j + u] = pt ? e[u] : pad;
-            pad = pt ? pad : -pad;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < L; ++j) {
-          const float e = seg[j];
-          const bool pt = fabsf(e) < cp.thr;
-          cnt += pt ? 1 : 0;
-          x[j] = pt ? e : pad;
-          pad = pt ? pad : -pad;
-        }
-      }
-      asm volatile("" ::: "memory");   // keep the write-back's LDS reads below the network
-      constexpr int PA = (L & 1) ? (L - 1) / 2 : L / 2 - 1;
-      constexpr int PB = PA + 1;
-      select_regs<L, PA, PB>(x);
-      asm volatile("" ::: "memory");
-      // toggle padding: L even -> odd count: x[L/2], even: mean of x[L/2-1], x[L/2];
-      //                 L odd  -> odd count: x[(L-1)/2], even: mean of x[(L-1)/2], x[(L+1)/2]
-      float med;
-      if constexpr ((L & 1) == 0) med = (cnt & 1) ? x[PB] : (x[PA] + x[PB]) * 0.5f;
-      else med = (cnt & 1) ? x[PA] : (x[PA] + x[PB]) * 0.5f;
-      if (cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
-        // every element minus the median: NaN (non-eligible) stays NaN
-        if constexpr (L % 4 == 0) {
-#pragma unroll
-          for (int j = 0; j < L; j += 4) {
-            float4 q = *reinterpret_cast<const float4*>(seg + j);
-            q.x -= med; q.y -= med; q.z -= med; q.w -= med;
-            *reinterpret_cast<float4*>(seg + j) = q;
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < L; ++j) seg[j] -= med;
-        }
-      }
-    }
+    cm_rows<L>(tile, P, R, C, cp, tid, blockDim.x);
     __syncthreads();
   }
 
-  // ---- phase 2b: columns, FOUR lanes (a quad) per column, M rows each ------------------------
-  //  each lane sorts its M values (sort_regs<M>); lanes (q, q^1) merge-split (lower lane keeps
-  //  min(x[i], partner[M-1-i]), upper the max) and sort the resulting bitonic sequences (the
-  //  lower lane negated so both are V-shaped: bitonic_merge_vpad); the two sorted halves of the
-  //  pair (0,1) and of the pair (2,3) are then merged by merge-path for k = 2M-1 and 2M with ONE
-  //  quad_perm(3,2,1,0) fetch per register.
+  // ---- phase 2b: columns ---------------------------------------------------------------------
   if (cp.flags & 2) {
-    const int nwork = 4 * C;
-    for (int w = tid; w < ((nwork + 63) / 64) * 64; w += blockDim.x) {
-      const bool act = w < nwork;
-      const int c = act ? (w >> 2) : 0;
-      const int q = w & 3;
-      const bool lower = (q & 1) == 0;
-      float* colp = tile + (q * M) * P + c;
-      float x[M];
-      int my_cnt = 0;
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        const bool in = act && q * M + i < R;
-        const float v = in ? colp[i * P] : QNAN;
-        const bool pt = fabsf(v) < cp.thr;
-        my_cnt += pt ? 1 : 0;
-        x[i] = pt ? v : QNAN;
-        if ((i & 15) == 15) asm volatile("" ::: "memory");
-      }
-      // quad totals + exclusive prefix of the non-participants: balanced +-inf padding
-      const int my_inv = M - my_cnt;
-      const int i0 = dpp_quad_i<0x00>(my_inv), i1 = dpp_quad_i<0x55>(my_inv);
-      const int i2 = dpp_quad_i<0xAA>(my_inv), i3 = dpp_quad_i<0xFF>(my_inv);
-      const int total_inv = i0 + i1 + i2 + i3;
-      const int cnt = 4 * M - total_inv;
-      const int a = total_inv >> 1;
-      const int prefix = (q > 0 ? i0 : 0) + (q > 1 ? i1 : 0) + (q > 2 ? i2 : 0);
-      const int neg_budget = min(my_inv, max(0, a - prefix));
-      int ninv = 0;
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        const bool inv = x[i] != x[i];
-        x[i] = inv ? (ninv < neg_budget ? -INF : INF) : x[i];
-        ninv += inv ? 1 : 0;
-      }
-      asm volatile("" ::: "memory");
-      sort_regs<M>(x);
-      // level 1: merge-split with lane q^1 (partner read reversed)
-      float z[M];
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        const float pv = dpp_quad<0xB1>(x[M - 1 - i]);
-        const float y = lower ? fminf(x[i], pv) : fmaxf(x[i], pv);
-        z[i] = lower ? -y : y;   // both lanes V-shaped
-      }
-      bitonic_merge_vpad<M>(z);
-#pragma unroll
-      for (int i = 0; i < M; ++i) x[i] = lower ? -z[M - 1 - i] : z[i];   // ascending half of the pair
-      asm volatile("" ::: "memory");
-      // level 2: merge-path of pair (0,1) with pair (2,3); lane 0 reads lane 3, lane 1 lane 2
-      float kh = INF, kl = INF, plast = INF;
-#pragma unroll
-      for (int j = 0; j < M; ++j) {
-        const float pj = dpp_quad<0x1B>(x[j]);
-        kh = fminf(kh, fmaxf(x[M - 1 - j], pj));
-        if (j <= M - 2) kl = fminf(kl, fmaxf(x[M - 2 - j], pj));
-        if (j == M - 1) plast = pj;
-      }
-      const float e = dpp_quad<0xAA>(x[M - 1]);   // lane 2's last element
-      const float extra = q == 0 ? fminf(plast, fmaxf(x[M - 1], e)) : x[M - 1];
-      kl = fminf(kl, extra);
-      kl = fminf(kl, dpp_quad<0xB1>(kl));
-      kh = fminf(kh, dpp_quad<0xB1>(kh));
-      const float k_lo = dpp_quad<0x00>(kl), k_hi = dpp_quad<0x00>(kh);   // lane 0 has the answer
-      const float med = (k_lo + ((cnt & 1) ? k_lo : k_hi)) * 0.5f;
-      asm volatile("" ::: "memory");
-      if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          if (q * M + i < R) colp[i * P] -= med;   // NaN (non-eligible) stays NaN
-          if ((i & 15) == 15) asm volatile("" ::: "memory");
-        }
-      }
-    }
+    cm_cols<M>(tile, P, R, C, cp, tid, blockDim.x);
     __syncthreads();
   }
 
@@ -918,9 +999,9 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
         cm_put8(tile + r * P + c, o);
       }
     }
-    cm_write_out(tile, P, R, C, tg, io, t.panel, t.ar * R, t.ac * C, t.base, out);
+    cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, t.base, out);
   } else {
-    cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.panel, t.ar * R, t.ac * C);
+    cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.tile, t.panel, t.ar * R, t.ac * C);
   }
 }
 
@@ -952,7 +1033,8 @@ static void cm_launch(K kernel, dim3 grid, int block, size_t lds, hipStream_t s,
 
 void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t planes, int kind,
                      int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
-                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream, uint64_t img_desc) {
+                     float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream, uint64_t img_desc,
+                     uint64_t gap_runs, int n_gap_runs) {
   check(nframes >= 1 && nframes <= kMaxFrames, "calib_cm: nframes out of range");
   check(asic_rows >= 1 && asic_rows <= 256, "calib_cm: ASIC rows must be in [1, 256]");
   check(asic_cols % 8 == 0 && asic_cols >= 8, "calib_cm: ASIC cols must be a multiple of 8");
@@ -993,7 +1075,9 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   check(aligned16(ped) && aligned16(gf) && (planes & 3) == 0, "calib_cm: misaligned constant tables");
   for (int f = 0; f < nframes; ++f)
     check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_cm: frame buffers must be 16-B aligned");
-  const ImgOut io{reinterpret_cast<const int32_t*>(img_desc)};
+  check(n_gap_runs == 0 || (img_desc != 0 && gap_runs != 0 && gap_runs % 8 == 0), "calib_cm: bad gap run table");
+  const ImgOut io{reinterpret_cast<const int32_t*>(img_desc), reinterpret_cast<const int2*>(gap_runs),
+                  img_desc != 0 ? n_gap_runs : 0};
   // LDS budget of one workgroup: the epix10k2M 176x48 stripe runs four workgroups per CU, the
   // narrow compile-time kernels two, everything else one; what the tile leaves is side slots
   const size_t budget = (epix_prod && asic_cols == 48) ? 40 * 1024 : (net && !jf_prod && asic_cols <= 128) ? 80 * 1024

@@ -51,8 +51,7 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
         check(p.use_cm && p.img_desc != 0, "run_calib_plan: fused image plan without common mode / placement");
         const FramePtrs fp = ptrs_of(in, out, a, b);
         launch_calib_cm(fp, n, p.ped, p.gf, p.elig, p.kind, p.n_panels, p.panel_rows, p.panel_cols, p.asic_rows,
-                        p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags, p.bank_cols, stream, p.img_desc);
-        launch_fill_runs(fp, n, p.gap_runs, p.n_gap_runs, stream);
+                        p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags, p.bank_cols, stream, p.img_desc, p.gap_runs, p.n_gap_runs);
         break;
       }
       case kPlanImageScratch: {
