@@ -164,41 +164,36 @@ PYBIND11_MODULE(_C, m) {
   m.def("peakfind",
         [](const std::vector<uint64_t>& in, int n_panels, int rows, int cols, float thr_peak, float son_min,
            int radius, int max_peaks, uint64_t peaks, uint64_t counts, uint64_t summary, uint64_t stream,
-           uint64_t total) {
+           uint64_t total, uint64_t scratch) {
           pr::launch_peakfind(make_ptrs(in, in), (int)in.size(), n_panels, rows, cols, thr_peak, son_min,
-                              radius, max_peaks, peaks, counts, summary, total, stream);
+                              radius, max_peaks, peaks, counts, summary, total, stream, scratch);
         },
         py::arg("in_ptrs"), py::arg("n_panels"), py::arg("rows"), py::arg("cols"), py::arg("thr_peak"),
         py::arg("son_min"), py::arg("radius"), py::arg("max_peaks"), py::arg("peaks"), py::arg("counts"),
-        py::arg("summary"), py::arg("stream"), py::arg("total") = 0);
-  // consumer hot path: ring slots -> zeroed per-batch outputs -> peak finder, one native call
+        py::arg("summary"), py::arg("stream"), py::arg("total") = 0, py::arg("scratch") = 0);
+  m.attr("PF_SCRATCH_BYTES") = pr::kPfScratchBytes;
+  // consumer hot path: ring slots -> peak finder with self-resetting outputs, one native call
   m.def("peakfind_slots",
         [](const pr::SlotPool& pool, int64_t slot_bytes, const std::vector<int>& slots, int n_panels, int rows,
            int cols, float thr_peak, float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
-           uint64_t summary, uint64_t total, uint64_t stream, uint64_t zero_ptr, int64_t zero_bytes) {
+           uint64_t summary, uint64_t total, uint64_t stream, uint64_t scratch) {
           const int n = (int)slots.size();
           pr::check(n >= 1, "peakfind_slots: no slots");
           pr::check(slot_bytes >= (int64_t)n_panels * rows * cols * 4, "peakfind_slots: frame larger than a slot");
-          hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-          if (zero_ptr != 0) {   // caller-provided region covering counts + summary: one fill
-            pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(zero_ptr), 0, (size_t)zero_bytes, s), "zero outputs");
-          } else {
-            pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(counts), 0, (size_t)n * 4, s), "zero counts");
-            pr::hip_check(hipMemsetAsync(reinterpret_cast<void*>(summary), 0, (size_t)n * 8, s), "zero summary");
-          }
+          pr::check(scratch != 0, "peakfind_slots: needs a zero-initialised scratch block (PF_SCRATCH_BYTES)");
           for (int a = 0; a < n; a += pr::kMaxFrames) {
             const int m = std::min(pr::kMaxFrames, n - a);
             std::vector<uint64_t> in(m);
             for (int i = 0; i < m; ++i) in[i] = pool.slot_ptr(slots[a + i]);
             pr::launch_peakfind(make_ptrs(in, in), m, n_panels, rows, cols, thr_peak, son_min, radius, max_peaks,
                                 peaks + (uint64_t)a * max_peaks * 32, counts + (uint64_t)a * 4,
-                                summary + (uint64_t)a * 8, total, stream);
+                                summary + (uint64_t)a * 8, total, stream, scratch);
           }
         },
         py::arg("pool"), py::arg("slot_bytes"), py::arg("slots"), py::arg("n_panels"), py::arg("rows"),
         py::arg("cols"), py::arg("thr_peak"), py::arg("son_min"), py::arg("radius"), py::arg("max_peaks"),
         py::arg("peaks"), py::arg("counts"), py::arg("summary"), py::arg("total"), py::arg("stream"),
-        py::arg("zero_ptr") = 0, py::arg("zero_bytes") = 0, py::call_guard<py::gil_scoped_release>());
+        py::arg("scratch"), py::call_guard<py::gil_scoped_release>());
 
   m.def("copy_h2d_kernel",
         [](uint64_t dst, uint64_t src, int64_t bytes, int workgroups, uint64_t stream) {

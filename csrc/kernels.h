@@ -33,7 +33,11 @@ void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool 
 bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgroups, uint64_t stream);
 void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nout, uint64_t omask,
                      uint64_t stream);
+// scratch: 0, or a zero-initialised PfScratch block (kPfScratchBytes) reused by every launch on one
+// stream: counts / summary then need no zeroing before the launch (csrc/peakfind.hip)
+constexpr int kPfScratchBytes = 4 * (3 * kMaxFrames + 1);
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
                      float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
-                     uint64_t summary, uint64_t total, uint64_t stream);
+                     uint64_t summary, uint64_t total, uint64_t stream,
+                     uint64_t scratch = 0);
 }  // namespace pr

@@ -104,13 +104,28 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
 // block 3.09 us/frame vs 1.81 with one per 16 KB), so a workgroup owns many chunks and issues its
 // two atomics once.  The next chunk's loads are issued before the current chunk's rare candidate
 // tests so the memory pipe stays busy.
+//
+// Self-resetting outputs (`scratch` != nullptr): the slot counters and hit statistics accumulate in
+// a persistent scratch block instead of in `counts` / `summary`; the LAST workgroup to finish
+// (device-scope done counter) moves them to the outputs and zeroes the scratch for the next
+// launch on the stream -- so a consumer needs no per-batch fill kernel before the peak finder.
+struct PfScratch {
+  int tickets[kMaxFrames];
+  float acc[2 * kMaxFrames];
+  unsigned int done;
+};
+
 template <int RAD, int K>
 __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp, const PfParams pp,
-                                                              float* __restrict__ peaks, int* __restrict__ counts,
-                                                              float* __restrict__ summary,
-                                                              unsigned long long* __restrict__ total) {
+                                                              float* __restrict__ peaks, int* __restrict__ counts_out,
+                                                              float* __restrict__ summary_out,
+                                                              unsigned long long* __restrict__ total,
+                                                              PfScratch* __restrict__ scratch, const int nframes) {
   __shared__ float red_sum[4];
   __shared__ int red_cnt[4];
+  __shared__ int is_last;
+  int* counts = scratch != nullptr ? scratch->tickets : counts_out;
+  float* summary = scratch != nullptr ? scratch->acc : summary_out;
   const int f = blockIdx.y;
   const PR_GLOBAL float* img = gin<float>(fp.in[f]);
   const int64_t hw = (int64_t)pp.rows * pp.cols;
@@ -183,11 +198,27 @@ __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp
       atomicAdd(summary + 2 * f + 1, sm);
     }
   }
+  if (scratch == nullptr) return;
+  __threadfence();   // this thread's slot / statistics atomics are performed before the done count
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(&scratch->done, 1u);
+    is_last = prev == gridDim.x * gridDim.y - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();
+  for (int i = threadIdx.x; i < nframes; i += blockDim.x) {
+    counts_out[i] = atomicExch(&scratch->tickets[i], 0);
+    summary_out[2 * i] = atomicExch(&scratch->acc[2 * i], 0.0f);
+    summary_out[2 * i + 1] = atomicExch(&scratch->acc[2 * i + 1], 0.0f);
+  }
+  if (threadIdx.x == 0) atomicExch(&scratch->done, 0u);
 }
 
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
                      float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
-                     uint64_t summary, uint64_t total, uint64_t stream) {
+                     uint64_t summary, uint64_t total, uint64_t stream, uint64_t scratch) {
   check(nframes >= 1 && nframes <= kMaxFrames, "peakfind: nframes out of range");
   check(radius == 1 || radius == 2, "peakfind: radius must be 1 or 2");
   check(max_peaks >= 1, "peakfind: max_peaks must be >= 1");
@@ -207,10 +238,12 @@ void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, i
   const int64_t target = 2048;
   const int64_t per_frame = std::min(nchunks, std::max<int64_t>(4, (target + nframes - 1) / nframes));
   const dim3 grid((unsigned)per_frame, (unsigned)nframes);
+  PfScratch* X = reinterpret_cast<PfScratch*>(scratch);
+  check(scratch % 8 == 0, "peakfind: misaligned scratch");
   if (radius == 1)
-    hipLaunchKernelGGL((peakfind_stream_kernel<1, K>), grid, dim3(256), 0, s, fp, pp, P, C, S, T);
+    hipLaunchKernelGGL((peakfind_stream_kernel<1, K>), grid, dim3(256), 0, s, fp, pp, P, C, S, T, X, nframes);
   else
-    hipLaunchKernelGGL((peakfind_stream_kernel<2, K>), grid, dim3(256), 0, s, fp, pp, P, C, S, T);
+    hipLaunchKernelGGL((peakfind_stream_kernel<2, K>), grid, dim3(256), 0, s, fp, pp, P, C, S, T, X, nframes);
   hip_check(hipGetLastError(), "peakfind launch");
 }
 

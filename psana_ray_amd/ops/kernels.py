@@ -13,6 +13,8 @@ import torch
 from . import _ext
 
 MAX_FRAMES = 32
+# int32 words of the peak finder's self-resetting scratch (csrc/peakfind.hip PfScratch)
+PF_SCRATCH_WORDS = 3 * MAX_FRAMES + 1
 
 
 def _ptr(t: torch.Tensor) -> int:
@@ -116,10 +118,16 @@ def assemble(frames, out, idx: torch.Tensor, npix: int, omask: Optional[torch.Te
 
 
 def peakfind(frames: Sequence[torch.Tensor], shape, params, peaks: torch.Tensor, counts: torch.Tensor,
-             summary: torch.Tensor, stream=None, total: Optional[torch.Tensor] = None):
-    """frames: F tensors of ``shape`` = (P, H, W) f32.  Outputs (zeroed here, on the stream):
-    peaks [F, max_peaks, 8] f32, counts [F] int32, summary [F, 2] f32.  ``total`` (int64 scalar on
-    the device, optional) is incremented by the number of peak records written."""
+             summary: torch.Tensor, stream=None, total: Optional[torch.Tensor] = None,
+             scratch: Optional[torch.Tensor] = None):
+    """frames: F tensors of ``shape`` = (P, H, W) f32.  Outputs: peaks [F, max_peaks, 8] f32,
+    counts [F] int32, summary [F, 2] f32.  ``total`` (int64 scalar on the device, optional) is
+    incremented by the number of peak records written.
+
+    ``scratch``: a zero-initialised int32 tensor of PF_SCRATCH_WORDS on the frames' device, reused
+    by every call on one stream.  The kernel then accumulates there and its last workgroup writes
+    counts / summary whole and re-zeroes the scratch -- no fill kernel per call.  Without it, counts
+    and summary are zeroed here on the stream first."""
     C = _ext.load()
     P, H, W = shape
     F = len(frames)
@@ -137,14 +145,18 @@ def peakfind(frames: Sequence[torch.Tensor], shape, params, peaks: torch.Tensor,
         raise ValueError("peakfind: radius must be 1 or 2")
     if total is not None and (total.dtype != torch.int64 or total.numel() != 1 or total.device != dev):
         raise ValueError("peakfind: total must be an int64 scalar on the frames' device")
+    if scratch is not None and (scratch.dtype != torch.int32 or scratch.numel() < PF_SCRATCH_WORDS
+                                or scratch.device != dev or not scratch.is_contiguous()):
+        raise ValueError(f"peakfind: scratch must be a contiguous int32 [{PF_SCRATCH_WORDS}] tensor on the frames' device")
     s = _ext.stream_handle(stream)
-    with torch.cuda.stream(stream) if stream is not None else torch.cuda.stream(torch.cuda.current_stream()):
-        counts.zero_()
-        summary.zero_()
+    if scratch is None:
+        with torch.cuda.stream(stream) if stream is not None else torch.cuda.stream(torch.cuda.current_stream()):
+            counts.zero_()
+            summary.zero_()
     for a, b in _chunks(F):
         C.peakfind([_ptr(t) for t in frames[a:b]], P, H, W, float(params.thr_peak), float(params.son_min),
                    int(params.radius), int(params.max_peaks), _ptr(peaks[a]), _ptr(counts[a:]), _ptr(summary[a]), s,
-                   0 if total is None else _ptr(total))
+                   0 if total is None else _ptr(total), 0 if scratch is None else _ptr(scratch))
 
 
 def gather_frames(frames: Sequence[torch.Tensor], out, stream=None):

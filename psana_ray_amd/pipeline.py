@@ -261,8 +261,10 @@ class PeakFinderConsumer:
             B = self.batch
             self._nbuf = 3
             self.peaks = torch.empty((self._nbuf, B, self.params.max_peaks, 8), dtype=torch.float32, device=self.device)
-            # counts [B] int32 and summary [B, 2] f32 of a batch share ONE row, zeroed by one fill
+            # counts [B] int32 and summary [B, 2] f32 of a batch share one row; the peak finder
+            # writes them whole from its self-resetting scratch (no per-batch fill)
             self._meta = torch.zeros((self._nbuf, 3 * B), dtype=torch.int32, device=self.device)
+            self._pf_scratch = torch.zeros(kernels.PF_SCRATCH_WORDS, dtype=torch.int32, device=self.device)
             self.counts = self._meta[:, :B]
             self.summary = self._meta[:, B:].view(torch.float32).view(self._nbuf, B, 2)
             self.count_acc = torch.zeros((), dtype=torch.int64, device=self.device)
@@ -277,7 +279,8 @@ class PeakFinderConsumer:
             self._b += 1
             with torch.cuda.stream(self.stream):
                 kernels.peakfind([it.data for it in items], self.shape, self.params, self.peaks[b, :n],
-                                 self.counts[b, :n], self.summary[b, :n], self.stream, total=self.count_acc)
+                                 self.counts[b, :n], self.summary[b, :n], self.stream, total=self.count_acc,
+                                 scratch=self._pf_scratch)
                 if self.keep_results:
                     self.results.append((self.peaks[b, :n].clone(), self.counts[b, :n].clone(),
                                          [(it.rank, it.idx, it.gevt) for it in items]))
@@ -326,13 +329,14 @@ class PeakFinderConsumer:
         sh = int(self.stream.cuda_stream)
         P, H, W = self.shape
         with trace_range("consumer.peakfind_batch"):
-            # one native call: zero this batch's outputs, run the peak finder on the ring slots,
-            # bump the on-device running peak total (no per-batch torch ops, no host sync)
+            # one native call: the peak finder on the ring slots with self-resetting outputs (no
+            # fill kernel), bumping the on-device running peak total (no per-batch torch ops, no
+            # host sync)
             C.peakfind_slots(self.ep.pool, self.ep._slot_bytes, slots, P, H, W, float(self.params.thr_peak),
                              float(self.params.son_min), int(self.params.radius), int(self.params.max_peaks),
                              int(self.peaks[b].data_ptr()), int(self.counts[b].data_ptr()),
                              int(self.summary[b].data_ptr()), int(self.count_acc.data_ptr()), sh,
-                             int(self._meta[b].data_ptr()), int(self._meta.shape[1] * 4))
+                             int(self._pf_scratch.data_ptr()))
             if self.keep_results:
                 hs = self.ep.pool.headers(slots)
                 with torch.cuda.stream(self.stream):

@@ -140,9 +140,13 @@ def _sorted_peaks(p):
     return p[torch.argsort(key)]
 
 
+@pytest.mark.parametrize("scratch", [False, True])
 @pytest.mark.parametrize("radius", [1, 2])
 @pytest.mark.parametrize("det", ["tiny_epix", "tiny_plain", "epix10k2M", "jungfrau05M"])
-def test_peakfind_vs_reference(cuda_device, det, radius):
+def test_peakfind_vs_reference(cuda_device, det, radius, scratch):
+    """scratch: the self-resetting outputs (no zeroing before the call); run twice with the same
+    scratch and garbage in counts / summary to show the last workgroup writes them whole and
+    re-zeroes the scratch."""
     spec, consts, raw = _setup(det, 3, seed=8, gain_config="AHL")
     frames = reference.calibrate_reference(raw.to(torch.int32), consts, None, None)
     params = PeakFinderParams(thr_peak=15.0, son_min=4.0, radius=radius, max_peaks=4096)
@@ -152,10 +156,17 @@ def test_peakfind_vs_reference(cuda_device, det, radius):
     counts = torch.zeros(F, dtype=torch.int32, device=cuda_device)
     summary = torch.zeros((F, 2), dtype=torch.float32, device=cuda_device)
     total = torch.zeros((), dtype=torch.int64, device=cuda_device)
-    kernels.peakfind([d[i] for i in range(F)], spec.frame_shape, params, peaks, counts, summary, total=total)
+    scr = torch.zeros(kernels.PF_SCRATCH_WORDS, dtype=torch.int32, device=cuda_device) if scratch else None
+    for _ in range(2 if scratch else 1):
+        counts.fill_(12345)
+        summary.fill_(-7.0)
+        kernels.peakfind([d[i] for i in range(F)], spec.frame_shape, params, peaks, counts, summary, total=total,
+                         scratch=scr)
     torch.cuda.synchronize()
     ref_peaks, ref_summary = reference.peakfind_reference(frames, params)
-    assert int(total) == sum(min(int(c), params.max_peaks) for c in counts.cpu())
+    if scratch:
+        assert int(scr.abs().sum()) == 0, "scratch not re-zeroed by the last workgroup"
+    assert int(total) == (2 if scratch else 1) * sum(min(int(c), params.max_peaks) for c in counts.cpu())
     for f in range(F):
         n = int(counts[f])
         assert n == ref_peaks[f].shape[0], f"frame {f}: {n} peaks vs reference {ref_peaks[f].shape[0]}"
