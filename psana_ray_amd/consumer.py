@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import argparse
 import logging
+import os
 import signal
 import sys
 import time
@@ -34,6 +35,9 @@ def build_parser():
                     help="train: online PeakNetLite training from peak-finder labels (trainer.py)")
     ap.add_argument("--lr", type=float, default=1e-3, help="--task train: AdamW learning rate")
     ap.add_argument("--save", type=str, default=None, help="--task train: write the model state_dict here")
+    ap.add_argument("--ddp", action="store_true",
+                    help="--task train: data-parallel training over the consumer processes of a torchrun launch "
+                         "(gradients all-reduced by RCCL on GPUs, gloo on the CPU)")
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--max_frames", type=int, default=None)
     ap.add_argument("--thr_peak", type=float, default=20.0)
@@ -44,6 +48,22 @@ def build_parser():
     ap.add_argument("--metrics_json", type=str, default=None, help="append per-interval metrics as JSON lines")
     ap.add_argument("--log_level", type=str, default=DEFAULT_LOG_LEVEL, choices=LOG_LEVELS)
     return ap
+
+
+def _init_data_parallel(device) -> int:
+    """Join the torchrun group of the training consumers: RCCL ("nccl") on GPUs, gloo on the CPU."""
+    import torch
+    import torch.distributed as dist
+
+    if "WORLD_SIZE" not in os.environ or "RANK" not in os.environ:
+        raise SystemExit("--ddp needs a torchrun launch (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT)")
+    dev = torch.device(device)
+    if not dist.is_initialized():
+        kw = {"device_id": dev} if dev.type == "cuda" else {}
+        dist.init_process_group("nccl" if dev.type == "cuda" else "gloo", **kw)
+    log.info("data-parallel training: rank %d of %d (%s)", dist.get_rank(), dist.get_world_size(),
+             dist.get_backend())
+    return dist.get_rank()
 
 
 def main(argv=None) -> int:
@@ -91,23 +111,33 @@ def main(argv=None) -> int:
 
             ring = reader.endpoint.ring
             shape = reader.calibrator.out_shape if reader.calibrator is not None else ring.frame_shape
+            dp_rank = 0
+            if args.ddp:
+                dp_rank = _init_data_parallel(ring.device)
             trainer = OnlinePeakNetTrainer(shape, ring.device, lr=args.lr,
-                                           params=PeakFinderParams(thr_peak=args.thr_peak, son_min=args.son_min))
+                                           params=PeakFinderParams(thr_peak=args.thr_peak, son_min=args.son_min),
+                                           ddp=args.ddp)
             registry.register("trainer", lambda: {"steps": trainer.steps, "loss": trainer.last_loss})
             try:
-                for batch in reader.batches(args.batch, torch.float32, timeout=1.0):
-                    trainer.step(batch.data)
-                    n += len(batch)
-                    peaks_total = trainer.positives
-                    if stop["flag"] or (args.max_frames is not None and n >= args.max_frames):
-                        break
+                with trainer.join():
+                    for batch in reader.batches(args.batch, torch.float32, timeout=1.0):
+                        trainer.step(batch.data)
+                        n += len(batch)
+                        peaks_total = trainer.positives
+                        if stop["flag"] or (args.max_frames is not None and n >= args.max_frames):
+                            break
             except DataReaderError as e:
                 print(f"DataReader error: {e}")
                 return 1
             log.info("Consumer %s: %d training steps, last loss %.4f", cid, trainer.steps, trainer.last_loss)
-            print(f"Consumer {cid} trained: steps={trainer.steps} frames={n} loss={trainer.last_loss:.4f}")
-            if args.save:
+            print(f"Consumer {cid} trained: steps={trainer.steps} frames={n} loss={trainer.last_loss:.4f} "
+                  f"params={trainer.param_checksum():.9e}", flush=True)
+            if args.save and dp_rank == 0:
                 torch.save(trainer.model.state_dict(), args.save)
+            if args.ddp:
+                import torch.distributed as dist
+
+                dist.destroy_process_group()
         while args.task != "train" and not stop["flag"] and (args.max_frames is None or n < args.max_frames):
             try:
                 if args.task == "peakfind" and reader.endpoint is not None:

@@ -7,6 +7,13 @@ labelled by the K-07 peak finder on the GPU, and one AdamW step of
 :class:`~psana_ray_amd.models.peaknet.PeakNetLite` runs in bf16 autocast.  Everything stays on the
 consumer's GPU; the queue keeps streaming while the step runs (slots were released after the
 gather).  ``psana-ray-consumer --task train`` drives it from the command line.
+
+Data parallel (``ddp=True``, ``psana-ray-consumer --task train --ddp`` under torchrun): several
+consumer processes -- one per GPU, each draining its own queue shard -- train ONE model: the
+gradients are all-reduced by DistributedDataParallel over RCCL (backend "nccl", xGMI between the
+GPUs; gloo on the CPU).  Consumers see different numbers of batches (the queue balances by
+speed), so the loop runs under :meth:`join` (DDP's uneven-input join: a rank that ran out shadows
+the others' all-reduces until every rank is done).
 """
 from __future__ import annotations
 
@@ -24,7 +31,7 @@ from .models.peaknet import PeakNetLite, normalize_panels, peak_masks
 class OnlinePeakNetTrainer:
     def __init__(self, frame_shape, device, width: int = 16, lr: float = 1e-3,
                  params: Optional[PeakFinderParams] = None, bf16: bool = True, pos_weight: float = 20.0,
-                 miopen: bool = True):
+                 miopen: bool = True, ddp: bool = False):
         if len(frame_shape) != 3:
             raise ValueError(f"PeakNetLite trains on (panels, H, W) frames, got {tuple(frame_shape)}")
         P, H, W = frame_shape
@@ -40,7 +47,19 @@ class OnlinePeakNetTrainer:
         self.miopen = miopen
         self.params = params or PeakFinderParams()
         self.model = PeakNetLite(width).to(self.device).to(memory_format=torch.channels_last)
+        self.net = self.model
+        if ddp:
+            import torch.distributed as dist
+            from torch.nn.parallel import DistributedDataParallel
+
+            if not dist.is_initialized():
+                raise RuntimeError("OnlinePeakNetTrainer(ddp=True) needs an initialised torch.distributed group")
+            # every rank starts from rank 0's weights (DDP broadcasts them at construction)
+            self.net = DistributedDataParallel(
+                self.model, device_ids=[self.device.index] if self.device.type == "cuda" else None,
+                broadcast_buffers=False)
         self.opt = torch.optim.AdamW(self.model.parameters(), lr=lr)
+        self._pf_scratch = None
         self.bf16 = bf16 and self.device.type == "cuda"
         self.pos_weight = torch.tensor([pos_weight], device=self.device)
         self.steps = 0
@@ -58,8 +77,10 @@ class OnlinePeakNetTrainer:
             pk = torch.empty((B, mp, 8), dtype=torch.float32, device=frames.device)
             cnt = torch.empty(B, dtype=torch.int32, device=frames.device)
             sm = torch.empty((B, 2), dtype=torch.float32, device=frames.device)
+            if self._pf_scratch is None:
+                self._pf_scratch = torch.zeros(kernels.PF_SCRATCH_WORDS, dtype=torch.int32, device=frames.device)
             kernels.peakfind([frames[i] for i in range(B)], self.shape, self.params, pk, cnt, sm,
-                             torch.cuda.current_stream(frames.device))
+                             torch.cuda.current_stream(frames.device), scratch=self._pf_scratch)
         else:
             from .ops import reference
 
@@ -80,7 +101,7 @@ class OnlinePeakNetTrainer:
         self.model.train()
         ctx = torch.autocast("cuda", dtype=torch.bfloat16) if self.bf16 else contextlib.nullcontext()
         with torch.backends.cudnn.flags(enabled=self.miopen), ctx:
-            logits = self.model(x)
+            logits = self.net(x)
             loss = F.binary_cross_entropy_with_logits(logits.float(), target, pos_weight=self.pos_weight)
             self.opt.zero_grad(set_to_none=True)
             loss.backward()
@@ -90,6 +111,15 @@ class OnlinePeakNetTrainer:
         self.last_loss = float(loss.detach())
         self.positives += int(cnt.sum())
         return self.last_loss
+
+    def join(self):
+        """Context for the training loop: DDP's uneven-input join when data parallel, else nothing."""
+        return self.net.join() if self.net is not self.model else contextlib.nullcontext()
+
+    @torch.no_grad()
+    def param_checksum(self) -> float:
+        """Sum of all parameters (float64): equal on every rank of a data-parallel run."""
+        return float(sum(p.detach().double().sum() for p in self.model.parameters()))
 
     @torch.no_grad()
     def predict(self, frames: torch.Tensor) -> torch.Tensor:

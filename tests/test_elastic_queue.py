@@ -162,3 +162,23 @@ def test_undrained_producer_times_out_with_a_clear_message(store_port):
     rc, out = finish(p)
     assert rc == 1
     assert "were not taken by any consumer within --timeout" in out
+
+
+def test_competing_consumers_share_by_speed(store_port, tmp_path):
+    """P-02 (reference: consumers compete for one actor's items, so a faster consumer takes more):
+    credit water-filling over the links -- a consumer re-grants a slot only after it took the frame
+    out, so the fast one receives clearly more; every frame exactly once."""
+    n = 200
+    fast = consumer(store_port, tmp_path / "fast.jsonl", "--sleep", "0.002", "--slots", "4")
+    slow = consumer(store_port, tmp_path / "slow.jsonl", "--sleep", "0.05", "--slots", "4")
+    time.sleep(1.0)   # both attached before the stream starts
+    prod = producer(store_port, n)
+    for c in (fast, slow):
+        rc, out = finish(c)
+        assert rc == 0, out
+    rc_p, out_p = finish(prod)
+    assert rc_p == 0, out_p
+    gf, gs = frames(records(tmp_path / "fast.jsonl")), frames(records(tmp_path / "slow.jsonl"))
+    assert sorted(gf + gs) == list(range(n)), "exactly-once delivery violated"
+    assert len(gs) > 0, "the slow consumer should still receive frames"
+    assert len(gf) > 2 * len(gs), (len(gf), len(gs))

@@ -79,6 +79,51 @@ def test_train_consumer_cli_cpu(native):
     assert "trained: steps=3 frames=12" in cout, cout[-2000:]
 
 
+def test_train_consumer_ddp_cpu(native):
+    """--task train --ddp: two consumer processes of one torchrun launch drain their own shards and
+    train ONE model (DDP all-reduce; gloo on the CPU, RCCL on GPUs); the shards see different
+    numbers of batches (uneven-input join).  Both ranks end with identical parameters."""
+    import re
+    import socket
+
+    def free_port():
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            return so.getsockname()[1]
+
+    addr = f"127.0.0.1:{free_port()}"
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    n = 40
+    prod = subprocess.Popen(
+        [sys.executable, "-m", "psana_ray_amd.producer", "--exp", "synthetic", "--run", "3", "--detector_name",
+         "tiny_epix", "--calib", "--common_mode", "default", "--num_events", str(n), "--ray_address", addr,
+         "--num_consumers", "2", "--queue_size", "8", "--device", "cpu", "--timeout", "90"],
+        env={**env, "RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"}, stdout=subprocess.PIPE,
+        stderr=subprocess.STDOUT, text=True)
+    cons = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                             "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+                             "psana_ray_amd.consumer", "--ray_address", addr, "--device", "cpu", "--task", "train",
+                             "--ddp", "--batch", "4", "--timeout", "90", "--metrics_interval", "0"],
+                            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        pout, _ = prod.communicate(timeout=300)
+        cout, _ = cons.communicate(timeout=300)
+    finally:
+        for p in (prod, cons):
+            if p.poll() is None:
+                p.kill()
+    assert prod.returncode == 0, pout[-3000:]
+    assert cons.returncode == 0, cout[-3000:]
+    done = re.findall(r"trained: steps=(\d+) frames=(\d+) loss=\S+ params=([-+0-9.]+e[-+][0-9]{2})", cout)
+    assert len(done) == 2, cout[-3000:]
+    assert sum(int(f) for _, f, _ in done) == n
+    assert all(int(st) > 0 for st, _, _ in done), done
+    assert done[0][2] == done[1][2], f"ranks diverged: {done}"
+
+
 @pytest.mark.gpu
 def test_trainer_gpu_overfits_ring_batch(native, cuda_device):
     """Frames leased from an HBM ring, gathered by the HIP kernel, labelled by the HIP peak finder;
@@ -102,3 +147,31 @@ def test_trainer_gpu_overfits_ring_batch(native, cuda_device):
         last = tr.step(batch.data)
     torch.cuda.synchronize()
     assert tr.positives > 0 and np.isfinite(first) and last < 0.7 * first, (first, last)
+
+
+@pytest.mark.gpu
+def test_trainer_ddp_rccl_one_rank(native, cuda_device, monkeypatch):
+    """The data-parallel trainer on the GPU: a one-rank RCCL ("nccl") group, DDP all-reduce inside
+    every step, uneven-input join context; the loss still falls on a fixed batch."""
+    import socket
+
+    import torch.distributed as dist
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(port))
+    fr = _frames("tiny_epix", 4, device=cuda_device)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda_device)
+    try:
+        assert dist.get_backend() == "nccl"
+        tr = OnlinePeakNetTrainer(fr.shape[1:], cuda_device, width=8, lr=3e-3, miopen=False, ddp=True)
+        with tr.join():
+            first = tr.step(fr)
+            for _ in range(15):
+                last = tr.step(fr)
+        torch.cuda.synchronize()
+        assert np.isfinite(first) and last < first, (first, last)
+    finally:
+        dist.destroy_process_group()
