@@ -194,12 +194,18 @@ __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp
     const float sm = red_sum[0] + red_sum[1] + red_sum[2] + red_sum[3];
     const int c = red_cnt[0] + red_cnt[1] + red_cnt[2] + red_cnt[3];
     if (c > 0) {
-      atomicAdd(summary + 2 * f, (float)c);
-      atomicAdd(summary + 2 * f + 1, sm);
+      const float o0 = atomicAdd(summary + 2 * f, (float)c);
+      const float o1 = atomicAdd(summary + 2 * f + 1, sm);
+      // returning atomics: the wave waits until both were performed (needed before the done
+      // count below; the values themselves are not used)
+      if (scratch != nullptr) asm volatile("" ::"v"(o0), "v"(o1));
     }
   }
   if (scratch == nullptr) return;
-  __threadfence();   // this thread's slot / statistics atomics are performed before the done count
+  // Every slot reservation above was a returning device-scope atomic (the thread used its value),
+  // the statistics too: after the barrier all of this workgroup's updates are performed, so the
+  // done count needs no fence (an agent-scope fence writes back L2 -- measured: it cut the
+  // device-resident pipeline from 117k to 52k fr/s).
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned prev = atomicAdd(&scratch->done, 1u);
@@ -207,7 +213,6 @@ __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp
   }
   __syncthreads();
   if (!is_last) return;
-  __threadfence();
   for (int i = threadIdx.x; i < nframes; i += blockDim.x) {
     counts_out[i] = atomicExch(&scratch->tickets[i], 0);
     summary_out[2 * i] = atomicExch(&scratch->acc[2 * i], 0.0f);
