@@ -76,6 +76,41 @@ __global__ __launch_bounds__(256) void k_tm(const uint16_t* raw, const float* pe
   work<NTL, NTS>(raw + (size_t)f * kNpix, ped, gf, out + (size_t)f * kNpix, g);
 }
 
+// 4 pixels per lane: 8-B raw load, one 16-B store, consecutive lanes on consecutive 16 B
+template <bool TABLES>
+__global__ __launch_bounds__(256) void k_fm4(const uint16_t* raw, const float* ped, const float* gf, float* out,
+                                             int nframes) {
+  const int bpf = kNpix / 4 / 256;
+  const int f = blockIdx.x / bpf, q = (blockIdx.x % bpf) * 256 + threadIdx.x;
+  const uint2 r = *reinterpret_cast<const uint2*>(raw + (size_t)f * kNpix + 4 * (size_t)q);
+  float4 p = make_float4(0.f, 0.f, 0.f, 0.f), g = make_float4(1.f, 1.f, 1.f, 1.f);
+  if (TABLES) {
+    p = reinterpret_cast<const float4*>(ped)[q];
+    g = reinterpret_cast<const float4*>(gf)[q];
+  }
+  const float4 o = make_float4(((float)(r.x & 0x3fff) - p.x) * g.x, ((float)(r.x >> 16 & 0x3fff) - p.y) * g.y,
+                               ((float)(r.y & 0x3fff) - p.z) * g.z, ((float)(r.y >> 16 & 0x3fff) - p.w) * g.w);
+  reinterpret_cast<float4*>(out + (size_t)f * kNpix)[q] = o;
+}
+// 8 pixels per lane, but the two 16-B stores of a wave each cover 1 KiB contiguous (lane l holds
+// pixels 4l..4l+3 and 256+4l..256+4l+3 of the wave's 512-pixel span)
+__global__ __launch_bounds__(256) void k_fm8c(const uint16_t* raw, const float* ped, const float* gf, float* out,
+                                              int nframes) {
+  const int bpf = kGroups / 256;
+  const int f = blockIdx.x / bpf;
+  const int w = (blockIdx.x % bpf) * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  const size_t base = (size_t)w * 512;
+  float4 o[2];
+  for (int h = 0; h < 2; ++h) {
+    const size_t px = base + 256 * h + 4 * l;
+    const uint2 r = *reinterpret_cast<const uint2*>(raw + (size_t)f * kNpix + px);
+    const float4 p = *reinterpret_cast<const float4*>(ped + px), g = *reinterpret_cast<const float4*>(gf + px);
+    o[h] = make_float4(((float)(r.x & 0x3fff) - p.x) * g.x, ((float)(r.x >> 16 & 0x3fff) - p.y) * g.y,
+                       ((float)(r.y & 0x3fff) - p.z) * g.z, ((float)(r.y >> 16 & 0x3fff) - p.w) * g.w);
+  }
+  for (int h = 0; h < 2; ++h) *reinterpret_cast<float4*>(out + (size_t)f * kNpix + base + 256 * h + 4 * l) = o[h];
+}
+
 // table-major: consecutive blocks = the same pixels of consecutive frames (the CM kernel's order)
 __global__ __launch_bounds__(256) void k_table_major(const uint16_t* raw, const float* ped, const float* gf, float* out,
                                                      int nframes) {
@@ -176,6 +211,9 @@ int main() {
               {"frame_major_plain", k_fm<false, false>, dim3(nblk * nf)},
               {"table_major_ntload_plainstore", k_tm<true, false>, dim3(nblk * nf)},
               {"table_major_plain", k_tm<false, false>, dim3(nblk * nf)},
+              {"fm4_tables", k_fm4<true>, dim3(kNpix / 4 / 256 * nf)},
+              {"fm4_no_tables", k_fm4<false>, dim3(kNpix / 4 / 256 * nf)},
+              {"fm8_contig_stores", k_fm8c, dim3(nblk * nf)},
               {"no_tables", k_no_tables, dim3(nblk * nf)},
               {"no_tables_plain", k_no_tables_plain, dim3(nblk * nf)},
               {"write_only_f32", k_write_only, dim3(nblk * nf)},
