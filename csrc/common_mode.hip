@@ -859,13 +859,22 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
     const int c = act ? (w >> 2) : 0;
     const int q = w & 3;
     const bool lower = (q & 1) == 0;
-    float* colp = tile + (q * M) * P + c;
+    // Rows of the column per lane.  M even: lane q takes rows 8j + 2q + b (b = 0, 1), so for a
+    // fixed element the quad's four addresses differ by 2P rows -- 8 banks apart for the pitches
+    // in use (P = 52: 2P = 104 = 8 mod 32; P = 140: 280 = 24 mod 32) -- and the 8 columns of a half
+    // wave fill all 32 banks (contiguous blocks of M rows put lanes q and q + 2 on the same banks:
+    // 2-way conflicts on every column load and write-back).  The median does not depend on which
+    // lane holds which row.  M odd: contiguous blocks.
+    constexpr bool SW = (M % 2) == 0;
+    float* colp = tile + (SW ? 2 * q : q * M) * P + c;
+    auto row_of = [&](int i) { return SW ? 8 * (i >> 1) + 2 * q + (i & 1) : q * M + i; };
+    auto off_of = [&](int i) { return (SW ? 8 * (i >> 1) + (i & 1) : i) * P; };
     float x[M];
     int my_cnt = 0;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      const bool in = act && q * M + i < R;
-      const float v = in ? colp[i * P] : QNAN;
+      const bool in = act && row_of(i) < R;
+      const float v = in ? colp[off_of(i)] : QNAN;
       const bool pt = fabsf(v) < cp.thr;
       my_cnt += pt ? 1 : 0;
       x[i] = pt ? v : QNAN;
@@ -921,7 +930,7 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
     if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
 #pragma unroll
       for (int i = 0; i < M; ++i) {
-        if (q * M + i < R) colp[i * P] -= med;   // NaN (non-eligible) stays NaN
+        if (row_of(i) < R) colp[off_of(i)] -= med;   // NaN (non-eligible) stays NaN
         if ((i & 15) == 15) asm volatile("" ::: "memory");
       }
     }
