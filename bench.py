@@ -70,20 +70,27 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def _wait_links(ep, n_members: int, expect_in: int, expect_out: int, timeout_s: float = 180.0):
-    """Every member registered and every link of this rank attached (or raise)."""
+def _wait_links(ep, n_members: int, expect_in: int, expect_out: int, timeout_s: float = 120.0) -> dict:
+    """Wait until every member registered and every link of this rank attached.  A link whose
+    consumer ring could not be mapped is dropped by the fabric (only that link); after
+    ``timeout_s`` the run goes on with the links it has (the headline's balanced route keeps frames
+    on their own GPU) and the result records what was missing."""
     t0 = time.time()
     while True:
         ls = ep.links()
         n_in = sum(1 for x in ls if not x.outgoing and x.attached)
         n_out = sum(1 for x in ls if x.outgoing and x.attached)
-        if len(ep.session.members) == n_members - 1 and n_in >= expect_in and n_out >= expect_out:
-            return
+        n_fail = int(ep.metrics().get("links_failed", 0))
+        members = len(ep.session.members) + 1
+        if members == n_members and n_in >= expect_in and n_out + n_fail >= expect_out:
+            return {"complete": n_fail == 0 and n_out >= expect_out, "in": n_in, "out": n_out, "failed": n_fail}
         if ep.failed is not None:
             raise RuntimeError(f"queue fabric failed while linking: {ep.failed}")
         if time.time() - t0 > timeout_s:
-            raise TimeoutError(f"links not attached after {timeout_s:.0f} s: members {len(ep.session.members) + 1}/"
-                               f"{n_members}, in {n_in}/{expect_in}, out {n_out}/{expect_out}")
+            print(f"bench.py: links incomplete after {timeout_s:.0f} s (members {members}/{n_members}, in "
+                  f"{n_in}/{expect_in}, out {n_out}/{expect_out}, failed {n_fail}); going on without them",
+                  file=sys.stderr, flush=True)
+            return {"complete": False, "in": n_in, "out": n_out, "failed": n_fail}
         time.sleep(0.01)
 
 
@@ -210,8 +217,12 @@ def main(argv=None):
 
     stop = threading.Event()
     ep.start()
+    linking = None
     if sess is not None:
-        _wait_links(ep, world, n_prod - (1 if is_prod else 0), (world - 1) if is_prod else 0)
+        linking = _wait_links(ep, world, n_prod - (1 if is_prod else 0), (world - 1) if is_prod else 0)
+        fab = getattr(ep, "_fabric", None)
+        if fab is not None and fab.last_link_error():
+            linking["last_link_error"] = fab.last_link_error()
         barrier()
     pt = threading.Thread(target=prod.run if prod is not None else ep.finish, kwargs=dict(stop=stop) if prod else {},
                           name="producer", daemon=True)
@@ -368,6 +379,7 @@ def main(argv=None):
             "frames_sent_rank0_headline": int(c1.get("frames_sent", 0) - c0.get("frames_sent", 0)),
             "bytes_sent_rank0": st.get("bytes_sent", 0),
             "xgmi_phase": cross,
+            "links_rank0": linking,
             "staging": staging,
             "staging_copies_span_frame_kernel": copies,
             "numa_node": numa,

@@ -243,6 +243,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("batches", &pr::FabricStats::batches)
       .def_readonly("links_opened", &pr::FabricStats::links_opened)
       .def_readonly("peers_dead", &pr::FabricStats::peers_dead)
+      .def_readonly("links_failed", &pr::FabricStats::links_failed)
       .def_readonly("copy_s", &pr::FabricStats::copy_s);
   py::class_<pr::LinkStatus>(m, "LinkStatus")
       .def_readonly("peer", &pr::LinkStatus::peer)
@@ -276,6 +277,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("consumer_quiesced", &pr::QueueFabric::consumer_quiesced)
       .def_property_readonly("policy", &pr::QueueFabric::policy)
       .def("error", &pr::QueueFabric::error)
+      .def("last_link_error", &pr::QueueFabric::last_link_error)
       .def("stats", &pr::QueueFabric::stats)
       .def("links", &pr::QueueFabric::links);
 

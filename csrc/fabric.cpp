@@ -260,6 +260,11 @@ QueueFabric::~QueueFabric() {
   }
 }
 
+std::string QueueFabric::last_link_error() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return link_error_;
+}
+
 std::string QueueFabric::error() const {
   std::lock_guard<std::mutex> lk(mu_);
   return error_;
@@ -463,25 +468,39 @@ bool QueueFabric::try_attach(Link& l, double now) {
                                           std::to_string(slot_bytes_) + " bytes)");
   l.n = s->n_slots;
   l.remote.assign((size_t)l.n, 0);
-  if (s->kind == 0) {
-    l.remote_ring.reset(new ShmRegion(std::string(s->ring_name), (int64_t)l.n * slot_bytes_, false, 5.0));
-    for (int k = 0; k < l.n; ++k) l.remote[k] = l.remote_ring->ptr() + (uint64_t)k * (uint64_t)slot_bytes_;
-  } else {
-    check(device_ >= 0, "QueueFabric: a GPU consumer's ring can only be written by a GPU producer");
-    check(s->n_segs >= 1 && s->n_segs <= kMaxSegments, "QueueFabric: bad segment table in " + l.name);
-    hip_check(hipSetDevice(device_), "hipSetDevice");
-    for (int k = 0; k < s->n_segs; ++k) {
-      const SegDesc& d = s->segs[k];
-      check(d.first >= 0 && d.n >= 1 && d.first + d.n <= l.n, "QueueFabric: bad segment in " + l.name);
-      hipIpcMemHandle_t h;
-      memcpy(h.reserved, d.handle, HIP_IPC_HANDLE_SIZE);
-      void* p = nullptr;
-      hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle (consumer ring)");
-      l.ipc_ptrs.push_back(p);
-      for (int j = 0; j < d.n; ++j)
-        l.remote[d.first + j] = reinterpret_cast<uint64_t>(p) + (uint64_t)d.offset + (uint64_t)j * (uint64_t)slot_bytes_;
+  // a consumer ring this process cannot map (no peer path to that GPU, a runtime refusing the
+  // handle, a vanished shared-memory ring) makes THIS link unusable -- never the fabric: the link is
+  // dropped before the producer announces itself (so the consumer never grants to it) and the
+  // error is kept
+  try {
+    if (s->kind == 0) {
+      l.remote_ring.reset(new ShmRegion(std::string(s->ring_name), (int64_t)l.n * slot_bytes_, false, 5.0));
+      for (int k = 0; k < l.n; ++k) l.remote[k] = l.remote_ring->ptr() + (uint64_t)k * (uint64_t)slot_bytes_;
+    } else {
+      check(device_ >= 0, "QueueFabric: a GPU consumer's ring can only be written by a GPU producer");
+      check(s->n_segs >= 1 && s->n_segs <= kMaxSegments, "QueueFabric: bad segment table in " + l.name);
+      hip_check(hipSetDevice(device_), "hipSetDevice");
+      for (int k = 0; k < s->n_segs; ++k) {
+        const SegDesc& d = s->segs[k];
+        check(d.first >= 0 && d.n >= 1 && d.first + d.n <= l.n, "QueueFabric: bad segment in " + l.name);
+        hipIpcMemHandle_t h;
+        memcpy(h.reserved, d.handle, HIP_IPC_HANDLE_SIZE);
+        void* p = nullptr;
+        hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle (consumer ring)");
+        l.ipc_ptrs.push_back(p);
+        for (int j = 0; j < d.n; ++j)
+          l.remote[d.first + j] = reinterpret_cast<uint64_t>(p) + (uint64_t)d.offset + (uint64_t)j * (uint64_t)slot_bytes_;
+      }
+      for (int k = 0; k < l.n; ++k) check(l.remote[k] != 0, "QueueFabric: segment table leaves a slot unmapped");
     }
-    for (int k = 0; k < l.n; ++k) check(l.remote[k] != 0, "QueueFabric: segment table leaves a slot unmapped");
+  } catch (const std::exception& e) {
+    if (device_ >= 0) (void)hipGetLastError();
+    release_out_link(l);
+    l.dead = true;
+    std::lock_guard<std::mutex> lk(mu_);
+    ++st_.links_failed;
+    link_error_ = "link to consumer " + std::to_string(l.peer) + ": " + e.what();
+    return false;
   }
   l.g_tail = s->g_tail.load(std::memory_order_acquire);
   l.n_head = s->n_head.load(std::memory_order_acquire);

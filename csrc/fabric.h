@@ -84,6 +84,7 @@ struct FabricStats {
   int64_t grants_given = 0, grants_returned = 0, grants_reclaimed = 0;
   int64_t bytes_sent = 0, bytes_recv = 0, batches = 0;
   int64_t links_opened = 0, peers_dead = 0;
+  int64_t links_failed = 0;      // consumer ring could not be mapped (link unusable, others unaffected)
   double copy_s = 0;             // sum over batches of issue -> completion observed
 };
 
@@ -136,6 +137,7 @@ class QueueFabric {
   bool running() const { return running_.load(); }
   bool producer_drained() const { return drained_.load(); }
   std::string error() const;
+  std::string last_link_error() const;   // why the last failed link could not be mapped
   FabricStats stats() const;
   std::vector<LinkStatus> links() const;
   int policy() const { return policy_.load(); }
@@ -193,7 +195,7 @@ class QueueFabric {
   std::vector<LinkStatus> retired_;
   std::thread th_;
   mutable std::mutex mu_;  // error_, st_, status_
-  std::string error_;
+  std::string error_, link_error_;
   FabricStats st_;
   std::vector<LinkStatus> status_;
 };

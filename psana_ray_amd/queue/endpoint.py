@@ -365,6 +365,7 @@ class QueueEndpoint:
                 "frames_requeued": st.frames_requeued, "bytes_sent": st.bytes_sent, "bytes_recv": st.bytes_recv,
                 "batches": st.batches, "grants_given": st.grants_given, "grants_returned": st.grants_returned,
                 "grants_reclaimed": st.grants_reclaimed, "peers_dead": st.peers_dead,
+                "links_failed": st.links_failed,
                 "links_opened": st.links_opened, "links_live": sum(1 for ls in links if ls.attached and not ls.dead),
                 "copy_ms_per_batch": 1e3 * st.copy_s / max(1, st.batches),
                 "iterations": st.iterations, "idle_iterations": st.idle_iterations}
