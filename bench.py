@@ -290,13 +290,20 @@ def main(argv=None):
     cross_steps = args.steps if args.cross_steps is None else args.cross_steps
     if world > 1 and cross_steps > 0:
         ep.set_route("spread")
-        consume(max(2, args.warmup // 2) * B)
+        # drain what the headline policy already put into this shard (FIFO), then warm up: the
+        # window must see frames routed by the new policy, not the old backlog
+        consume(int(ep.metrics().get("ready", 0)) + max(2, args.warmup // 2) * B)
         xdt, xpw, _, x0, x1 = window(cross_steps)
         xtotal = world * cross_steps * B
         sent = allsum(int(x1.get("bytes_sent", 0) - x0.get("bytes_sent", 0)))
         fr_sent = allsum(int(x1.get("frames_sent", 0) - x0.get("frames_sent", 0)))
         fr_local = allsum(int(x1.get("frames_local", 0) - x0.get("frames_local", 0)))
         cms = allsum(round(float(x1.get("copy_ms_per_batch", 0.0)), 3))
+        keys = ("grants_given", "grants_returned", "grants_reclaimed", "frames_recv", "frames_requeued")
+        fab = allsum({k: int(x1.get(k, 0) - x0.get(k, 0)) for k in keys} |
+                     {"credits": int(x1.get("credits", 0)), "ready": int(x1.get("ready", 0)),
+                      "held": int(x1.get("held", 0)),
+                      "links": [[int(l.peer), bool(l.outgoing), int(l.outstanding), int(l.frames)] for l in ep.links()]})
         cross = {
             "route": "spread", "steps": cross_steps, "ms_per_step": round(1e3 * xdt / cross_steps, 4),
             "frames_per_s": round(min(xtotal, xpw) / xdt, 2),
@@ -304,6 +311,7 @@ def main(argv=None):
             "cross_gpu_fraction": round(sum(fr_sent) / max(1, sum(fr_sent) + sum(fr_local)), 3),
             "bytes_sent_per_rank": sent, "frames_sent_per_rank": fr_sent, "frames_local_per_rank": fr_local,
             "copy_ms_per_batch_per_rank": cms,
+            "fabric_per_rank": fab,
             "data_plane": "HIP IPC peer copies (hipMemcpyAsync D2D into the consumer's ring) over xGMI",
         }
         ep.set_route(args.route)

@@ -183,6 +183,8 @@ struct QueueFabric::Link {
   std::vector<uint64_t> remote;       // address of every slot of the consumer ring (this process's view)
   std::vector<void*> ipc_ptrs;        // one mapping per ring segment
   std::unique_ptr<ShmRegion> remote_ring;
+  hipStream_t stream = nullptr;       // this link's copy stream: copies to different consumers
+                                      // (different xGMI links) run concurrently
   int inflight = 0;
   bool eos_posted = false, acked_close = false;
   // consumer side (incoming)
@@ -210,6 +212,7 @@ struct QueueFabric::Link {
 
 struct QueueFabric::Batch {
   std::shared_ptr<Link> link;
+  hipStream_t stream = nullptr;
   std::vector<int> slots, rslots;
   std::vector<SlotHeader> hdrs;
   hipEvent_t ev = nullptr;
@@ -502,6 +505,10 @@ bool QueueFabric::try_attach(Link& l, double now) {
     link_error_ = "link to consumer " + std::to_string(l.peer) + ": " + e.what();
     return false;
   }
+  if (device_ >= 0 && l.stream == nullptr) {
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    hip_check(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking), "hipStreamCreate (fabric link)");
+  }
   l.g_tail = s->g_tail.load(std::memory_order_acquire);
   l.n_head = s->n_head.load(std::memory_order_acquire);
   s->producer_pid.store((int64_t)getpid(), std::memory_order_release);
@@ -510,7 +517,12 @@ bool QueueFabric::try_attach(Link& l, double now) {
 }
 
 void QueueFabric::release_out_link(Link& l) {
-  if (!l.ipc_ptrs.empty() && device_ >= 0) (void)hipSetDevice(device_);
+  if ((!l.ipc_ptrs.empty() || l.stream != nullptr) && device_ >= 0) (void)hipSetDevice(device_);
+  if (l.stream != nullptr) {
+    (void)hipStreamSynchronize(l.stream);
+    (void)hipStreamDestroy(l.stream);
+    l.stream = nullptr;
+  }
   for (void* p : l.ipc_ptrs) (void)hipIpcCloseMemHandle(p);
   l.ipc_ptrs.clear();
   l.remote_ring.reset();
@@ -702,12 +714,22 @@ int64_t QueueFabric::producer_pass(double now) {
       ++work;
     }
   }
-  // 2. completed copies: notice the frames, or requeue them if their consumer left meanwhile
-  while (!inflight_.empty()) {
-    Batch& b = inflight_.front();
+  // 2. completed copies: notice the frames, or requeue them if their consumer left meanwhile.
+  //    Batches of one link complete in order (one stream per link); links are independent.
+  std::vector<const Link*> blocked;
+  for (auto it = inflight_.begin(); it != inflight_.end();) {
+    Batch& b = *it;
+    if (std::find(blocked.begin(), blocked.end(), b.link.get()) != blocked.end()) {
+      ++it;
+      continue;
+    }
     if (b.ev != nullptr) {
       const hipError_t q = hipEventQuery(b.ev);
-      if (q == hipErrorNotReady) break;
+      if (q == hipErrorNotReady) {
+        blocked.push_back(b.link.get());
+        ++it;
+        continue;
+      }
       hip_check(q, "hipEventQuery (frame copy)");
     }
     Link& l = *b.link;
@@ -727,7 +749,7 @@ int64_t QueueFabric::producer_pass(double now) {
         ++l.n_head;
       }
       l.seg->n_head.store(l.n_head, std::memory_order_release);
-      pool_->end_send_batch(b.slots, reinterpret_cast<uint64_t>(stream_));
+      pool_->end_send_batch(b.slots, reinterpret_cast<uint64_t>(b.stream != nullptr ? b.stream : stream_));
       l.frames += n;
       std::lock_guard<std::mutex> lk(mu_);
       st_.frames_sent += n;
@@ -739,7 +761,7 @@ int64_t QueueFabric::producer_pass(double now) {
       st_.frames_requeued += n;
     }
     if (b.ev != nullptr) free_events_.push_back(b.ev);
-    inflight_.pop_front();
+    it = inflight_.erase(it);
     work += n;
   }
   // 3. route produced frames (FIFO) to this process's own consumer or to granted remote slots
@@ -751,6 +773,22 @@ int64_t QueueFabric::producer_pass(double now) {
     std::vector<int64_t> avail(cands.size());
     for (size_t i = 0; i < cands.size(); ++i) avail[i] = (int64_t)cands[i]->grants.size();
     int64_t local_credit = (is_consumer_ && !consumer_closed_.load()) ? pool_->credits() : 0;
+    if (policy == 2 && local_credit > 0) {
+      // spread: the own producer must not take the consumer credit that the remote producers'
+      // grants need.  A local route needs only credit, a grant needs a FREE slot whose release
+      // event has completed -- so without a reservation the local route wins every race and all
+      // frames stay local.  Keep each live remote producer's grant floor (consumer_pass) reserved.
+      std::vector<const Link*> in;
+      for (auto& lp : links_)
+        if (!lp->outgoing && lp->attached && !lp->eos && !lp->dead && !lp->detached) in.push_back(lp.get());
+      if (!in.empty()) {
+        const int cb = pool_->consumer_budget();
+        const int64_t floor_g = std::max(kMinGrants, std::min(64, cb / (2 * (int)in.size())));
+        int64_t reserve = 0;
+        for (const Link* l : in) reserve += std::max<int64_t>(0, floor_g - l->outstanding);
+        local_credit = std::max<int64_t>(0, local_credit - reserve);
+      }
+    }
     std::vector<std::vector<int>> assign(cands.size());
     std::vector<int> local;
     const int K = (int)cands.size() + 1;   // position K-1 = this process's own consumer
@@ -804,7 +842,8 @@ int64_t QueueFabric::producer_pass(double now) {
       b.t_issue = now;
       if (device_ >= 0) {
         trace::Range tr("fabric.copy_batch");
-        pool_->begin_send_batch(slots, reinterpret_cast<uint64_t>(stream_));   // stream waits for the frames
+        b.stream = l.stream != nullptr ? l.stream : stream_;
+        pool_->begin_send_batch(slots, reinterpret_cast<uint64_t>(b.stream));   // stream waits for the frames
         int a = 0;
         const uint64_t sb = (uint64_t)slot_bytes_;
         while (a < n) {   // coalesce runs contiguous on both sides
@@ -814,12 +853,12 @@ int64_t QueueFabric::producer_pass(double now) {
             ++e;
           hip_check(hipMemcpyAsync(reinterpret_cast<void*>(l.remote[b.rslots[a]]),
                                    reinterpret_cast<const void*>(pool_->slot_ptr(slots[a])), (size_t)sb * (size_t)(e - a),
-                                   hipMemcpyDeviceToDevice, stream_),
+                                   hipMemcpyDeviceToDevice, b.stream),
                     "hipMemcpyAsync (frame -> consumer ring)");
           a = e;
         }
         b.ev = take_event();
-        hip_check(hipEventRecord(b.ev, stream_), "hipEventRecord (frame copy)");
+        hip_check(hipEventRecord(b.ev, b.stream), "hipEventRecord (frame copy)");
       } else {
         pool_->begin_send_batch(slots, 0);
         for (int j = 0; j < n; ++j)

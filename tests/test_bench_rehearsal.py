@@ -40,4 +40,8 @@ def test_bench_multirank_cpu(native, nproc, route, producers):
     # frames cross ranks in the cross window (from most producers), consumer-only ranks send nothing
     assert sum(x["bytes_sent_per_rank"]) > 0, x
     assert sum(b > 0 for b in x["bytes_sent_per_rank"][:n_p]) >= max(1, n_p // 2), x
+    if producers == 0:
+        # all ranks produce AND consume: spread keeps the own consumer to its 1/(remote + 1) share
+        # of the free slots (fabric.cpp), so most frames cross (a 4-step window on the CPU)
+        assert x["cross_gpu_fraction"] >= 0.25, x
     assert all(b == 0 for b in x["bytes_sent_per_rank"][n_p:]), x
