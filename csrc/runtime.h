@@ -5,7 +5,7 @@
 //  * SlotPool replaces the single-threaded Ray actor `Queue` (psana_ray/shared_queue.py:4-31):
 //    bounded capacity with put->False backpressure (Q-4), FIFO get, non-blocking get->None,
 //    size().  Unlike the actor it is sharded (one pool per GPU), lock-protected for many
-//    threads, and every slot carries HIP events so producers, the RCCL transport and
+//    threads, and every slot carries HIP events so producers, the queue fabric (peer copies) and
 //    consumers order on-device work without host synchronisation.
 //  * PinnedBuffer / memcpy_h2d_async implement the "stage raw events into pinned host pages
 //    with hipMemcpyAsync on a side stream" path that replaces psana's CPU-side numpy frames

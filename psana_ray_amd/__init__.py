@@ -1,11 +1,11 @@
 """psana_ray_amd -- an MI355X-native detector-frame streaming framework with the capabilities of
 carbonscott/psana-ray: MPI-launched producers calibrate LCLS detector frames with hand-written
-gfx950 HIP kernels and stream them through a sharded HBM ring queue (RCCL over xGMI) to
-``DataReader`` consumers.
+gfx950 HIP kernels and stream them through an elastic queue of HBM rings (independent
+producer -> consumer links, HIP IPC peer copies over xGMI) to ``DataReader`` consumers.
 
 Layout: ``models`` (detectors, constants, geometry, calibration pipeline), ``ops`` (HIP kernel
-wrappers + fp32 golden models), ``queue`` (HBM ring / endpoint / CPU queue), ``parallel``
-(launch env, rendezvous, comm, routing), ``source`` (synthetic / raw-run / psana), ``utils``.
+wrappers + fp32 golden models), ``queue`` (HBM ring / session / endpoint / CPU queue),
+``parallel`` (launch env, rendezvous), ``source`` (synthetic / raw-run / psana), ``utils``.
 """
 __version__ = "0.1.0"
 

@@ -112,7 +112,6 @@ class QueueConfig:
     # a LOGICAL bound, the reference never pre-allocates: shared_queue.py:7)
     hbm_fraction: float = 0.80
     producer_slots: int = 64          # calibrated frames a producer may hold un-routed
-    max_offer: int = 64               # frames a producer offers per transport round
     route: str = "balanced"           # balanced | local_first | spread
     connect_timeout_s: float = 300.0
     extra: dict = field(default_factory=dict)

@@ -5,8 +5,10 @@ Same surface as the reference -- ``DataReader(address, queue_name, ray_namespace
 MI355X-native semantics:
 
 * ``connect()`` joins the queue session at the rendezvous store (``address``; the reference's
-  ``ray.init`` + ``ray.get_actor``, data_reader.py:11-24), gets this consumer's HBM ring shard and
-  starts the transport thread (frames arrive by RCCL send/recv over xGMI, or gloo on the CPU).
+  ``ray.init`` + ``ray.get_actor``, data_reader.py:11-24) -- at any time, before, during or after
+  the producers -- gets this consumer's HBM ring shard and starts the fabric thread: every live
+  producer writes frames straight into the shard (HIP IPC peer copies over xGMI; shared memory
+  for host rings).
   Defaults come from ONE shared module, so they match the producer's (fixes Q-3).
 * ``read()`` is non-blocking by default and returns None when nothing is ready (data_reader.py:35);
   items are the reference's ``[rank, idx, data, photon_energy]`` (4 fields, producer.py:101; the

@@ -3,7 +3,8 @@
 Replaces the reference's ``deque(maxlen=maxsize)`` inside the Ray actor
 (psana_ray/shared_queue.py:6-7).  Slots are preallocated once in device memory (HBM3E) and
 recycled, so steady-state streaming performs no allocation; frames are written in place by the
-calibration kernels (local producer) or by RCCL receives (remote producer).  The slot state
+calibration kernels (local producer) or by a remote producer's peer copy into a granted slot
+(queue fabric, csrc/fabric.cpp).  The slot state
 machine, per-slot HIP events and blocking waits live in C++ (``_C.SlotPool``).
 
 Capacity (SURVEY H-8): ``queue_size`` is the LOGICAL bound of the whole queue (the reference

@@ -1,4 +1,4 @@
-"""Counters, rates and a periodic summary for producers / consumers / the transport.
+"""Counters, rates and a periodic summary for producers / consumers / the queue fabric.
 
 Reference parity (SURVEY §5 "Metrics / logging / observability"): psana-ray only has
 ``--log_level`` (psana_ray/producer.py:31-32,135-136), a per-event INFO line (:103) and a
@@ -6,7 +6,7 @@ full-queue INFO line (:106); ``Queue.size()`` exists but is unused (shared_queue
 At 10^4 frames/s a per-event log line IS the bottleneck, so here:
 
   * components expose cumulative counters as plain callables (``register(name, fn)``); the hot
-    paths (native producer engine, slot pool, transport) already count, so nothing extra runs
+    paths (native producer engine, slot pool, queue fabric) already count, so nothing extra runs
     per frame;
   * a :class:`Reporter` thread samples every source every ``interval`` seconds, derives rates
     from the deltas, logs ONE summary line per interval and optionally appends a JSON line to

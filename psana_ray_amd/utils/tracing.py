@@ -1,4 +1,4 @@
-"""roctx ranges from Python (transport rounds, consumer batches) next to the native ones
+"""roctx ranges from Python (consumer batches) next to the native ones
 (``producer.chunk`` / ``producer.stage_h2d`` / ``producer.acquire`` / ``producer.launch_calib``,
 csrc/engine.cpp).  View them with ``rocprofv3 --marker-trace --kernel-trace -- python ...``.
 
