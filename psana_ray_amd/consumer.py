@@ -204,5 +204,15 @@ def main(argv=None) -> int:
     return 0
 
 
+def cli(argv=None) -> int:
+    """Console entry: startup failures (no store, no queue session, a queue of another frame
+    shape) end with one clear line and rc 1 instead of a traceback."""
+    try:
+        return main(argv)
+    except (TimeoutError, ConnectionError, RuntimeError) as e:
+        log.error("consumer could not join the queue: %s", e)
+        return 1
+
+
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(cli())

@@ -89,4 +89,4 @@ def open_store(address: Optional[str], spawn_if_absent: bool = True, timeout_s: 
                  host, port)   # producer.py:63
         time.sleep(retry_delay_s)
     raise TimeoutError(f"no psana-ray rendezvous store reachable at {host}:{port} "
-                       f"(start one with `psana-ray-server --port {port}`): {last}")
+                       f"(start one with `psana-ray-server --port {port}`)" + (f": {last}" if last else ""))
