@@ -278,6 +278,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("policy", &pr::QueueFabric::policy)
       .def("error", &pr::QueueFabric::error)
       .def("last_link_error", &pr::QueueFabric::last_link_error)
+      .def("set_grant_filter", &pr::QueueFabric::set_grant_filter, py::arg("on"))
+      .def("set_peer_grantable", &pr::QueueFabric::set_peer_grantable, py::arg("mid"), py::arg("on"))
       .def("stats", &pr::QueueFabric::stats)
       .def("links", &pr::QueueFabric::links);
 
@@ -367,6 +369,7 @@ PYBIND11_MODULE(_C, m) {
       .def("grant_batch", &SP::grant_batch, py::arg("max_n"))
       .def("complete_recv_batch", &SP::complete_recv_batch, py::arg("slots"), py::arg("headers"))
       .def("cancel_recv_batch", &SP::cancel_recv_batch, py::arg("slots"))
+      .def("reoffer_batch", &SP::reoffer_batch, py::arg("slots"), py::arg("stream"))
       .def("unsend_batch", &SP::unsend_batch, py::arg("slots"))
       .def_property_readonly("event_records", &SP::event_records);
 

@@ -225,7 +225,7 @@ QueueFabric::QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is
       policy_(policy), self_mid_(self_mid) {
   check(pool != nullptr && slot_bytes > 0, "QueueFabric: empty ring");
   check((int)pool->slot_ptrs().size() == pool->n_slots(), "QueueFabric: the pool has no slot addresses");
-  check(policy >= 0 && policy <= 2, "QueueFabric: unknown routing policy");
+  check(policy >= 0 && policy <= 3, "QueueFabric: unknown routing policy");
   check(is_producer || is_consumer, "QueueFabric: a member must produce or consume");
   if (device_ >= 0) {
     hip_check(hipSetDevice(device_), "hipSetDevice");
@@ -354,8 +354,13 @@ void QueueFabric::drop_peer(int64_t mid) {
 }
 
 void QueueFabric::set_policy(int policy) {
-  check(policy >= 0 && policy <= 2, "QueueFabric: unknown routing policy");
+  check(policy >= 0 && policy <= 3, "QueueFabric: unknown routing policy");
   policy_.store(policy);
+}
+
+void QueueFabric::set_peer_grantable(int64_t mid, bool on) {
+  std::lock_guard<std::mutex> lk(ops_mu_);
+  ops_.push_back(Op{on ? 3 : 4, mid, ""});
 }
 
 hipEvent_t QueueFabric::take_event() {
@@ -377,6 +382,12 @@ void QueueFabric::apply_ops() {
     ops.swap(ops_);
   }
   for (const Op& op : ops) {
+    if (op.kind == 3 || op.kind == 4) {
+      auto it = std::find(grantable_.begin(), grantable_.end(), op.mid);
+      if (op.kind == 3 && it == grantable_.end()) grantable_.push_back(op.mid);
+      if (op.kind == 4 && it != grantable_.end()) grantable_.erase(it);
+      continue;
+    }
     if (op.kind == 2) {
       for (auto& l : links_)
         if (l->peer == op.mid && !l->dead) {
@@ -619,7 +630,9 @@ int64_t QueueFabric::consumer_pass(double now) {
   if (!closing) {
     std::vector<Link*> act;
     for (auto& lp : links_)
-      if (!lp->outgoing && lp->attached && !lp->eos && !lp->dead && !lp->detached) act.push_back(lp.get());
+      if (!lp->outgoing && lp->attached && !lp->eos && !lp->dead && !lp->detached &&
+          (!grant_filter_.load() || std::find(grantable_.begin(), grantable_.end(), lp->peer) != grantable_.end()))
+        act.push_back(lp.get());
     if (!act.empty()) {
       const int cb = pool_->consumer_budget();
       const int floor_g = std::max(kMinGrants, std::min(64, cb / (2 * (int)act.size())));
@@ -772,7 +785,7 @@ int64_t QueueFabric::producer_pass(double now) {
       if (lp->outgoing && lp->attached && !lp->dead && !lp->closed && !lp->eos_posted) cands.push_back(lp.get());
     std::vector<int64_t> avail(cands.size());
     for (size_t i = 0; i < cands.size(); ++i) avail[i] = (int64_t)cands[i]->grants.size();
-    int64_t local_credit = (is_consumer_ && !consumer_closed_.load()) ? pool_->credits() : 0;
+    int64_t local_credit = (is_consumer_ && !consumer_closed_.load() && policy != 3) ? pool_->credits() : 0;
     if (policy == 2 && local_credit > 0) {
       // spread: the own producer must not take the consumer credit that the remote producers'
       // grants need.  A local route needs only credit, a grant needs a FREE slot whose release

@@ -103,7 +103,8 @@ struct LinkStatus {
 class QueueFabric {
  public:
   // policy: 0 balanced (local unless a remote consumer has kLocalSlack more free slots granted),
-  //         1 local_first, 2 spread (round-robin over every consumer with credit).
+  //         1 local_first, 2 spread (round-robin over every consumer with credit),
+  //         3 relay (queue keeper: never to its own consumer side; most granted credit first).
   // slot addresses come from the pool (SlotPool::set_slot_ptrs): rings are built from segments
   QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is_producer, bool is_consumer, int policy,
               int64_t self_mid);
@@ -123,6 +124,10 @@ class QueueFabric {
   void add_out_link(int64_t consumer_mid, const std::string& name);  // producer: open it
   void drop_peer(int64_t mid);                                        // peer gone (store view)
   void set_policy(int policy);
+  // consumer role: grant only to producers marked grantable (queue keeper: absorbs the frames of
+  // producers that finished and wait for consumers, never competes with live ones)
+  void set_grant_filter(bool on) { grant_filter_.store(on); }
+  void set_peer_grantable(int64_t mid, bool on);
   void set_producer_finished() { finished_.store(true); }
   void set_consumer_closed() { consumer_closed_.store(true); }
   // consumer: true once no live producer can still be writing into this ring (every attached
@@ -183,15 +188,17 @@ class QueueFabric {
   int rr_ = 0;
 
   struct Op {
-    int kind;  // 0 in, 1 out, 2 drop
+    int kind;  // 0 in, 1 out, 2 drop, 3 grantable on, 4 grantable off
     int64_t mid;
     std::string name;
   };
   std::mutex ops_mu_;
   std::vector<Op> ops_;
+  std::vector<int64_t> grantable_;   // engine thread: peers a filtered consumer grants to
 
   std::atomic<bool> finished_{false}, consumer_closed_{false}, stop_{false}, running_{false}, drained_{false};
   std::atomic<bool> quiesced_{false};
+  std::atomic<bool> grant_filter_{false};
   std::vector<LinkStatus> retired_;
   std::thread th_;
   mutable std::mutex mu_;  // error_, st_, status_

@@ -639,6 +639,24 @@ void SlotPool::unsend_batch(const std::vector<int>& slots) {
   }
 }
 
+int SlotPool::reoffer_batch(const std::vector<int>& slots, uint64_t stream) {
+  std::lock_guard<std::mutex> lk(mu_);
+  int n = 0;
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kLeased, state_msg("reoffer_batch", kLeased, state_[s]));
+    if (producer_held_ >= pb_) break;
+    ready_ref_[s] = record_shared_locked(stream);
+    state_[s] = kProduced;
+    --consumer_held_;
+    ++producer_held_;
+    produced_fifo_.push_back(s);
+    ++n;
+  }
+  if (n > 0) cv_produce_.notify_one();
+  return n;
+}
+
 std::vector<SlotHeader> SlotPool::headers(const std::vector<int>& slots) const {
   std::lock_guard<std::mutex> lk(mu_);
   std::vector<SlotHeader> out;

@@ -163,6 +163,10 @@ class SlotPool {
   void complete_recv_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs);  // -> READY
   void cancel_recv_batch(const std::vector<int>& slots);                      // RECEIVING -> FREE
   void unsend_batch(const std::vector<int>& slots);  // SENDING -> PRODUCED, back at the FIFO front
+  // queue keeper: received frames (LEASED) go back on offer as this process's own production
+  // (LEASED -> PRODUCED, headers kept; consumer budget -> producer budget).  Returns how many
+  // moved (stops when the producer budget is full).
+  int reoffer_batch(const std::vector<int>& slots, uint64_t stream);
 
  private:
   void set_device() const;

@@ -40,7 +40,7 @@ from .ring import FrameRing
 
 log = logging.getLogger(__name__)
 
-POLICIES = {"balanced": 0, "local_first": 1, "spread": 2}
+POLICIES = {"balanced": 0, "local_first": 1, "spread": 2, "relay": 3}   # relay: queue keeper
 
 
 class QueueError(RuntimeError):

@@ -39,8 +39,8 @@ log = logging.getLogger(__name__)
 HEARTBEAT_S = 1.0
 STALE_S = 10.0          # heartbeat age after which a member on another host counts as dead
 CREATE_GRACE_S = 10.0   # a freshly created session counts as live before its members registered
-PRODUCER_ROLES = ("producer", "prosumer")
-CONSUMER_ROLES = ("consumer", "prosumer")
+PRODUCER_ROLES = ("producer", "prosumer", "keeper")
+CONSUMER_ROLES = ("consumer", "prosumer", "keeper")   # keeper: psana_ray_amd/keeper.py
 
 
 def queue_key(namespace: str, queue_name: str) -> str:
@@ -156,7 +156,7 @@ class QueueSession:
 
     def __init__(self, store, namespace: str, queue_name: str, meta: dict, role: str, device: int = -1,
                  job: Optional[str] = None, rank: Optional[int] = None, own_store: bool = False):
-        assert role in ("producer", "consumer", "prosumer"), role
+        assert role in ("producer", "consumer", "prosumer", "keeper"), role
         self.store = store
         self.namespace, self.queue_name = namespace, queue_name
         self.meta = meta
@@ -211,6 +211,10 @@ class QueueSession:
     def producers(self) -> Dict[int, dict]:
         with self._lock:
             return {m: i for m, i in self.members.items() if i["role"] in PRODUCER_ROLES}
+
+    def state(self, mid: int) -> str:
+        with self._lock:
+            return self.states.get(mid, "running")
 
     def finished(self, mid: int) -> bool:
         """Producer member ``mid`` will send nothing more (done, failed, left, or dead)."""

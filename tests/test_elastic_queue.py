@@ -182,3 +182,47 @@ def test_competing_consumers_share_by_speed(store_port, tmp_path):
     assert sorted(gf + gs) == list(range(n)), "exactly-once delivery violated"
     assert len(gs) > 0, "the slow consumer should still receive frames"
     assert len(gf) > 2 * len(gs), (len(gf), len(gs))
+
+
+def keeper(port, *extra):
+    cmd = [sys.executable, "-m", "psana_ray_amd.keeper", "--ray_address", f"127.0.0.1:{port}", "--slots", "64",
+           "--timeout", "60", "--log_level", "INFO", *extra]
+    return subprocess.Popen(cmd, env=ENV, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+
+def test_keeper_holds_frames_after_the_producer_exits(store_port, tmp_path):
+    """R-11 (the reference's queue is a DETACHED actor, shared_queue.py:35): with a keeper in the
+    session the producer drains into it and exits 0 without any consumer; a consumer started
+    afterwards receives every frame exactly once, bit-exact, plus EOS; the keeper then leaves."""
+    prod = producer(store_port, 40, queue_size=48)   # the queue holds the run (reference: maxsize)
+    time.sleep(1.0)
+    kp = keeper(store_port)
+    rc_p, out_p = finish(prod, timeout=60)
+    assert rc_p == 0, out_p
+    assert kp.poll() is None, "the keeper must stay while it holds frames"
+    time.sleep(2.0)
+    c = consumer(store_port, tmp_path / "c.jsonl")
+    rc_c, out_c = finish(c)
+    rc_k, out_k = finish(kp)
+    assert rc_c == 0, out_c
+    assert rc_k == 0, out_k
+    recs = records(tmp_path / "c.jsonl")
+    assert sorted(frames(recs)) == list(range(40))
+    assert recs[-1].get("eos") is True
+    assert "keeper done: kept=40" in out_k, out_k[-2000:]
+
+
+def test_keeper_with_a_live_consumer_stays_out_of_the_way(store_port, tmp_path):
+    """Keeper and consumer both present from the start: the consumer receives every frame exactly
+    once (frames the keeper took after the producer finished are relayed on), and both exit 0."""
+    c = consumer(store_port, tmp_path / "c.jsonl")
+    prod = producer(store_port, 64, queue_size=16)
+    time.sleep(1.0)
+    kp = keeper(store_port)
+    rc_p, out_p = finish(prod)
+    rc_c, out_c = finish(c)
+    rc_k, out_k = finish(kp)
+    assert (rc_p, rc_c, rc_k) == (0, 0, 0), (out_p[-1500:], out_c[-1500:], out_k[-1500:])
+    recs = records(tmp_path / "c.jsonl")
+    assert sorted(frames(recs)) == list(range(64))
+    assert recs[-1].get("eos") is True

@@ -15,7 +15,7 @@ import torch  # noqa: E402
 
 from psana_ray_amd.config import CommonModeParams  # noqa: E402
 from psana_ray_amd.models import Calibrator, Mode  # noqa: E402
-from psana_ray_amd.models.geometry import Geometry, _epix_quads  # noqa: E402
+from psana_ray_amd.models.geometry import Geometry, _epix_quads, _panel_grid  # noqa: E402
 from psana_ray_amd.source import SyntheticRun  # noqa: E402
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "bench"))
@@ -34,8 +34,10 @@ def main():
     cal = Calibrator(src.consts, dev, Mode.calib, common_mode=CommonModeParams())
     out = torch.empty((F, *cal.out_shape), dtype=torch.float32, device=dev)
     res["frame_us"] = round(timeit(lambda: cal.run(rl, [out[i] for i in range(F)]))[0] * 1e6 / F, 3)
-    for gap in (10, 16):
-        rows, cols, shape = _epix_quads(spec, gap)
+    layouts = [("quads_gap10", lambda: _epix_quads(spec, 10)), ("quads_gap16", lambda: _epix_quads(spec, 16)),
+               ("grid_unrotated_gap16", lambda: _panel_grid(spec, 16))]
+    for gap, make in layouts:
+        rows, cols, shape = make()
         geo = Geometry(spec, tuple(int(s) for s in shape), rows, cols)
         place = geo.panel_placement().reshape(-1, 3)
         c = Calibrator(src.consts, dev, Mode.image, common_mode=CommonModeParams(), geometry=geo)
