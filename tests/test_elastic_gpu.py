@@ -51,3 +51,25 @@ def test_gpu_kill9_consumer_survivor_gets_the_rest(store_port, tmp_path):  # noq
     lost = set(range(n)) - set(ga) - set(gb)
     assert len(lost) <= slots_a, lost
     assert records(tmp_path / "b.jsonl")[-1].get("eos") is True
+
+
+def test_gpu_keeper_holds_frames_after_the_producer_exits(store_port, tmp_path):  # noqa: F811
+    """R-11 on HBM: the producer drains into the keeper's HBM ring (IPC peer copies) and exits with
+    no consumer; a consumer started later receives every frame bit-exactly, plus EOS."""
+    from tests.test_elastic_queue import keeper
+
+    prod = gpu_producer(store_port, 40, queue_size=48)
+    time.sleep(2.0)
+    kp = keeper(store_port, "--device", "cuda:0")
+    rc_p, out_p = finish(prod, 120)
+    assert rc_p == 0, out_p[-3000:]
+    assert kp.poll() is None, "the keeper must stay while it holds frames"
+    c = consumer(store_port, tmp_path / "c.jsonl", "--device", "cuda:0", "--gen_device", "cuda")
+    rc_c, out_c = finish(c, 120)
+    rc_k, out_k = finish(kp, 120)
+    assert rc_c == 0, out_c[-3000:]
+    assert rc_k == 0, out_k[-3000:]
+    recs = records(tmp_path / "c.jsonl")
+    assert sorted(frames(recs)) == list(range(40))
+    assert recs[-1].get("eos") is True
+    assert "keeper done: kept=40" in out_k, out_k[-2000:]
