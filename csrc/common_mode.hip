@@ -250,6 +250,14 @@ __device__ __forceinline__ uint32_t side_put(SideCtx& sc, bool needs, const floa
   return (uint32_t)slot;
 }
 
+// (m & a) | (~m & b) as ONE v_bfi_b32 (the compiler emits and / xor / and / or for the
+// constant-operand and sign-extended-mask forms below: 4-5 VALU per pixel)
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+
 // Decode one 8-pixel group: v = ADU - pedestal (0 for Jungfrau's invalid gain code), el = CM
 // eligibility bits, cbits = candidate bits for the store phase.
 //   rw: raw words (2 pixels each), pa: candidate pedestals, ep: eligibility bit-planes
@@ -268,7 +276,7 @@ __device__ __forceinline__ void cm_decode8(const uint4 rw, const uint32_t ep, co
       const float adu = (float)__builtin_amdgcn_ubfe(wj, sh, 14);
       const uint32_t g0 = (uint32_t)__builtin_amdgcn_sbfe((int)wj, sh + 14, 1);   // all ones: gain bit 14
       if constexpr (KIND == kEpix10ka) {
-        v[j] = adu - __uint_as_float((g0 & __float_as_uint(pa[1][j])) | (~g0 & __float_as_uint(pa[0][j])));
+        v[j] = adu - __uint_as_float(bfi(g0, __float_as_uint(pa[1][j]), __float_as_uint(pa[0][j])));
         c0 |= g0 & (1u << j);
       } else {   // Jungfrau: gain bits 0 -> G0, 1 -> G1, 3 -> G2, 2 -> invalid (never eligible, output 0)
         const uint32_t g1 = (uint32_t)__builtin_amdgcn_sbfe((int)wj, sh + 15, 1);
@@ -303,7 +311,7 @@ __device__ __forceinline__ void cm_tile_values(const float (&v)[8], uint32_t el,
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)el, j, 1);
-    x[j] = __uint_as_float((m & __float_as_uint(v[j])) | (~m & qnan));
+    x[j] = __uint_as_float(bfi(m, __float_as_uint(v[j]), qnan));
   }
 }
 
@@ -368,7 +376,7 @@ __device__ __forceinline__ float cm_gain(const float (&ga)[NT][8], uint32_t cb, 
     return ga[0][j];
   } else if constexpr (NT == 2) {
     const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)cb, j, 1);
-    return __uint_as_float((m & __float_as_uint(ga[1][j])) | (~m & __float_as_uint(ga[0][j])));
+    return __uint_as_float(bfi(m, __float_as_uint(ga[1][j]), __float_as_uint(ga[0][j])));
   } else {
     const uint32_t cj = (cb >> (2 * j)) & 3u;
     return bsel(cj == 0, ga[0][j], bsel(cj == 1, ga[1][j], ga[2][j]));
@@ -699,11 +707,11 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
 // ==========================================================================================
 template <int CTRL>
 __device__ __forceinline__ float dpp_quad(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 template <int CTRL>
 __device__ __forceinline__ int dpp_quad_i(int x) {
-  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
 }
 
 // Ascending sort of a V-shaped (non-increasing then non-decreasing) register sequence, virtually
@@ -719,8 +727,8 @@ __device__ __forceinline__ void bitonic_merge_vpad(float (&z)[N]) {
     for (int i = 0; i < N; ++i) {
       if ((i & j) == 0 && i + j < N) {
         const float a = z[i], b = z[i + j];
-        z[i] = fminf(a, b);
-        z[i + j] = fmaxf(a, b);
+        z[i] = vmin(a, b);
+        z[i + j] = vmax(a, b);
       }
     }
   }
@@ -842,15 +850,25 @@ __device__ __forceinline__ void cm_rows(float* tile, const int P, const int R, c
   }
 }
 
-// Column medians, FOUR lanes (a quad) per column, M rows each (t0 a multiple of 4):
-//  each lane sorts its M values (sort_regs<M>); lanes (q, q^1) merge-split (lower lane keeps
-//  min(x[i], partner[M-1-i]), upper the max) and sort the resulting bitonic sequences (the
-//  lower lane negated so both are V-shaped: bitonic_merge_vpad); the two sorted halves of the
-//  pair (0,1) and of the pair (2,3) are then merged by merge-path for k = 2M-1 and 2M with ONE
-//  quad_perm(3,2,1,0) fetch per register.
+// Column medians, FOUR lanes (a quad) per column, M rows each (t0 a multiple of 4).
+//  Sign domain: the odd lane of each pair (q = 1, 3) holds its values NEGATED, so both lanes of a
+//  pair run identical instructions where the classic merge-split needs lane-dependent min / max:
+//   1. pass 1 counts the participants (|v| < thr); the quad's totals fix how many non-participants
+//      become -inf (the rest +inf: balanced padding puts the median at fixed ranks 2M-1, 2M);
+//      pass 2 reloads the column and writes sign-domain values and pads (no NaN survives);
+//   2. every lane sorts its M values ascending (sort_regs<M>);
+//   3. level 1, lanes (q, q^1): z[i] = max(partner[i], -x[i]) is the V-shaped merge-split half for
+//      BOTH lanes (even lane: -min(l[i], u[M-1-i]); odd lane: max(l[i], u[M-1-i])), one DPP fetch
+//      and ONE v_maximum3 (neg modifier) per register; bitonic_merge_vpad sorts it.  Afterwards
+//      the even lane holds -A[M-1-i], the odd lane A[M+i] (A = the pair's 2M sorted values);
+//   4. level 2, lanes (q, q^3) -- merge path of pair (0,1) with pair (2,3): lanes 1 and 3 each
+//      see half of the split terms max(A[a], B[k-1-a]) as max(z[t], -partner[t]) (k = 2M) and
+//      max(z[t], -partner[t+1]) (k = 2M-1), plus the end terms z[M-1] and max(A[M-1], B[M-1]);
+//      the k-th value is the min over both lanes.
 template <int M>
 __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, const int C, const CmParams& cp,
                                         const int t0, const int nt) {
+  static_assert(M % 2 == 0, "cm_cols: M must be even (interleaved rows)");
   const float INF = __int_as_float(0x7f800000);
   const float QNAN = __int_as_float(0x7fc00000);
   const int nwork = 4 * C;
@@ -858,26 +876,19 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
     const bool act = w < nwork;
     const int c = act ? (w >> 2) : 0;
     const int q = w & 3;
-    const bool lower = (q & 1) == 0;
-    // Rows of the column per lane.  M even: lane q takes rows 8j + 2q + b (b = 0, 1), so for a
-    // fixed element the quad's four addresses differ by 2P rows -- 8 banks apart for the pitches
-    // in use (P = 52: 2P = 104 = 8 mod 32; P = 140: 280 = 24 mod 32) -- and the 8 columns of a half
-    // wave fill all 32 banks (contiguous blocks of M rows put lanes q and q + 2 on the same banks:
-    // 2-way conflicts on every column load and write-back).  The median does not depend on which
-    // lane holds which row.  M odd: contiguous blocks.
-    constexpr bool SW = (M % 2) == 0;
-    float* colp = tile + (SW ? 2 * q : q * M) * P + c;
-    auto row_of = [&](int i) { return SW ? 8 * (i >> 1) + 2 * q + (i & 1) : q * M + i; };
-    auto off_of = [&](int i) { return (SW ? 8 * (i >> 1) + (i & 1) : i) * P; };
-    float x[M];
+    // Rows of the column per lane: lane q takes rows 8j + 2q + b (b = 0, 1), so for a fixed
+    // element the quad's four addresses differ by 2P rows -- 8 banks apart for the pitches in use
+    // (P = 52: 2P = 104 = 8 mod 32; P = 140: 280 = 24 mod 32) -- and the 8 columns of a half wave
+    // fill all 32 banks.  The median does not depend on which lane holds which row.
+    float* colp = tile + 2 * q * P + c;
+    auto row_of = [&](int i) { return 8 * (i >> 1) + 2 * q + (i & 1); };
+    auto off_of = [&](int i) { return (8 * (i >> 1) + (i & 1)) * P; };
+    auto load = [&](int i) { return (act && row_of(i) < R) ? colp[off_of(i)] : QNAN; };
+    // pass 1: participants of this lane
     int my_cnt = 0;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      const bool in = act && row_of(i) < R;
-      const float v = in ? colp[off_of(i)] : QNAN;
-      const bool pt = fabsf(v) < cp.thr;
-      my_cnt += pt ? 1 : 0;
-      x[i] = pt ? v : QNAN;
+      my_cnt += fabsf(load(i)) < cp.thr ? 1 : 0;
       if ((i & 15) == 15) asm volatile("" ::: "memory");
     }
     // quad totals + exclusive prefix of the non-participants: balanced +-inf padding
@@ -888,43 +899,44 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
     const int cnt = 4 * M - total_inv;
     const int a = total_inv >> 1;
     const int prefix = (q > 0 ? i0 : 0) + (q > 1 ? i1 : 0) + (q > 2 ? i2 : 0);
-    const int neg_budget = min(my_inv, max(0, a - prefix));
-    int ninv = 0;
+    // pass 2: sign-domain values; pads are -inf while s >= 0 (the first neg_budget of them)
+    int s = min(my_inv, max(0, a - prefix)) - 1;
+    const uint32_t flip = (q & 1) ? 0x80000000u : 0u;
+    uint32_t pad_base = 0xff800000u ^ flip;
+    asm volatile("" : "+v"(pad_base));   // one v_bitop3 per pad below, not bitop3 + xor
+    float x[M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      const bool inv = x[i] != x[i];
-      x[i] = inv ? (ninv < neg_budget ? -INF : INF) : x[i];
-      ninv += inv ? 1 : 0;
+      const float v = load(i);
+      const bool pt = fabsf(v) < cp.thr;
+      const uint32_t padb = ((uint32_t)s & 0x80000000u) ^ pad_base;
+      x[i] = __uint_as_float(pt ? (__float_as_uint(v) ^ flip) : padb);
+      s -= pt ? 0 : 1;
+      if ((i & 15) == 15) asm volatile("" ::: "memory");
     }
     asm volatile("" ::: "memory");
     sort_regs<M>(x);
-    // level 1: merge-split with lane q^1 (partner read reversed)
+    // level 1: merge-split with lane q^1, both lanes V-shaped
     float z[M];
 #pragma unroll
-    for (int i = 0; i < M; ++i) {
-      const float pv = dpp_quad<0xB1>(x[M - 1 - i]);
-      const float y = lower ? fminf(x[i], pv) : fmaxf(x[i], pv);
-      z[i] = lower ? -y : y;   // both lanes V-shaped
-    }
+    for (int i = 0; i < M; ++i) z[i] = vmax(dpp_quad<0xB1>(x[i]), -x[i]);
     bitonic_merge_vpad<M>(z);
-#pragma unroll
-    for (int i = 0; i < M; ++i) x[i] = lower ? -z[M - 1 - i] : z[i];   // ascending half of the pair
     asm volatile("" ::: "memory");
-    // level 2: merge-path of pair (0,1) with pair (2,3); lane 0 reads lane 3, lane 1 lane 2
-    float kh = INF, kl = INF, plast = INF;
+    // level 2: merge path with lane q^3 (lanes 1 and 3 hold the terms)
+    float kh = INF, kl = INF;
+    float pn = dpp_quad<0x1B>(z[0]);
+    const float p0 = pn;
 #pragma unroll
-    for (int j = 0; j < M; ++j) {
-      const float pj = dpp_quad<0x1B>(x[j]);
-      kh = fminf(kh, fmaxf(x[M - 1 - j], pj));
-      if (j <= M - 2) kl = fminf(kl, fmaxf(x[M - 2 - j], pj));
-      if (j == M - 1) plast = pj;
+    for (int t = 0; t < M; ++t) {
+      const float pt = pn;
+      if (t + 1 < M) pn = dpp_quad<0x1B>(z[t + 1]);
+      kh = vmin(kh, vmax(z[t], -pt));
+      if (t + 1 < M) kl = vmin(kl, vmax(z[t], -pn));
     }
-    const float e = dpp_quad<0xAA>(x[M - 1]);   // lane 2's last element
-    const float extra = q == 0 ? fminf(plast, fmaxf(x[M - 1], e)) : x[M - 1];
-    kl = fminf(kl, extra);
-    kl = fminf(kl, dpp_quad<0xB1>(kl));
-    kh = fminf(kh, dpp_quad<0xB1>(kh));
-    const float k_lo = dpp_quad<0x00>(kl), k_hi = dpp_quad<0x00>(kh);   // lane 0 has the answer
+    const float e = -vmin(p0, dpp_quad<0xB1>(z[0]));   // max(A[M-1], B[M-1]) on lanes 1 and 3
+    kl = vmin(kl, vmin(z[M - 1], e));
+    const float k_lo = vmin(dpp_quad<0x55>(kl), dpp_quad<0xFF>(kl));
+    const float k_hi = vmin(dpp_quad<0x55>(kh), dpp_quad<0xFF>(kh));
     const float med = (k_lo + ((cnt & 1) ? k_lo : k_hi)) * 0.5f;
     asm volatile("" ::: "memory");
     if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
