@@ -115,6 +115,8 @@ struct PfScratch {
   unsigned int done;
 };
 
+constexpr int kPfCandCap = 512;   // candidates parked per workgroup (2 KiB of LDS)
+
 template <int RAD, int K>
 __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp, const PfParams pp,
                                                               float* __restrict__ peaks, int* __restrict__ counts_out,
@@ -124,6 +126,8 @@ __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp
   __shared__ float red_sum[4];
   __shared__ int red_cnt[4];
   __shared__ int is_last;
+  __shared__ int cand_n;
+  __shared__ int cand_p[kPfCandCap];
   int* counts = scratch != nullptr ? scratch->tickets : counts_out;
   float* summary = scratch != nullptr ? scratch->acc : summary_out;
   const int f = blockIdx.y;
@@ -143,6 +147,22 @@ __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp
       v[k] = q < n4 ? *(const PR_GLOBAL f32x4_t*)(img + 4 * q) : f32x4_t{NaN, NaN, NaN, NaN};
     }
   };
+  // the neighbourhood test of one candidate pixel p (frame-linear index)
+  auto test = [&](int64_t p) {
+    const float val = img[p];
+    const int panel = (int)(p / hw);
+    const int64_t rem = p - (int64_t)panel * hw;
+    const int y = (int)(rem / pp.cols), x = (int)(rem - (int64_t)(rem / pp.cols) * pp.cols);
+    const PR_GLOBAL float* pim = img + (int64_t)panel * hw;
+    pf_candidate<RAD>(
+        [&](int dy, int dx) {
+          const int yy = y + dy, xx = x + dx;
+          return (yy >= 0 && yy < pp.rows && xx >= 0 && xx < pp.cols) ? pim[(int64_t)yy * pp.cols + xx] : NaN;
+        },
+        val, pp, f, panel, y, x, peaks, counts, total);
+  };
+  if (threadIdx.x == 0) cand_n = 0;
+  __syncthreads();
   int64_t chunk = blockIdx.x;
   if (chunk < nchunks) load(chunk);
   for (; chunk < nchunks; chunk += gridDim.x) {
@@ -161,25 +181,24 @@ __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp
     }
     const int64_t q0 = chunk * 256 * K + threadIdx.x;
     if (chunk + gridDim.x < nchunks) load(chunk + gridDim.x);   // prefetch the next chunk
-    // pass 2 (rare): ONE copy of the candidate test, looped over the set bits; the value is
-    // re-read (an L1 hit) instead of indexing the register array at run time
-    while (cand) {
-      const int b = __builtin_ctzll(cand);
-      cand &= cand - 1;
-      const int64_t p = 4 * (q0 + 256 * (b >> 2)) + (b & 3);
-      const float val = img[p];
-      const int panel = (int)(p / hw);
-      const int64_t rem = p - (int64_t)panel * hw;
-      const int y = (int)(rem / pp.cols), x = (int)(rem - (int64_t)(rem / pp.cols) * pp.cols);
-      const PR_GLOBAL float* pim = img + (int64_t)panel * hw;
-      pf_candidate<RAD>(
-          [&](int dy, int dx) {
-            const int yy = y + dy, xx = x + dx;
-            return (yy >= 0 && yy < pp.rows && xx >= 0 && xx < pp.cols) ? pim[(int64_t)yy * pp.cols + xx] : NaN;
-          },
-          val, pp, f, panel, y, x, peaks, counts, total);
+    // pass 2 (rare): park the candidates in LDS; they are tested after the stream, one per lane
+    // (tested here, one lane at a time, the wave stalls on each candidate's dependent
+    // neighbourhood loads: 2.60 vs 1.72 us/frame without the test, epix10k2M)
+    if (cand) {
+      int slot = atomicAdd(&cand_n, __popcll(cand));
+      while (cand) {
+        const int b = __builtin_ctzll(cand);
+        cand &= cand - 1;
+        const int64_t p = 4 * (q0 + 256 * (b >> 2)) + (b & 3);
+        if (slot < kPfCandCap) cand_p[slot] = (int)p;
+        else test(p);   // list full: test in place
+        ++slot;
+      }
     }
   }
+  __syncthreads();
+  const int nc = min(cand_n, kPfCandCap);
+  for (int i = threadIdx.x; i < nc; i += blockDim.x) test(cand_p[i]);
   for (int o = 32; o > 0; o >>= 1) {
     above_sum += __shfl_down(above_sum, o);
     above_cnt += __shfl_down(above_cnt, o);
@@ -228,6 +247,7 @@ void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, i
   check(radius == 1 || radius == 2, "peakfind: radius must be 1 or 2");
   check(max_peaks >= 1, "peakfind: max_peaks must be >= 1");
   check(cols % 4 == 0, "peakfind: panel width must be a multiple of 4");
+  check((int64_t)n_panels * rows * cols < (int64_t)1 << 31, "peakfind: frame too large for 32-bit pixel ids");
   for (int f = 0; f < nframes; ++f) check(aligned16(fp.in[f]), "peakfind: frames must be 16-B aligned");
   PfParams pp{thr_peak, son_min, max_peaks, n_panels, rows, cols};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
