@@ -54,8 +54,9 @@ def parse(argv=None):
                          "constant queue depth per consumer shard). BASELINE config 3: --gpus 8 --queue-size 400")
     ap.add_argument("--source", default="host", choices=["host", "device"],
                     help="host: pinned host pool + H2D (real pipeline); device: raw frames already in HBM")
-    ap.add_argument("--chunk", type=int, default=32,
-                    help="frames per producer kernel launch / H2D copy (32: 13.0k vs 16: 11.7k fr/s, profiles/bench_ab_r1.md)")
+    ap.add_argument("--chunk", type=int, default=64,
+                    help="frames per producer kernel launch / H2D copy (device-resident: 64 134.0-139.0k vs "
+                         "32 132.0-134.5k vs 16 119.9k fr/s; host-staged 13.03k vs 12.90k; profiles/r2/pipeline_chunks.md)")
     ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--producers", type=int, default=0,

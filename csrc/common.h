@@ -15,7 +15,7 @@ namespace pr {
 constexpr int kWave = 64;
 // Max frames per launch: per-frame input/output pointers travel in the kernel argument
 // block (2 * 32 * 8 B = 512 B), so ring slots need not be contiguous.
-constexpr int kMaxFrames = 32;
+constexpr int kMaxFrames = 64;
 
 struct FramePtrs {
   uint64_t in[kMaxFrames];

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void gather_frames_kernel(const FramePtrs fp, 
 }
 
 void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool bf16, uint64_t stream) {
-  check(nframes >= 1 && nframes <= kMaxFrames, "gather_frames: 1..32 frames per launch");
+  check(nframes >= 1 && nframes <= kMaxFrames, "gather_frames: 1..kMaxFrames frames per launch");
   check(nelem > 0 && nelem % 4 == 0, "gather_frames: frame size must be a multiple of 4 elements");
   for (int i = 0; i < nframes; ++i)
     check(aligned16(fp.in[i]) && (fp.out[i] % (bf16 ? 8 : 16)) == 0, "gather_frames: misaligned frame");
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void fill_runs_kernel(const FramePtrs fp, cons
 }
 
 void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_runs, uint64_t stream) {
-  check(nframes >= 1 && nframes <= kMaxFrames, "fill_runs: 1..32 frames per launch");
+  check(nframes >= 1 && nframes <= kMaxFrames, "fill_runs: 1..kMaxFrames frames per launch");
   if (n_runs <= 0) return;
   check(runs % 8 == 0, "fill_runs: misaligned run table");
   const dim3 grid((unsigned)((n_runs + 3) / 4), (unsigned)nframes);

@@ -99,11 +99,11 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
 // global memory (just-touched lines, L1/L2 hits).  No halo over-fetch, no LDS, no barrier except
 // the per-block reduction of the hit statistics.
 // ---------------------------------------------------------------------------------------------
-// Grid-stride over 16-KB chunks (~2048 workgroups for the whole batch = 8 per CU): the per-frame
-// hit statistics are device-scope atomics to ONE address pair per frame, and same-address atomics serialise (~3 ns each, measured: read_f32 with one atomic per 8-KB
-// block 3.09 us/frame vs 1.81 with one per 16 KB), so a workgroup owns many chunks and issues its
-// two atomics once.  The next chunk's loads are issued before the current chunk's rare candidate
-// tests so the memory pipe stays busy.
+// The per-frame hit statistics are device-scope atomics to ONE address pair per frame, and
+// same-address atomics serialise (~3 ns each, measured: read_f32 with one atomic per 8-KB block
+// 3.09 us/frame vs 1.81 with one per 16 KB), so a workgroup owns many 16-KB chunks and issues its
+// two atomics once per frame it touches.  The next chunk's loads are issued before the current
+// chunk's rare candidates are parked, so the memory pipe stays busy.
 //
 // Self-resetting outputs (`scratch` != nullptr): the slot counters and hit statistics accumulate in
 // a persistent scratch block instead of in `counts` / `summary`; the LAST workgroup to finish
@@ -117,38 +117,46 @@ struct PfScratch {
 
 constexpr int kPfCandCap = 512;   // candidates parked per workgroup (2 KiB of LDS)
 
+// Balanced grid: ONE resident wave of workgroups (CUs x occupancy) over the batch's (frame, chunk)
+// sequence, each taking a contiguous range of T / G chunks, so every workgroup ends within one
+// chunk of the others.  (The round-2 2-D grid -- 64 workgroups per frame striding over the frame's
+// 528 chunks -- gave 16 of every 64 a ninth chunk: 1.92-1.99 vs 1.88-1.89 us/frame for this form,
+// 32 epix10k2M frames, tools/pf_probe.py; K = 8 / 16 float4 per lane: 2.19 / 2.25, lower occupancy.)
+// A range crosses at most a couple of frame boundaries; the hit statistics are flushed at each.
 template <int RAD, int K>
-__global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp, const PfParams pp,
-                                                              float* __restrict__ peaks, int* __restrict__ counts_out,
-                                                              float* __restrict__ summary_out,
-                                                              unsigned long long* __restrict__ total,
-                                                              PfScratch* __restrict__ scratch, const int nframes) {
+__global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp, const PfParams pp,
+                                                             float* __restrict__ peaks, int* __restrict__ counts_out,
+                                                             float* __restrict__ summary_out,
+                                                             unsigned long long* __restrict__ total,
+                                                             PfScratch* __restrict__ scratch, const int nframes) {
   __shared__ float red_sum[4];
   __shared__ int red_cnt[4];
   __shared__ int is_last;
   __shared__ int cand_n;
   __shared__ int cand_p[kPfCandCap];
+  __shared__ unsigned char cand_f[kPfCandCap];
   int* counts = scratch != nullptr ? scratch->tickets : counts_out;
   float* summary = scratch != nullptr ? scratch->acc : summary_out;
-  const int f = blockIdx.y;
-  const PR_GLOBAL float* img = gin<float>(fp.in[f]);
   const int64_t hw = (int64_t)pp.rows * pp.cols;
   const int64_t n4 = (int64_t)pp.n_panels * hw / 4;
-  const int64_t nchunks = (n4 + 256 * K - 1) / (256 * K);
+  const int ncpf = (int)((n4 + 256 * K - 1) / (256 * K));
+  const int64_t T = (int64_t)ncpf * nframes;
+  const int64_t g0 = T * blockIdx.x / gridDim.x, g1 = T * (blockIdx.x + 1) / gridDim.x;
   const float NaN = __int_as_float(0x7fc00000);
-  float above_sum = 0.0f;
-  int above_cnt = 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   f32x4_t v[K];
-  auto load = [&](int64_t chunk) {
-    const int64_t q0 = chunk * 256 * K + threadIdx.x;
+  auto load = [&](int64_t g) {
+    const int f = (int)(g / ncpf);
+    const PR_GLOBAL float* img = gin<float>(fp.in[f]);
+    const int64_t q0 = (g - (int64_t)f * ncpf) * 256 * K + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int64_t q = q0 + 256 * k;
       v[k] = q < n4 ? *(const PR_GLOBAL f32x4_t*)(img + 4 * q) : f32x4_t{NaN, NaN, NaN, NaN};
     }
   };
-  // the neighbourhood test of one candidate pixel p (frame-linear index)
-  auto test = [&](int64_t p) {
+  auto test = [&](int f, int64_t p) {
+    const PR_GLOBAL float* img = gin<float>(fp.in[f]);
     const float val = img[p];
     const int panel = (int)(p / hw);
     const int64_t rem = p - (int64_t)panel * hw;
@@ -161,74 +169,81 @@ __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp
         },
         val, pp, f, panel, y, x, peaks, counts, total);
   };
+  // block-reduce this frame's statistics and add them (one atomic pair per workgroup and frame)
+  auto flush = [&](int f, float s, int c) {
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_down(s, o);
+      c += __shfl_down(c, o);
+    }
+    __syncthreads();
+    if (lane == 0) {
+      red_sum[wave] = s;
+      red_cnt[wave] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float sm = red_sum[0] + red_sum[1] + red_sum[2] + red_sum[3];
+      const int cn = red_cnt[0] + red_cnt[1] + red_cnt[2] + red_cnt[3];
+      if (cn > 0) {
+        const float o0 = atomicAdd(summary + 2 * f, (float)cn);
+        const float o1 = atomicAdd(summary + 2 * f + 1, sm);
+        if (scratch != nullptr) asm volatile("" ::"v"(o0), "v"(o1));
+      }
+    }
+  };
   if (threadIdx.x == 0) cand_n = 0;
   __syncthreads();
-  int64_t chunk = blockIdx.x;
-  if (chunk < nchunks) load(chunk);
-  for (; chunk < nchunks; chunk += gridDim.x) {
-    // pass 1 (unrolled, registers only): hit statistics + a bitmask of the candidates
+  float above_sum = 0.0f;
+  int above_cnt = 0;
+  int fcur = (int)(g0 / ncpf);
+  if (g0 < g1) load(g0);
+  for (int64_t g = g0; g < g1; ++g) {
+    const int f = (int)(g / ncpf);   // wave-uniform
+    if (f != fcur) {
+      flush(fcur, above_sum, above_cnt);
+      above_sum = 0.0f;
+      above_cnt = 0;
+      fcur = f;
+    }
     uint64_t cand = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float val = v[k][e];
-        const bool hit = val > pp.thr_peak;   // rejects NaN padding too
+        const bool hit = val > pp.thr_peak;
         above_sum += hit ? val : 0.0f;
         above_cnt += hit ? 1 : 0;
         cand |= (uint64_t)hit << (4 * k + e);
       }
     }
-    const int64_t q0 = chunk * 256 * K + threadIdx.x;
-    if (chunk + gridDim.x < nchunks) load(chunk + gridDim.x);   // prefetch the next chunk
-    // pass 2 (rare): park the candidates in LDS; they are tested after the stream, one per lane
-    // (tested here, one lane at a time, the wave stalls on each candidate's dependent
-    // neighbourhood loads: 2.60 vs 1.72 us/frame without the test, epix10k2M)
+    const int64_t q0 = (g - (int64_t)f * ncpf) * 256 * K + threadIdx.x;
+    if (g + 1 < g1) load(g + 1);
     if (cand) {
       int slot = atomicAdd(&cand_n, __popcll(cand));
       while (cand) {
         const int b = __builtin_ctzll(cand);
         cand &= cand - 1;
         const int64_t p = 4 * (q0 + 256 * (b >> 2)) + (b & 3);
-        if (slot < kPfCandCap) cand_p[slot] = (int)p;
-        else test(p);   // list full: test in place
+        if (slot < kPfCandCap) {
+          cand_p[slot] = (int)p;
+          cand_f[slot] = (unsigned char)f;
+        } else {
+          test(f, p);
+        }
         ++slot;
       }
     }
   }
+  if (g0 < g1) flush(fcur, above_sum, above_cnt);
   __syncthreads();
   const int nc = min(cand_n, kPfCandCap);
-  for (int i = threadIdx.x; i < nc; i += blockDim.x) test(cand_p[i]);
-  for (int o = 32; o > 0; o >>= 1) {
-    above_sum += __shfl_down(above_sum, o);
-    above_cnt += __shfl_down(above_cnt, o);
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    red_sum[wave] = above_sum;
-    red_cnt[wave] = above_cnt;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float sm = red_sum[0] + red_sum[1] + red_sum[2] + red_sum[3];
-    const int c = red_cnt[0] + red_cnt[1] + red_cnt[2] + red_cnt[3];
-    if (c > 0) {
-      const float o0 = atomicAdd(summary + 2 * f, (float)c);
-      const float o1 = atomicAdd(summary + 2 * f + 1, sm);
-      // returning atomics: the wave waits until both were performed (needed before the done
-      // count below; the values themselves are not used)
-      if (scratch != nullptr) asm volatile("" ::"v"(o0), "v"(o1));
-    }
-  }
+  for (int i = threadIdx.x; i < nc; i += blockDim.x) test(cand_f[i], cand_p[i]);
   if (scratch == nullptr) return;
-  // Every slot reservation above was a returning device-scope atomic (the thread used its value),
-  // the statistics too: after the barrier all of this workgroup's updates are performed, so the
-  // done count needs no fence (an agent-scope fence writes back L2 -- measured: it cut the
-  // device-resident pipeline from 117k to 52k fr/s).
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned prev = atomicAdd(&scratch->done, 1u);
-    is_last = prev == gridDim.x * gridDim.y - 1;
+    is_last = prev == gridDim.x - 1;
   }
   __syncthreads();
   if (!is_last) return;
@@ -238,6 +253,21 @@ __global__ __launch_bounds__(256) void peakfind_stream_kernel(const FramePtrs fp
     summary_out[2 * i + 1] = atomicExch(&scratch->acc[2 * i + 1], 0.0f);
   }
   if (threadIdx.x == 0) atomicExch(&scratch->done, 0u);
+}
+
+// resident workgroups of a 256-thread kernel on the whole device (queried once per kernel)
+template <typename Kern>
+static int pf_resident_blocks(int which, Kern k) {
+  static int cache[2] = {0, 0};
+  int& n = cache[which];
+  if (n == 0) {
+    int dev = 0, cus = 0, per = 0;
+    hip_check(hipGetDevice(&dev), "pf device");
+    hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "pf cu count");
+    hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, 256, 0), "pf occupancy");
+    n = std::max(1, cus * std::max(1, per));
+  }
+  return n;
 }
 
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
@@ -255,20 +285,14 @@ void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, i
   int* C = reinterpret_cast<int*>(counts);
   float* S = reinterpret_cast<float*>(summary);
   unsigned long long* T = reinterpret_cast<unsigned long long*>(total);
-  // 4 float4 per lane (round-1 A/B: K=4 2.21, 8 2.22, 16 2.26 us/frame; nontemporal loads no
-  // faster; profiles/kernels_r1_peakfind_ab.jsonl); ~2048 workgroups for the whole batch (8 per CU)
-  constexpr int K = 4;
-  const int64_t n4 = (int64_t)n_panels * rows * cols / 4;
-  const int64_t nchunks = (n4 + 256 * K - 1) / (256 * K);
-  const int64_t target = 2048;
-  const int64_t per_frame = std::min(nchunks, std::max<int64_t>(4, (target + nframes - 1) / nframes));
-  const dim3 grid((unsigned)per_frame, (unsigned)nframes);
   PfScratch* X = reinterpret_cast<PfScratch*>(scratch);
   check(scratch % 8 == 0, "peakfind: misaligned scratch");
-  if (radius == 1)
-    hipLaunchKernelGGL((peakfind_stream_kernel<1, K>), grid, dim3(256), 0, s, fp, pp, P, C, S, T, X, nframes);
-  else
-    hipLaunchKernelGGL((peakfind_stream_kernel<2, K>), grid, dim3(256), 0, s, fp, pp, P, C, S, T, X, nframes);
+  constexpr int K = 4;   // float4 per lane per chunk (16 KB per 256-thread chunk)
+  const int64_t n4 = (int64_t)n_panels * rows * cols / 4;
+  const int64_t chunks = (n4 + 256 * K - 1) / (256 * K) * nframes;
+  auto kern = radius == 1 ? peakfind_range_kernel<1, K> : peakfind_range_kernel<2, K>;
+  const int g = (int)std::min<int64_t>(chunks, pf_resident_blocks(radius == 1 ? 0 : 1, kern));
+  hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, s, fp, pp, P, C, S, T, X, nframes);
   hip_check(hipGetLastError(), "peakfind launch");
 }
 

@@ -12,7 +12,7 @@ import torch
 
 from . import _ext
 
-MAX_FRAMES = 32
+MAX_FRAMES = 64
 # int32 words of the peak finder's self-resetting scratch (csrc/peakfind.hip PfScratch)
 PF_SCRATCH_WORDS = 3 * MAX_FRAMES + 1
 

@@ -60,7 +60,7 @@ def build_parser() -> argparse.ArgumentParser:
                    help="common-mode correction: off | default | flags,thr,maxcorr,npix_min[,bank_cols]")
     g.add_argument("--num_events", type=int, default=None, help="events in a synthetic run (default: endless)")
     g.add_argument("--data_dir", type=str, default=None, help="raw-run files directory (or $PSANA_RAY_DATA)")
-    g.add_argument("--chunk", type=int, default=32, help="frames per H2D copy / kernel launch")
+    g.add_argument("--chunk", type=int, default=64, help="frames per H2D copy / kernel launch (<= 64)")
     g.add_argument("--route", type=str, default="balanced", choices=["balanced", "local_first", "spread"])
     g.add_argument("--consumer_task", type=str, default="none", choices=["none", "peakfind"],
                    help="also consume on every producer rank (co-located consumer, BASELINE config 5)")

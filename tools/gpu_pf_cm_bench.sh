@@ -6,8 +6,8 @@ export PYTHONPATH=$R
 O=$R/gpurun_out/pcb
 mkdir -p $O
 timeout -k 10 300 python3 -u -m pytest $R/tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > $O/kernels_gpu.log 2>&1; rc=$?; tail -1 $O/kernels_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python3 $R/tools/pf_probe.py --vars 0,0 > $O/pf.log 2>&1 || exit $?
-grep variant $O/pf.log
+timeout -k 10 200 python3 $R/tools/pf_probe.py --repeat 2 > $O/pf.log 2>&1 || exit $?
+grep us_per_frame $O/pf.log
 timeout -k 10 200 python3 $R/tools/cm_probe.py --repeat 1 > $O/cm.log 2>&1 || exit $?
 grep round $O/cm.log
 cd $R

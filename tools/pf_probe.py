@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Peak-finder probe: device time per epix10k2M frame of peakfind_stream_kernel on 32
-calibrated frames (graph-replayed, event-timed), with the record count checked against variant 0.
+"""Peak-finder probe: device time per epix10k2M frame of the shipped peak finder on 32 (or
+--frames) calibrated frames (graph-replayed, event-timed), repeated --repeat times with the record
+count checked against the first launch.
 
-    python tools/pf_probe.py --vars 0,0
+    python tools/pf_probe.py --repeat 2
 """
 import argparse
 import json
@@ -21,7 +22,7 @@ from psana_ray_amd.source import SyntheticRun  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--vars", default="0")
+    ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--frames", type=int, default=32)
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
@@ -43,14 +44,14 @@ def main():
     ptrs = [int(f.data_ptr()) for f in frames]
 
     def launch(var):
-        C.peakfind(ptrs, P, H, W, float(pp.thr_peak), float(pp.son_min), int(pp.radius) + 16 * var,
+        C.peakfind(ptrs, P, H, W, float(pp.thr_peak), float(pp.son_min), int(pp.radius),
                    int(pp.max_peaks), int(peaks.data_ptr()), int(counts.data_ptr()), int(summary.data_ptr()),
                    _ext.stream_handle(), 0, int(scratch.data_ptr()))
 
     launch(0)
     torch.cuda.synchronize()
     ref_counts, ref_sum = counts.clone(), summary.clone()
-    for var in [int(v) for v in a.vars.split(",")]:
+    for var in range(a.repeat):
         launch(var)
         torch.cuda.synchronize()
         same = bool(torch.equal(counts, ref_counts)) and bool(torch.allclose(summary, ref_sum, rtol=1e-5))
@@ -72,7 +73,7 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) / 8)
         ts.sort()
-        res = {"variant": var, "same_counts": same, "peaks_frame0": int(ref_counts[0]),
+        res = {"run": var, "frames": F, "same_counts": same, "peaks_frame0": int(ref_counts[0]),
                "us_per_frame": round(1e3 * ts[len(ts) // 2] / F, 3)}
         line = json.dumps(res)
         print(line, flush=True)
