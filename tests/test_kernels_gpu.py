@@ -179,6 +179,31 @@ def test_peakfind_vs_reference(cuda_device, det, radius, scratch):
     assert torch.allclose(summary[:, 1].cpu(), ref_summary[:, 1], rtol=1e-4)
 
 
+@pytest.mark.parametrize("det,F", [("tiny_epix", kernels.MAX_FRAMES), ("jungfrau05M", 7)])
+def test_peakfind_full_batch(cuda_device, det, F):
+    """A whole launch (64 frames) and an odd frame count: the balanced grid's contiguous chunk
+    ranges cross frame boundaries at arbitrary points; every frame's statistics and records must
+    still match the golden model."""
+    spec, consts, raw = _setup(det, F, seed=11, gain_config="AHL")
+    frames = reference.calibrate_reference(raw.to(torch.int32), consts, None, None)
+    params = PeakFinderParams(thr_peak=15.0, son_min=4.0, radius=1, max_peaks=4096)
+    d = frames.to(cuda_device).contiguous()
+    peaks = torch.zeros((F, params.max_peaks, 8), dtype=torch.float32, device=cuda_device)
+    counts = torch.zeros(F, dtype=torch.int32, device=cuda_device)
+    summary = torch.zeros((F, 2), dtype=torch.float32, device=cuda_device)
+    scr = torch.zeros(kernels.PF_SCRATCH_WORDS, dtype=torch.int32, device=cuda_device)
+    kernels.peakfind([d[i] for i in range(F)], spec.frame_shape, params, peaks, counts, summary, scratch=scr)
+    torch.cuda.synchronize()
+    ref_peaks, ref_summary = reference.peakfind_reference(frames, params)
+    assert int(scr.abs().sum()) == 0
+    for f in range(F):
+        n = int(counts[f])
+        assert n == ref_peaks[f].shape[0], f"frame {f}: {n} peaks vs reference {ref_peaks[f].shape[0]}"
+        assert torch.equal(_sorted_peaks(peaks[f, :n])[:, :4], _sorted_peaks(ref_peaks[f])[:, :4])
+    assert torch.equal(summary[:, 0].cpu(), ref_summary[:, 0])
+    assert torch.allclose(summary[:, 1].cpu(), ref_summary[:, 1], rtol=1e-4)
+
+
 def test_kernel_rejects_bad_shapes(cuda_device):
     spec, consts, raw = _setup("tiny_epix", 1)
     cal = Calibrator(consts, cuda_device, Mode.calib)
