@@ -12,7 +12,7 @@
 // Per-frame summary: number of pixels above thr_peak and their sum (hit-finding statistics),
 // reduced wave -> LDS -> one atomic per workgroup.
 //
-// MI355X design: candidates are rare in detector frames, so the default (v3 "stream") reads every
+// MI355X design: candidates are rare in detector frames, so the kernel reads every
 // pixel once with coalesced 16-B loads, thresholds in registers, and sends only the rare
 // candidates through the neighbourhood test (direct, cache-hit reads); one atomic per accepted
 // peak reserves its record slot (and bumps an optional 64-bit running total, so consumers never
@@ -92,12 +92,12 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
 }
 
 // ---------------------------------------------------------------------------------------------
-// v3 "stream" (default): candidates are rare in detector frames (synthetic epix10k2M: 0.02 % of
-// pixels above thr_peak, 0.5 % of 64-pixel wave rows contain one), so an LDS halo tile is
-// overhead: here every pixel is read ONCE with coalesced 16-B loads (4 float4 per lane in flight),
-// thresholded in registers, and only the rare candidates read their neighbourhood directly from
-// global memory (just-touched lines, L1/L2 hits).  No halo over-fetch, no LDS, no barrier except
-// the per-block reduction of the hit statistics.
+// Streaming form: candidates are rare in detector frames (synthetic epix10k2M: 0.02 % of pixels
+// above thr_peak, 0.5 % of 64-pixel wave rows contain one), so an LDS halo tile is overhead: every
+// pixel is read ONCE with coalesced 16-B loads (4 float4 per lane in flight), thresholded in
+// registers, and only the rare candidates -- parked in LDS until the stream ends, then tested one
+// per lane -- read their neighbourhood directly from global memory (just-touched lines, L1/L2
+// hits).  No halo over-fetch; LDS only for the parked candidates and the statistics reduction.
 // ---------------------------------------------------------------------------------------------
 // The per-frame hit statistics are device-scope atomics to ONE address pair per frame, and
 // same-address atomics serialise (~3 ns each, measured: read_f32 with one atomic per 8-KB block
