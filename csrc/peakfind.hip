@@ -39,12 +39,21 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
                                              int gx, float* __restrict__ peaks, int* __restrict__ counts,
                                              unsigned long long* __restrict__ total) {
   constexpr int H = RAD + 2;
+  constexpr int D = 2 * H + 1;
+  // the whole (2H+1)^2 neighbourhood is loaded up front: ONE round of independent loads instead of
+  // one per test below (the tests run after the stream, so their latency is the kernel's tail;
+  // measured 1.824-1.828 vs 1.836-1.842 us/frame, 32 epix10k2M frames)
+  float w[D][D];
+#pragma unroll
+  for (int dy = -H; dy <= H; ++dy)
+#pragma unroll
+    for (int dx = -H; dx <= H; ++dx) w[dy + H][dx + H] = (dy == 0 && dx == 0) ? v : at(dy, dx);
 #pragma unroll
   for (int dy = -RAD; dy <= RAD; ++dy)
 #pragma unroll
     for (int dx = -RAD; dx <= RAD; ++dx) {
       if (dy == 0 && dx == 0) continue;
-      const float n = at(dy, dx);
+      const float n = w[dy + H][dx + H];
       if (n != n) continue;
       const bool before = (dy < 0) || (dy == 0 && dx < 0);
       if (before ? !(v > n) : !(v >= n)) return;   // not the strict local max (ties: lower index wins)
@@ -57,7 +66,7 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
     for (int dx = -H; dx <= H; ++dx) {
       const int d = max(abs(dy), abs(dx));
       if (d <= RAD) continue;
-      const float n = at(dy, dx);
+      const float n = w[dy + H][dx + H];
       if (n != n) continue;
       s += n;
       s2 += n * n;
@@ -73,7 +82,7 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
   for (int dy = -RAD; dy <= RAD; ++dy)
 #pragma unroll
     for (int dx = -RAD; dx <= RAD; ++dx) {
-      const float n = at(dy, dx);
+      const float n = w[dy + H][dx + H];
       if (n == n) inten += n - bkg;
     }
   const int slot = atomicAdd(counts + f, 1);

@@ -23,6 +23,7 @@ from psana_ray_amd.source import SyntheticRun  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--thr", type=float, default=None, help="thr_peak (default: PeakFinderParams)")
     ap.add_argument("--frames", type=int, default=32)
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
@@ -35,7 +36,7 @@ def main():
     frames = [cal(raw[i % raw.shape[0]]).contiguous() for i in range(F)]
     # every buffer distinct and cold-ish: 32 x 8.65 MB
     frames = [f.clone() for f in frames]
-    pp = PeakFinderParams()
+    pp = PeakFinderParams() if a.thr is None else PeakFinderParams(thr_peak=a.thr)
     P, H, W = src.spec.frame_shape
     peaks = torch.zeros((F, pp.max_peaks, 8), dtype=torch.float32, device=dev)
     counts = torch.zeros(F, dtype=torch.int32, device=dev)
