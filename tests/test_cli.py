@@ -187,3 +187,21 @@ def test_sigint_on_endless_producer_ends_stream_cleanly(native):
     assert "end of stream" in out, out[-3000:]
     idx = [int(l.split("idx=")[1].split()[0]) for l in lines if "processed:" in l]
     assert idx == list(range(len(idx))), "frames lost or duplicated before EOS"
+
+
+def test_consumer_without_a_store_fails_with_one_line():
+    """No rendezvous store at the address: the consumer CLI ends with one clear error line and
+    rc 1 (no traceback)."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    p = subprocess.run([sys.executable, "-m", "psana_ray_amd.consumer", "--ray_address", f"127.0.0.1:{port}",
+                        "--timeout", "2", "--metrics_interval", "0"], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 1, p.stdout + p.stderr
+    assert "Traceback" not in p.stderr, p.stderr
+    assert "could not join the queue" in p.stderr and f"127.0.0.1:{port}" in p.stderr, p.stderr
