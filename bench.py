@@ -14,9 +14,11 @@ GPU that produced them unless another shard is starving).
 
 N > 1: every rank is a member of one queue session on torchrun's store and links to every other
 rank through the elastic fabric (csrc/fabric.h).  After the headline window a SECOND fixed-step
-window runs with ``route=spread`` (each producer deals its frames round-robin over all consumer
-GPUs, so (N-1)/N of them cross xGMI as HIP-IPC peer copies); its frames/s, cross-GPU GB/s and
-bytes per rank are reported under ``extra.xgmi_phase`` (``--cross-steps 0`` skips it).
+window runs with ``route=remote_only`` (a producer never keeps a frame on its own GPU while a
+consumer on another GPU is linked: every frame crosses xGMI as a HIP-IPC peer copy); its frames/s,
+cross-GPU GB/s and bytes per rank are reported under ``extra.xgmi_phase`` (``--cross-steps 0``
+skips it).  The run is self-validating: it exits non-zero (after printing its line) when a link
+failed or never attached, or when less than 90% of that window's frames crossed GPUs.
 
 Synthetic data: random-init calibration constants and a pre-generated pool of raw frames
 (cycled), because no LCLS data / psana exists offline (BASELINE.json).
@@ -44,10 +46,10 @@ def parse(argv=None):
     ap.add_argument("--mode", default="calib", choices=["calib", "image", "raw"])
     ap.add_argument("--common-mode", default="default", help="off | default | flags,thr,maxcorr,npix_min[,bank]")
     ap.add_argument("--consumer", default="peakfind", choices=["peakfind", "none"])
-    ap.add_argument("--route", default="balanced", choices=["balanced", "local_first", "spread"],
+    ap.add_argument("--route", default="balanced", choices=["balanced", "local_first", "spread", "remote_only"],
                     help="routing policy of the headline window")
     ap.add_argument("--cross-steps", type=int, default=None,
-                    help="N > 1: steps of the second, route=spread window that pushes frames across GPUs over xGMI "
+                    help="N > 1: steps of the second, route=remote_only window that pushes frames across GPUs over xGMI "
                          "(default: --steps; 0 skips it)")
     ap.add_argument("--queue-size", type=int, default=None,
                     help="logical (global) queue capacity; default 400 per GPU (README.md:20 example, weak scaling: "
@@ -59,6 +61,9 @@ def parse(argv=None):
                          "32 132.0-134.5k vs 16 119.9k fr/s; host-staged 13.03k vs 12.90k; profiles/r2/pipeline_chunks.md)")
     ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--preroll-s", type=float, default=0.5,
+                    help="untimed streaming before the warmup steps: the queue fills and the GPU clocks settle, so "
+                         "a 20-step window measures the same steady state as a 200-step one")
     ap.add_argument("--producers", type=int, default=0,
                     help="producer ranks P (ranks < P produce, every rank consumes; 0 = all).  BASELINE config 3: "
                          "--gpus 8 --producers 4")
@@ -112,6 +117,7 @@ def main(argv=None):
     from psana_ray_amd.queue.ring import physical_slots
     from psana_ray_amd.queue.session import QueueSession, create_or_attach
     from psana_ray_amd.source import SyntheticRun
+    from psana_ray_amd.utils.metrics import sustained_rate
 
     sys.setswitchinterval(5e-4)   # short GIL hand-off: fabric / consumer threads stay responsive
     li = detect()
@@ -243,34 +249,61 @@ def main(argv=None):
                 raise RuntimeError(f"queue fabric failed: {ep.failed!r}")
         return got
 
-    def sync():
+    def csync():
+        """This rank's consumer work issued so far has finished (its stream, not the device: a
+        device-wide synchronize would also drain the producer's queued copies and kernels, and the
+        frames they complete would then be consumed inside the window for free -- VERDICT r2 #1)."""
         if gpu:
-            torch.cuda.synchronize(device)
+            (consumer.stream if consumer is not None else torch.cuda.current_stream(device)).synchronize()
+
+    cstream = (consumer.stream if consumer is not None else torch.cuda.current_stream(device)) if gpu else None
 
     def window(steps):
-        """``steps`` timed steps between barriers: (seconds (max over ranks), frames produced in the
-        window (sum over ranks), fabric counters before and after on this rank)."""
-        sync()
+        """``steps`` timed steps between barriers, in steady state.  Returns (host seconds, max over
+        ranks; sustained frames/s of the node = min(sum over producers of the production rate,
+        frames consumed / seconds); frames completed by the producers inside the window (sum);
+        details; fabric counters before and after on this rank).
+
+        Production is counted at DEVICE COMPLETION (one timing event per producer chunk) and only
+        for chunks that completed after t0: frames already READY when the window opened are
+        excluded, and the rate runs between two chunk completions (utils.metrics.sustained_rate),
+        so a short window and a long one measure the same steady state."""
+        csync()
         barrier()
-        sync()
+        csync()
         c0 = ep.metrics()
+        m0 = prod.clock(cstream) if prod is not None else None
         t0 = time.perf_counter()
-        p0 = prod.produced if prod is not None else 0
         consume(steps * B)
-        sync()
+        csync()
         t1 = time.perf_counter()
-        p1 = prod.produced if prod is not None else 0
+        m1 = prod.clock(cstream) if prod is not None else None
         c1 = ep.metrics()
+        if gpu:
+            torch.cuda.synchronize(device)   # untimed: the whole device is idle-consistent before the barrier
         barrier()
-        dt, pw = t1 - t0, p1 - p0
+        dt = t1 - t0
+        fr_p, rate_p = 0, 0.0
+        if prod is not None:
+            _, lg = prod.completion_log(0)
+            fr_p, r = sustained_rate(lg, m0, m1)
+            # fewer than two chunk completions around the window (a producer slower than one chunk
+            # per window): frames completed inside it over the whole window
+            rate_p = r if r is not None else fr_p / max(dt, 1e-9)
         if coord is not None:
             t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=coord)
             dt = float(t[0])
-            v = torch.tensor([pw], dtype=torch.int64)
+            v = torch.tensor([rate_p, float(fr_p)], dtype=torch.float64)
             dist.all_reduce(v, op=dist.ReduceOp.SUM, group=coord)
-            pw = int(v[0])
-        return dt, pw, p1 - p0, c0, c1
+            rate_sum, fr_sum = float(v[0]), int(v[1])
+        else:
+            rate_sum, fr_sum = rate_p, fr_p
+        consumed_rate = world * steps * B / dt
+        value = min(rate_sum, consumed_rate)
+        det = {"production_frames_per_s": round(rate_sum, 1), "consumer_frames_per_s": round(consumed_rate, 1),
+               "produced_in_window": fr_sum, "produced_in_window_rank0": fr_p}
+        return dt, value, fr_sum, det, c0, c1
 
     def allsum(x):
         if coord is None:
@@ -280,25 +313,25 @@ def main(argv=None):
         return out
 
     B = args.batch
-    total = world * args.steps * B
+    t_pre = time.perf_counter()
+    while time.perf_counter() - t_pre < args.preroll_s:
+        consume(B)
+    barrier()
     consume(args.warmup * B)
-    dt, produced_window, p_rank0, c0, c1 = window(args.steps)
-    # sustained throughput through the queue: frames can only leave as fast as they enter, so a
-    # ring that was already (partly) full at t0 must not count -- report min(consumed, produced)
-    value = min(total, produced_window) / dt
+    dt, value, produced_window, rate_detail, c0, c1 = window(args.steps)
 
     cross = None
     cross_steps = args.steps if args.cross_steps is None else args.cross_steps
     if world > 1 and cross_steps > 0:
-        ep.set_route("spread")
+        ep.set_route("remote_only")
         # drain what the headline policy already put into this shard (FIFO), then warm up: the
         # window must see frames routed by the new policy, not the old backlog
         consume(int(ep.metrics().get("ready", 0)) + max(2, args.warmup // 2) * B)
-        xdt, xpw, _, x0, x1 = window(cross_steps)
-        xtotal = world * cross_steps * B
+        xdt, xval, xpw, xdet, x0, x1 = window(cross_steps)
         sent = allsum(int(x1.get("bytes_sent", 0) - x0.get("bytes_sent", 0)))
         fr_sent = allsum(int(x1.get("frames_sent", 0) - x0.get("frames_sent", 0)))
         fr_local = allsum(int(x1.get("frames_local", 0) - x0.get("frames_local", 0)))
+        fr_recv = allsum(int(x1.get("frames_recv", 0) - x0.get("frames_recv", 0)))
         cms = allsum(round(float(x1.get("copy_ms_per_batch", 0.0)), 3))
         keys = ("grants_given", "grants_returned", "grants_reclaimed", "frames_recv", "frames_requeued")
         fab = allsum({k: int(x1.get(k, 0) - x0.get(k, 0)) for k in keys} |
@@ -306,10 +339,11 @@ def main(argv=None):
                       "held": int(x1.get("held", 0)),
                       "links": [[int(l.peer), bool(l.outgoing), int(l.outstanding), int(l.frames)] for l in ep.links()]})
         cross = {
-            "route": "spread", "steps": cross_steps, "ms_per_step": round(1e3 * xdt / cross_steps, 4),
-            "frames_per_s": round(min(xtotal, xpw) / xdt, 2),
+            "route": "remote_only", "steps": cross_steps, "ms_per_step": round(1e3 * xdt / cross_steps, 4),
+            "frames_per_s": round(xval, 2), **xdet,
             "cross_gpu_GB_per_s": round(sum(sent) / xdt / 1e9, 2),
             "cross_gpu_fraction": round(sum(fr_sent) / max(1, sum(fr_sent) + sum(fr_local)), 3),
+            "received_cross_per_consumed": round(sum(fr_recv) / max(1, world * cross_steps * B), 3),
             "bytes_sent_per_rank": sent, "frames_sent_per_rank": fr_sent, "frames_local_per_rank": fr_local,
             "copy_ms_per_batch_per_rank": cms,
             "fabric_per_rank": fab,
@@ -375,9 +409,10 @@ def main(argv=None):
             "queue": "local (single process)" if sess is None else "elastic fabric session",
         },
         "extra": {
-            "producer_frames_per_s_rank0": round(p_rank0 / max(dt, 1e-9), 1),
-            "consumed_frames_per_s": round(total / dt, 1),
-            "produced_frames_per_s": round(produced_window / dt, 1),
+            **rate_detail,
+            "timing": "t0/t1: barrier + consumer-stream synchronize (steady state; a device-wide synchronize "
+                      "would drain the producer pipeline into the window), device-wide synchronize after t1; "
+                      "production counted at device completion of each chunk, chunks ready at t0 excluded",
             "frame_bytes": ring.frame_bytes,
             "queue_slots_physical_rank0": cslots,
             "ring_GB_rank0": round(ring.nbytes / 1e9, 1),
@@ -398,6 +433,18 @@ def main(argv=None):
                 else None),
         },
     }
+    # self-validation: every link attached, none failed, and the cross window
+    # really crossed GPUs -- otherwise the line is printed for diagnosis but the run fails
+    problems = []
+    if sess is not None:
+        failed_links = sum(allsum(int(ep.metrics().get("links_failed", 0))))
+        if failed_links:
+            problems.append(f"{failed_links} fabric link(s) failed")
+        if linking is not None and not all(allsum(bool(linking.get("complete")))):
+            problems.append("some rank's links never completed")
+        if cross is not None and cross["cross_gpu_fraction"] < 0.9:
+            problems.append(f"only {cross['cross_gpu_fraction']:.3f} of the cross window's frames crossed GPUs")
+    result["extra"]["validation"] = problems or "ok"
     if rank == 0:
         line = json.dumps(result)
         print(line, flush=True)
@@ -423,6 +470,9 @@ def main(argv=None):
         if not clean:
             print(f"bench.py rank {rank}: queue fabric reported {ep.failed!r}", file=sys.stderr, flush=True)
             return 3
+    if problems:
+        print(f"bench.py rank {rank}: INVALID run: {'; '.join(problems)}", file=sys.stderr, flush=True)
+        return 4
     return 0
 
 

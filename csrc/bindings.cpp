@@ -244,6 +244,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("links_opened", &pr::FabricStats::links_opened)
       .def_readonly("peers_dead", &pr::FabricStats::peers_dead)
       .def_readonly("links_failed", &pr::FabricStats::links_failed)
+      .def_readonly("frames_returned", &pr::FabricStats::frames_returned)
+      .def_readonly("frames_reclaimed", &pr::FabricStats::frames_reclaimed)
+      .def_readonly("frames_dropped", &pr::FabricStats::frames_dropped)
+      .def_readonly("returns_rejected", &pr::FabricStats::returns_rejected)
+      .def_readonly("readahead", &pr::FabricStats::readahead)
       .def_readonly("copy_s", &pr::FabricStats::copy_s);
   py::class_<pr::LinkStatus>(m, "LinkStatus")
       .def_readonly("peer", &pr::LinkStatus::peer)
@@ -253,6 +258,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("detached", &pr::LinkStatus::detached)
       .def_readonly("dead", &pr::LinkStatus::dead)
       .def_readonly("closed", &pr::LinkStatus::closed)
+      .def_readonly("keeper", &pr::LinkStatus::keeper)
+      .def_readonly("taken", &pr::LinkStatus::taken)
       .def_readonly("outstanding", &pr::LinkStatus::outstanding)
       .def_readonly("frames", &pr::LinkStatus::frames);
   py::class_<pr::QueueFabric>(m, "QueueFabric")
@@ -279,6 +286,9 @@ PYBIND11_MODULE(_C, m) {
       .def("error", &pr::QueueFabric::error)
       .def("last_link_error", &pr::QueueFabric::last_link_error)
       .def("set_grant_filter", &pr::QueueFabric::set_grant_filter, py::arg("on"))
+      .def("set_prefetch", &pr::QueueFabric::set_prefetch, py::arg("n"))
+      .def_property_readonly("prefetch", &pr::QueueFabric::prefetch)
+      .def("set_keeper", &pr::QueueFabric::set_keeper, py::arg("on"))
       .def("set_peer_grantable", &pr::QueueFabric::set_peer_grantable, py::arg("mid"), py::arg("on"))
       .def("stats", &pr::QueueFabric::stats)
       .def("links", &pr::QueueFabric::links);
@@ -370,6 +380,12 @@ PYBIND11_MODULE(_C, m) {
       .def("complete_recv_batch", &SP::complete_recv_batch, py::arg("slots"), py::arg("headers"))
       .def("cancel_recv_batch", &SP::cancel_recv_batch, py::arg("slots"))
       .def("reoffer_batch", &SP::reoffer_batch, py::arg("slots"), py::arg("stream"))
+      .def("set_external_held", &SP::set_external_held, py::arg("n"))
+      .def("producer_room", &SP::producer_room)
+      .def("set_track_origins", &SP::set_track_origins, py::arg("on"))
+      .def("take_got_origins", &SP::take_got_origins)
+      .def("origin", &SP::origin, py::arg("slot"))
+      .def("pop_ready_for_return", &SP::pop_ready_for_return, py::arg("max_n"))
       .def("unsend_batch", &SP::unsend_batch, py::arg("slots"))
       .def_property_readonly("event_records", &SP::event_records);
 
@@ -425,6 +441,16 @@ PYBIND11_MODULE(_C, m) {
       .def("join", &pr::ProducerEngine::join, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &pr::ProducerEngine::running)
       .def_property_readonly("frames", &pr::ProducerEngine::frames)
+      .def_property_readonly("completed", &pr::ProducerEngine::completed)
+      .def(
+          "completions",
+          [](const pr::ProducerEngine& e, int64_t since) {
+            int64_t first = 0;
+            auto v = e.completions(since, &first);
+            return py::make_tuple(first, v);
+          },
+          py::arg("since") = 0)
+      .def("mark", &pr::ProducerEngine::mark, py::arg("stream"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("full_waits", &pr::ProducerEngine::full_waits)
       .def("error", &pr::ProducerEngine::error)
       .def("timing", &pr::ProducerEngine::timing)

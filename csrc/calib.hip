@@ -60,7 +60,7 @@ __device__ __forceinline__ float4 calib4(const uint2 r, const float (&p)[NT][4],
       pp = bsel(c == 0, p[0][i], bsel(c == 1, p[1][i], p[2][i]));
       gg = bsel(c == 0, g[0][i], bsel(c == 1, g[1][i], g[2][i]));
     }
-    const float v = (decode_adu(raw, KIND) - pp) * gg;
+    const float v = gmul(decode_adu(raw, KIND) - pp, gg);
     o[i] = valid ? v : 0.0f;
   }
   return make_float4(o[0], o[1], o[2], o[3]);
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void calib_image_kernel(const FramePtrs fp, co
           pp = bsel(c == 0, p[0][i], bsel(c == 1, p[1][i], p[2][i]));
           gg = bsel(c == 0, g[0][i], bsel(c == 1, g[1][i], g[2][i]));
         }
-        val = valid ? (decode_adu(r, KIND) - pp) * gg : 0.0f;
+        val = valid ? gmul(decode_adu(r, KIND) - pp, gg) : 0.0f;
       }
       o[i] = val;
     }

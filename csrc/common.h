@@ -46,6 +46,12 @@ __device__ __forceinline__ float decode_adu(uint32_t raw, int kind) {
   return (float)(kind == kPlain ? raw : (raw & 0x3FFFu));
 }
 
+// value x gain factor with a +0 addend: a pixel the mask folded to gain factor 0 comes out +0 for
+// a negative value too (a plain product gives -0), bit-identical to the reference's
+// np.where(mask, data, 0) (psana_ray/producer.py:92-95).  Same instruction count: the multiply
+// becomes v_fma_f32 / v_pk_fma_f32; every non-zero product is unchanged.
+__device__ __forceinline__ float gmul(float v, float g) { return __builtin_fmaf(v, g, 0.0f); }
+
 inline void check(bool ok, const std::string& msg) {
   if (!ok) throw std::runtime_error("psana_ray_amd: " + msg);
 }

@@ -411,7 +411,7 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
     for (int j = 0; j < 8; ++j) xv[j] = xv[j] != xv[j] ? v[j] : xv[j];
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = xv[j] * cm_gain<NT>(ga, cb, j);
+  for (int j = 0; j < 8; ++j) o[j] = gmul(xv[j], cm_gain<NT>(ga, cb, j));
 }
 
 // Store phase, part 2.  Part 1 leaves the finished output tile in LDS; part 2 only reads LDS

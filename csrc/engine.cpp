@@ -107,6 +107,7 @@ ProducerEngine::ProducerEngine(SlotPool* pool, int64_t slot_bytes, int device,
     h2d_pending_.assign(n_raw_bufs_, 0);
     calib_pending_.assign(n_raw_bufs_, 0);
   }
+  hip_check(hipEventCreate(&origin_), "hipEventCreate (origin)");
   region_bytes_ = (int64_t)chunk_ * (plan.raw_frame_bytes + kCopySlack);
   hip_check(hipMalloc(&raw_bufs_, (size_t)n_raw_bufs_ * region_bytes_), "hipMalloc raw chunks");
   dev_in_.assign(n_raw_bufs_, std::vector<uint64_t>(chunk_, 0));
@@ -123,6 +124,8 @@ ProducerEngine::~ProducerEngine() {
   for (auto e : h2d_done_) (void)hipEventDestroy(e);
   for (auto e : h2d_start_) (void)hipEventDestroy(e);
   for (auto e : calib_start_) (void)hipEventDestroy(e);
+  for (auto e : done_all_) (void)hipEventDestroy(e);
+  if (origin_) (void)hipEventDestroy(origin_);
   if (raw_bufs_) (void)hipFree(raw_bufs_);
   if (file_staging_) (void)hipHostFree(file_staging_);
   if (h2d_) (void)hipStreamDestroy(h2d_);
@@ -170,6 +173,14 @@ void ProducerEngine::start(int64_t n_local_events, int64_t max_steps, int64_t k0
   check(k0 >= 0, "ProducerEngine: negative start event");
   check(!running_.load() && !thread_.joinable(), "ProducerEngine: already started");
   stop_.store(false);
+  {
+    std::lock_guard<std::mutex> lk(done_mu_);
+    if (!origin_recorded_) {   // the completion log's clock starts here
+      hip_check(hipSetDevice(device_), "hipSetDevice");
+      hip_check(hipEventRecord(origin_, compute_), "record origin");
+      origin_recorded_ = true;
+    }
+  }
   running_.store(true);
   thread_ = std::thread([this, n_local_events, max_steps, k0] { loop(n_local_events, max_steps, k0); });
 }
@@ -213,6 +224,79 @@ void ProducerEngine::harvest(int b, bool block) {
 std::vector<double> ProducerEngine::gpu_timing() const {
   std::lock_guard<std::mutex> lk(err_mu_);
   return {gpu_h2d_ms_, (double)gpu_h2d_n_, gpu_calib_ms_, (double)gpu_calib_n_};
+}
+
+// Move completed chunks from the pending queue into the log (done_mu_ held).  Events complete in
+// stream order, so polling stops at the first chunk still running.
+void ProducerEngine::note_chunk_done_locked() const {
+  while (!done_pending_.empty()) {
+    hipEvent_t e = done_pending_.front().first;
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipErrorNotReady) return;
+    hip_check(q, "hipEventQuery (chunk done)");
+    float ms = 0.f;
+    hip_check(hipEventElapsedTime(&ms, origin_, e), "hipEventElapsedTime (chunk done)");
+    done_frames_ = done_pending_.front().second;
+    done_log_.emplace_back(done_frames_, (double)ms);
+    done_pending_.pop_front();
+    done_free_.push_back(e);
+  }
+  if (done_log_.size() > (size_t(1) << 17)) {   // bounded: keep the newest 64k chunks
+    const size_t drop = done_log_.size() - (size_t(1) << 16);
+    done_log_.erase(done_log_.begin(), done_log_.begin() + (ptrdiff_t)drop);
+    done_base_ += (int64_t)drop;
+  }
+}
+
+void ProducerEngine::record_chunk_done(int n) {
+  std::lock_guard<std::mutex> lk(done_mu_);
+  note_chunk_done_locked();
+  hipEvent_t e;
+  if (!done_free_.empty()) {
+    e = done_free_.back();
+    done_free_.pop_back();
+  } else {
+    hip_check(hipEventCreate(&e), "hipEventCreate (chunk done)");
+    done_all_.push_back(e);
+  }
+  hip_check(hipEventRecord(e, compute_), "record chunk done");
+  enq_frames_ += n;
+  done_pending_.emplace_back(e, enq_frames_);
+}
+
+int64_t ProducerEngine::completed() const {
+  std::lock_guard<std::mutex> lk(done_mu_);
+  (void)hipSetDevice(device_);
+  note_chunk_done_locked();
+  return done_frames_;
+}
+
+std::vector<std::pair<int64_t, double>> ProducerEngine::completions(int64_t since, int64_t* first_index) const {
+  std::lock_guard<std::mutex> lk(done_mu_);
+  (void)hipSetDevice(device_);
+  note_chunk_done_locked();
+  const int64_t a = std::max(since, done_base_);
+  if (first_index != nullptr) *first_index = a;
+  std::vector<std::pair<int64_t, double>> out;
+  for (int64_t i = a; i < done_base_ + (int64_t)done_log_.size(); ++i) out.push_back(done_log_[(size_t)(i - done_base_)]);
+  return out;
+}
+
+double ProducerEngine::mark(uint64_t stream) const {
+  hipEvent_t e;
+  {
+    std::lock_guard<std::mutex> lk(done_mu_);
+    check(origin_recorded_, "ProducerEngine.mark: the engine has not started");
+  }
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipEventCreate(&e), "hipEventCreate (mark)");
+  float ms = 0.f;
+  hipError_t err = hipEventRecord(e, reinterpret_cast<hipStream_t>(stream));
+  if (err == hipSuccess) err = hipEventSynchronize(e);
+  if (err == hipSuccess) err = hipEventElapsedTime(&ms, origin_, e);
+  (void)hipEventDestroy(e);
+  hip_check(err, "ProducerEngine.mark");
+  return (double)ms;
 }
 
 std::string ProducerEngine::error() const {
@@ -409,6 +493,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
         }
       }
       pool_->commit_batch(slots, hdrs, stream_c);   // one ready event for the whole chunk
+      record_chunk_done(n);
       t_commit_ += secs(t3, clk::now());
       frames_.fetch_add(n);
       k = k_next;
@@ -417,6 +502,10 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
     }
     hip_check(hipStreamSynchronize(compute_), "final sync");
     hip_check(hipStreamSynchronize(h2d_), "final sync");
+    {
+      std::lock_guard<std::mutex> lk(done_mu_);
+      note_chunk_done_locked();
+    }
     for (int b = 0; b < n_raw_bufs_; ++b) harvest(b, true);
   } catch (const std::exception& e) {
     std::lock_guard<std::mutex> lk(err_mu_);

@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -87,7 +88,17 @@ class ProducerEngine {
   void request_stop() { stop_.store(true); }
   bool join(double timeout_s);   // true when the thread has exited
   bool running() const { return running_.load(); }
+  // frames whose calibration was ENQUEUED (committed to the pool; the kernels may still run)
   int64_t frames() const { return frames_.load(); }
+  // Completion log (sustained-rate accounting): every chunk records a timing event
+  // after its calibration; once it has completed on the device the chunk is logged as
+  // (frames completed so far, device ms since the engine's origin event).  completions(i) returns
+  // the entries with index >= i (older entries are trimmed past 64k chunks) and polls first.
+  int64_t completed() const;
+  std::vector<std::pair<int64_t, double>> completions(int64_t since, int64_t* first_index) const;
+  // Device ms since the origin of the event recorded now on `stream` (host waits for it): puts a
+  // point of another stream (a consumer's) on the completion log's clock.
+  double mark(uint64_t stream) const;
   int64_t full_waits() const { return full_waits_.load(); }
   std::string error() const;
   // host-side time (seconds) spent per loop part: [stage copies, acquire slots, launch kernels, commit, total]
@@ -135,6 +146,18 @@ class ProducerEngine {
   int64_t region_bytes_ = 0;
   std::vector<std::vector<uint64_t>> dev_in_;
   std::atomic<int64_t> span_copies_{0}, frame_copies_{0}, kernel_copies_{0};
+  // completion log (see completed()); done_mu_ guards everything below it
+  void note_chunk_done_locked() const;
+  void record_chunk_done(int n);
+  mutable std::mutex done_mu_;
+  hipEvent_t origin_ = nullptr;
+  bool origin_recorded_ = false;
+  mutable std::vector<hipEvent_t> done_free_;
+  std::vector<hipEvent_t> done_all_;
+  mutable std::deque<std::pair<hipEvent_t, int64_t>> done_pending_;   // (event, cumulative frames)
+  mutable std::vector<std::pair<int64_t, double>> done_log_;
+  mutable int64_t done_base_ = 0, done_frames_ = 0;
+  int64_t enq_frames_ = 0;
   std::thread thread_;
   std::atomic<bool> stop_{false}, running_{false};
   std::atomic<int64_t> frames_{0}, full_waits_{0};

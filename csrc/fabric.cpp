@@ -22,9 +22,12 @@ namespace pr {
 namespace {
 
 constexpr uint64_t kLinkMagic = 0x314B4E494C525350ull;  // "PSRLINK1"
-constexpr int32_t kLinkVersion = 1;
+constexpr int32_t kLinkVersion = 2;
 constexpr int32_t kNoticeReturned = 1;   // the grant comes back unused (producer finished / closing)
+constexpr int32_t kNoticeReclaimed = 2;  // a returned frame was copied out: its slot is free again
+constexpr int32_t kNoticeRejected = 4;   // a returned frame was refused (EOS posted): route it elsewhere
 constexpr double kPidCheckS = 0.05;
+constexpr double kKeeperDebounceS = 0.1;   // a live producer's backlog must lack other credit this long
 
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -47,10 +50,11 @@ struct Notice {
 static_assert(sizeof(Notice) == 48, "Notice layout");
 
 // The mailbox of one link.  Written by the consumer at creation; afterwards every field has ONE
-// writer: grants/g_head/consumer_closed by the consumer, the rest by the producer.  Counters are
-// monotonic; ring entries are written before the counter is released and read after it is
-// acquired.  Occupancy of both rings is bounded by the outstanding grants (<= n_slots): a slot
-// is granted again only after the consumer took its notice and the frame was released.
+// writer: grants/g_head, returns/r_head, taken and consumer_closed by the consumer, the rest by the
+// producer.  Counters are monotonic; ring entries are written before the counter is released and
+// read after it is acquired.  Every slot of the consumer ring has at most one open exchange on a
+// link (granted and not answered, or returned and not answered), so no ring holds more than
+// n_slots entries.
 struct SegDesc {          // one allocation of an HBM consumer ring
   uint8_t handle[HIP_IPC_HANDLE_SIZE];
   int64_t offset;         // of slot `first` inside the allocation
@@ -67,7 +71,7 @@ struct alignas(64) LinkSeg {
   int32_t kind;           // 0 host shared memory, 1 HIP IPC
   int32_t consumer_device;
   int32_t n_segs;
-  int32_t pad_;
+  int32_t consumer_kind;  // 0 consumer, 1 queue keeper
   char ring_name[128];
   SegDesc segs[QueueFabric::kMaxSegments];
   std::atomic<uint64_t> ready;
@@ -81,16 +85,47 @@ struct alignas(64) LinkSeg {
   std::atomic<uint32_t> producer_detached;
   std::atomic<uint32_t> producer_ack_closed;           // no copy into this ring is in flight any more
   std::atomic<int64_t> producer_backlog;               // frames waiting at the producer (demand hint)
+  std::atomic<int64_t> producer_budget;                // its pool budget (keeper watermark)
+  std::atomic<int64_t> producer_other_credit;          // credit it holds from non-keeper consumers
+  alignas(64) std::atomic<uint64_t> taken;             // consumer: frames of this link it took (get)
+  std::atomic<uint32_t> returns_final;                 // consumer (closing): no return will follow
+  std::atomic<uint32_t> producer_seen_closed;          // producer: no frame notice will follow
+  alignas(64) std::atomic<uint64_t> r_head;            // consumer -> producer: returned frames
+  alignas(64) std::atomic<uint64_t> r_tail;
 };
 static_assert(std::atomic<uint64_t>::is_always_lock_free && std::atomic<int64_t>::is_always_lock_free,
               "lock-free 64-bit atomics are required in shared memory");
 
 size_t grants_off() { return round_up(sizeof(LinkSeg), 64); }
 size_t notices_off(int n) { return grants_off() + round_up((size_t)n * sizeof(int32_t), 64); }
-size_t seg_bytes(int n) { return round_up(notices_off(n) + (size_t)n * sizeof(Notice), 4096); }
+size_t returns_off(int n) { return notices_off(n) + round_up((size_t)n * sizeof(Notice), 64); }
+size_t seg_bytes(int n) { return round_up(returns_off(n) + (size_t)n * sizeof(Notice), 4096); }
 int32_t* seg_grants(LinkSeg* s) { return reinterpret_cast<int32_t*>(reinterpret_cast<uint8_t*>(s) + grants_off()); }
 Notice* seg_notices(LinkSeg* s) {
   return reinterpret_cast<Notice*>(reinterpret_cast<uint8_t*>(s) + notices_off(s->n_slots));
+}
+Notice* seg_returns(LinkSeg* s) {
+  return reinterpret_cast<Notice*>(reinterpret_cast<uint8_t*>(s) + returns_off(s->n_slots));
+}
+Notice make_notice(int32_t slot, int32_t flags, const SlotHeader& h) {
+  Notice nt;
+  nt.slot = slot;
+  nt.flags = flags;
+  nt.rank = h.rank;
+  nt.idx = h.idx;
+  nt.gevt = h.gevt;
+  nt.photon_energy = h.photon_energy;
+  nt.aux = h.aux;
+  return nt;
+}
+SlotHeader header_of(const Notice& nt) {
+  SlotHeader hd;
+  hd.rank = nt.rank;
+  hd.idx = nt.idx;
+  hd.gevt = nt.gevt;
+  hd.photon_energy = nt.photon_energy;
+  hd.aux = nt.aux;
+  return hd;
 }
 
 }  // namespace
@@ -175,6 +210,7 @@ struct QueueFabric::Link {
   size_t map_bytes = 0;
   int n = 0;
   bool attached = false, dead = false, closed = false, eos = false, detached = false, named = true;
+  bool keeper = false;                // the consumer end is a queue keeper
   double t_added = 0, last_check = 0;
   int64_t frames = 0;
   // producer side (outgoing)
@@ -187,10 +223,17 @@ struct QueueFabric::Link {
                                       // (different xGMI links) run concurrently
   int inflight = 0;
   bool eos_posted = false, acked_close = false;
+  uint64_t r_tail = 0;
+  int64_t noticed = 0;                // frames noticed on this link
+  uint64_t taken_seen = 0;            // the consumer's `taken` counter, last read
+  std::deque<Notice> returns;         // returned frames waiting for a free slot of this pool
+  int reclaiming = 0;                 // copies of returned frames in flight
   // consumer side (incoming)
-  uint64_t g_head = 0, n_tail = 0;
+  uint64_t g_head = 0, n_tail = 0, r_head = 0, taken = 0;
   std::vector<uint8_t> owed;  // slot -> granted to this producer and not answered
-  int64_t outstanding = 0;
+  std::vector<uint8_t> ret;   // slot -> returned to this producer and not answered
+  int64_t outstanding = 0, returned = 0;
+  double starved_since = -1;  // keeper: since when this producer's backlog had no other credit
 
   ~Link() {
     if (seg != nullptr) munmap(seg, map_bytes);
@@ -204,8 +247,10 @@ struct QueueFabric::Link {
     s.detached = detached;
     s.dead = dead;
     s.closed = closed;
+    s.keeper = keeper;
     s.outstanding = outgoing ? (int64_t)grants.size() : outstanding;
     s.frames = frames;
+    s.taken = outgoing ? (int64_t)taken_seen : (int64_t)taken;
     return s;
   }
 };
@@ -225,8 +270,9 @@ QueueFabric::QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is
       policy_(policy), self_mid_(self_mid) {
   check(pool != nullptr && slot_bytes > 0, "QueueFabric: empty ring");
   check((int)pool->slot_ptrs().size() == pool->n_slots(), "QueueFabric: the pool has no slot addresses");
-  check(policy >= 0 && policy <= 3, "QueueFabric: unknown routing policy");
+  check(policy >= 0 && policy <= 4, "QueueFabric: unknown routing policy");
   check(is_producer || is_consumer, "QueueFabric: a member must produce or consume");
+  if (is_consumer) pool_->set_track_origins(true);
   if (device_ >= 0) {
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate (fabric)");
@@ -354,7 +400,7 @@ void QueueFabric::drop_peer(int64_t mid) {
 }
 
 void QueueFabric::set_policy(int policy) {
-  check(policy >= 0 && policy <= 3, "QueueFabric: unknown routing policy");
+  check(policy >= 0 && policy <= 4, "QueueFabric: unknown routing policy");
   policy_.store(policy);
 }
 
@@ -434,6 +480,7 @@ void QueueFabric::apply_ops() {
       s->consumer_pid = (int64_t)getpid();
       s->kind = export_kind_;
       s->consumer_device = device_;
+      s->consumer_kind = keeper_ ? 1 : 0;
       snprintf(s->ring_name, sizeof(s->ring_name), "%s", export_name_.c_str());
       s->n_segs = (int32_t)segs_.size();
       for (size_t k = 0; k < segs_.size(); ++k) {
@@ -447,6 +494,8 @@ void QueueFabric::apply_ops() {
       l->map_bytes = bytes;
       l->n = n;
       l->owed.assign((size_t)pool_->n_slots(), 0);
+      l->ret.assign((size_t)pool_->n_slots(), 0);
+      l->keeper = keeper_;
     }
     links_.push_back(l);
     std::lock_guard<std::mutex> lk(mu_);
@@ -494,6 +543,16 @@ bool QueueFabric::try_attach(Link& l, double now) {
       check(device_ >= 0, "QueueFabric: a GPU consumer's ring can only be written by a GPU producer");
       check(s->n_segs >= 1 && s->n_segs <= kMaxSegments, "QueueFabric: bad segment table in " + l.name);
       hip_check(hipSetDevice(device_), "hipSetDevice");
+      int ndev = 0;
+      hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+      const int cdev = s->consumer_device;
+      if (cdev >= 0 && cdev < ndev && cdev != device_) {
+        // the copy engine / blit kernels of THIS GPU write the consumer GPU's HBM over xGMI
+        int can = 0;
+        hip_check(hipDeviceCanAccessPeer(&can, device_, cdev), "hipDeviceCanAccessPeer");
+        check(can != 0, "GPU " + std::to_string(device_) + " has no peer access to GPU " + std::to_string(cdev) +
+                            " (hipDeviceCanAccessPeer = 0)");
+      }
       for (int k = 0; k < s->n_segs; ++k) {
         const SegDesc& d = s->segs[k];
         check(d.first >= 0 && d.n >= 1 && d.first + d.n <= l.n, "QueueFabric: bad segment in " + l.name);
@@ -522,6 +581,9 @@ bool QueueFabric::try_attach(Link& l, double now) {
   }
   l.g_tail = s->g_tail.load(std::memory_order_acquire);
   l.n_head = s->n_head.load(std::memory_order_acquire);
+  l.r_tail = s->r_tail.load(std::memory_order_acquire);
+  l.keeper = s->consumer_kind == 1;
+  s->producer_budget.store(pool_->producer_budget(), std::memory_order_relaxed);
   s->producer_pid.store((int64_t)getpid(), std::memory_order_release);
   l.attached = true;
   return true;
@@ -540,12 +602,61 @@ void QueueFabric::release_out_link(Link& l) {
   l.remote.clear();
 }
 
+// Hand a read-ahead frame (consumer slot, LEASED) back: to `pref` when it can take it, else to any
+// live producer that has not posted EOS.  False: nobody can (the caller drops it).
+bool QueueFabric::post_return(Link* pref, int slot, const SlotHeader& h) {
+  auto ok = [](const Link* l) {
+    return l != nullptr && !l->outgoing && l->seg != nullptr && l->attached && !l->dead && !l->detached && !l->eos;
+  };
+  Link* to = ok(pref) ? pref : nullptr;
+  if (to == nullptr)
+    for (auto& lp : links_)
+      if (ok(lp.get())) {
+        to = lp.get();
+        break;
+      }
+  if (to == nullptr) return false;
+  LinkSeg* s = to->seg;
+  seg_returns(s)[to->r_head % (uint64_t)to->n] = make_notice(slot, 0, h);
+  ++to->r_head;
+  s->r_head.store(to->r_head, std::memory_order_release);
+  to->ret[slot] = 1;
+  ++to->returned;
+  ++returns_pending_;
+  std::lock_guard<std::mutex> lk(mu_);
+  ++st_.frames_returned;
+  return true;
+}
+
+void QueueFabric::drop_returned(int slot) {
+  pool_->release(slot, 0);
+  std::lock_guard<std::mutex> lk(mu_);
+  ++st_.frames_dropped;
+}
+
 // ---------------------------------------------------------------------------------------
 int64_t QueueFabric::consumer_pass(double now) {
   int64_t work = 0;
   const bool closing = consumer_closed_.load();
+  // 0. frames the reader took since the last pass: tell each producer (its budget counts them
+  //    until then -- queue_size is one logical bound)
+  for (int64_t o : pool_->take_got_origins()) {
+    if (o < 0) continue;
+    for (auto& lp : links_)
+      if (!lp->outgoing && lp->peer == o) {
+        ++lp->taken;
+        break;
+      }
+  }
+  for (auto& lp : links_)
+    if (!lp->outgoing && lp->seg != nullptr) lp->seg->taken.store(lp->taken, std::memory_order_release);
+  // 1. notices: frames (-> READY), unused grants, answers to returned frames.  n_tail is stored only
+  //    after the returns of this pass were posted (a closing consumer hands back every frame noticed
+  //    before a producer sees n_tail catch up and acknowledges the close)
   std::vector<int> done_slots, ret_slots;
   std::vector<SlotHeader> done_hdr;
+  std::vector<std::pair<Link*, uint64_t>> tails;
+  std::vector<std::pair<Link*, Notice>> rejected;
   for (auto& lp : links_) {
     Link& l = *lp;
     if (l.outgoing || l.seg == nullptr) continue;
@@ -557,7 +668,6 @@ int64_t QueueFabric::consumer_pass(double now) {
         l.named = false;
       }
     }
-    if (closing) s->consumer_closed.store(1, std::memory_order_release);
     // EOS / detach flags BEFORE the notice head: a producer releases them after its last notice
     const bool eos_flag = s->producer_eos.load(std::memory_order_acquire) != 0;
     const bool det_flag = s->producer_detached.load(std::memory_order_acquire) != 0;
@@ -567,30 +677,40 @@ int64_t QueueFabric::consumer_pass(double now) {
       done_slots.clear();
       ret_slots.clear();
       done_hdr.clear();
+      int64_t reclaimed = 0;
       for (; l.n_tail < h; ++l.n_tail) {
         const Notice nt = ns[l.n_tail % (uint64_t)l.n];
-        check(nt.slot >= 0 && nt.slot < (int)l.owed.size() && l.owed[nt.slot],
-              "QueueFabric: producer " + std::to_string(l.peer) + " answered a slot it was never granted");
+        check(nt.slot >= 0 && nt.slot < (int)l.owed.size(),
+              "QueueFabric: producer " + std::to_string(l.peer) + " answered a slot outside the ring");
+        if (nt.flags & (kNoticeReclaimed | kNoticeRejected)) {
+          check(l.ret[nt.slot], "QueueFabric: producer " + std::to_string(l.peer) +
+                                    " answered a frame that was not returned to it");
+          l.ret[nt.slot] = 0;
+          --l.returned;
+          --returns_pending_;
+          if (nt.flags & kNoticeReclaimed) {
+            pool_->release(nt.slot, 0);   // copied out by the producer: the slot is free again
+            ++reclaimed;
+          } else {
+            rejected.emplace_back(&l, nt);
+          }
+          continue;
+        }
+        check(l.owed[nt.slot], "QueueFabric: producer " + std::to_string(l.peer) + " answered a slot it was never granted");
         l.owed[nt.slot] = 0;
         --l.outstanding;
         if (nt.flags & kNoticeReturned) {
           ret_slots.push_back(nt.slot);
         } else {
-          SlotHeader hd;
-          hd.rank = nt.rank;
-          hd.idx = nt.idx;
-          hd.gevt = nt.gevt;
-          hd.photon_energy = nt.photon_energy;
-          hd.aux = nt.aux;
           done_slots.push_back(nt.slot);
-          done_hdr.push_back(hd);
+          done_hdr.push_back(header_of(nt));
         }
       }
-      s->n_tail.store(l.n_tail, std::memory_order_release);
-      pool_->complete_recv_batch(done_slots, done_hdr);
+      tails.emplace_back(&l, l.n_tail);
+      pool_->complete_recv_batch_from(done_slots, done_hdr, l.peer);
       pool_->cancel_recv_batch(ret_slots);
       l.frames += (int64_t)done_slots.size();
-      work += (int64_t)(done_slots.size() + ret_slots.size());
+      work += (int64_t)(done_slots.size() + ret_slots.size()) + reclaimed;
       std::lock_guard<std::mutex> lk(mu_);
       st_.frames_recv += (int64_t)done_slots.size();
       st_.bytes_recv += (int64_t)done_slots.size() * slot_bytes_;
@@ -621,20 +741,104 @@ int64_t QueueFabric::consumer_pass(double now) {
       st_.grants_reclaimed += (int64_t)back.size();
       work += (int64_t)back.size();
     }
+    if ((l.dead || l.detached) && l.returned > 0) {
+      // returned frames it never answered: try the other producers
+      for (size_t i = 0; i < l.ret.size(); ++i)
+        if (l.ret[i]) {
+          l.ret[i] = 0;
+          --l.returned;
+          --returns_pending_;
+          const SlotHeader hd = pool_->header((int)i);
+          if (!post_return(nullptr, (int)i, hd)) drop_returned((int)i);
+          ++work;
+        }
+    }
     if ((l.dead || l.detached) && l.named) {
       shm_remove(l.name);
       l.named = false;
     }
   }
-  // grants: free slots of this shard to the live producers that may still send
+  for (auto& r : rejected) {   // that producer posted EOS meanwhile: another one, or drop
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++st_.returns_rejected;
+    }
+    r.first->eos = true;   // it will not accept more (its EOS flag follows)
+    if (!post_return(nullptr, r.second.slot, header_of(r.second))) drop_returned(r.second.slot);
+    ++work;
+  }
+  // 2. closing: hand every frame that arrived and was not taken back to a producer.  Once every live
+  //    producer confirmed it will notice no more frames (producer_seen_closed), nothing is ready
+  //    and every return was answered, `returns_final` tells the producers no return will follow:
+  //    only then may they acknowledge the close (a return can never reach a link whose producer
+  //    already let go of it)
+  if (closing) {
+    const std::vector<int> back = pool_->pop_ready_for_return(1 << 30);
+    for (int slot : back) {
+      const int64_t o = pool_->origin(slot);
+      Link* pref = nullptr;
+      for (auto& lp : links_)
+        if (!lp->outgoing && lp->peer == o) pref = lp.get();
+      if (!post_return(pref, slot, pool_->header(slot))) drop_returned(slot);
+      ++work;
+    }
+  }
+  for (auto& t : tails) t.first->seg->n_tail.store(t.second, std::memory_order_release);
+  if (closing && !closed_posted_) {
+    for (auto& lp : links_)
+      if (!lp->outgoing && lp->seg != nullptr) lp->seg->consumer_closed.store(1, std::memory_order_release);
+    closed_posted_ = true;
+  }
+  if (closing && closed_posted_ && !returns_final_ && returns_pending_ == 0 && pool_->n_ready() == 0) {
+    bool all_seen = true;
+    for (auto& lp : links_) {
+      const Link& l = *lp;
+      if (l.outgoing || l.seg == nullptr || !l.attached || l.dead || l.detached) continue;
+      if (l.seg->producer_seen_closed.load(std::memory_order_acquire) == 0 ||
+          l.seg->n_head.load(std::memory_order_acquire) != l.n_tail)
+        all_seen = false;
+    }
+    if (all_seen) {
+      for (auto& lp : links_)
+        if (!lp->outgoing && lp->seg != nullptr) lp->seg->returns_final.store(1, std::memory_order_release);
+      returns_final_ = true;
+      ++work;
+    }
+  }
+  // 3. grants: free slots of this shard to the live producers that may still send, bounded by the
+  //    read-ahead allowance (prefetch - noticed-but-untaken - outstanding)
   if (!closing) {
     std::vector<Link*> act;
-    for (auto& lp : links_)
-      if (!lp->outgoing && lp->attached && !lp->eos && !lp->dead && !lp->detached &&
-          (!grant_filter_.load() || std::find(grantable_.begin(), grantable_.end(), lp->peer) != grantable_.end()))
-        act.push_back(lp.get());
+    for (auto& lp : links_) {
+      Link* l = lp.get();
+      if (l->outgoing || !l->attached || l->eos || l->dead || l->detached) continue;
+      if (grant_filter_.load()) {
+        // queue keeper: producers that finished (draining), or live ones whose backlog nobody
+        // else can take (no other credit)
+        // (debounced: a consumer between two grant rounds holds no credit for a moment)
+        const bool listed = std::find(grantable_.begin(), grantable_.end(), l->peer) != grantable_.end();
+        const int64_t backlog = l->seg->producer_backlog.load(std::memory_order_relaxed);
+        const int64_t other = l->seg->producer_other_credit.load(std::memory_order_relaxed);
+        if (backlog > 0 && other <= 0) {
+          if (l->starved_since < 0) l->starved_since = now;
+        } else {
+          l->starved_since = -1;
+        }
+        const bool starved = l->starved_since >= 0 && now - l->starved_since >= kKeeperDebounceS;
+        if (!listed && !(backlog > 0 && starved)) continue;
+      }
+      act.push_back(l);
+    }
     if (!act.empty()) {
       const int cb = pool_->consumer_budget();
+      int64_t allowance = cb;
+      const int pf = prefetch_.load();
+      if (pf > 0) {
+        int64_t held = pool_->n_ready();
+        for (auto& lp : links_)
+          if (!lp->outgoing) held += lp->outstanding;
+        allowance = std::max<int64_t>(0, (int64_t)pf - held);
+      }
       const int floor_g = std::max(kMinGrants, std::min(64, cb / (2 * (int)act.size())));
       std::vector<int64_t> want(act.size());
       int64_t total = 0;
@@ -643,6 +847,7 @@ int64_t QueueFabric::consumer_pass(double now) {
         want[i] = std::max<int64_t>(0, std::min<int64_t>(cb, floor_g + backlog) - act[i]->outstanding);
         total += want[i];
       }
+      total = std::min(total, allowance);
       if (total > 0) {
         const std::vector<int> slots = pool_->grant_batch((int)std::min<int64_t>(total, cb));
         size_t k = 0;
@@ -676,9 +881,10 @@ int64_t QueueFabric::consumer_pass(double now) {
       }
     }
   }
-  // quiesced: no producer can still write into the ring (close() waits for this before freeing)
+  // quiesced: no producer can still write into the ring and every returned frame was answered
+  // (close() waits for this before freeing the ring)
   if (closing) {
-    bool q = true;
+    bool q = returns_pending_ == 0 && returns_final_;
     for (auto& lp : links_) {
       const Link& l = *lp;
       if (l.outgoing || l.seg == nullptr || !l.attached || l.dead || l.detached) continue;
@@ -692,7 +898,11 @@ int64_t QueueFabric::consumer_pass(double now) {
 int64_t QueueFabric::producer_pass(double now) {
   int64_t work = 0;
   const int policy = policy_.load();
-  // 1. attach / liveness / incoming grants
+  auto post_notice = [&](Link& l, const Notice& nt) {
+    seg_notices(l.seg)[l.n_head % (uint64_t)l.n] = nt;
+    ++l.n_head;
+  };
+  // 1. attach / liveness / incoming grants, taken counters and returned frames
   for (auto& lp : links_) {
     Link& l = *lp;
     if (!l.outgoing || l.dead) continue;
@@ -709,8 +919,35 @@ int64_t QueueFabric::producer_pass(double now) {
         ++st_.peers_dead;
       }
     }
-    if (!l.closed && s->consumer_closed.load(std::memory_order_acquire) != 0) l.closed = true;
-    if (l.dead || l.closed) {
+    if (l.dead) {
+      l.grants.clear();
+      l.returns.clear();
+      continue;
+    }
+    // returns first: a closing consumer posts them before consumer_closed
+    const uint64_t rh = s->r_head.load(std::memory_order_acquire);
+    if (l.r_tail < rh) {
+      const Notice* rs = seg_returns(s);
+      for (; l.r_tail < rh; ++l.r_tail) {
+        const Notice nt = rs[l.r_tail % (uint64_t)l.n];
+        check(nt.slot >= 0 && nt.slot < l.n, "QueueFabric: consumer " + std::to_string(l.peer) +
+                                                 " returned a slot outside its ring");
+        l.returns.push_back(nt);
+      }
+      s->r_tail.store(l.r_tail, std::memory_order_release);
+      ++work;
+    }
+    const uint64_t tk = s->taken.load(std::memory_order_acquire);
+    if (tk != l.taken_seen) {
+      l.taken_seen = tk;
+      ++work;
+    }
+    if (!l.closed && s->consumer_closed.load(std::memory_order_acquire) != 0) {
+      // from now on copies completing towards this link are requeued, never noticed
+      l.closed = true;
+      s->producer_seen_closed.store(1, std::memory_order_release);
+    }
+    if (l.closed) {
       l.grants.clear();
       continue;
     }
@@ -726,8 +963,89 @@ int64_t QueueFabric::producer_pass(double now) {
       s->g_tail.store(l.g_tail, std::memory_order_release);
       ++work;
     }
+    if (l.eos_posted && !l.grants.empty()) {
+      // grants that raced with our EOS: hand them straight back (the consumer must not keep
+      // credit owed by a producer that will never send)
+      for (int slot : l.grants) post_notice(l, make_notice(slot, kNoticeReturned, SlotHeader{}));
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        st_.grants_returned += (int64_t)l.grants.size();
+      }
+      l.grants.clear();
+      s->n_head.store(l.n_head, std::memory_order_release);
+    }
   }
-  // 2. completed copies: notice the frames, or requeue them if their consumer left meanwhile.
+  // 2. returned frames: copy them back into this pool (front of the FIFO), or refuse them after EOS
+  for (auto& lp : links_) {
+    Link& l = *lp;
+    if (!l.outgoing || l.dead || l.returns.empty()) continue;
+    if (eos_any_) {
+      for (const Notice& nt : l.returns) post_notice(l, make_notice(nt.slot, kNoticeRejected, header_of(nt)));
+      l.returns.clear();
+      l.seg->n_head.store(l.n_head, std::memory_order_release);
+      ++work;
+      continue;
+    }
+    const int want = (int)std::min<size_t>(l.returns.size(), 64);
+    hipStream_t st = device_ >= 0 ? (l.stream != nullptr ? l.stream : stream_) : nullptr;
+    const std::vector<int> mine = pool_->reclaim_batch(want, reinterpret_cast<uint64_t>(st));
+    if (mine.empty()) continue;   // no free slot right now: retry next pass
+    Batch b;
+    b.link = lp;
+    b.slots = mine;
+    b.stream = st;
+    b.t_issue = now;
+    for (size_t i = 0; i < mine.size(); ++i) {
+      const Notice nt = l.returns.front();
+      l.returns.pop_front();
+      b.rslots.push_back(nt.slot);
+      b.hdrs.push_back(header_of(nt));
+      if (device_ >= 0)
+        hip_check(hipMemcpyAsync(reinterpret_cast<void*>(pool_->slot_ptr(mine[i])),
+                                 reinterpret_cast<const void*>(l.remote[nt.slot]), (size_t)slot_bytes_,
+                                 hipMemcpyDeviceToDevice, st),
+                  "hipMemcpyAsync (returned frame -> producer pool)");
+      else
+        memcpy(reinterpret_cast<void*>(pool_->slot_ptr(mine[i])), reinterpret_cast<const void*>(l.remote[nt.slot]),
+               (size_t)slot_bytes_);
+    }
+    if (device_ >= 0) {
+      b.ev = take_event();
+      hip_check(hipEventRecord(b.ev, st), "hipEventRecord (reclaim copy)");
+    }
+    l.reclaiming += (int)mine.size();
+    reclaims_.push_back(std::move(b));
+    work += (int64_t)mine.size();
+  }
+  for (auto it = reclaims_.begin(); it != reclaims_.end();) {
+    Batch& b = *it;
+    if (b.ev != nullptr) {
+      const hipError_t q = hipEventQuery(b.ev);
+      if (q == hipErrorNotReady) {
+        ++it;
+        continue;
+      }
+      hip_check(q, "hipEventQuery (reclaim copy)");
+    }
+    Link& l = *b.link;
+    const int n = (int)b.slots.size();
+    // the frames are ours again (even if that consumer died meanwhile: the copy completed)
+    pool_->commit_front_batch(b.slots, b.hdrs, reinterpret_cast<uint64_t>(b.stream));
+    l.reclaiming -= n;
+    l.noticed = std::max<int64_t>((int64_t)l.taken_seen, l.noticed - n);
+    if (!l.dead) {
+      for (int i = 0; i < n; ++i) post_notice(l, make_notice(b.rslots[i], kNoticeReclaimed, b.hdrs[i]));
+      l.seg->n_head.store(l.n_head, std::memory_order_release);
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.frames_reclaimed += n;
+    }
+    if (b.ev != nullptr) free_events_.push_back(b.ev);
+    it = reclaims_.erase(it);
+    work += n;
+  }
+  // 3. completed copies: notice the frames, or requeue them if their consumer left meanwhile.
   //    Batches of one link complete in order (one stream per link); links are independent.
   std::vector<const Link*> blocked;
   for (auto it = inflight_.begin(); it != inflight_.end();) {
@@ -749,21 +1067,11 @@ int64_t QueueFabric::producer_pass(double now) {
     const int n = (int)b.slots.size();
     l.inflight -= n;
     if (l.attached && !l.dead && !l.closed) {
-      Notice* ns = seg_notices(l.seg);
-      for (int i = 0; i < n; ++i) {
-        Notice& nt = ns[l.n_head % (uint64_t)l.n];
-        nt.slot = b.rslots[i];
-        nt.flags = 0;
-        nt.rank = b.hdrs[i].rank;
-        nt.idx = b.hdrs[i].idx;
-        nt.gevt = b.hdrs[i].gevt;
-        nt.photon_energy = b.hdrs[i].photon_energy;
-        nt.aux = b.hdrs[i].aux;
-        ++l.n_head;
-      }
+      for (int i = 0; i < n; ++i) post_notice(l, make_notice(b.rslots[i], 0, b.hdrs[i]));
       l.seg->n_head.store(l.n_head, std::memory_order_release);
       pool_->end_send_batch(b.slots, reinterpret_cast<uint64_t>(b.stream != nullptr ? b.stream : stream_));
       l.frames += n;
+      l.noticed += n;
       std::lock_guard<std::mutex> lk(mu_);
       st_.frames_sent += n;
       st_.bytes_sent += (int64_t)n * slot_bytes_;
@@ -777,15 +1085,22 @@ int64_t QueueFabric::producer_pass(double now) {
     it = inflight_.erase(it);
     work += n;
   }
-  // 3. route produced frames (FIFO) to this process's own consumer or to granted remote slots
+  // 4. route produced frames (FIFO) to this process's own consumer or to granted remote slots.
+  //    Keeper links are the last resort: a frame goes there only when no real consumer (and not
+  //    this process's own) has credit for it.
   const std::vector<int> offers = pool_->produced(kMaxDispatch);
+  int64_t local_credit = (is_consumer_ && !consumer_closed_.load() && policy != 3) ? pool_->credits() : 0;
+  std::vector<Link*> cands;
+  for (auto& lp : links_)
+    if (lp->outgoing && lp->attached && !lp->dead && !lp->closed && !lp->eos_posted) cands.push_back(lp.get());
+  if (policy == 4) {
+    // remote_only: frames cross to another process whenever a remote consumer is linked
+    for (const Link* c : cands)
+      if (!c->keeper) local_credit = 0;
+  }
   if (!offers.empty()) {
-    std::vector<Link*> cands;
-    for (auto& lp : links_)
-      if (lp->outgoing && lp->attached && !lp->dead && !lp->closed && !lp->eos_posted) cands.push_back(lp.get());
     std::vector<int64_t> avail(cands.size());
     for (size_t i = 0; i < cands.size(); ++i) avail[i] = (int64_t)cands[i]->grants.size();
-    int64_t local_credit = (is_consumer_ && !consumer_closed_.load() && policy != 3) ? pool_->credits() : 0;
     if (policy == 2 && local_credit > 0) {
       // spread: the own producer must not take the consumer credit that the remote producers'
       // grants need.  A local route needs only credit, a grant needs a FREE slot whose release
@@ -812,7 +1127,7 @@ int64_t QueueFabric::producer_pass(double now) {
           const int p = (rr_ + t) % K;
           if (p == K - 1) {
             if (local_credit > 0) pick = -1;
-          } else if (avail[p] > 0) {
+          } else if (avail[p] > 0 && !cands[p]->keeper) {
             pick = p;
           }
           if (pick != -2) rr_ = (p + 1) % K;
@@ -820,11 +1135,17 @@ int64_t QueueFabric::producer_pass(double now) {
       } else {
         int best = -1;
         for (size_t i = 0; i < cands.size(); ++i)
-          if (avail[i] > 0 && (best < 0 || avail[i] > avail[best])) best = (int)i;
+          if (avail[i] > 0 && !cands[i]->keeper && (best < 0 || avail[i] > avail[best])) best = (int)i;
         const int64_t best_n = best >= 0 ? avail[best] : 0;
         if (local_credit > 0 && (policy == 1 || local_credit + kLocalSlack >= best_n)) pick = -1;
         else if (best >= 0) pick = best;
       }
+      if (pick == -2)   // nobody else: a keeper with credit
+        for (size_t i = 0; i < cands.size(); ++i)
+          if (avail[i] > 0 && cands[i]->keeper) {
+            pick = (int)i;
+            break;
+          }
       if (pick == -2) break;
       if (pick == -1) {
         local.push_back(s);
@@ -887,16 +1208,41 @@ int64_t QueueFabric::producer_pass(double now) {
       work += n;
     }
   }
-  // 4. demand hint, close acknowledgements, end of stream, retirement of finished links
+  // 5. read-ahead accounting (frames noticed and not taken still count against this producer's
+  //    budget), demand hints, close acknowledgements, end of stream
+  int64_t readahead = 0, other_credit = local_credit;
+  bool returns_open = !reclaims_.empty();
+  for (auto& lp : links_) {
+    const Link& l = *lp;
+    if (!l.outgoing || !l.attached || l.dead) continue;
+    if (!l.acked_close) readahead += std::max<int64_t>(0, l.noticed - (int64_t)l.taken_seen);
+    if (!l.closed && !l.keeper && !l.eos_posted) other_credit += (int64_t)l.grants.size();
+    returns_open |= !l.returns.empty() || l.reclaiming > 0;
+  }
+  pool_->set_external_held((int)std::min<int64_t>(readahead, 1 << 30));
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    st_.readahead = readahead;
+  }
   const int64_t backlog = pool_->n_produced();
-  const bool all_routed = finished_.load() && backlog == 0 && inflight_.empty();
+  const bool all_routed = finished_.load() && backlog == 0 && inflight_.empty() && !returns_open;
   bool drained = all_routed;
   for (auto& lp : links_) {
     Link& l = *lp;
     if (!l.outgoing || !l.attached) continue;
     LinkSeg* s = l.seg;
-    if (!l.dead && !l.closed) s->producer_backlog.store(backlog, std::memory_order_relaxed);
-    if ((l.dead || l.closed) && l.inflight == 0 && !l.acked_close) {
+    if (!l.dead && !l.closed) {
+      s->producer_backlog.store(backlog, std::memory_order_relaxed);
+      s->producer_other_credit.store(other_credit, std::memory_order_relaxed);
+    }
+    // a closed link is acknowledged once nothing is in flight towards it, every returned frame was
+    // answered and the consumer read every notice (so it has handed back every frame it received)
+    const bool settled =
+        l.inflight == 0 && l.returns.empty() && l.reclaiming == 0 &&
+        (l.dead || (s->returns_final.load(std::memory_order_acquire) != 0 &&
+                    s->r_head.load(std::memory_order_acquire) == l.r_tail &&
+                    s->n_tail.load(std::memory_order_acquire) == l.n_head));
+    if ((l.dead || l.closed) && settled && !l.acked_close) {
       s->producer_ack_closed.store(1, std::memory_order_release);
       l.acked_close = true;
       release_out_link(l);
@@ -908,14 +1254,7 @@ int64_t QueueFabric::producer_pass(double now) {
     }
     if (all_routed && !l.dead && !l.closed && !l.eos_posted) {
       // give unused grants back, then EOS (released after the last notice)
-      Notice* ns = seg_notices(s);
-      for (int slot : l.grants) {
-        Notice& nt = ns[l.n_head % (uint64_t)l.n];
-        memset(&nt, 0, sizeof(nt));
-        nt.slot = slot;
-        nt.flags = kNoticeReturned;
-        ++l.n_head;
-      }
+      for (int slot : l.grants) post_notice(l, make_notice(slot, kNoticeReturned, SlotHeader{}));
       {
         std::lock_guard<std::mutex> lk(mu_);
         st_.grants_returned += (int64_t)l.grants.size();
@@ -925,6 +1264,7 @@ int64_t QueueFabric::producer_pass(double now) {
       s->producer_eos.store(1, std::memory_order_release);
       l.eos_posted = true;
       l.eos = true;
+      eos_any_ = true;
       ++work;
     }
   }

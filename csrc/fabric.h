@@ -29,11 +29,44 @@
 //   * producers run with no consumer at all (frames wait in their pool, backpressure when full);
 //   * consumers attach at any time and any number of them (a new link per live producer);
 //   * a consumer that dies or closes: its producers stop using its grants, and frames whose copy
-//     was still in flight go back to the FRONT of the producer's FIFO for another consumer; only
-//     frames already noticed to the dead consumer's shard are lost;
+//     was still in flight go back to the FRONT of the producer's FIFO for another consumer;
+//   * a consumer that CLOSES hands the frames it received but never read back: it posts them on a
+//     return ring, a live producer copies them out of the consumer's ring into its own pool and
+//     queues them at the front of its FIFO for the other consumers (the reference's items stay
+//     in the actor until somebody get()s them, psana_ray/shared_queue.py:19-24);
+//   * a consumer that DIES loses only its read-ahead: grants are bounded so that (noticed but
+//     unread + outstanding grants) <= `prefetch` (set_prefetch), i.e. item-granular like the
+//     reference's one-item get(), not a whole shard;
 //   * a producer that dies: its consumers take back the slots granted to it;
 //   * a producer that finishes returns unused grants and posts EOS on every link.
 // Liveness is the peer's pid (same host; zombies count as dead), checked every 50 ms.
+//
+// queue_size is ONE logical bound (the reference's deque(maxlen), shared_queue.py:7,11): a frame
+// counts against its producer's budget from production until a consumer TAKES it (get), including
+// while it sits in a consumer's read-ahead -- every consumer reports per link how many frames it
+// took (`taken`), the producer feeds (noticed - taken) into SlotPool::set_external_held.  So a
+// joining consumer adds landing space, never queue capacity.
+//
+// Queue keeper (keeper.py) links are marked in their mailbox: producers route to them only when no
+// other consumer has credit, and the keeper grants to a LIVE producer only while nobody else can
+// take its backlog (for 0.1 s in a row) -- so committed frames move into the
+// keeper (and survive a producer crash, like puts into the detached actor) without competing with
+// real consumers.
+//
+// Visibility of peer-written slots (SURVEY H-10; /opt/skills/guides/MI355X_MICROARCH.md:150-236):
+// the frame bytes are written by the PRODUCER's copy (hipMemcpyAsync D2D: a blit kernel or an SDMA
+// transfer writing the consumer's HBM through the IPC mapping, over xGMI when the GPUs differ).
+// The consumer is told only by a notice posted after hipEventQuery reported that copy complete,
+// i.e. after the copy's end-of-operation release (agent scope: buffer_wbl2 -- dirty lines,
+// including lines of peer memory, leave the producer GPU's L2).  The consumer reads a leased slot
+// ONLY from kernels it launches after the host took the notice (get / get_batch return first);
+// every kernel dispatch begins with the packet's acquire, which invalidates the consumer GPU's
+// L1/L2 lines that may still hold the slot's previous frame -- the same kernel-boundary rule that
+// makes one kernel's output visible to the next kernel on another XCD of the same GPU.  No
+// persistent kernel polls ring slots, and nothing reads a slot between grant and notice.  This is
+// what the bit-exact multi-process tests rely on (test_elastic_gpu.py: producer and consumer
+// processes on one GPU, slots reused many times); a consumer that ever polled slots from a
+// resident kernel would need an explicit agent acquire (Guideline 16) after its poll.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -85,6 +118,11 @@ struct FabricStats {
   int64_t bytes_sent = 0, bytes_recv = 0, batches = 0;
   int64_t links_opened = 0, peers_dead = 0;
   int64_t links_failed = 0;      // consumer ring could not be mapped (link unusable, others unaffected)
+  int64_t frames_returned = 0;   // consumer: read-ahead frames handed back to a producer on close
+  int64_t frames_reclaimed = 0;  // producer: frames taken back from closing consumers (requeued)
+  int64_t frames_dropped = 0;    // consumer: read-ahead frames no live producer could take back
+  int64_t returns_rejected = 0;  // consumer: returns refused (that producer had posted EOS) and re-routed
+  int64_t readahead = 0;         // producer: frames in consumers' read-ahead not taken yet (gauge)
   double copy_s = 0;             // sum over batches of issue -> completion observed
 };
 
@@ -96,15 +134,19 @@ struct LinkStatus {
   bool detached = false;     // producer left after EOS
   bool dead = false;         // the peer process exited
   bool closed = false;       // the consumer closed the link
+  bool keeper = false;       // the consumer end is a queue keeper
   int64_t outstanding = 0;   // grants not answered yet
   int64_t frames = 0;        // frames moved over the link
+  int64_t taken = 0;         // frames of this link the consumer took (get)
 };
 
 class QueueFabric {
  public:
   // policy: 0 balanced (local unless a remote consumer has kLocalSlack more free slots granted),
   //         1 local_first, 2 spread (round-robin over every consumer with credit),
-  //         3 relay (queue keeper: never to its own consumer side; most granted credit first).
+  //         3 relay (queue keeper: never to its own consumer side; most granted credit first),
+  //         4 remote_only (never to its own consumer while a remote consumer link is attached:
+  //           the bench's cross-GPU window, every frame crosses xGMI).
   // slot addresses come from the pool (SlotPool::set_slot_ptrs): rings are built from segments
   QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is_producer, bool is_consumer, int policy,
               int64_t self_mid);
@@ -130,6 +172,13 @@ class QueueFabric {
   void set_peer_grantable(int64_t mid, bool on);
   void set_producer_finished() { finished_.store(true); }
   void set_consumer_closed() { consumer_closed_.store(true); }
+  // consumer role: bound on (frames noticed but not taken + grants outstanding), summed over links;
+  // 0 = unbounded (only the ring's free slots limit grants).  A consumer that dies loses at most
+  // this many frames plus the ones it had taken and not finished.
+  void set_prefetch(int n) { prefetch_.store(n < 0 ? 0 : n); }
+  int prefetch() const { return prefetch_.load(); }
+  // consumer role: mark every mailbox this process creates as a queue keeper's (before links exist)
+  void set_keeper(bool on) { keeper_ = on; }
   // consumer: true once no live producer can still be writing into this ring (every attached
   // producer acknowledged the close, detached or died) -- only then may the ring be freed
   bool consumer_quiesced() const { return quiesced_.load(); }
@@ -162,6 +211,8 @@ class QueueFabric {
   bool try_attach(Link& l, double now);
   void release_out_link(Link& l);
   void finish_in_link(Link& l);
+  bool post_return(Link* pref, int slot, const SlotHeader& h);
+  void drop_returned(int slot);
   void publish_status();
   hipEvent_t take_event();
 
@@ -185,7 +236,12 @@ class QueueFabric {
   std::vector<hipEvent_t> free_events_, all_events_;
   std::vector<std::shared_ptr<Link>> links_;
   std::deque<Batch> inflight_;
+  std::deque<Batch> reclaims_;   // producer: copies of returned frames back into this pool
   int rr_ = 0;
+  int64_t returns_pending_ = 0;  // consumer: returned frames not answered yet
+  bool eos_any_ = false;         // producer: EOS posted (returns are refused from then on)
+  bool keeper_ = false;
+  std::atomic<int> prefetch_{0};
 
   struct Op {
     int kind;  // 0 in, 1 out, 2 drop, 3 grantable on, 4 grantable off
@@ -197,6 +253,8 @@ class QueueFabric {
   std::vector<int64_t> grantable_;   // engine thread: peers a filtered consumer grants to
 
   std::atomic<bool> finished_{false}, consumer_closed_{false}, stop_{false}, running_{false}, drained_{false};
+  bool closed_posted_ = false;   // consumer: consumer_closed stored in every mailbox
+  bool returns_final_ = false;   // consumer: returns_final stored in every mailbox
   std::atomic<bool> quiesced_{false};
   std::atomic<bool> grant_filter_{false};
   std::vector<LinkStatus> retired_;

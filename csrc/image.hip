@@ -131,7 +131,7 @@ __global__ __launch_bounds__(BLOCK) void image_tile_kernel(const FramePtrs fp, c
         const uint32_t r = cur[j];
         bool valid;
         const int c = decode_cand(r, KIND, valid);
-        v = valid ? (decode_adu(r, KIND) - img_pick<NT>(p[j], c)) * img_pick<NT>(q[j], c) : 0.0f;
+        v = valid ? gmul(decode_adu(r, KIND) - img_pick<NT>(p[j], c), img_pick<NT>(q[j], c)) : 0.0f;
       } else {
         v = cur[j];
       }
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(BLOCK) void image_tile_kernel(const FramePtrs fp, c
             pp[m] = ped[m * g.npix + s];
             qq[m] = gf[m * g.npix + s];
           }
-          v = valid ? (decode_adu(r, KIND) - img_pick<NT>(pp, c)) * img_pick<NT>(qq, c) : 0.0f;
+          v = valid ? gmul(decode_adu(r, KIND) - img_pick<NT>(pp, c), img_pick<NT>(qq, c)) : 0.0f;
         } else {
           v = gin<float>(fp.in[f])[s];
         }

@@ -21,6 +21,9 @@
 // the losing variants are retired).
 #include "common.h"
 
+#include <map>
+#include <mutex>
+
 #include <algorithm>
 
 namespace pr {
@@ -118,6 +121,9 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
 // a persistent scratch block instead of in `counts` / `summary`; the LAST workgroup to finish
 // (device-scope done counter) moves them to the outputs and zeroes the scratch for the next
 // launch on the stream -- so a consumer needs no per-batch fill kernel before the peak finder.
+// ONE scratch block per stream: two launches in flight on different streams sharing a block would
+// mix their counters and race on the done ticket (PeakFinderConsumer owns one per consumer stream;
+// kernels.peakfind documents the rule).
 struct PfScratch {
   int tickets[kMaxFrames];
   float acc[2 * kMaxFrames];
@@ -264,14 +270,20 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
   if (threadIdx.x == 0) atomicExch(&scratch->done, 0u);
 }
 
-// resident workgroups of a 256-thread kernel on the whole device (queried once per kernel)
+// resident workgroups of a 256-thread kernel on the CURRENT device, queried once per (device,
+// kernel) under a lock: a process that drives several GPUs, or launches from several threads, sizes
+// every grid from its own device's answer (speed only: the last-workgroup protocol needs no
+// co-residency)
 template <typename Kern>
 static int pf_resident_blocks(int which, Kern k) {
-  static int cache[2] = {0, 0};
-  int& n = cache[which];
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, int> cache;
+  int dev = 0;
+  hip_check(hipGetDevice(&dev), "pf device");
+  std::lock_guard<std::mutex> lk(mu);
+  int& n = cache[{dev, which}];
   if (n == 0) {
-    int dev = 0, cus = 0, per = 0;
-    hip_check(hipGetDevice(&dev), "pf device");
+    int cus = 0, per = 0;
     hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "pf cu count");
     hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, 256, 0), "pf occupancy");
     n = std::max(1, cus * std::max(1, per));

@@ -46,6 +46,7 @@ SlotPool::SlotPool(int producer_budget, int consumer_budget, int device)
     : pb_(producer_budget), cb_(consumer_budget), n_(producer_budget + consumer_budget), device_(device) {
   check(producer_budget >= 0 && consumer_budget >= 0 && n_ > 0, "SlotPool: budgets must be >= 0 and sum > 0");
   state_.assign(n_, kFree);
+  origin_.assign(n_, -1);
   hdr_.resize(n_);
   ready_ref_.resize(n_);
   free_ref_.resize(n_);
@@ -106,7 +107,7 @@ static std::string state_msg(const char* op, int want, int got) {
 
 int SlotPool::try_acquire_produce() {
   std::lock_guard<std::mutex> lk(mu_);
-  if (producer_held_ >= pb_ || free_list_.empty()) {
+  if (producer_held_ + ext_held_ >= pb_ || free_list_.empty()) {
     ++st_.produce_full;
     return -1;
   }
@@ -119,7 +120,7 @@ int SlotPool::try_acquire_produce() {
 
 int SlotPool::acquire_produce(double timeout_s) {
   std::unique_lock<std::mutex> lk(mu_);
-  const auto pred = [&] { return closed_ || (producer_held_ < pb_ && !free_list_.empty()); };
+  const auto pred = [&] { return closed_ || (producer_held_ + ext_held_ < pb_ && !free_list_.empty()); };
   if (!pred()) ++st_.produce_full;
   if (timeout_s < 0) {
     cv_produce_.wait(lk, pred);
@@ -192,6 +193,7 @@ void SlotPool::route_local(int slot) {
   check(consumer_held_ < cb_, "SlotPool.route_local: no consumer credit");
   erase_value(produced_fifo_, slot);
   state_[slot] = kReady;
+  origin_[slot] = -1;
   --producer_held_;
   ++consumer_held_;
   ready_fifo_.push_back(slot);
@@ -251,11 +253,7 @@ void SlotPool::end_recv(int slot, const SlotHeader& h, uint64_t stream) {
 int SlotPool::try_get() {
   std::lock_guard<std::mutex> lk(mu_);
   if (ready_fifo_.empty()) return -1;
-  const int s = ready_fifo_.front();
-  ready_fifo_.pop_front();
-  state_[s] = kLeased;
-  ++st_.got;
-  return s;
+  return pop_ready_locked();
 }
 
 int SlotPool::get(double timeout_s) {
@@ -267,11 +265,7 @@ int SlotPool::get(double timeout_s) {
     return -1;
   }
   if (ready_fifo_.empty()) return -1;
-  const int s = ready_fifo_.front();
-  ready_fifo_.pop_front();
-  state_[s] = kLeased;
-  ++st_.got;
-  return s;
+  return pop_ready_locked();
 }
 
 void SlotPool::release(int slot, uint64_t stream) {
@@ -341,7 +335,7 @@ std::vector<int> SlotPool::acquire_batch(int n, double timeout_s, uint64_t strea
   std::vector<EvRef> waits;
   {
     std::unique_lock<std::mutex> lk(mu_);
-    const auto pred = [&] { return closed_ || (producer_held_ + n <= pb_ && (int)free_list_.size() >= n); };
+    const auto pred = [&] { return closed_ || (producer_held_ + ext_held_ + n <= pb_ && (int)free_list_.size() >= n); };
     if (!pred()) {
       ++st_.produce_full;
       if (timeout_s < 0) cv_produce_.wait(lk, pred);
@@ -522,7 +516,117 @@ int SlotPool::pop_ready_locked() {
   ready_fifo_.pop_front();
   state_[s] = kLeased;
   ++st_.got;
+  if (track_origins_) got_origins_.push_back(origin_[s]);
   return s;
+}
+
+void SlotPool::set_external_held(int n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  const bool less = n < ext_held_;
+  ext_held_ = std::max(0, n);
+  if (less) cv_produce_.notify_all();
+}
+
+int SlotPool::producer_room() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return pb_ - producer_held_ - ext_held_;
+}
+
+void SlotPool::set_track_origins(bool on) {
+  std::lock_guard<std::mutex> lk(mu_);
+  track_origins_ = on;
+}
+
+void SlotPool::complete_recv_batch_from(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs,
+                                        int64_t origin) {
+  check(slots.size() == hdrs.size(), "complete_recv_batch: size mismatch");
+  if (slots.empty()) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kReceiving, state_msg("complete_recv_batch", kReceiving, state_[s]));
+  }
+  for (size_t i = 0; i < slots.size(); ++i) {
+    const int s = slots[i];
+    hdr_[s] = hdrs[i];
+    ready_ref_[s] = EvRef{};   // the writer completed its copy before the notice: nothing to wait on
+    origin_[s] = origin;
+    state_[s] = kReady;
+    ready_fifo_.push_back(s);
+    ++st_.received;
+  }
+  cv_ready_.notify_all();
+}
+
+std::vector<int64_t> SlotPool::take_got_origins() {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<int64_t> out;
+  out.swap(got_origins_);
+  return out;
+}
+
+int64_t SlotPool::origin(int slot) const {
+  check_slot(slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  return origin_[slot];
+}
+
+std::vector<int> SlotPool::pop_ready_for_return(int max_n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<int> out;
+  while ((int)out.size() < max_n && !ready_fifo_.empty()) {
+    const int s = ready_fifo_.front();
+    ready_fifo_.pop_front();
+    state_[s] = kLeased;
+    out.push_back(s);
+  }
+  return out;
+}
+
+std::vector<int> SlotPool::reclaim_batch(int n, uint64_t stream) {
+  std::vector<int> out;
+  std::vector<EvRef> waits;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    while ((int)out.size() < n && producer_held_ < pb_ && !free_list_.empty()) {
+      const int s = free_list_.front();
+      free_list_.pop_front();
+      state_[s] = kProducing;
+      ++producer_held_;
+      out.push_back(s);
+      const EvRef r = free_ref_[s];
+      if (!ref_live_locked(r)) continue;
+      bool dup = false;
+      for (const auto& w : waits) dup |= (w.idx == r.idx && w.gen == r.gen);
+      if (!dup) waits.push_back(r);
+    }
+  }
+  if (device_ >= 0 && !waits.empty()) {
+    set_device();
+    for (const auto& w : waits) wait_ref(w, stream);
+  }
+  return out;
+}
+
+void SlotPool::commit_front_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs,
+                                  uint64_t stream) {
+  check(slots.size() == hdrs.size(), "commit_front_batch: size mismatch");
+  if (slots.empty()) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kProducing, state_msg("commit_front_batch", kProducing, state_[s]));
+  }
+  const EvRef r = record_shared_locked(stream);
+  for (size_t i = slots.size(); i-- > 0;) {
+    const int s = slots[i];
+    hdr_[s] = hdrs[i];
+    ready_ref_[s] = r;
+    state_[s] = kProduced;
+    produced_fifo_.push_front(s);
+    ++st_.produced;
+  }
+  if (auto_route_) route_pending_locked();
 }
 
 std::vector<int> SlotPool::get_batch(int max_n, double timeout_s, uint64_t stream) {
@@ -645,7 +749,7 @@ int SlotPool::reoffer_batch(const std::vector<int>& slots, uint64_t stream) {
   for (int s : slots) {
     check_slot(s);
     check(state_[s] == kLeased, state_msg("reoffer_batch", kLeased, state_[s]));
-    if (producer_held_ >= pb_) break;
+    if (producer_held_ + ext_held_ >= pb_) break;
     ready_ref_[s] = record_shared_locked(stream);
     state_[s] = kProduced;
     --consumer_held_;

@@ -105,6 +105,12 @@ class SlotPool {
   const std::vector<uint64_t>& slot_ptrs() const { return ptrs_; }
   int producer_budget() const { return pb_; }
   int consumer_budget() const { return cb_; }
+  // Frames this producer delivered into consumers' read-ahead that no consumer has taken yet.  They
+  // still count against the producer budget (queue_size stays ONE logical bound: the reference's
+  // deque(maxlen) holds every item not yet got, psana_ray/shared_queue.py:7,11); the queue fabric
+  // keeps this up to date from the consumers' `taken` counters.
+  void set_external_held(int n);
+  int producer_room() const;   // pb - producer_held - external_held
 
   // producer side
   int try_acquire_produce();
@@ -167,6 +173,21 @@ class SlotPool {
   // (LEASED -> PRODUCED, headers kept; consumer budget -> producer budget).  Returns how many
   // moved (stops when the producer budget is full).
   int reoffer_batch(const std::vector<int>& slots, uint64_t stream);
+  // Origins of consumed frames (elastic fabric): a received frame remembers the producer member it
+  // came from (-1: routed locally); every frame a consumer takes (get / get_batch) appends its
+  // origin to a log the fabric drains, so each producer learns how many of its frames were taken.
+  void set_track_origins(bool on);
+  void complete_recv_batch_from(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, int64_t origin);
+  std::vector<int64_t> take_got_origins();
+  int64_t origin(int slot) const;
+  // Consumer close: READY frames taken out of the FIFO to be handed back to a producer (LEASED,
+  // not counted as got); free them with release() once a producer copied them out.
+  std::vector<int> pop_ready_for_return(int max_n);
+  // Producer: up to n free slots for frames handed back by a closing consumer (PRODUCING; may
+  // exceed the logical budget by frames that were counted as external read-ahead), and their
+  // commit at the FRONT of the produced FIFO (they were queued before anything produced now).
+  std::vector<int> reclaim_batch(int n, uint64_t stream);
+  void commit_front_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream);
 
  private:
   void set_device() const;
@@ -196,7 +217,10 @@ class SlotPool {
   int64_t ev_records_ = 0;
   std::vector<EvRef> ready_ref_, free_ref_;
   std::deque<int> free_list_, produced_fifo_, ready_fifo_;
-  int producer_held_ = 0, consumer_held_ = 0;
+  int producer_held_ = 0, consumer_held_ = 0, ext_held_ = 0;
+  bool track_origins_ = false;
+  std::vector<int64_t> origin_;
+  std::vector<int64_t> got_origins_;
   bool closed_ = false;
   bool auto_route_ = false;
   PoolStats st_;

@@ -32,6 +32,13 @@ QUEUE_LOOKUP_RETRIES = 10             # producer.py:35
 QUEUE_LOOKUP_DELAY_S = 1.0            # producer.py:35
 CONSUMER_POLL_SLEEP_S = 1.0           # examples/psana_consumer.py:40
 
+# --- consumer read-ahead (elastic fabric) ----------------------------------------------------
+# A consumer holds at most this many frames noticed-but-not-taken plus grants outstanding: the
+# bound on what a crashed consumer loses (the reference's get() pops ONE item,
+# psana_ray/shared_queue.py:19-24).  One producer chunk (64 frames) keeps a copy in flight while the
+# previous one is read; DataReader.batches(n) raises it to 2 x n.
+DEFAULT_PREFETCH = 64
+
 # --- rendezvous ---------------------------------------------------------------------------
 DEFAULT_STORE_PORT = 6379             # the Ray head port of README.md:15, reused for the store
 ENV_ADDRESS = "PSANA_RAY_ADDRESS"

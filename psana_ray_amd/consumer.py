@@ -18,7 +18,8 @@ import signal
 import sys
 import time
 
-from .config import DEFAULT_LOG_LEVEL, DEFAULT_QUEUE_NAME, DEFAULT_RAY_ADDRESS, DEFAULT_RAY_NAMESPACE, LOG_LEVELS
+from .config import (DEFAULT_LOG_LEVEL, DEFAULT_PREFETCH, DEFAULT_QUEUE_NAME, DEFAULT_RAY_ADDRESS,
+                     DEFAULT_RAY_NAMESPACE, LOG_LEVELS)
 
 log = logging.getLogger("psana_ray_amd.consumer")
 
@@ -39,6 +40,9 @@ def build_parser():
                     help="--task train: data-parallel training over the consumer processes of a torchrun launch "
                          "(gradients all-reduced by RCCL on GPUs, gloo on the CPU)")
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--prefetch", type=int, default=None,
+                    help=f"read-ahead bound: frames delivered but not read yet + grants outstanding (default "
+                         f"max({DEFAULT_PREFETCH}, 2 x --batch)); what a crashed consumer can lose")
     ap.add_argument("--max_frames", type=int, default=None)
     ap.add_argument("--thr_peak", type=float, default=20.0)
     ap.add_argument("--son_min", type=float, default=5.0)
@@ -92,7 +96,8 @@ def main(argv=None) -> int:
     registry.register("consumer", lambda: {"frames_consumed": n, "peaks": peaks_total})
     reporter = None
     with DataReader(args.ray_address, args.queue_name, args.ray_namespace, consumer_id=args.consumer_id,
-                    device=args.device, timeout_s=args.timeout) as reader:
+                    device=args.device, timeout_s=args.timeout,
+                    prefetch=args.prefetch or max(DEFAULT_PREFETCH, 2 * args.batch)) as reader:
         cid = reader.consumer_id
         if reader.endpoint is not None:
             registry.register("queue", reader.endpoint.metrics)

@@ -30,13 +30,12 @@ when it exists in this process.
 from __future__ import annotations
 
 import logging
-import math
 from typing import List, Optional
 
 import numpy as np
 import torch
 
-from .config import DEFAULT_QUEUE_NAME, DEFAULT_RAY_ADDRESS, DEFAULT_RAY_NAMESPACE
+from .config import DEFAULT_PREFETCH, DEFAULT_QUEUE_NAME, DEFAULT_RAY_ADDRESS, DEFAULT_RAY_NAMESPACE
 from .queue.endpoint import EndOfStream as _QueueEOS
 from .queue.endpoint import FrameItem, QueuePeerError
 
@@ -55,7 +54,7 @@ class DataReader:
     def __init__(self, address: str = DEFAULT_RAY_ADDRESS, queue_name: str = DEFAULT_QUEUE_NAME,
                  ray_namespace: str = DEFAULT_RAY_NAMESPACE, consumer_id: Optional[int] = None,
                  device: Optional[str] = None, as_numpy: bool = False, timeout_s: float = 300.0,
-                 slots: Optional[int] = None):
+                 slots: Optional[int] = None, prefetch: Optional[int] = None):
         self.address = address
         self.queue_name = queue_name
         self.ray_namespace = ray_namespace
@@ -63,7 +62,11 @@ class DataReader:
         self.device_req = device
         self.as_numpy = as_numpy
         self.timeout_s = timeout_s
-        self.slots = slots          # shard size (default: queue_size / --num_consumers of the producer)
+        # read-ahead bound (frames noticed-but-not-taken + grants outstanding): what a crashed reader
+        # can lose; its ring is landing space for that plus the frames it leased, never queue
+        # capacity (queue_size stays the producers' one logical bound)
+        self.prefetch = int(prefetch) if prefetch is not None else DEFAULT_PREFETCH
+        self.slots = slots          # ring slots (default: 2 x prefetch)
         self._queue = None       # the reference's actor handle slot: endpoint or in-process queue
         self._local = None
         self._sess = None
@@ -116,10 +119,10 @@ class DataReader:
             dtype = {"float32": torch.float32, "uint16": torch.uint16}[meta["dtype"]]
             shape = tuple(meta["frame_shape"])
             frame_bytes = int(np.prod(shape)) * (4 if meta["dtype"] == "float32" else 2)
-            share = self.slots or max(1, math.ceil(int(meta["queue_size"]) / max(1, int(meta.get("num_consumers", 1)))))
-            slots = physical_slots(share, frame_bytes, device, 0.8)
+            want = self.slots or 2 * max(1, self.prefetch)
+            slots = physical_slots(want, frame_bytes, device, 0.8)
             ring = FrameRing(shape, dtype, device, 0, slots, shm_name=sess.ring_name() if device.type == "cpu" else None)
-            ep = QueueEndpoint(ring, sess, is_producer=False, is_consumer=True)
+            ep = QueueEndpoint(ring, sess, is_producer=False, is_consumer=True, prefetch=self.prefetch)
             ep.start()
         except BaseException:
             sess.close("failed")
@@ -268,6 +271,10 @@ class DataReader:
         from .batching import collate_items
 
         self._check()
+        ep = self.endpoint
+        if ep is not None and ep._fabric is not None and ep._fabric.prefetch < 2 * batch_size:
+            # keep one batch in flight while the previous one is collated
+            ep._fabric.set_prefetch(min(2 * batch_size, ep.ring.n_slots))
         if self._local is not None:
             # in-process CPU queue (config 1): reference semantics have no end-of-stream marker
             # (a None get is "empty", Q-2), so the iteration ends after `timeout` s without a frame

@@ -7,9 +7,12 @@ live in the producers' own HBM pools; a producer that finished waits (bounded by
 for consumers to take them.  The keeper removes that wait: it is a session member in the
 ``keeper`` role with a ring of its own, and
 
-  * as a CONSUMER it grants slots only to producers that finished producing and still hold
-    undelivered frames (state ``draining``) -- it never competes with live consumers for a
-    running stream (``QueueFabric.set_grant_filter``);
+  * as a CONSUMER it grants slots to producers that finished producing and still hold
+    undelivered frames (state ``draining``), and to LIVE producers whose backlog no other
+    consumer has credit for (0.1 s in a row) -- so committed frames move into
+    the keeper as they are produced and survive a producer crash, like puts into the detached
+    actor; producers route to a keeper only when no real consumer has credit, so it never
+    competes with live consumers (``QueueFabric.set_grant_filter`` / ``set_keeper``);
   * every frame it receives goes straight back on offer (``SlotPool.reoffer_batch``: headers kept)
     and, as a PRODUCER with the ``relay`` policy (never to itself), it delivers them to any
     consumer that attaches, whenever that is;
@@ -29,6 +32,7 @@ import argparse
 import logging
 import signal
 import sys
+import time
 
 from .config import DEFAULT_LOG_LEVEL, DEFAULT_QUEUE_NAME, DEFAULT_RAY_ADDRESS, DEFAULT_RAY_NAMESPACE, LOG_LEVELS
 
@@ -75,7 +79,7 @@ def run(args) -> int:
     try:
         n = int(args.slots)
         ring = FrameRing(shape, dtype, device, n, n, shm_name=sess.ring_name() if device.type == "cpu" else None)
-        ep = QueueEndpoint(ring, sess, is_producer=True, is_consumer=True, route="relay")
+        ep = QueueEndpoint(ring, sess, is_producer=True, is_consumer=True, route="relay", keeper=True)
         fab = ep._fabric
         fab.set_grant_filter(True)
         ep.start()
@@ -92,12 +96,17 @@ def run(args) -> int:
                 if mid not in granted and (sess.state(mid) == "draining" or sess.finished(mid)):
                     fab.set_peer_grantable(mid, True)
                     granted.add(mid)
-            slots = pool.get_batch(64, 0.05, 0)
+            # lease only what can go back on offer: a frame taken out of the receive side and not
+            # re-offered would be lost (the producer already counted it as delivered)
+            room = min(64, pool.producer_room())
+            slots = pool.get_batch(room, 0.05, 0) if room > 0 else []
+            if room <= 0:
+                time.sleep(0.05)   # every held frame is on offer: wait for consumers to take some
             if slots:
                 moved = pool.reoffer_batch(slots, 0)
                 kept += moved
-                for s in slots[moved:]:   # producer budget full (cannot happen: equal budgets)
-                    pool.release(s, 0)
+                if moved != len(slots):
+                    raise RuntimeError(f"keeper: {len(slots) - moved} leased frames could not be re-offered")
             if ep.failed is not None:
                 raise RuntimeError(f"queue fabric failed: {ep.failed}")
             idle = pool.n_ready() == 0 and pool.n_produced() == 0 and pool.consumer_held() == 0 \

@@ -70,6 +70,9 @@ class ProducerPipeline:
             self.buf_used = [False] * n_raw_buffers
             self.h2d_done = [torch.cuda.Event() for _ in range(n_raw_buffers)]
         self._k = 0
+        # completion log of the Python paths: (frames so far, perf_counter s) at commit -- the CPU
+        # calibration is synchronous, so commit == completion (the native engine logs device events)
+        self._done_log: List[tuple] = []
         self._inflight = collections.deque()
         self._reuses = hasattr(source, "n_staging")
         self.engine = None
@@ -156,6 +159,8 @@ class ProducerPipeline:
             for s, e in zip(slots, evs):
                 self.ep.commit(s, self.rank, e.idx, e.gevt, e.photon_energy)
         self.frames += n
+        if not self.gpu:
+            self._done_log.append((self.frames, time.perf_counter()))
         if self.log_every and self.frames % self.log_every < n:
             log.info("Rank %d produced: idx=%d | shape=%s | photon_energy=%s", self.rank, evs[-1].idx,
                      tuple(self.ep.ring.frame_shape), evs[-1].photon_energy)
@@ -184,7 +189,30 @@ class ProducerPipeline:
 
     @property
     def produced(self) -> int:
+        """Frames whose calibration has COMPLETED (native engine: the chunk's device event; CPU: the
+        commit).  ``enqueued`` counts frames committed with kernels possibly still running."""
+        return int(self.engine.completed) if self.engine is not None else self.frames
+
+    @property
+    def enqueued(self) -> int:
         return int(self.engine.frames) if self.engine is not None else self.frames
+
+    def completion_log(self, since: int = 0):
+        """``(first_index, [(frames completed so far, t_seconds), ...])`` -- one entry per completed
+        chunk from index ``since`` on, times on the :meth:`clock` of this producer."""
+        if self.engine is not None:
+            first, v = self.engine.completions(int(since))
+            return int(first), [(int(f), ms * 1e-3) for f, ms in v]
+        return int(since), list(self._done_log[int(since):])
+
+    def clock(self, stream=None) -> float:
+        """Now on the completion log's clock (seconds).  Native engine: device time of an event
+        recorded on ``stream`` (default: current) -- the host waits for it, so a consumer stream's
+        work issued before is finished at that point."""
+        if self.engine is not None:
+            h = _ext.stream_handle(stream) if stream is not None else int(torch.cuda.current_stream(self.device).cuda_stream)
+            return float(self.engine.mark(h)) * 1e-3
+        return time.perf_counter()
 
     def metrics(self) -> dict:
         """Cumulative counters for utils.metrics (sampled, nothing runs per frame)."""

@@ -40,7 +40,8 @@ from .ring import FrameRing
 
 log = logging.getLogger(__name__)
 
-POLICIES = {"balanced": 0, "local_first": 1, "spread": 2, "relay": 3}   # relay: queue keeper
+# relay: queue keeper; remote_only: every frame crosses to another process while one is linked
+POLICIES = {"balanced": 0, "local_first": 1, "spread": 2, "relay": 3, "remote_only": 4}
 
 
 class QueueError(RuntimeError):
@@ -104,7 +105,11 @@ class FrameItem:
 
 class QueueEndpoint:
     def __init__(self, ring: FrameRing, session=None, is_producer: bool = True, is_consumer: bool = True,
-                 route: str = "balanced"):
+                 route: str = "balanced", prefetch: int = 0, keeper: bool = False):
+        """``prefetch`` (consumer role, fabric mode): at most this many frames noticed-but-not-taken
+        plus grants outstanding -- the read-ahead a crashed consumer can lose (0: the ring's free
+        slots only).  ``keeper``: this member is a queue keeper (its links are marked so producers
+        use it only as the last resort)."""
         if route not in POLICIES:
             raise ValueError(f"unknown routing policy {route!r} ({' | '.join(POLICIES)})")
         self.ring = ring
@@ -133,6 +138,8 @@ class QueueEndpoint:
             dev = ring.device.index if ring.device.index is not None else torch.cuda.current_device()
         self._fabric = C.QueueFabric(self.pool, self._slot_bytes, dev, self.is_producer, self.is_consumer,
                                      POLICIES[route], session.mid)
+        self._fabric.set_prefetch(int(prefetch))
+        self._fabric.set_keeper(bool(keeper))
         if self.is_consumer:
             if self.gpu:
                 self._fabric.export_ipc_ring()
@@ -283,7 +290,10 @@ class QueueEndpoint:
 
     def close_consumer(self):
         """Stop taking frames: producers stop writing into this shard (frames whose copy was in
-        flight go to other consumers; frames already in the shard are dropped with it)."""
+        flight go back to their producer's FIFO), and every frame that arrived here and was not
+        taken is handed back to a live producer for the other consumers (reference: items nobody
+        got stay in the actor).  Call it once this process stopped reading.  Frames no live
+        producer can take back (all finished) are counted in ``frames_dropped``."""
         if self._consumer_closed:
             return
         self._consumer_closed = True
@@ -365,7 +375,9 @@ class QueueEndpoint:
                 "frames_requeued": st.frames_requeued, "bytes_sent": st.bytes_sent, "bytes_recv": st.bytes_recv,
                 "batches": st.batches, "grants_given": st.grants_given, "grants_returned": st.grants_returned,
                 "grants_reclaimed": st.grants_reclaimed, "peers_dead": st.peers_dead,
-                "links_failed": st.links_failed,
+                "links_failed": st.links_failed, "frames_returned": st.frames_returned,
+                "frames_reclaimed": st.frames_reclaimed, "frames_dropped": st.frames_dropped,
+                "returns_rejected": st.returns_rejected, "readahead": st.readahead,
                 "links_opened": st.links_opened, "links_live": sum(1 for ls in links if ls.attached and not ls.dead),
                 "copy_ms_per_batch": 1e3 * st.copy_s / max(1, st.batches),
                 "iterations": st.iterations, "idle_iterations": st.idle_iterations}

@@ -30,6 +30,33 @@ RATE_KEYS = ("frames", "frames_produced", "frames_consumed", "frames_routed", "b
              "peaks", "rounds", "full_waits")
 
 
+def sustained_rate(log_entries, t0: float, t1: float):
+    """Sustained production rate inside the window ``(t0, t1]`` from a completion log.
+
+    ``log_entries``: ``[(frames completed so far, completion time), ...]`` in completion order (one
+    entry per chunk; ``ProducerPipeline.completion_log``).  Frames of chunks that completed at or
+    before ``t0`` -- already READY when the window opened -- are excluded; the rate runs from the
+    last completion at or before ``t0`` to the last completion at or before ``t1``, i.e. between
+    two chunk completions, so a window never gains or loses a fraction of a chunk.
+
+    Returns ``(frames completed inside the window, frames / s or None when fewer than one
+    completion on each side of t0)``."""
+    before = None
+    last = None
+    for f, t in log_entries:
+        if t <= t0:
+            before = (f, t)
+        elif t <= t1:
+            last = (f, t)
+        else:
+            break
+    if before is None or last is None:
+        return (0 if last is None else last[0] - (before[0] if before else 0)), None
+    frames = last[0] - before[0]
+    dt = last[1] - before[1]
+    return frames, (frames / dt if dt > 0 else None)
+
+
 class Registry:
     def __init__(self):
         self._lock = threading.Lock()

@@ -20,7 +20,10 @@ def main():
     ap.add_argument("--queue_name", default="my")
     ap.add_argument("--namespace", default="default")
     ap.add_argument("--slots", type=int, default=None)
+    ap.add_argument("--prefetch", type=int, default=None)
     ap.add_argument("--die_after", type=int, default=-1)
+    ap.add_argument("--stop_after", type=int, default=-1,
+                    help="leave normally (DataReader.close) after N frames: unread frames go back to the queue")
     ap.add_argument("--sleep", type=float, default=0.0, help="seconds per frame (a slow consumer)")
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--verify", default="synthetic:2:tiny_epix:1", help="exp:run:detector:n_producers")
@@ -47,14 +50,14 @@ def main():
     out = open(a.out, "w", buffering=1)
     n = 0
     with DataReader(a.address, queue_name=a.queue_name, ray_namespace=a.namespace, device=a.device,
-                    timeout_s=a.timeout, slots=a.slots) as r:
+                    timeout_s=a.timeout, slots=a.slots, prefetch=a.prefetch) as r:
         out.write(json.dumps({"joined": r.consumer_id, "pid": os.getpid()}) + "\n")
         t0 = time.time()
         while True:
             try:
                 it = r.lease(timeout=0.5)
             except EndOfStream:
-                out.write(json.dumps({"eos": True, "t": time.time() - t0}) + "\n")
+                out.write(json.dumps({"eos": True, "t": time.time() - t0, "t_end": time.time()}) + "\n")
                 break
             if it is None:
                 continue
@@ -68,6 +71,14 @@ def main():
             if a.die_after >= 0 and n >= a.die_after:
                 out.flush()
                 os.kill(os.getpid(), signal.SIGKILL)
+            if a.stop_after >= 0 and n >= a.stop_after:
+                if a.sleep:
+                    time.sleep(0.5)   # let the read-ahead refill: close() must hand it back
+                break
+        ep = r.endpoint
+    if a.stop_after >= 0 and ep is not None:
+        st = ep.metrics()   # the counters as of the close (returns answered)
+        out.write(json.dumps({"closed": True, **{k: st.get(k) for k in ("frames_returned", "frames_dropped")}}) + "\n")
     out.close()
 
 

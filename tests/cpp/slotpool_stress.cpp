@@ -15,7 +15,8 @@
 //                           thread; links created through the same mailbox protocol separate
 //                           processes use; checks payload bytes, exactly-once delivery, per-producer
 //                           FIFO order within a shard and EOS, for every routing policy.
-//   scenario 4 (fabric, consumer leaves): the consumer-only member closes mid-stream and is
+//   scenario 4 (fabric, consumer leaves): the consumer-only member closes mid-stream, hands back its
+//                           unread frames, and is
 //                           dropped; producers requeue its in-flight frames; the surviving consumer
 //                           gets every frame the leaver had not taken, and the stream still ends.
 #include <stdint.h>
@@ -302,8 +303,12 @@ static void scenario_fabric(int64_t n_per_producer, int policy, bool leave) {
     require(seen[i].load() <= 1, "fabric: event duplicated");
     lost += seen[i].load() == 0;
   }
-  // only frames that were already READY in the leaver's shard may be lost (<= its 10 slots)
-  require(leave ? lost <= 10 : lost == 0, "fabric: events lost");
+  // the leaver hands the frames it received and did not take back to the producers (they are
+  // still producing when it leaves): nothing may be lost
+  require(lost == 0, "fabric: events lost");
+  if (leave) require(m[2].fab->stats().frames_returned == m[0].fab->stats().frames_reclaimed +
+                                                             m[1].fab->stats().frames_reclaimed,
+                     "fabric: returned frames not all reclaimed");
   const pr::FabricStats s1 = m[1].fab->stats();
   printf("fabric scenario (policy %d%s): %lld events, %lld lost, %lld sent by member 1, %lld requeued\n", policy,
          leave ? ", consumer leaves" : "", (long long)seen.size(), (long long)lost, (long long)s1.frames_sent,

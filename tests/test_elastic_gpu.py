@@ -33,12 +33,17 @@ def test_gpu_producer_first_consumer_later(store_port, tmp_path):  # noqa: F811
     assert recs[-1].get("eos") is True
 
 
+GPU_C = ("--device", "cuda:0", "--gen_device", "cuda")
+
+
 def test_gpu_kill9_consumer_survivor_gets_the_rest(store_port, tmp_path):  # noqa: F811
-    n, slots_a = 160, 4
-    prod = gpu_producer(store_port, n)
-    a = consumer(store_port, tmp_path / "a.jsonl", "--device", "cuda:0", "--gen_device", "cuda", "--sleep", "0.01", "--slots", str(slots_a),
-                 "--die_after", "16")
-    b = consumer(store_port, tmp_path / "b.jsonl", "--device", "cuda:0", "--gen_device", "cuda", "--sleep", "0.01", "--slots", "4")
+    """Default ring and read-ahead: the killed consumer loses at most its prefetch."""
+    from psana_ray_amd.config import DEFAULT_PREFETCH
+
+    n = 240
+    prod = gpu_producer(store_port, n, queue_size=100)
+    a = consumer(store_port, tmp_path / "a.jsonl", *GPU_C, "--sleep", "0.01", "--die_after", "16")
+    b = consumer(store_port, tmp_path / "b.jsonl", *GPU_C, "--sleep", "0.01")
     rc_a, _ = finish(a, 120)
     assert rc_a == -9
     rc_b, out_b = finish(b, 120)
@@ -49,8 +54,70 @@ def test_gpu_kill9_consumer_survivor_gets_the_rest(store_port, tmp_path):  # noq
     assert len(ga) == 16
     assert not set(ga) & set(gb)
     lost = set(range(n)) - set(ga) - set(gb)
-    assert len(lost) <= slots_a, lost
+    assert len(lost) <= DEFAULT_PREFETCH, lost
     assert records(tmp_path / "b.jsonl")[-1].get("eos") is True
+
+
+def test_gpu_consumer_that_leaves_hands_its_read_ahead_back(store_port, tmp_path):  # noqa: F811
+    """HBM read-ahead handed back on close: the producer copies the unread frames out of the
+    leaving consumer's ring (IPC) and the other consumer receives them, bit-exact, exactly once."""
+    n = 200
+    prod = gpu_producer(store_port, n, queue_size=64)
+    a = consumer(store_port, tmp_path / "a.jsonl", *GPU_C, "--sleep", "0.02", "--stop_after", "10")
+    b = consumer(store_port, tmp_path / "b.jsonl", *GPU_C, "--sleep", "0.02")
+    rc_a, out_a = finish(a, 120)
+    rc_b, out_b = finish(b, 120)
+    rc_p, out_p = finish(prod, 120)
+    assert (rc_a, rc_b, rc_p) == (0, 0, 0), (out_a[-2000:], out_b[-2000:], out_p[-2000:])
+    ra = records(tmp_path / "a.jsonl")
+    ga, gb = frames(ra), frames(records(tmp_path / "b.jsonl"))
+    assert len(ga) == 10
+    assert sorted(ga + gb) == list(range(n))
+    assert ra[-1].get("closed") and ra[-1]["frames_dropped"] == 0 and ra[-1]["frames_returned"] > 0, ra[-1]
+
+
+def test_gpu_competing_consumers_default_read_ahead(store_port, tmp_path):  # noqa: F811
+    """Fast and slow HBM consumers at the default ring: exactly once, the fast one takes more, and
+    the slow one finishes within one read-ahead window of the fast one."""
+    n = 200
+    fast = consumer(store_port, tmp_path / "fast.jsonl", *GPU_C, "--sleep", "0.002")
+    slow = consumer(store_port, tmp_path / "slow.jsonl", *GPU_C, "--sleep", "0.05")
+    time.sleep(3.0)
+    prod = gpu_producer(store_port, n)
+    for c in (fast, slow):
+        rc, out = finish(c, 120)
+        assert rc == 0, out[-2000:]
+    rc_p, out_p = finish(prod, 120)
+    assert rc_p == 0, out_p[-2000:]
+    gf, gs = frames(records(tmp_path / "fast.jsonl")), frames(records(tmp_path / "slow.jsonl"))
+    assert sorted(gf + gs) == list(range(n))
+    assert len(gf) > 2 * len(gs) and len(gs) > 0, (len(gf), len(gs))
+    t_fast = records(tmp_path / "fast.jsonl")[-1]["t_end"]
+    t_slow = records(tmp_path / "slow.jsonl")[-1]["t_end"]
+    assert t_slow - t_fast <= 16 * 0.05 + 3.0, (t_slow - t_fast)
+
+
+def test_gpu_keeper_keeps_committed_frames_across_a_producer_crash(store_port, tmp_path):  # noqa: F811
+    """A live GPU producer's committed frames move into the keeper's HBM ring while nobody else can
+    take them; kill -9 of the producer loses none of them (<= one chunk in flight allowed)."""
+    from tests.test_elastic_queue import hang_producer, keeper, wait_line
+
+    kp = keeper(store_port, "--device", "cuda:0")
+    time.sleep(2.0)
+    n, chunk = 40, 4
+    hp = hang_producer(store_port, n, "--chunk", str(chunk), "--queue_size", "16", "--device", "cuda:0")
+    wait_line(hp, "COMMITTED", timeout=120)
+    time.sleep(2.0)
+    hp.kill()
+    hp.wait(10)
+    c = consumer(store_port, tmp_path / "c.jsonl", *GPU_C)
+    rc_c, out_c = finish(c, 120)
+    rc_k, out_k = finish(kp, 120)
+    assert rc_c == 0, out_c[-2000:]
+    assert rc_k == 0, out_k[-2000:]
+    got = frames(records(tmp_path / "c.jsonl"))
+    assert len(got) == len(set(got)) and set(got) <= set(range(n)), got
+    assert len(got) >= n - chunk, f"only {len(got)} of {n} committed frames survived the producer"
 
 
 def test_gpu_keeper_holds_frames_after_the_producer_exits(store_port, tmp_path):  # noqa: F811

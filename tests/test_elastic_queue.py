@@ -6,8 +6,9 @@ rendezvous store; frames move through the native fabric's shared-memory links:
   (a) a producer runs with NO consumer, buffers its frames, a consumer started 10 s later drains
       all of them plus EOS, and the producer exits 0 (drain before exit);
   (b) a consumer that joins mid-stream receives frames; delivery stays exactly-once;
-  (c) kill -9 of one of two consumers mid-stream: the survivor gets every frame not already in the
-      dead consumer's shard, plus EOS, and the producer exits 0;
+  (c) kill -9 of one of two consumers mid-stream (default ring and read-ahead): the survivor gets
+      every frame not already in the dead consumer's read-ahead (<= its prefetch), plus EOS, and
+      the producer exits 0; a consumer that LEAVES normally hands its read-ahead back (no loss);
   (d) a second producer job attaches to the live queue; one consumer receives both jobs' frames
       exactly once;
   plus: a producer that nobody drains fails after --timeout with a clear message (rc 1).
@@ -125,10 +126,15 @@ def test_consumer_joins_mid_stream(store_port, tmp_path):
 
 
 def test_kill9_consumer_survivor_gets_the_rest(store_port, tmp_path):
-    slots_a = 4
-    prod = producer(store_port, 120)
-    a = consumer(store_port, tmp_path / "a.jsonl", "--sleep", "0.01", "--slots", str(slots_a), "--die_after", "12")
-    b = consumer(store_port, tmp_path / "b.jsonl", "--sleep", "0.01", "--slots", "4")
+    """Default ring and read-ahead (no --slots): a killed consumer loses at most its prefetch --
+    the frames delivered to it and not read -- not a shard (reference: get() pops one item,
+    psana_ray/shared_queue.py:19-24, examples/psana_consumer.py:41-47)."""
+    from psana_ray_amd.config import DEFAULT_PREFETCH
+
+    n = 240
+    prod = producer(store_port, n, queue_size=100)
+    a = consumer(store_port, tmp_path / "a.jsonl", "--sleep", "0.01", "--die_after", "12")
+    b = consumer(store_port, tmp_path / "b.jsonl", "--sleep", "0.01")
     rc_a, _ = finish(a)
     assert rc_a == -9
     rc_b, out_b = finish(b)
@@ -138,10 +144,29 @@ def test_kill9_consumer_survivor_gets_the_rest(store_port, tmp_path):
     ga, gb = frames(records(tmp_path / "a.jsonl")), frames(records(tmp_path / "b.jsonl"))
     assert len(ga) == 12
     assert not set(ga) & set(gb), "a frame was delivered twice"
-    lost = set(range(120)) - set(ga) - set(gb)
-    assert len(lost) <= slots_a, f"lost {len(lost)} frames, more than the dead consumer's shard ({slots_a})"
+    lost = set(range(n)) - set(ga) - set(gb)
+    assert len(lost) <= DEFAULT_PREFETCH, f"lost {len(lost)} frames, more than the dead consumer's prefetch"
     assert records(tmp_path / "b.jsonl")[-1].get("eos") is True
     assert "died" in out_p, out_p[-2000:]
+
+
+def test_consumer_that_leaves_hands_its_read_ahead_back(store_port, tmp_path):
+    """A consumer that stops after 10 frames and closes: the frames delivered into its ring and not
+    read go back to the producer, the other consumer receives them -- nothing lost, exactly once."""
+    n = 200
+    prod = producer(store_port, n, queue_size=64)
+    a = consumer(store_port, tmp_path / "a.jsonl", "--sleep", "0.02", "--stop_after", "10")
+    b = consumer(store_port, tmp_path / "b.jsonl", "--sleep", "0.02")
+    rc_a, out_a = finish(a)
+    rc_b, out_b = finish(b)
+    rc_p, out_p = finish(prod)
+    assert (rc_a, rc_b, rc_p) == (0, 0, 0), (out_a[-2000:], out_b[-2000:], out_p[-2000:])
+    ra = records(tmp_path / "a.jsonl")
+    ga, gb = frames(ra), frames(records(tmp_path / "b.jsonl"))
+    assert len(ga) == 10
+    assert sorted(ga + gb) == list(range(n)), "a frame was lost or delivered twice"
+    closed = ra[-1]
+    assert closed.get("closed") and closed["frames_dropped"] == 0 and closed["frames_returned"] > 0, closed
 
 
 def test_second_producer_job_attaches(store_port, tmp_path):
@@ -166,11 +191,12 @@ def test_undrained_producer_times_out_with_a_clear_message(store_port):
 
 def test_competing_consumers_share_by_speed(store_port, tmp_path):
     """P-02 (reference: consumers compete for one actor's items, so a faster consumer takes more):
-    credit water-filling over the links -- a consumer re-grants a slot only after it took the frame
-    out, so the fast one receives clearly more; every frame exactly once."""
+    at the DEFAULT ring and read-ahead, a consumer holds at most its prefetch (and the producer's
+    queue_size bounds what waits anywhere), so the fast one takes clearly more, both finish within
+    one read-ahead window of each other, and every frame arrives exactly once."""
     n = 200
-    fast = consumer(store_port, tmp_path / "fast.jsonl", "--sleep", "0.002", "--slots", "4")
-    slow = consumer(store_port, tmp_path / "slow.jsonl", "--sleep", "0.05", "--slots", "4")
+    fast = consumer(store_port, tmp_path / "fast.jsonl", "--sleep", "0.002")
+    slow = consumer(store_port, tmp_path / "slow.jsonl", "--sleep", "0.05")
     time.sleep(1.0)   # both attached before the stream starts
     prod = producer(store_port, n)
     for c in (fast, slow):
@@ -182,6 +208,11 @@ def test_competing_consumers_share_by_speed(store_port, tmp_path):
     assert sorted(gf + gs) == list(range(n)), "exactly-once delivery violated"
     assert len(gs) > 0, "the slow consumer should still receive frames"
     assert len(gf) > 2 * len(gs), (len(gf), len(gs))
+    # the slow one cannot have hoarded: it ends at most one read-ahead (its unread frames, <= the
+    # producer's queue_size of 16 here) after the fast one
+    t_fast = records(tmp_path / "fast.jsonl")[-1]["t_end"]
+    t_slow = records(tmp_path / "slow.jsonl")[-1]["t_end"]
+    assert t_slow - t_fast <= 16 * 0.05 + 2.0, (t_slow - t_fast)
 
 
 def keeper(port, *extra):
@@ -225,4 +256,62 @@ def test_keeper_with_a_live_consumer_stays_out_of_the_way(store_port, tmp_path):
     assert (rc_p, rc_c, rc_k) == (0, 0, 0), (out_p[-1500:], out_c[-1500:], out_k[-1500:])
     recs = records(tmp_path / "c.jsonl")
     assert sorted(frames(recs)) == list(range(64))
+    assert recs[-1].get("eos") is True
+
+
+def hang_producer(port, n, *extra):
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "_hang_producer.py"), "--address", f"127.0.0.1:{port}",
+           "--n", str(n), *extra]
+    return subprocess.Popen(cmd, env=ENV, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+
+def wait_line(p, prefix, timeout=60):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        line = p.stdout.readline()
+        if line.startswith(prefix):
+            return line
+        if not line and p.poll() is not None:
+            break
+    raise AssertionError(f"no {prefix!r} line from the process")
+
+
+def test_keeper_keeps_committed_frames_across_a_producer_crash(store_port, tmp_path):
+    """R-11: a LIVE producer's committed frames move into the keeper while no consumer can take
+    them, so a kill -9 of the producer loses none of them (<= one chunk in flight is allowed); a
+    consumer started afterwards receives them, bit-exact, exactly once."""
+    kp = keeper(store_port)
+    time.sleep(1.0)
+    n, chunk = 40, 4
+    hp = hang_producer(store_port, n, "--chunk", str(chunk), "--queue_size", "16")
+    wait_line(hp, "COMMITTED")
+    time.sleep(1.5)
+    hp.kill()
+    hp.wait(10)
+    c = consumer(store_port, tmp_path / "c.jsonl")
+    rc_c, out_c = finish(c)
+    rc_k, out_k = finish(kp)
+    assert rc_c == 0, out_c[-2000:]
+    assert rc_k == 0, out_k[-2000:]
+    got = frames(records(tmp_path / "c.jsonl"))
+    assert len(got) == len(set(got)) and set(got) <= set(range(n)), got
+    assert len(got) >= n - chunk, f"only {len(got)} of {n} committed frames survived the producer"
+
+
+def test_keeper_holds_more_than_its_receive_slots(store_port, tmp_path):
+    """a producer draining MORE frames than the keeper's --slots into a keeper with
+    no consumer -- every frame reaches a late consumer (the keeper leases only what it can re-offer;
+    the frames in its receive ring still count against the producer's queue_size until taken, so
+    the queue holds queue_size + keeper slots = 40 here)."""
+    prod = producer(store_port, 40, queue_size=16)
+    time.sleep(1.0)
+    kp = keeper(store_port, "--slots", "24")
+    rc_p, out_p = finish(prod, timeout=60)
+    assert rc_p == 0, out_p[-2000:]
+    c = consumer(store_port, tmp_path / "c.jsonl")
+    rc_c, out_c = finish(c)
+    rc_k, out_k = finish(kp)
+    assert (rc_c, rc_k) == (0, 0), (out_c[-2000:], out_k[-2000:])
+    recs = records(tmp_path / "c.jsonl")
+    assert sorted(frames(recs)) == list(range(40))
     assert recs[-1].get("eos") is True

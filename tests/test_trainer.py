@@ -106,7 +106,7 @@ def test_train_consumer_ddp_cpu(native):
     cons = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
                              "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
                              "psana_ray_amd.consumer", "--ray_address", addr, "--device", "cpu", "--task", "train",
-                             "--ddp", "--batch", "4", "--timeout", "90", "--metrics_interval", "0"],
+                             "--ddp", "--batch", "4", "--prefetch", "4", "--timeout", "90", "--metrics_interval", "0"],
                             env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     try:
         pout, _ = prod.communicate(timeout=300)
