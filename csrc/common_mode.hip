@@ -41,6 +41,13 @@
 
 #include <algorithm>
 
+// Workgroups of the epix10k2M kernel per CU (LDS sizing).  4: the kernel alone fills the CU; 3: a
+// quarter of every CU's LDS and VGPRs stays free, so the consumer's peak finder can run BESIDE the
+// producer's common mode on the same CUs (device-resident pipeline).
+#ifndef PR_CM_EPIX_WG_PER_CU
+#define PR_CM_EPIX_WG_PER_CU 4
+#endif
+
 namespace pr {
 
 // ---- lane exchange: y = x from lane (lane ^ J), VALU-only (no LDS-pipe round trip) ----
@@ -1099,10 +1106,12 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   check(n_gap_runs == 0 || (img_desc != 0 && gap_runs != 0 && gap_runs % 8 == 0), "calib_cm: bad gap run table");
   const ImgOut io{reinterpret_cast<const int32_t*>(img_desc), reinterpret_cast<const int2*>(gap_runs),
                   img_desc != 0 ? n_gap_runs : 0};
-  // LDS budget of one workgroup: the epix10k2M 176x48 stripe runs four workgroups per CU, the
-  // narrow compile-time kernels two, everything else one; what the tile leaves is side slots
-  const size_t budget = (epix_prod && asic_cols == 48) ? 40 * 1024 : (net && !jf_prod && asic_cols <= 128) ? 80 * 1024
-                                                                                                              : 160 * 1024;
+  // LDS budget of one workgroup: the epix10k2M 176x48 stripe runs PR_CM_EPIX_WG_PER_CU workgroups
+  // per CU, the narrow compile-time kernels two, everything else one; what the tile leaves is side
+  // slots
+  const size_t budget = (epix_prod && asic_cols == 48) ? (160 * 1024) / PR_CM_EPIX_WG_PER_CU
+                        : (net && !jf_prod && asic_cols <= 128) ? 80 * 1024
+                                                                : 160 * 1024;
   const int side_slots = (int)std::min<size_t>(kMaxSideSlots, lds < budget ? (budget - lds) / 32 : 0);
   TileGeom tg;
   tg.panel_rows = panel_rows;

@@ -270,7 +270,11 @@ class ProducerPipeline:
 
 
 class PeakFinderConsumer:
-    """Consumer engine: batches of leased slots -> K-07 peak finder -> stream-ordered release."""
+    """Consumer engine: batches of leased slots -> K-07 peak finder -> stream-ordered release.
+
+    GPU: consecutive batches alternate between TWO consumer streams, each with its own peak-finder
+    scratch, so one launch's candidate-test tail (every workgroup tests its parked candidates after
+    its stream of reads) overlaps the next launch's streaming reads instead of idling HBM."""
 
     def __init__(self, endpoint: QueueEndpoint, frame_shape, params: Optional[PeakFinderParams] = None,
                  batch: int = 16, keep_results: bool = False):
@@ -285,14 +289,17 @@ class PeakFinderConsumer:
         self.keep_results = keep_results
         self.results = []
         if self.gpu:
-            self.stream = torch.cuda.Stream(device=self.device)
+            self.streams = [torch.cuda.Stream(device=self.device) for _ in range(2)]
+            self.stream = self.streams[0]
             B = self.batch
-            self._nbuf = 3
+            self._nbuf = 4   # even: buffer k % 4 is reused by launch k + 4, on the same stream as k
             self.peaks = torch.empty((self._nbuf, B, self.params.max_peaks, 8), dtype=torch.float32, device=self.device)
             # counts [B] int32 and summary [B, 2] f32 of a batch share one row; the peak finder
             # writes them whole from its self-resetting scratch (no per-batch fill)
             self._meta = torch.zeros((self._nbuf, 3 * B), dtype=torch.int32, device=self.device)
-            self._pf_scratch = torch.zeros(kernels.PF_SCRATCH_WORDS, dtype=torch.int32, device=self.device)
+            # one scratch block per stream (a block must never serve two launches in flight)
+            self._pf_scratch = [torch.zeros(kernels.PF_SCRATCH_WORDS, dtype=torch.int32, device=self.device)
+                                for _ in self.streams]
             self.counts = self._meta[:, :B]
             self.summary = self._meta[:, B:].view(torch.float32).view(self._nbuf, B, 2)
             self.count_acc = torch.zeros((), dtype=torch.int64, device=self.device)
@@ -304,16 +311,19 @@ class PeakFinderConsumer:
             return
         if self.gpu:
             b = self._b % self._nbuf
+            k = self._b % len(self.streams)
+            st = self.streams[k]
             self._b += 1
-            with torch.cuda.stream(self.stream):
+            st.wait_stream(torch.cuda.current_stream(self.device))   # the items were leased on it
+            with torch.cuda.stream(st):
                 kernels.peakfind([it.data for it in items], self.shape, self.params, self.peaks[b, :n],
-                                 self.counts[b, :n], self.summary[b, :n], self.stream, total=self.count_acc,
-                                 scratch=self._pf_scratch)
+                                 self.counts[b, :n], self.summary[b, :n], st, total=self.count_acc,
+                                 scratch=self._pf_scratch[k])
                 if self.keep_results:
                     self.results.append((self.peaks[b, :n].clone(), self.counts[b, :n].clone(),
                                          [(it.rank, it.idx, it.gevt) for it in items]))
             for it in items:
-                it.release(self.stream)
+                it.release(st)
         else:
             from .ops import reference
 
@@ -347,14 +357,16 @@ class PeakFinderConsumer:
             self.process(items)
             return len(items)
         # GPU: one native call to lease, one kernel launch, one native call to release
-        slots = self.ep.get_batch(n_max, timeout, self.stream)
+        k = self._b % len(self.streams)
+        st = self.streams[k]
+        slots = self.ep.get_batch(n_max, timeout, st)
         n = len(slots)
         if n == 0:
             return 0
         C = _ext.load()
         b = self._b % self._nbuf
         self._b += 1
-        sh = int(self.stream.cuda_stream)
+        sh = int(st.cuda_stream)
         P, H, W = self.shape
         with trace_range("consumer.peakfind_batch"):
             # one native call: the peak finder on the ring slots with self-resetting outputs (no
@@ -364,21 +376,27 @@ class PeakFinderConsumer:
                              float(self.params.son_min), int(self.params.radius), int(self.params.max_peaks),
                              int(self.peaks[b].data_ptr()), int(self.counts[b].data_ptr()),
                              int(self.summary[b].data_ptr()), int(self.count_acc.data_ptr()), sh,
-                             int(self._pf_scratch.data_ptr()))
+                             int(self._pf_scratch[k].data_ptr()))
             if self.keep_results:
                 hs = self.ep.pool.headers(slots)
-                with torch.cuda.stream(self.stream):
+                with torch.cuda.stream(st):
                     self.results.append((self.peaks[b, :n].clone(), self.counts[b, :n].clone(),
                                          [(h.rank, h.idx, h.gevt) for h in hs]))
-        self.ep.release_batch(slots, self.stream)
+        self.ep.release_batch(slots, st)
         self.frames += n
         return n
 
     def metrics(self) -> dict:
         return {"frames_consumed": self.frames}
 
+    def sync_streams(self):
+        """Host waits for every batch issued so far (both consumer streams)."""
+        if self.gpu:
+            for st in self.streams:
+                st.synchronize()
+
     def synchronize(self):
         if self.gpu:
-            self.stream.synchronize()
+            self.sync_streams()
             self.peaks_total = int(self.count_acc.item())
         return self.peaks_total

@@ -6,6 +6,7 @@ Parity note: the container structure follows LCLS-II xtcdata, but no psana / XTC
 offline, so byte-exactness with psana-written files is "parity unpinned"; these tests pin our own
 writer <-> reader contract."""
 import math
+import os
 import subprocess
 import sys
 import threading
@@ -122,7 +123,8 @@ def test_corrupt_or_mismatched_files_raise(native, tmp_path):
 def test_mkrun_cli_xtc2(native, tmp_path):
     r = subprocess.run([sys.executable, "-m", "psana_ray_amd.mkrun", "--data_dir", str(tmp_path), "--exp", "e1",
                         "--run", "5", "--detector_name", "tiny_epix", "--num_events", "6"],
-                       capture_output=True, text=True, timeout=120)
+                       capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stderr
     big, smd = xtc2_paths(tmp_path, "e1", 5)
     assert big.exists() and smd.exists() and str(big) in r.stdout
