@@ -44,8 +44,15 @@
 // Workgroups of the epix10k2M kernel per CU (LDS sizing).  4: the kernel alone fills the CU; 3: a
 // quarter of every CU's LDS and VGPRs stays free, so the consumer's peak finder can run BESIDE the
 // producer's common mode on the same CUs (device-resident pipeline).
+// Frames per workgroup of the epix10k2M kernel.  2 = frame k+1's raw words prefetched during frame
+// k's medians (3 workgroups per CU, 168 VGPRs): measured equal to 1 on the same MI355X (6.59-6.60
+// vs 6.59-6.61 us/frame, device-resident pipeline 118.9k vs 118.4k fr/s on that box,
+// tools/gpu_cm_ab.sh), so the simpler single-frame form ships.
+#ifndef PR_CM_FPW
+#define PR_CM_FPW 1
+#endif
 #ifndef PR_CM_EPIX_WG_PER_CU
-#define PR_CM_EPIX_WG_PER_CU 4
+#define PR_CM_EPIX_WG_PER_CU (PR_CM_FPW > 1 ? 3 : 4)
 #endif
 
 namespace pr {
@@ -185,7 +192,8 @@ struct TileGeom {
   int asic_rows, asic_cols;          // R, C of one tile (a full-height ASIC stripe)
   int asics_per_col, asics_per_row;  // H / R, W / C
   int64_t npix;                      // pixels per frame
-  int nframes;                       // frames of this launch (grid = n_tiles * nframes, 1-D)
+  int nframes;                       // frames of this launch
+  int fpw;                           // frames per workgroup (grid = n_tiles * ceil(nframes / fpw), 1-D)
   int side_slots;                    // LDS side slots after the tile (SideCtx)
   int pitch;                         // LDS floats per tile row (values + candidate bits + pad)
 };
@@ -344,15 +352,29 @@ __device__ __forceinline__ uint32_t cm_need(uint32_t cbits) {
   else return 1u | ((cbits & 0x5555u) ? 2u : 0u) | ((cbits & 0xAAAAu) ? 4u : 0u);
 }
 
+#ifndef PR_CM_UNDEF_TABLES
+#define PR_CM_UNDEF_TABLES 1
+#endif
+// A table the group does not need (no pixel selects that candidate) is left UNDEFINED, not zeroed:
+// every consumer selects it only for pixels of that candidate (v_bfi on the candidate bits), and a
+// zero fill costs 8 v_mov per group (phase 1 and phase 3: 80 VALU per lane of the production kernel).
 template <int NT>
 __device__ __forceinline__ void load8(const float* __restrict__ t, int64_t npix, int64_t pix, uint32_t need,
                                       float (&a)[NT][8], int k0 = 0) {
 #pragma unroll
   for (int k = k0; k < NT; ++k) {
-    float4 u = make_float4(0.f, 0.f, 0.f, 0.f), w = u;
+    f32x4_t u, w;
     if ((need >> k) & 1u) {
-      u = *reinterpret_cast<const float4*>(t + k * npix + pix);
-      w = *reinterpret_cast<const float4*>(t + k * npix + pix + 4);
+      u = *reinterpret_cast<const f32x4_t*>(t + k * npix + pix);
+      w = *reinterpret_cast<const f32x4_t*>(t + k * npix + pix + 4);
+    } else {   // an empty asm "defines" the registers: no instruction (freeze(undef) would be a v_mov 0)
+#if PR_CM_UNDEF_TABLES
+      asm("" : "=v"(u));
+      asm("" : "=v"(w));
+#else
+      u = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      w = u;
+#endif
     }
     a[k][0] = u.x; a[k][1] = u.y; a[k][2] = u.z; a[k][3] = u.w;
     a[k][4] = w.x; a[k][5] = w.y; a[k][6] = w.z; a[k][7] = w.w;
@@ -528,7 +550,7 @@ __device__ __forceinline__ void cm_write_out(const float* tile, int P, int R, in
   __syncthreads();
   if (io.desc != nullptr) {
     cm_place(tile, P, R, C, io, panel, y0, x0, out);
-    cm_fill_gaps(io, tile_id, (int)gridDim.x / tg.nframes, out);
+    cm_fill_gaps(io, tile_id, (int)gridDim.x / ((tg.nframes + tg.fpw - 1) / tg.fpw), out);
   } else {
     cm_flush(tile, P, R, C, out, base, tg.panel_cols);
   }
@@ -566,11 +588,13 @@ struct TileCoord {
 // MI355X, 32 epix10k2M frames: frame-major order 5.7 us/frame vs 5.0 table-major with the medians
 // off; an XCD-grouping remap of the table-major order changed nothing, 4.75 vs 4.65, and an
 // XCD-local frame-major order lost, 5.29 vs 4.90.)
+// With tg.fpw > 1 a workgroup takes fpw consecutive frames of its tile (t.f = the first).
 __device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C) {
   TileCoord t;
   const int id = (int)blockIdx.x;
-  const int tile = id / tg.nframes;
-  t.f = id - tile * tg.nframes;
+  const int ng = (tg.nframes + tg.fpw - 1) / tg.fpw;
+  const int tile = id / ng;
+  t.f = (id - tile * ng) * tg.fpw;
   t.tile = tile;
   const int per_panel = tg.asics_per_col * tg.asics_per_row;
   t.panel = tile / per_panel;
@@ -721,6 +745,42 @@ __device__ __forceinline__ int dpp_quad_i(int x) {
   return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
 }
 
+// max(+-quad_perm(a), +-b) as ONE v_max_f32 with a DPP source (the builtin mov_dpp + v_maximum3 is
+// two VALU: v_maximum3 is VOP3, which takes no DPP operand on gfx950).  v_max_f32 is IEEE maxNum: it
+// differs from maximum only for NaN operands and the order of -0 / +0, and the median networks
+// carry neither a NaN nor a sign of zero that matters (a -0 median subtracts like +0).  The s_nop
+// covers the VALU-write -> DPP-read hazard (2 wait states), which the compiler does not insert for
+// inline asm.  PERM: 0xB1 = quad_perm [1,0,3,2] (lane q^1), 0x1B = [3,2,1,0] (lane q^3).
+#ifndef PR_CM_DPP_MAX
+#define PR_CM_DPP_MAX 1
+#endif
+#define PR_DPP_MAX_ASM(PERMSTR, SA, SB) \
+  asm("s_nop 1\n\tv_max_f32_dpp %0, " SA "%1, " SB "%2 quad_perm:" PERMSTR " row_mask:0xf bank_mask:0xf" \
+      : "=v"(r) : "v"(a), "v"(b))
+template <int PERM, bool NEG_A, bool NEG_B>
+__device__ __forceinline__ float max_dpp(float a, float b) {
+#if PR_CM_DPP_MAX
+  static_assert(PERM == 0xB1 || PERM == 0x1B, "max_dpp: quad permutation");
+  float r;
+  if constexpr (PERM == 0xB1) {
+    if constexpr (NEG_A && NEG_B) PR_DPP_MAX_ASM("[1,0,3,2]", "-", "-");
+    else if constexpr (NEG_A) PR_DPP_MAX_ASM("[1,0,3,2]", "-", "");
+    else if constexpr (NEG_B) PR_DPP_MAX_ASM("[1,0,3,2]", "", "-");
+    else PR_DPP_MAX_ASM("[1,0,3,2]", "", "");
+  } else {
+    if constexpr (NEG_A && NEG_B) PR_DPP_MAX_ASM("[3,2,1,0]", "-", "-");
+    else if constexpr (NEG_A) PR_DPP_MAX_ASM("[3,2,1,0]", "-", "");
+    else if constexpr (NEG_B) PR_DPP_MAX_ASM("[3,2,1,0]", "", "-");
+    else PR_DPP_MAX_ASM("[3,2,1,0]", "", "");
+  }
+  return r;
+#else
+  const float p = dpp_quad<PERM>(a);
+  return vmax(NEG_A ? -p : p, NEG_B ? -b : b);
+#endif
+}
+#undef PR_DPP_MAX_ASM
+
 // Ascending sort of a V-shaped (non-increasing then non-decreasing) register sequence, virtually
 // padded with +inf to the next power of two: the bitonic half-cleaner network restricted to the
 // comparators between real positions (a comparator against a +inf pad is a no-op).
@@ -745,18 +805,20 @@ __device__ __forceinline__ void bitonic_merge_vpad(float (&z)[N]) {
 // TileGeom): every LDS address in the unrolled loops is then a base VGPR + immediate offset.
 // Phase 1, compile-time tile shape: decode + pedestal of the tile into LDS by BLOCK threads
 // (thread index tid in [0, BLOCK)).
-template <int KIND, int NT, int BLOCK, int TR, int TC>
+template <int KIND, int NT, int BLOCK, int TR, int TC, bool RAW_IN>
 __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int P, const TileGeom& tg,
                                             const PR_GLOBAL uint16_t* raw, const float* __restrict__ ped,
-                                            const uint8_t* __restrict__ planes, const int64_t base, const int tid) {
+                                            const uint8_t* __restrict__ planes, const int64_t base, const int tid,
+                                            uint4 (&rw)[(TR * (TC / 8) + BLOCK - 1) / BLOCK],
+                                            const PR_GLOBAL uint16_t* raw_next) {
   constexpr int C = TC;
   constexpr int NITEMS = TR * (TC / 8);
   constexpr int NI = (NITEMS + BLOCK - 1) / BLOCK;
   // all of this lane's raw / plane / first-table loads in flight at once; the rare switched-gain
   // tables are loaded per group while decoding (select-then-load, the wave waits only when one of
-  // its lanes needs them), which keeps the live registers at raw + planes + one table
+  // its lanes needs them), which keeps the live registers at raw + planes + one table.  RAW_IN: the
+  // raw words were prefetched by the previous frame's phase 1 (they arrived during its medians).
   constexpr int C8 = TC / 8;
-  uint4 rw[NI];
   uint32_t ep[NI];
   float pa0[NI][1][8];
 #pragma unroll
@@ -765,7 +827,7 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
     if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
       const int r = i / C8, c = (i % C8) * 8;
       const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
-      rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
+      if constexpr (!RAW_IN) rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
       ep[u] = load_planes<NT>(planes, pix);
       load8<1>(ped, tg.npix, pix, 1u, pa0[u]);
     }
@@ -792,6 +854,18 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
     }
     const uint32_t slot = side_put(sc, act && el != 0xFFu, v);   // convergent: whole wave
     if (act) cm_put_meta<NT>(reinterpret_cast<uint8_t*>(tile + r * P + C), C, k, cb, slot);
+  }
+  // the next frame's raw words: in flight during this frame's medians and store (no barrier waits
+  // on vector memory; the registers are free again)
+  if (raw_next != nullptr) {
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = tid + u * BLOCK;
+      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
+        const int r = i / C8, c = (i % C8) * 8;
+        rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw_next + base + (int64_t)r * tg.panel_cols + c));
+      }
+    }
   }
 }
 
@@ -926,19 +1000,16 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
     // level 1: merge-split with lane q^1, both lanes V-shaped
     float z[M];
 #pragma unroll
-    for (int i = 0; i < M; ++i) z[i] = vmax(dpp_quad<0xB1>(x[i]), -x[i]);
+    for (int i = 0; i < M; ++i) z[i] = max_dpp<0xB1, false, true>(x[i], x[i]);
     bitonic_merge_vpad<M>(z);
     asm volatile("" ::: "memory");
     // level 2: merge path with lane q^3 (lanes 1 and 3 hold the terms)
     float kh = INF, kl = INF;
-    float pn = dpp_quad<0x1B>(z[0]);
-    const float p0 = pn;
+    const float p0 = dpp_quad<0x1B>(z[0]);
 #pragma unroll
     for (int t = 0; t < M; ++t) {
-      const float pt = pn;
-      if (t + 1 < M) pn = dpp_quad<0x1B>(z[t + 1]);
-      kh = vmin(kh, vmax(z[t], -pt));
-      if (t + 1 < M) kl = vmin(kl, vmax(z[t], -pn));
+      kh = vmin(kh, max_dpp<0x1B, true, false>(z[t], z[t]));            // max(z[t], -partner z[t])
+      if (t + 1 < M) kl = vmin(kl, max_dpp<0x1B, true, false>(z[t + 1], z[t]));   // max(z[t], -partner z[t+1])
     }
     const float e = -vmin(p0, dpp_quad<0xB1>(z[0]));   // max(A[M-1], B[M-1]) on lanes 1 and 3
     kl = vmin(kl, vmin(z[M - 1], e));
@@ -957,7 +1028,7 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
 }
 
 template <int KIND, int L, int M, int BLOCK, int TR = 0, int TC = 0>
-__global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
+__global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void calib_cm_net_kernel(
     const FramePtrs fp, const float* __restrict__ ped, const float* __restrict__ gf,
     const uint8_t* __restrict__ planes, const TileGeom tg, const CmParams cp, const ImgOut io) {
   constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
@@ -970,66 +1041,98 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? 4 : 2) void calib_cm_net_kernel(
   SideCtx sc = side_ctx(side, tg.side_slots);
   const TileCoord t = cm_coords(tg, R, C);
   const int tid = threadIdx.x;
-  const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[t.f]);
-  PR_GLOBAL float* out = gout<float>(fp.out[t.f]);
-
-  // ---- phase 1: decode + pedestal into LDS ------------------------------------------------
   constexpr int NITEMS = (TR > 0 && TC > 0) ? TR * (TC / 8) : 0;
   constexpr int NI = NITEMS > 0 ? (NITEMS + BLOCK - 1) / BLOCK : 0;
-  if constexpr (NI > 0 && NI <= 6) {
-    cm_load_net<KIND, NT, BLOCK, TR, TC>(tile, sc, P, tg, raw, ped, planes, t.base, tid);
-  } else {
-    cm_phase1<KIND, NT>(tile, sc, P, R, C, tg, raw, ped, planes, t.base);
-  }
-  __syncthreads();
-
-  // ---- phase 2a: rows by bank, one lane per segment ----------------------------------------
-  if (cp.flags & 1) {
-    cm_rows<L>(tile, P, R, C, cp, tid, blockDim.x);
-    __syncthreads();
-  }
-
-  // ---- phase 2b: columns ---------------------------------------------------------------------
-  if (cp.flags & 2) {
-    cm_cols<M>(tile, P, R, C, cp, tid, blockDim.x);
-    __syncthreads();
-  }
-
-  // ---- phase 3: gain factor + mask, store ---------------------------------------------------
-  if constexpr (NI > 0 && NI <= 6) {
-    // compile-time shape: every gain-factor load of this lane in flight before the first use
-    constexpr int C8 = TC / 8;
-    // (the first gain table of every item up front; the switched-gain tables are rare and are
-    // loaded per item, which keeps the production kernel within 128 VGPRs)
-    uint32_t cbs[NI], slots[NI];
-    float g0[NI][1][8];
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      const int i = tid + u * BLOCK;
-      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
-        const int r = i / C8, k = i % C8, c = k * 8;
-        cm_get_meta<NT>(reinterpret_cast<const uint8_t*>(tile + r * P + C), C, k, cbs[u], slots[u]);
-        load8<1>(gf, tg.npix, t.base + (int64_t)r * tg.panel_cols + c, 1u, g0[u]);
-      }
+  constexpr bool kNet = NI > 0 && NI <= 6;
+  // frames of this workgroup (tg.fpw consecutive frames of one tile; the compile-time production
+  // shapes prefetch frame k+1's raw words during frame k's medians)
+  const int nf = min(tg.fpw, tg.nframes - t.f);
+  uint4 rw[kNet ? NI : 1];
+  auto frame = [&](const int fi) {
+    const int f = t.f + fi;
+    const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[f]);
+    PR_GLOBAL float* out = gout<float>(fp.out[f]);
+    if (fi > 0) {
+      __syncthreads();   // the previous frame's store phase read the tile
+      sc.used = 0;
     }
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      const int i = tid + u * BLOCK;
-      if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
-        const int r = i / C8, c = (i % C8) * 8;
-        const int64_t pix = t.base + (int64_t)r * tg.panel_cols + c;
-        float ga[NT][8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ga[0][j] = g0[u][0][j];
-        if constexpr (NT > 1) load8<NT>(gf, tg.npix, pix, cm_need<NT>(cbs[u]), ga, 1);
-        float o[8];
-        cm_out8<KIND, NT>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, ped, tg.npix, pix, o);
-        cm_put8(tile + r * P + c, o);
-      }
+    // opaque per-frame copies of the tile base and the table pointers: the compiler must not keep
+    // every per-item address of the frame body live across the loop (loop-invariant hoisting of
+    // ~40 VGPRs of 64-bit addresses spills the kernel)
+    int64_t tb = t.base;
+    const float* pedp = ped;
+    const float* gfp = gf;
+    const uint8_t* plp = planes;
+    asm volatile("" : "+s"(tb), "+s"(pedp), "+s"(gfp), "+s"(plp));
+
+    // ---- phase 1: decode + pedestal into LDS ----------------------------------------------
+    if constexpr (kNet) {
+      const PR_GLOBAL uint16_t* raw_next = fi + 1 < nf ? gin<uint16_t>(fp.in[f + 1]) : nullptr;
+      if (fi == 0)
+        cm_load_net<KIND, NT, BLOCK, TR, TC, false>(tile, sc, P, tg, raw, pedp, plp, tb, tid, rw, raw_next);
+      else
+        cm_load_net<KIND, NT, BLOCK, TR, TC, true>(tile, sc, P, tg, raw, pedp, plp, tb, tid, rw, raw_next);
+    } else {
+      cm_phase1<KIND, NT>(tile, sc, P, R, C, tg, raw, pedp, plp, tb);
     }
-    cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, t.base, out);
+    __syncthreads();
+
+    // ---- phase 2a: rows by bank, one lane per segment ------------------------------------
+    if (cp.flags & 1) {
+      cm_rows<L>(tile, P, R, C, cp, tid, blockDim.x);
+      __syncthreads();
+    }
+
+    // ---- phase 2b: columns -----------------------------------------------------------------
+    if (cp.flags & 2) {
+      cm_cols<M>(tile, P, R, C, cp, tid, blockDim.x);
+      __syncthreads();
+    }
+
+    // ---- phase 3: gain factor + mask, store ----------------------------------------------
+    if constexpr (kNet) {
+      // compile-time shape: every gain-factor load of this lane in flight before the first use
+      constexpr int C8 = TC / 8;
+      // (the first gain table of every item up front; the switched-gain tables are rare and are
+      // loaded per item, which keeps the production kernel within 128 VGPRs)
+      uint32_t cbs[NI], slots[NI];
+      float g0[NI][1][8];
+#pragma unroll
+      for (int u = 0; u < NI; ++u) {
+        const int i = tid + u * BLOCK;
+        if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
+          const int r = i / C8, k = i % C8, c = k * 8;
+          cm_get_meta<NT>(reinterpret_cast<const uint8_t*>(tile + r * P + C), C, k, cbs[u], slots[u]);
+          load8<1>(gfp, tg.npix, tb + (int64_t)r * tg.panel_cols + c, 1u, g0[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NI; ++u) {
+        const int i = tid + u * BLOCK;
+        if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
+          const int r = i / C8, c = (i % C8) * 8;
+          const int64_t pix = tb + (int64_t)r * tg.panel_cols + c;
+          float ga[NT][8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ga[0][j] = g0[u][0][j];
+          if constexpr (NT > 1) load8<NT>(gfp, tg.npix, pix, cm_need<NT>(cbs[u]), ga, 1);
+          float o[8];
+          cm_out8<KIND, NT>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, pedp, tg.npix, pix, o);
+          cm_put8(tile + r * P + c, o);
+        }
+      }
+      cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out);
+    } else {
+      cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, pedp, gfp, tb, out, io, t.tile, t.panel, t.ar * R,
+                         t.ac * C);
+    }
+  };
+  if constexpr (kNet) {
+#pragma unroll
+    for (int fi = 0; fi < PR_CM_FPW; ++fi)   // straight-line frames (a loop hoists every address)
+      if (fi < nf) frame(fi);
   } else {
-    cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.tile, t.panel, t.ar * R, t.ac * C);
+    for (int fi = 0; fi < nf; ++fi) frame(fi);
   }
 }
 
@@ -1122,10 +1225,13 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   tg.asics_per_row = panel_cols / asic_cols;
   tg.npix = (int64_t)n_panels * panel_rows * panel_cols;
   tg.nframes = nframes;
+  // frames per workgroup: the epix10k2M production kernel takes PR_CM_FPW consecutive frames of
+  // its tile (next frame's raw words prefetched during the medians); everything else one
+  tg.fpw = (epix_prod && asic_cols == 48) ? PR_CM_FPW : 1;
   tg.side_slots = side_slots;
   tg.pitch = cm_pitch(asic_cols, kind == kJungfrau ? 2 : 1);
   const CmParams cp{thr, maxcorr, npix_min, flags, bank_cols};
-  const dim3 grid((unsigned)(n_panels * tg.asics_per_col * tg.asics_per_row * nframes));
+  const dim3 grid((unsigned)(n_panels * tg.asics_per_col * tg.asics_per_row * ((nframes + tg.fpw - 1) / tg.fpw)));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float* P = reinterpret_cast<const float*>(ped);
   const float* G = reinterpret_cast<const float*>(gf);
