@@ -51,8 +51,11 @@
 #ifndef PR_CM_FPW
 #define PR_CM_FPW 1
 #endif
+#ifndef PR_CM_GPRE
+#define PR_CM_GPRE 0
+#endif
 #ifndef PR_CM_EPIX_WG_PER_CU
-#define PR_CM_EPIX_WG_PER_CU (PR_CM_FPW > 1 ? 3 : 4)
+#define PR_CM_EPIX_WG_PER_CU ((PR_CM_FPW > 1 || PR_CM_GPRE) ? 3 : 4)
 #endif
 
 namespace pr {
@@ -1075,6 +1078,18 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
     } else {
       cm_phase1<KIND, NT>(tile, sc, P, R, C, tg, raw, pedp, plp, tb);
     }
+    // PR_CM_GPRE: the first gain table of every item is loaded now and arrives during the medians,
+    // so the store phase has no memory round trip before its first output (+40 VGPRs)
+    float g0[kNet ? NI : 1][1][8];
+    if constexpr (kNet && PR_CM_GPRE) {
+      constexpr int C8 = TC / 8;
+#pragma unroll
+      for (int u = 0; u < NI; ++u) {
+        const int i = tid + u * BLOCK;
+        if ((u + 1) * BLOCK <= NITEMS || i < NITEMS)
+          load8<1>(gfp, tg.npix, tb + (int64_t)(i / C8) * tg.panel_cols + (i % C8) * 8, 1u, g0[u]);
+      }
+    }
     __syncthreads();
 
     // ---- phase 2a: rows by bank, one lane per segment ------------------------------------
@@ -1096,14 +1111,13 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
       // (the first gain table of every item up front; the switched-gain tables are rare and are
       // loaded per item, which keeps the production kernel within 128 VGPRs)
       uint32_t cbs[NI], slots[NI];
-      float g0[NI][1][8];
 #pragma unroll
       for (int u = 0; u < NI; ++u) {
         const int i = tid + u * BLOCK;
         if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
           const int r = i / C8, k = i % C8, c = k * 8;
           cm_get_meta<NT>(reinterpret_cast<const uint8_t*>(tile + r * P + C), C, k, cbs[u], slots[u]);
-          load8<1>(gfp, tg.npix, tb + (int64_t)r * tg.panel_cols + c, 1u, g0[u]);
+          if constexpr (!PR_CM_GPRE) load8<1>(gfp, tg.npix, tb + (int64_t)r * tg.panel_cols + c, 1u, g0[u]);
         }
       }
 #pragma unroll
