@@ -60,6 +60,8 @@ def parse(argv=None):
                     help="frames per producer kernel launch / H2D copy (device-resident: 64 134.0-139.0k vs "
                          "32 132.0-134.5k vs 16 119.9k fr/s; host-staged 13.03k vs 12.90k; profiles/r2/pipeline_chunks.md)")
     ap.add_argument("--pool-frames", type=int, default=64)
+    ap.add_argument("--compute-streams", type=int, default=None,
+                    help="producer chunks alternate over this many HIP streams (default: config.COMPUTE_STREAMS)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--preroll-s", type=float, default=0.5,
                     help="untimed streaming before the warmup steps: the queue fills and the GPU clocks settle, so "
@@ -218,7 +220,8 @@ def main(argv=None):
         source = _DevSrc()
     else:
         source = src
-    prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk) if is_prod else None
+    cs_kw = {} if args.compute_streams is None else {"compute_streams": args.compute_streams}
+    prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk, **cs_kw) if is_prod else None
     consumer = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=args.batch) \
         if args.consumer == "peakfind" else None
 

@@ -436,6 +436,8 @@ PYBIND11_MODULE(_C, m) {
       .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"), py::arg("k0") = 0)
       .def("set_file_source", &pr::ProducerEngine::set_file_source, py::arg("reader"), py::keep_alive<1, 2>())
       .def("set_header_rank", &pr::ProducerEngine::set_header_rank, py::arg("rank"))
+      .def("set_compute_streams", &pr::ProducerEngine::set_compute_streams, py::arg("n"))
+      .def_property_readonly("compute_streams", &pr::ProducerEngine::compute_streams)
       .def("request_stop", &pr::ProducerEngine::request_stop)
       .def_property_readonly("device_resident", &pr::ProducerEngine::device_resident)
       .def("join", &pr::ProducerEngine::join, py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>())

@@ -90,6 +90,7 @@ ProducerEngine::ProducerEngine(SlotPool* pool, int64_t slot_bytes, int device,
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
   hip_check(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate");
+  cstreams_.push_back(compute_);
   const unsigned ev_flags = gpu_timing_ ? hipEventDefault : hipEventDisableTiming;
   buf_free_.resize(n_raw_bufs_);
   h2d_done_.resize(n_raw_bufs_);
@@ -119,7 +120,7 @@ ProducerEngine::~ProducerEngine() {
   if (thread_.joinable()) thread_.join();
   (void)hipSetDevice(device_);
   if (h2d_) (void)hipStreamSynchronize(h2d_);
-  if (compute_) (void)hipStreamSynchronize(compute_);
+  for (auto cs : cstreams_) (void)hipStreamSynchronize(cs);
   for (auto e : buf_free_) (void)hipEventDestroy(e);
   for (auto e : h2d_done_) (void)hipEventDestroy(e);
   for (auto e : h2d_start_) (void)hipEventDestroy(e);
@@ -129,7 +130,24 @@ ProducerEngine::~ProducerEngine() {
   if (raw_bufs_) (void)hipFree(raw_bufs_);
   if (file_staging_) (void)hipHostFree(file_staging_);
   if (h2d_) (void)hipStreamDestroy(h2d_);
-  if (compute_) (void)hipStreamDestroy(compute_);
+  for (auto cs : cstreams_) (void)hipStreamDestroy(cs);
+}
+
+void ProducerEngine::set_compute_streams(int n) {
+  check(!running_.load() && !thread_.joinable(), "ProducerEngine: set_compute_streams before start");
+  check(n >= 1 && n <= 4, "ProducerEngine: compute streams must be 1..4");
+  if (plan_.mode == kPlanImageScratch) n = 1;   // one scratch buffer: never two launches in flight
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  while ((int)cstreams_.size() > n) {
+    (void)hipStreamSynchronize(cstreams_.back());
+    (void)hipStreamDestroy(cstreams_.back());
+    cstreams_.pop_back();
+  }
+  while ((int)cstreams_.size() < n) {
+    hipStream_t s;
+    hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    cstreams_.push_back(s);
+  }
 }
 
 void ProducerEngine::set_cycled_source(const std::vector<uint64_t>& frames, const std::vector<double>& pe) {
@@ -226,8 +244,9 @@ std::vector<double> ProducerEngine::gpu_timing() const {
   return {gpu_h2d_ms_, (double)gpu_h2d_n_, gpu_calib_ms_, (double)gpu_calib_n_};
 }
 
-// Move completed chunks from the pending queue into the log (done_mu_ held).  Events complete in
-// stream order, so polling stops at the first chunk still running.
+// Move completed chunks from the pending queue into the log (done_mu_ held).  Polling stops at the
+// first chunk still running; with several compute streams a later chunk can finish first, so an
+// entry's time is when ALL frames up to it had completed (the max over the prefix).
 void ProducerEngine::note_chunk_done_locked() const {
   while (!done_pending_.empty()) {
     hipEvent_t e = done_pending_.front().first;
@@ -237,7 +256,8 @@ void ProducerEngine::note_chunk_done_locked() const {
     float ms = 0.f;
     hip_check(hipEventElapsedTime(&ms, origin_, e), "hipEventElapsedTime (chunk done)");
     done_frames_ = done_pending_.front().second;
-    done_log_.emplace_back(done_frames_, (double)ms);
+    done_ms_ = std::max(done_ms_, (double)ms);
+    done_log_.emplace_back(done_frames_, done_ms_);
     done_pending_.pop_front();
     done_free_.push_back(e);
   }
@@ -248,7 +268,7 @@ void ProducerEngine::note_chunk_done_locked() const {
   }
 }
 
-void ProducerEngine::record_chunk_done(int n) {
+void ProducerEngine::record_chunk_done(int n, hipStream_t s) {
   std::lock_guard<std::mutex> lk(done_mu_);
   note_chunk_done_locked();
   hipEvent_t e;
@@ -259,7 +279,7 @@ void ProducerEngine::record_chunk_done(int n) {
     hip_check(hipEventCreate(&e), "hipEventCreate (chunk done)");
     done_all_.push_back(e);
   }
-  hip_check(hipEventRecord(e, compute_), "record chunk done");
+  hip_check(hipEventRecord(e, s), "record chunk done");
   enq_frames_ += n;
   done_pending_.emplace_back(e, enq_frames_);
 }
@@ -313,7 +333,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
     // absolute rank-local event bound: [k0, limit)
     int64_t limit = n_local_events;
     if (max_steps >= 0 && (limit < 0 || k0 + max_steps < limit)) limit = k0 + max_steps;
-    const uint64_t stream_c = reinterpret_cast<uint64_t>(compute_);
+    const int n_cs = (int)cstreams_.size();
     std::vector<char> used(n_raw_bufs_, 0);
     std::vector<uint64_t> in, out;
     std::vector<int> slots;
@@ -436,6 +456,8 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
     }
     while (n > 0 && !stop_.load()) {
       const int b = (int)(chunk_no % n_raw_bufs_);
+      hipStream_t cs = cstreams_[(size_t)(chunk_no % n_cs)];
+      const uint64_t stream_c = reinterpret_cast<uint64_t>(cs);
       const int64_t k_next = k + n;
       const int n_next = chunk_len(k_next);
       trace::Range chunk_range("producer.chunk");
@@ -464,20 +486,20 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       if (device_resident_) {   // calibrate straight from the resident source frames
         for (int q = 0; q < n; ++q) in[q] = src_frames_[(size_t)((k + q) % (int64_t)nsrc)];
       } else {
-        hip_check(hipStreamWaitEvent(compute_, h2d_done_[b], 0), "wait h2d");
+        hip_check(hipStreamWaitEvent(cs, h2d_done_[b], 0), "wait h2d");
         for (int q = 0; q < n; ++q) in[q] = dev_in_[b][q];
       }
       for (int q = 0; q < n; ++q) out[q] = pool_->slot_ptr(slots[q]);
       if (gpu_timing_) {
         if (device_resident_) harvest(b, false);
-        hip_check(hipEventRecord(calib_start_[b], compute_), "record calib start");
+        hip_check(hipEventRecord(calib_start_[b], cs), "record calib start");
         calib_pending_[b] = 1;
       }
       {
         trace::Range r("producer.launch_calib");
         run_calib_plan(plan_, in, out, stream_c);
       }
-      if (!device_resident_ || gpu_timing_) hip_check(hipEventRecord(buf_free_[b], compute_), "record buf free");
+      if (!device_resident_ || gpu_timing_) hip_check(hipEventRecord(buf_free_[b], cs), "record buf free");
       auto t3 = clk::now();
       t_launch_ += secs(t2, t3);
       hdrs.resize(n);
@@ -493,14 +515,14 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
         }
       }
       pool_->commit_batch(slots, hdrs, stream_c);   // one ready event for the whole chunk
-      record_chunk_done(n);
+      record_chunk_done(n, cs);
       t_commit_ += secs(t3, clk::now());
       frames_.fetch_add(n);
       k = k_next;
       n = n_next;
       ++chunk_no;
     }
-    hip_check(hipStreamSynchronize(compute_), "final sync");
+    for (auto c : cstreams_) hip_check(hipStreamSynchronize(c), "final sync");
     hip_check(hipStreamSynchronize(h2d_), "final sync");
     {
       std::lock_guard<std::mutex> lk(done_mu_);

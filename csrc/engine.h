@@ -110,6 +110,11 @@ class ProducerEngine {
   // {span copies, single-frame copies, copies done by copy_h2d_kernel (the rest went through hipMemcpyAsync)}
   std::vector<int64_t> copy_stats() const { return {span_copies_.load(), frame_copies_.load(), kernel_copies_.load()}; }
   bool gpu_timing_enabled() const { return gpu_timing_; }
+  // Chunks alternate over n compute streams (before start; 1..4): chunk c+1's calibration starts
+  // filling the CUs while chunk c's last workgroups drain, instead of after them.  Plans with one
+  // shared scratch buffer (kPlanImageScratch) stay on one stream.
+  void set_compute_streams(int n);
+  int compute_streams() const { return (int)cstreams_.size(); }
 
  private:
   void loop(int64_t n_local_events, int64_t max_steps, int64_t k0);
@@ -127,7 +132,8 @@ class ProducerEngine {
   RawRunReader* file_ = nullptr;   // file source (instead of the cycled pool)
   void* file_staging_ = nullptr;   // pinned, n_raw_bufs x chunk frames
   std::vector<std::vector<std::pair<int64_t, double>>> buf_meta_;   // per raw buffer: (gevt, pe)
-  hipStream_t h2d_ = nullptr, compute_ = nullptr;
+  hipStream_t h2d_ = nullptr, compute_ = nullptr;   // compute_ == cstreams_[0]
+  std::vector<hipStream_t> cstreams_;
   std::vector<hipEvent_t> buf_free_, h2d_done_;
   // optional GPU timing: start events per raw buffer, harvested (non-blocking) when the buffer is
   // reused or at the end of the run
@@ -148,7 +154,7 @@ class ProducerEngine {
   std::atomic<int64_t> span_copies_{0}, frame_copies_{0}, kernel_copies_{0};
   // completion log (see completed()); done_mu_ guards everything below it
   void note_chunk_done_locked() const;
-  void record_chunk_done(int n);
+  void record_chunk_done(int n, hipStream_t s);
   mutable std::mutex done_mu_;
   hipEvent_t origin_ = nullptr;
   bool origin_recorded_ = false;
@@ -157,6 +163,7 @@ class ProducerEngine {
   mutable std::deque<std::pair<hipEvent_t, int64_t>> done_pending_;   // (event, cumulative frames)
   mutable std::vector<std::pair<int64_t, double>> done_log_;
   mutable int64_t done_base_ = 0, done_frames_ = 0;
+  mutable double done_ms_ = 0;   // the log's times are prefix-completion times (monotone)
   int64_t enq_frames_ = 0;
   std::thread thread_;
   std::atomic<bool> stop_{false}, running_{false};

@@ -38,6 +38,8 @@ CONSUMER_POLL_SLEEP_S = 1.0           # examples/psana_consumer.py:40
 # psana_ray/shared_queue.py:19-24).  One producer chunk (64 frames) keeps a copy in flight while the
 # previous one is read; DataReader.batches(n) raises it to 2 x n.
 DEFAULT_PREFETCH = 64
+# Producer chunks alternate over this many HIP compute streams (ProducerEngine.set_compute_streams)
+COMPUTE_STREAMS = 1
 
 # --- rendezvous ---------------------------------------------------------------------------
 DEFAULT_STORE_PORT = 6379             # the Ray head port of README.md:15, reused for the store

@@ -24,7 +24,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from .config import PeakFinderParams
+from .config import COMPUTE_STREAMS, PeakFinderParams
 from .models.calibrator import Calibrator
 from .ops import _ext, kernels
 from .queue.endpoint import EndOfStream, FrameItem, QueueEndpoint
@@ -36,9 +36,12 @@ log = logging.getLogger(__name__)
 class ProducerPipeline:
     def __init__(self, source, calibrator: Optional[Calibrator], endpoint: QueueEndpoint, rank: int = 0,
                  chunk: int = 32, n_raw_buffers: int = 6, acquire_timeout_s: float = 1.0,
-                 log_every: int = 0, copy_workgroups: int = 32, gpu_timing: bool = False):
+                 log_every: int = 0, copy_workgroups: int = 32, gpu_timing: bool = False,
+                 compute_streams: int = COMPUTE_STREAMS):
         """copy_workgroups: host->HBM staging by copy_h2d_kernel with that many workgroups (0 = the
-        runtime's hipMemcpyAsync); gpu_timing: event-time each chunk's copy and calibration."""
+        runtime's hipMemcpyAsync); gpu_timing: event-time each chunk's copy and calibration;
+        compute_streams: chunks alternate over that many HIP streams (native engine), so one chunk's
+        calibration fills the CUs its predecessor's tail leaves idle."""
         self.source = source
         self.cal = calibrator
         self.ep = endpoint
@@ -89,6 +92,7 @@ class ProducerPipeline:
                                            int(getattr(source, "size", 1)),
                                            copy_workgroups=int(copy_workgroups), gpu_timing=bool(gpu_timing))
             self.engine.set_header_rank(int(rank))
+            self.engine.set_compute_streams(int(compute_streams))
             if zero_copy is not None:
                 ptrs, pe = zero_copy
                 self._source_map = source._map       # keep the registered mapping alive

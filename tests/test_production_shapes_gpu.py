@@ -56,21 +56,25 @@ def test_common_mode_production_launch_bitwise(cuda_device, mode, nframes):
         del ref
 
 
-def test_pipeline_exact_at_production_chunk(cuda_device):
+@pytest.mark.parametrize("chunk,streams", [(64, None), (16, 3), (64, 1)])
+def test_pipeline_exact_at_production_chunk(cuda_device, chunk, streams):
     """The producer engine at its shipped chunk (64) with bench.py's default ring sizes: every frame
-    of 200 events bit-exact, FIFO, with the sustained-rate completion log covering all of them."""
+    of 200 events bit-exact, FIFO, with the sustained-rate completion log covering all of them --
+    with the shipped compute streams, chunks spread over 3 streams, and one stream."""
+    from psana_ray_amd.config import COMPUTE_STREAMS
     from psana_ray_amd.pipeline import ProducerPipeline
     from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
     from psana_ray_amd.source import SyntheticRun
 
-    n_events, chunk, batch = 200, 64, 32
+    n_events, batch = 200, 32
     src = SyntheticRun("synthetic", 5, "epix10k2M", n_events=n_events, pool_frames=8, pinned=True,
                        gen_device="cuda")
     cal = Calibrator(src.consts, cuda_device, Mode.calib, common_mode=CommonModeParams())
     ring = FrameRing(cal.out_shape, cal.out_dtype, cuda_device, 4 * chunk + batch, 400)
     ep = QueueEndpoint(ring)
-    prod = ProducerPipeline(src, cal, ep, chunk=chunk)
-    assert prod.chunk == 64 and prod.engine is not None
+    prod = ProducerPipeline(src, cal, ep, chunk=chunk, compute_streams=streams or COMPUTE_STREAMS)
+    assert prod.chunk == chunk and prod.engine is not None
+    assert prod.engine.compute_streams == (streams or COMPUTE_STREAMS)
     t = threading.Thread(target=prod.run)
     t.start()
     ref = reference.calibrate_reference(torch.from_numpy(src.pool.astype(np.int32)).to(cuda_device), src.consts, None,
