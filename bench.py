@@ -62,6 +62,8 @@ def parse(argv=None):
     ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--compute-streams", type=int, default=None,
                     help="producer chunks alternate over this many HIP streams (default: config.COMPUTE_STREAMS)")
+    ap.add_argument("--stream-kind", default=None, choices=["shared", "dedicated", "high"],
+                    help="hardware-queue placement of the producer / consumer streams (default: config.STREAM_KIND)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--preroll-s", type=float, default=0.5,
                     help="untimed streaming before the warmup steps: the queue fills and the GPU clocks settle, so "
@@ -221,8 +223,10 @@ def main(argv=None):
     else:
         source = src
     cs_kw = {} if args.compute_streams is None else {"compute_streams": args.compute_streams}
+    sk_kw = {} if args.stream_kind is None else {"stream_kind": args.stream_kind}
+    cs_kw.update(sk_kw)
     prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk, **cs_kw) if is_prod else None
-    consumer = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=args.batch) \
+    consumer = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=args.batch, **sk_kw) \
         if args.consumer == "peakfind" else None
 
     stop = threading.Event()

@@ -15,6 +15,7 @@ namespace py = pybind11;
 #include "engine.h"
 #include "fabric.h"
 #include "kernels.h"
+#include "streams.h"
 #include "trace.h"
 #include "xtc2.h"
 
@@ -216,6 +217,14 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- elastic queue fabric (fabric.h)
   m.def("pid_alive", &pr::pid_alive, py::arg("pid"));
+  // streams with a chosen hardware-queue placement (streams.h); torch wraps them as ExternalStream
+  m.def("stream_create", [](int device, int kind) { return reinterpret_cast<uint64_t>(pr::make_stream(device, kind)); },
+        py::arg("device"), py::arg("kind"));
+  m.def("stream_destroy", [](int device, uint64_t s) {
+        (void)hipSetDevice(device);
+        (void)hipStreamSynchronize(reinterpret_cast<hipStream_t>(s));
+        (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(s));
+      }, py::arg("device"), py::arg("stream"), py::call_guard<py::gil_scoped_release>());
   m.def("shm_remove", &pr::shm_remove, py::arg("name"));
   py::class_<pr::ShmRegion>(m, "ShmRegion", py::buffer_protocol())
       .def(py::init<const std::string&, int64_t, bool, double>(), py::arg("name"), py::arg("bytes"),
@@ -436,7 +445,7 @@ PYBIND11_MODULE(_C, m) {
       .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"), py::arg("k0") = 0)
       .def("set_file_source", &pr::ProducerEngine::set_file_source, py::arg("reader"), py::keep_alive<1, 2>())
       .def("set_header_rank", &pr::ProducerEngine::set_header_rank, py::arg("rank"))
-      .def("set_compute_streams", &pr::ProducerEngine::set_compute_streams, py::arg("n"))
+      .def("set_compute_streams", &pr::ProducerEngine::set_compute_streams, py::arg("n"), py::arg("kind") = 0)
       .def_property_readonly("compute_streams", &pr::ProducerEngine::compute_streams)
       .def("request_stop", &pr::ProducerEngine::request_stop)
       .def_property_readonly("device_resident", &pr::ProducerEngine::device_resident)

@@ -6,6 +6,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "streams.h"
 
 namespace pr {
 
@@ -133,21 +134,22 @@ ProducerEngine::~ProducerEngine() {
   for (auto cs : cstreams_) (void)hipStreamDestroy(cs);
 }
 
-void ProducerEngine::set_compute_streams(int n) {
+void ProducerEngine::set_compute_streams(int n, int kind) {
   check(!running_.load() && !thread_.joinable(), "ProducerEngine: set_compute_streams before start");
   check(n >= 1 && n <= 4, "ProducerEngine: compute streams must be 1..4");
+  {
+    std::lock_guard<std::mutex> lk(done_mu_);
+    check(!origin_recorded_, "ProducerEngine: set_compute_streams after the first start");
+  }
   if (plan_.mode == kPlanImageScratch) n = 1;   // one scratch buffer: never two launches in flight
   hip_check(hipSetDevice(device_), "hipSetDevice");
-  while ((int)cstreams_.size() > n) {
-    (void)hipStreamSynchronize(cstreams_.back());
-    (void)hipStreamDestroy(cstreams_.back());
-    cstreams_.pop_back();
+  for (auto cs : cstreams_) {
+    (void)hipStreamSynchronize(cs);
+    (void)hipStreamDestroy(cs);
   }
-  while ((int)cstreams_.size() < n) {
-    hipStream_t s;
-    hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
-    cstreams_.push_back(s);
-  }
+  cstreams_.clear();
+  for (int i = 0; i < n; ++i) cstreams_.push_back(make_stream(device_, kind));
+  compute_ = cstreams_[0];
 }
 
 void ProducerEngine::set_cycled_source(const std::vector<uint64_t>& frames, const std::vector<double>& pe) {

@@ -113,7 +113,9 @@ class ProducerEngine {
   // Chunks alternate over n compute streams (before start; 1..4): chunk c+1's calibration starts
   // filling the CUs while chunk c's last workgroups drain, instead of after them.  Plans with one
   // shared scratch buffer (kPlanImageScratch) stay on one stream.
-  void set_compute_streams(int n);
+  // kind: StreamKind (streams.h) -- kStreamDedicated gives every compute stream its own hardware
+  // queue.
+  void set_compute_streams(int n, int kind = 0);
   int compute_streams() const { return (int)cstreams_.size(); }
 
  private:

@@ -97,6 +97,11 @@ SlotPool::EvRef SlotPool::record_shared_locked(uint64_t stream) {
 
 void SlotPool::wait_ref(const EvRef& r, uint64_t stream) const {
   if (device_ < 0 || r.idx < 0) return;
+  // an event that already completed needs no barrier packet: every packet between two producer
+  // chunks on the compute queue delays the next chunk's dispatch (tools/gap_probe.py)
+  const hipError_t q = hipEventQuery(ev_[r.idx]);
+  if (q == hipSuccess) return;
+  if (q != hipErrorNotReady) hip_check(q, "hipEventQuery (wait)");
   hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ev_[r.idx], 0), "hipStreamWaitEvent");
 }
 

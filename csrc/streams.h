@@ -1,0 +1,20 @@
+// HIP streams with a chosen hardware-queue placement.
+//
+// A process gets GPU_MAX_HW_QUEUES hardware queues per device (4 on the MI355X boxes; HIP's
+// default) and HIP multiplexes every ordinary stream onto them: two streams that land on the same
+// queue execute one after the other, whatever their events say.  Measured in the device-resident
+// pipeline (tools/gpu_r3_streams_trace.sh, rocprofv3 Queue_Id): the consumer's two peak-finder
+// streams shared one queue, and with two producer streams the peak finder shared the producers'
+// queues -- launches meant to overlap were serialised.  A stream created with a CU mask owns its
+// hardware queue (the mask is a queue property); an all-CUs mask restricts nothing.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pr {
+
+enum StreamKind { kStreamShared = 0, kStreamDedicated = 1, kStreamHighPriority = 2 };
+hipStream_t make_stream(int device, int kind);
+
+}  // namespace pr

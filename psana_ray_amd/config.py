@@ -40,6 +40,11 @@ CONSUMER_POLL_SLEEP_S = 1.0           # examples/psana_consumer.py:40
 DEFAULT_PREFETCH = 64
 # Producer chunks alternate over this many HIP compute streams (ProducerEngine.set_compute_streams)
 COMPUTE_STREAMS = 1
+# Hardware-queue placement of the pipeline's own streams (producer compute, consumer peak finder):
+# "shared" = ordinary HIP streams multiplexed onto the process's hardware queues, "dedicated" = one
+# hardware queue per stream (csrc/streams.h), "high" = high-priority streams
+STREAM_KINDS = {"shared": 0, "dedicated": 1, "high": 2}
+STREAM_KIND = "shared"
 
 # --- rendezvous ---------------------------------------------------------------------------
 DEFAULT_STORE_PORT = 6379             # the Ray head port of README.md:15, reused for the store

@@ -24,7 +24,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from .config import COMPUTE_STREAMS, PeakFinderParams
+from .config import COMPUTE_STREAMS, STREAM_KIND, STREAM_KINDS, PeakFinderParams
 from .models.calibrator import Calibrator
 from .ops import _ext, kernels
 from .queue.endpoint import EndOfStream, FrameItem, QueueEndpoint
@@ -37,11 +37,12 @@ class ProducerPipeline:
     def __init__(self, source, calibrator: Optional[Calibrator], endpoint: QueueEndpoint, rank: int = 0,
                  chunk: int = 32, n_raw_buffers: int = 6, acquire_timeout_s: float = 1.0,
                  log_every: int = 0, copy_workgroups: int = 32, gpu_timing: bool = False,
-                 compute_streams: int = COMPUTE_STREAMS):
+                 compute_streams: int = COMPUTE_STREAMS, stream_kind: str = STREAM_KIND):
         """copy_workgroups: host->HBM staging by copy_h2d_kernel with that many workgroups (0 = the
         runtime's hipMemcpyAsync); gpu_timing: event-time each chunk's copy and calibration;
         compute_streams: chunks alternate over that many HIP streams (native engine), so one chunk's
-        calibration fills the CUs its predecessor's tail leaves idle."""
+        calibration fills the CUs its predecessor's tail leaves idle; stream_kind: their
+        hardware-queue placement (config.STREAM_KINDS)."""
         self.source = source
         self.cal = calibrator
         self.ep = endpoint
@@ -92,7 +93,7 @@ class ProducerPipeline:
                                            int(getattr(source, "size", 1)),
                                            copy_workgroups=int(copy_workgroups), gpu_timing=bool(gpu_timing))
             self.engine.set_header_rank(int(rank))
-            self.engine.set_compute_streams(int(compute_streams))
+            self.engine.set_compute_streams(int(compute_streams), STREAM_KINDS[stream_kind])
             if zero_copy is not None:
                 ptrs, pe = zero_copy
                 self._source_map = source._map       # keep the registered mapping alive
@@ -273,6 +274,24 @@ class ProducerPipeline:
         return self.frames
 
 
+def _make_streams(device, n: int, kind: str):
+    """n torch streams with the given hardware-queue placement (config.STREAM_KINDS); native
+    streams are destroyed when the last wrapper is collected."""
+    if STREAM_KINDS[kind] == 0:
+        return [torch.cuda.Stream(device=device) for _ in range(n)]
+    import weakref
+
+    C = _ext.load()
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    out = []
+    for _ in range(n):
+        h = int(C.stream_create(dev, STREAM_KINDS[kind]))
+        st = torch.cuda.ExternalStream(h, device=device)
+        weakref.finalize(st, C.stream_destroy, dev, h)
+        out.append(st)
+    return out
+
+
 class PeakFinderConsumer:
     """Consumer engine: batches of leased slots -> K-07 peak finder -> stream-ordered release.
 
@@ -281,7 +300,7 @@ class PeakFinderConsumer:
     its stream of reads) overlaps the next launch's streaming reads instead of idling HBM."""
 
     def __init__(self, endpoint: QueueEndpoint, frame_shape, params: Optional[PeakFinderParams] = None,
-                 batch: int = 16, keep_results: bool = False):
+                 batch: int = 16, keep_results: bool = False, stream_kind: str = STREAM_KIND):
         self.ep = endpoint
         self.params = params or PeakFinderParams()
         self.batch = min(batch, kernels.MAX_FRAMES)
@@ -293,7 +312,7 @@ class PeakFinderConsumer:
         self.keep_results = keep_results
         self.results = []
         if self.gpu:
-            self.streams = [torch.cuda.Stream(device=self.device) for _ in range(2)]
+            self.streams = _make_streams(self.device, 2, stream_kind)
             self.stream = self.streams[0]
             B = self.batch
             self._nbuf = 4   # even: buffer k % 4 is reused by launch k + 4, on the same stream as k
