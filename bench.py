@@ -61,9 +61,11 @@ def parse(argv=None):
                          "32 132.0-134.5k vs 16 119.9k fr/s; host-staged 13.03k vs 12.90k; profiles/r2/pipeline_chunks.md)")
     ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--compute-streams", type=int, default=None,
-                    help="producer chunks alternate over this many HIP streams (default: config.COMPUTE_STREAMS)")
+                    help="producer chunks alternate over this many HIP streams (default: config.PRODUCER_STREAMS)")
     ap.add_argument("--stream-kind", default=None, choices=["shared", "dedicated", "high"],
-                    help="hardware-queue placement of the producer / consumer streams (default: config.STREAM_KIND)")
+                    help="hardware-queue placement of the producer streams (default: config.PRODUCER_STREAM_KIND)")
+    ap.add_argument("--consumer-stream-kind", default=None, choices=["shared", "dedicated", "high"],
+                    help="placement of the peak finder's streams (default: config.CONSUMER_STREAM_KIND)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--preroll-s", type=float, default=0.5,
                     help="untimed streaming before the warmup steps: the queue fills and the GPU clocks settle, so "
@@ -113,7 +115,7 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
-    from psana_ray_amd.config import CommonModeParams, PeakFinderParams
+    from psana_ray_amd.config import CONSUMER_STREAM_KIND, CommonModeParams, PeakFinderParams
     from psana_ray_amd.models import Calibrator, Mode
     from psana_ray_amd.parallel.launch import bind_numa_to_device, detect
     from psana_ray_amd.pipeline import PeakFinderConsumer, ProducerPipeline
@@ -223,8 +225,9 @@ def main(argv=None):
     else:
         source = src
     cs_kw = {} if args.compute_streams is None else {"compute_streams": args.compute_streams}
-    sk_kw = {} if args.stream_kind is None else {"stream_kind": args.stream_kind}
-    cs_kw.update(sk_kw)
+    if args.stream_kind is not None:
+        cs_kw["stream_kind"] = args.stream_kind
+    sk_kw = {} if args.consumer_stream_kind is None else {"stream_kind": args.consumer_stream_kind}
     prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk, **cs_kw) if is_prod else None
     consumer = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=args.batch, **sk_kw) \
         if args.consumer == "peakfind" else None
@@ -440,6 +443,8 @@ def main(argv=None):
             "staging_copies_span_frame_kernel": copies,
             "numa_node": numa,
             "cpus_allowed": len(os.sched_getaffinity(0)),
+            "producer_streams": list(prod.stream_config) if prod is not None and prod.stream_config else None,
+            "consumer_stream_kind": args.consumer_stream_kind or CONSUMER_STREAM_KIND,
             "producer_host_s_stage_acquire_launch_commit_total": (
                 [round(x, 4) for x in prod.engine.timing()] if prod is not None and prod.engine is not None
                 else None),

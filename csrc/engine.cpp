@@ -150,6 +150,11 @@ void ProducerEngine::set_compute_streams(int n, int kind) {
   cstreams_.clear();
   for (int i = 0; i < n; ++i) cstreams_.push_back(make_stream(device_, kind));
   compute_ = cstreams_[0];
+  // the staging copies get the same placement: a copy stream multiplexed onto a queue that runs
+  // calibration or peak-finder kernels would wait behind them and idle the PCIe link
+  (void)hipStreamSynchronize(h2d_);
+  (void)hipStreamDestroy(h2d_);
+  h2d_ = make_stream(device_, kind);
 }
 
 void ProducerEngine::set_cycled_source(const std::vector<uint64_t>& frames, const std::vector<double>& pe) {

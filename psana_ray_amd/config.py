@@ -38,13 +38,22 @@ CONSUMER_POLL_SLEEP_S = 1.0           # examples/psana_consumer.py:40
 # psana_ray/shared_queue.py:19-24).  One producer chunk (64 frames) keeps a copy in flight while the
 # previous one is read; DataReader.batches(n) raises it to 2 x n.
 DEFAULT_PREFETCH = 64
-# Producer chunks alternate over this many HIP compute streams (ProducerEngine.set_compute_streams)
-COMPUTE_STREAMS = 1
-# Hardware-queue placement of the pipeline's own streams (producer compute, consumer peak finder):
-# "shared" = ordinary HIP streams multiplexed onto the process's hardware queues, "dedicated" = one
-# hardware queue per stream (csrc/streams.h), "high" = high-priority streams
+# Hardware-queue placement of the pipeline's own streams: "shared" = ordinary HIP streams,
+# multiplexed onto the process's GPU_MAX_HW_QUEUES hardware queues (two streams on one queue run
+# one after the other); "dedicated" = one hardware queue per stream (csrc/streams.h); "high" =
+# high-priority streams.
 STREAM_KINDS = {"shared": 0, "dedicated": 1, "high": 2}
-STREAM_KIND = "shared"
+# Producer: chunks alternate over this many compute streams.  Measured on MI355X (bench.py, 200
+# steps, profiles/r3/streams*/): raw frames already in HBM -> 3 dedicated streams (140.9-143.6k
+# fr/s vs 134.5-134.6k on one ordinary stream; image mode 110.4-115.5k vs 104.7-105.5k: one
+# chunk's calibration fills the CUs its predecessor's tail leaves, and the peak finder no longer
+# queues behind it); host-staged (PCIe-bound) -> one ordinary stream (13,064-13,069 vs
+# 12,852-12,858 with 3: concurrent calibrations delay the staging copy kernel).
+PRODUCER_STREAMS = {"device": 3, "staged": 1}
+PRODUCER_STREAM_KIND = {"device": "dedicated", "staged": "shared"}
+# Consumer: the peak finder's two alternating streams, each on its own hardware queue (ordinary
+# streams landed both on ONE queue: rocprofv3 Queue_Id, profiles/r3/streams2/)
+CONSUMER_STREAM_KIND = "dedicated"
 
 # --- rendezvous ---------------------------------------------------------------------------
 DEFAULT_STORE_PORT = 6379             # the Ray head port of README.md:15, reused for the store

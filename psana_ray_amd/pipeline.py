@@ -24,7 +24,8 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from .config import COMPUTE_STREAMS, STREAM_KIND, STREAM_KINDS, PeakFinderParams
+from .config import (CONSUMER_STREAM_KIND, PRODUCER_STREAM_KIND, PRODUCER_STREAMS, STREAM_KINDS,
+                     PeakFinderParams)
 from .models.calibrator import Calibrator
 from .ops import _ext, kernels
 from .queue.endpoint import EndOfStream, FrameItem, QueueEndpoint
@@ -37,12 +38,13 @@ class ProducerPipeline:
     def __init__(self, source, calibrator: Optional[Calibrator], endpoint: QueueEndpoint, rank: int = 0,
                  chunk: int = 32, n_raw_buffers: int = 6, acquire_timeout_s: float = 1.0,
                  log_every: int = 0, copy_workgroups: int = 32, gpu_timing: bool = False,
-                 compute_streams: int = COMPUTE_STREAMS, stream_kind: str = STREAM_KIND):
+                 compute_streams: Optional[int] = None, stream_kind: Optional[str] = None):
         """copy_workgroups: host->HBM staging by copy_h2d_kernel with that many workgroups (0 = the
         runtime's hipMemcpyAsync); gpu_timing: event-time each chunk's copy and calibration;
         compute_streams: chunks alternate over that many HIP streams (native engine), so one chunk's
         calibration fills the CUs its predecessor's tail leaves idle; stream_kind: their
-        hardware-queue placement (config.STREAM_KINDS)."""
+        hardware-queue placement (config.STREAM_KINDS).  None: config.PRODUCER_STREAMS /
+        PRODUCER_STREAM_KIND for the source (raw frames already in HBM or staged)."""
         self.source = source
         self.cal = calibrator
         self.ep = endpoint
@@ -80,6 +82,7 @@ class ProducerPipeline:
         self._inflight = collections.deque()
         self._reuses = hasattr(source, "n_staging")
         self.engine = None
+        self.stream_config = None   # (compute streams, kind) of the native engine
         if use_engine:
             # native hot loop: no Python (and no GIL) per frame or per chunk
             C = _ext.load()
@@ -93,7 +96,6 @@ class ProducerPipeline:
                                            int(getattr(source, "size", 1)),
                                            copy_workgroups=int(copy_workgroups), gpu_timing=bool(gpu_timing))
             self.engine.set_header_rank(int(rank))
-            self.engine.set_compute_streams(int(compute_streams), STREAM_KINDS[stream_kind])
             if zero_copy is not None:
                 ptrs, pe = zero_copy
                 self._source_map = source._map       # keep the registered mapping alive
@@ -104,6 +106,11 @@ class ProducerPipeline:
                 ptrs, pe = source.cycled_frames()
                 self.engine.set_cycled_source([int(x) for x in ptrs],
                                               [float("nan") if v is None else float(v) for v in pe])
+            where = "device" if self.engine.device_resident else "staged"
+            n_cs = PRODUCER_STREAMS[where] if compute_streams is None else int(compute_streams)
+            kind = PRODUCER_STREAM_KIND[where] if stream_kind is None else stream_kind
+            self.engine.set_compute_streams(n_cs, STREAM_KINDS[kind])
+            self.stream_config = (n_cs, kind)
 
     # --------------------------------------------------------------------------------
     def _acquire(self, n: int, stream) -> List[int]:
@@ -276,7 +283,7 @@ class ProducerPipeline:
 
 def _make_streams(device, n: int, kind: str):
     """n torch streams with the given hardware-queue placement (config.STREAM_KINDS); native
-    streams are destroyed when the last wrapper is collected."""
+    streams are destroyed when the last wrapper is collected (not at interpreter exit)."""
     if STREAM_KINDS[kind] == 0:
         return [torch.cuda.Stream(device=device) for _ in range(n)]
     import weakref
@@ -287,8 +294,9 @@ def _make_streams(device, n: int, kind: str):
     for _ in range(n):
         h = int(C.stream_create(dev, STREAM_KINDS[kind]))
         st = torch.cuda.ExternalStream(h, device=device)
-        weakref.finalize(st, C.stream_destroy, dev, h)
-        out.append(st)
+        fin = weakref.finalize(st, C.stream_destroy, dev, h)
+        fin.atexit = False   # at interpreter exit the HIP runtime may be torn down already; the
+        out.append(st)       # process exit releases the queue anyway
     return out
 
 
@@ -300,7 +308,7 @@ class PeakFinderConsumer:
     its stream of reads) overlaps the next launch's streaming reads instead of idling HBM."""
 
     def __init__(self, endpoint: QueueEndpoint, frame_shape, params: Optional[PeakFinderParams] = None,
-                 batch: int = 16, keep_results: bool = False, stream_kind: str = STREAM_KIND):
+                 batch: int = 16, keep_results: bool = False, stream_kind: str = CONSUMER_STREAM_KIND):
         self.ep = endpoint
         self.params = params or PeakFinderParams()
         self.batch = min(batch, kernels.MAX_FRAMES)

@@ -56,14 +56,17 @@ def test_local_pipeline_frames_exact(cuda_device, cm, copy_kernel):
     assert (by_kernel == span + single) if copy_kernel != 0 else by_kernel == 0
 
 
-def test_peakfinder_consumer_counts(cuda_device):
+@pytest.mark.parametrize("kind", ["shared", "dedicated"])
+def test_peakfinder_consumer_counts(cuda_device, kind):
+    """Peak totals of a producer -> consumer run equal the golden model's, with ordinary streams
+    and with streams that own their hardware queues (producer and consumer sides)."""
     src = SyntheticRun("synthetic", 4, "epix10k2M", n_events=40, pool_frames=4, pinned=True, gen_device="cuda")
     cal = Calibrator(src.consts, cuda_device, Mode.calib)
     ring = FrameRing(cal.out_shape, cal.out_dtype, cuda_device, 16, 32)
     ep = QueueEndpoint(ring)
-    prod = ProducerPipeline(src, cal, ep, chunk=16)
+    prod = ProducerPipeline(src, cal, ep, chunk=16, compute_streams=2, stream_kind=kind)
     params = PeakFinderParams()
-    cons = PeakFinderConsumer(ep, cal.out_shape, params, batch=16)
+    cons = PeakFinderConsumer(ep, cal.out_shape, params, batch=16, stream_kind=kind)
     t = threading.Thread(target=prod.run)
     t.start()
     n = 0

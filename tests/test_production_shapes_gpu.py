@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from psana_ray_amd.config import CommonModeParams, PeakFinderParams
+from psana_ray_amd.config import PRODUCER_STREAM_KIND, PRODUCER_STREAMS, CommonModeParams, PeakFinderParams
 from psana_ray_amd.models import CalibConstants, Calibrator, Mode, get_detector
 from psana_ray_amd.ops import kernels, reference
 from psana_ray_amd.source import generate_raw
@@ -56,12 +56,13 @@ def test_common_mode_production_launch_bitwise(cuda_device, mode, nframes):
         del ref
 
 
-@pytest.mark.parametrize("chunk,streams", [(64, None), (16, 3), (64, 1)])
-def test_pipeline_exact_at_production_chunk(cuda_device, chunk, streams):
+@pytest.mark.parametrize("chunk,streams,kind", [(64, None, None), (16, 3, "dedicated"), (64, 1, "shared"),
+                                               (32, 2, "high")])
+def test_pipeline_exact_at_production_chunk(cuda_device, chunk, streams, kind):
     """The producer engine at its shipped chunk (64) with bench.py's default ring sizes: every frame
     of 200 events bit-exact, FIFO, with the sustained-rate completion log covering all of them --
-    with the shipped compute streams, chunks spread over 3 streams, and one stream."""
-    from psana_ray_amd.config import COMPUTE_STREAMS
+    with the shipped compute streams, chunks spread over 3 streams with their own hardware queues,
+    one ordinary stream, and two high-priority streams."""
     from psana_ray_amd.pipeline import ProducerPipeline
     from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
     from psana_ray_amd.source import SyntheticRun
@@ -72,9 +73,10 @@ def test_pipeline_exact_at_production_chunk(cuda_device, chunk, streams):
     cal = Calibrator(src.consts, cuda_device, Mode.calib, common_mode=CommonModeParams())
     ring = FrameRing(cal.out_shape, cal.out_dtype, cuda_device, 4 * chunk + batch, 400)
     ep = QueueEndpoint(ring)
-    prod = ProducerPipeline(src, cal, ep, chunk=chunk, compute_streams=streams or COMPUTE_STREAMS)
+    prod = ProducerPipeline(src, cal, ep, chunk=chunk, compute_streams=streams, stream_kind=kind)
     assert prod.chunk == chunk and prod.engine is not None
-    assert prod.engine.compute_streams == (streams or COMPUTE_STREAMS)
+    assert prod.engine.compute_streams == (streams or PRODUCER_STREAMS["staged"])
+    assert prod.stream_config == (streams or PRODUCER_STREAMS["staged"], kind or PRODUCER_STREAM_KIND["staged"])
     t = threading.Thread(target=prod.run)
     t.start()
     ref = reference.calibrate_reference(torch.from_numpy(src.pool.astype(np.int32)).to(cuda_device), src.consts, None,

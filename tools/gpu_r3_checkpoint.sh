@@ -4,7 +4,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 export PYTHONPATH=$R
-O=$R/gpurun_out/r3_ckpt
+O=$R/gpurun_out/${CKPT:-r3_ckpt}
 mkdir -p $O
 timeout -k 10 900 python3 -u -m pytest $R/tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -1 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 cd $R && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit $?
