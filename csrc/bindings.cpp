@@ -155,6 +155,7 @@ PYBIND11_MODULE(_C, m) {
         },
         "bandwidth reference: read-only f32 frame sweep (what the peak finder's input read can reach)");
   m.def("xor_lane_selftest", &pr::launch_xor_selftest, py::arg("out"), py::arg("stream"));
+  m.def("cm_set_stamp_buffer", &pr::cm_set_stamp_buffer, py::arg("ptr"));
   m.def("assemble",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t idx, int64_t nout,
            uint64_t omask, uint64_t stream) {

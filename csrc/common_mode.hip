@@ -60,6 +60,31 @@
 
 namespace pr {
 
+// ---- phase stamps (diagnostic build only: -DPR_CM_STAMPS=1, tools/cm_stamps.py) ----------------
+// Every wave of the epix10k2M production kernel records the shader clock at its phase boundaries
+// (before and after each barrier) and the 100-MHz real-time clock at entry and exit; lane 0 writes
+// them with ONE vector store per value at the end.  Record per wave (16 x u64):
+//   [0] realtime entry  [1] realtime exit  [2] HW_ID  [3] XCC_ID  [4..15] shader-clock stamps
+constexpr int kCmStampWords = 16;
+#ifndef PR_CM_STAMPS
+#define PR_CM_STAMPS 0
+#endif
+#if PR_CM_STAMPS
+__device__ uint64_t* g_cm_stamps = nullptr;
+#define PR_STAMP(k) st_[(k)] = __builtin_amdgcn_s_memtime()
+#else
+#define PR_STAMP(k) ((void)0)
+#endif
+void cm_set_stamp_buffer(uint64_t p) {
+#if PR_CM_STAMPS
+  uint64_t* q = reinterpret_cast<uint64_t*>(p);
+  hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_cm_stamps), &q, sizeof(q)), "cm stamps");
+#else
+  (void)p;
+  check(false, "cm_set_stamp_buffer: this build has no phase stamps (-DPR_CM_STAMPS=1)");
+#endif
+}
+
 // ---- lane exchange: y = x from lane (lane ^ J), VALU-only (no LDS-pipe round trip) ----
 //  J = 1, 2 : one DPP quad_perm
 //  J = 4, 8 : DPP row_shl:J / row_shr:J (16-lane rows) + lane select
@@ -1051,6 +1076,11 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
   // shapes prefetch frame k+1's raw words during frame k's medians)
   const int nf = min(tg.fpw, tg.nframes - t.f);
   uint4 rw[kNet ? NI : 1];
+#if PR_CM_STAMPS
+  uint64_t st_[12] = {};
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+  PR_STAMP(0);
+#endif
   auto frame = [&](const int fi) {
     const int f = t.f + fi;
     const PR_GLOBAL uint16_t* raw = gin<uint16_t>(fp.in[f]);
@@ -1078,6 +1108,7 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
     } else {
       cm_phase1<KIND, NT>(tile, sc, P, R, C, tg, raw, pedp, plp, tb);
     }
+    PR_STAMP(1);
     // PR_CM_GPRE: the first gain table of every item is loaded now and arrives during the medians,
     // so the store phase has no memory round trip before its first output (+40 VGPRs)
     float g0[kNet ? NI : 1][1][8];
@@ -1091,17 +1122,22 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
       }
     }
     __syncthreads();
+    PR_STAMP(2);
 
     // ---- phase 2a: rows by bank, one lane per segment ------------------------------------
     if (cp.flags & 1) {
       cm_rows<L>(tile, P, R, C, cp, tid, blockDim.x);
+      PR_STAMP(3);
       __syncthreads();
+      PR_STAMP(4);
     }
 
     // ---- phase 2b: columns -----------------------------------------------------------------
     if (cp.flags & 2) {
       cm_cols<M>(tile, P, R, C, cp, tid, blockDim.x);
+      PR_STAMP(5);
       __syncthreads();
+      PR_STAMP(6);
     }
 
     // ---- phase 3: gain factor + mask, store ----------------------------------------------
@@ -1135,7 +1171,9 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
           cm_put8(tile + r * P + c, o);
         }
       }
+      PR_STAMP(7);
       cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out);
+      PR_STAMP(8);
     } else {
       cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, pedp, gfp, tb, out, io, t.tile, t.panel, t.ar * R,
                          t.ac * C);
@@ -1148,6 +1186,18 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
   } else {
     for (int fi = 0; fi < nf; ++fi) frame(fi);
   }
+#if PR_CM_STAMPS
+  if (kNet && g_cm_stamps != nullptr && (threadIdx.x & 63) == 0) {
+    // stores of wave-uniform values: plain global stores from VGPRs
+    uint64_t* rec = g_cm_stamps + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kCmStampWords;
+    rec[0] = rt0;
+    rec[1] = __builtin_amdgcn_s_memrealtime();
+    rec[2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+    rec[3] = (uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));   // HW_REG_XCC_ID
+#pragma unroll
+    for (int k = 0; k < 12; ++k) rec[4 + k] = st_[k];
+  }
+#endif
 }
 
 size_t cm_lds_bytes(int asic_rows, int asic_cols, int kind) {

@@ -27,6 +27,8 @@ int cm_tile_cols(int asic_rows, int asic_cols, int bank_cols, int max_cols, int 
 void launch_convert_u16_f32(const FramePtrs& fp, int nframes, int64_t npix, uint64_t stream);
 void launch_read_f32(const FramePtrs& fp, int nframes, int64_t npix, int k, bool nt, uint64_t sums, uint64_t stream);
 void launch_xor_selftest(uint64_t out, uint64_t stream);
+// diagnostic builds only (-DPR_CM_STAMPS=1): per-wave phase stamps of the epix10k2M CM kernel
+void cm_set_stamp_buffer(uint64_t p);
 void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_runs, uint64_t stream);
 void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool bf16, uint64_t stream);
 // host (pinned / registered) -> HBM copy by a kernel; false = not applicable, use hipMemcpyAsync
