@@ -14,6 +14,7 @@ namespace py = pybind11;
 
 #include "engine.h"
 #include "fabric.h"
+#include "lifecycle.h"
 #include "kernels.h"
 #include "streams.h"
 #include "trace.h"
@@ -218,6 +219,8 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- elastic queue fabric (fabric.h)
   m.def("pid_alive", &pr::pid_alive, py::arg("pid"));
+  // stop and join every fabric / engine thread still running (registered with atexit by the loader)
+  m.def("halt_native_threads", &pr::halt_native_threads, py::call_guard<py::gil_scoped_release>());
   // streams with a chosen hardware-queue placement (streams.h); torch wraps them as ExternalStream
   m.def("stream_create", [](int device, int kind) { return reinterpret_cast<uint64_t>(pr::make_stream(device, kind)); },
         py::arg("device"), py::arg("kind"));

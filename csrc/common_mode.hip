@@ -54,6 +54,12 @@
 #ifndef PR_CM_GPRE
 #define PR_CM_GPRE 0
 #endif
+// Raw-word loads of the compile-time (production) kernels: 1 = non-temporal (stream cache policy),
+// 0 = plain.  (The read-ceiling probe at four workgroups per CU read 5.00 TB/s non-temporal vs 6.03
+// plain, profiles/r2/pf/read_ceiling.md.)
+#ifndef PR_CM_RAW_NT
+#define PR_CM_RAW_NT 1
+#endif
 #ifndef PR_CM_EPIX_WG_PER_CU
 #define PR_CM_EPIX_WG_PER_CU ((PR_CM_FPW > 1 || PR_CM_GPRE) ? 3 : 4)
 #endif
@@ -572,12 +578,19 @@ __device__ __forceinline__ void cm_put8(float* trow, const float (&o)[8]) {
   *reinterpret_cast<float4*>(trow + 4) = make_float4(o[4], o[5], o[6], o[7]);
 }
 
+struct NoMark {
+  __device__ void operator()(int) const {}
+};
+// mark(k): phase-stamp hook of the diagnostic build (k = 9 after the barrier, 10 after placement)
+template <typename Mark = NoMark>
 __device__ __forceinline__ void cm_write_out(const float* tile, int P, int R, int C, const TileGeom& tg,
                                              const ImgOut& io, int tile_id, int panel, int y0, int x0, int64_t base,
-                                             PR_GLOBAL float* out) {
+                                             PR_GLOBAL float* out, const Mark& mark = Mark()) {
   __syncthreads();
+  mark(9);
   if (io.desc != nullptr) {
     cm_place(tile, P, R, C, io, panel, y0, x0, out);
+    mark(10);
     cm_fill_gaps(io, tile_id, (int)gridDim.x / ((tg.nframes + tg.fpw - 1) / tg.fpw), out);
   } else {
     cm_flush(tile, P, R, C, out, base, tg.panel_cols);
@@ -829,6 +842,15 @@ __device__ __forceinline__ void bitonic_merge_vpad(float (&z)[N]) {
   }
 }
 
+__device__ __forceinline__ uint4 ld_raw_u4(const PR_GLOBAL uint4* p) {
+#if PR_CM_RAW_NT
+  return ld_nt_u4(p);
+#else
+  const u32x4_t v = *(const PR_GLOBAL u32x4_t*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+#endif
+}
+
 // TR / TC: the tile rows / columns as compile-time constants for the production shapes (0 = from
 // TileGeom): every LDS address in the unrolled loops is then a base VGPR + immediate offset.
 // Phase 1, compile-time tile shape: decode + pedestal of the tile into LDS by BLOCK threads
@@ -855,7 +877,7 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
     if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
       const int r = i / C8, c = (i % C8) * 8;
       const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
-      if constexpr (!RAW_IN) rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
+      if constexpr (!RAW_IN) rw[u] = ld_raw_u4((const PR_GLOBAL uint4*)(raw + pix));
       ep[u] = load_planes<NT>(planes, pix);
       load8<1>(ped, tg.npix, pix, 1u, pa0[u]);
     }
@@ -891,7 +913,7 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
       const int i = tid + u * BLOCK;
       if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
         const int r = i / C8, c = (i % C8) * 8;
-        rw[u] = ld_nt_u4((const PR_GLOBAL uint4*)(raw_next + base + (int64_t)r * tg.panel_cols + c));
+        rw[u] = ld_raw_u4((const PR_GLOBAL uint4*)(raw_next + base + (int64_t)r * tg.panel_cols + c));
       }
     }
   }
@@ -1172,7 +1194,12 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
         }
       }
       PR_STAMP(7);
+#if PR_CM_STAMPS
+      cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out,
+                   [&](int k) { st_[k] = __builtin_amdgcn_s_memtime(); });
+#else
       cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out);
+#endif
       PR_STAMP(8);
     } else {
       cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, pedp, gfp, tb, out, io, t.tile, t.panel, t.ar * R,

@@ -6,6 +6,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "lifecycle.h"
 #include "streams.h"
 
 namespace pr {
@@ -113,12 +114,19 @@ ProducerEngine::ProducerEngine(SlotPool* pool, int64_t slot_bytes, int device,
   region_bytes_ = (int64_t)chunk_ * (plan.raw_frame_bytes + kCopySlack);
   hip_check(hipMalloc(&raw_bufs_, (size_t)n_raw_bufs_ * region_bytes_), "hipMalloc raw chunks");
   dev_in_.assign(n_raw_bufs_, std::vector<uint64_t>(chunk_, 0));
+  register_native_thread_owner(this, [this] { halt(); });
 }
 
-ProducerEngine::~ProducerEngine() {
+void ProducerEngine::halt() {
+  std::lock_guard<std::mutex> lk(halt_mu_);
   stop_.store(true);
   pool_->wake_producers();
   if (thread_.joinable()) thread_.join();
+}
+
+ProducerEngine::~ProducerEngine() {
+  unregister_native_thread_owner(this);
+  halt();
   (void)hipSetDevice(device_);
   if (h2d_) (void)hipStreamSynchronize(h2d_);
   for (auto cs : cstreams_) (void)hipStreamSynchronize(cs);

@@ -87,6 +87,7 @@ class ProducerEngine {
   void start(int64_t n_local_events, int64_t max_steps, int64_t k0 = 0);
   void request_stop() { stop_.store(true); }
   bool join(double timeout_s);   // true when the thread has exited
+  void halt();                   // stop the producing thread and join it (process exit)
   bool running() const { return running_.load(); }
   // frames whose calibration was ENQUEUED (committed to the pool; the kernels may still run)
   int64_t frames() const { return frames_.load(); }
@@ -169,6 +170,7 @@ class ProducerEngine {
   int64_t enq_frames_ = 0;
   std::thread thread_;
   std::atomic<bool> stop_{false}, running_{false};
+  std::mutex halt_mu_;   // halt() from the destructor and from halt_native_threads()
   std::atomic<int64_t> frames_{0}, full_waits_{0};
   double t_stage_ = 0, t_acquire_ = 0, t_launch_ = 0, t_commit_ = 0, t_total_ = 0;
   mutable std::mutex err_mu_;

@@ -15,6 +15,7 @@
 #include <cstring>
 
 #include "common.h"
+#include "lifecycle.h"
 #include "trace.h"
 
 namespace pr {
@@ -278,11 +279,18 @@ QueueFabric::QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate (fabric)");
   }
   if (!is_producer) drained_.store(true);
+  register_native_thread_owner(this, [this] { halt(); });
+}
+
+void QueueFabric::halt() {
+  std::lock_guard<std::mutex> lk(halt_mu_);
+  stop_.store(true);
+  if (th_.joinable()) th_.join();
 }
 
 QueueFabric::~QueueFabric() {
-  stop_.store(true);
-  if (th_.joinable()) th_.join();
+  unregister_native_thread_owner(this);
+  halt();
   try {
     if (device_ >= 0) hip_check(hipSetDevice(device_), "hipSetDevice");
     // copies still in flight complete into memory we keep mapped until here

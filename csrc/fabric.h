@@ -186,6 +186,7 @@ class QueueFabric {
   void start();
   void request_stop() { stop_.store(true); }
   bool join(double timeout_s);
+  void halt();     // stop the progress thread and join it (process exit: halt_native_threads)
   int64_t step();  // one engine iteration on the caller's thread (tests); returns work items
 
   bool running() const { return running_.load(); }
@@ -253,6 +254,7 @@ class QueueFabric {
   std::vector<int64_t> grantable_;   // engine thread: peers a filtered consumer grants to
 
   std::atomic<bool> finished_{false}, consumer_closed_{false}, stop_{false}, running_{false}, drained_{false};
+  std::mutex halt_mu_;   // halt() from the destructor and from halt_native_threads()
   bool closed_posted_ = false;   // consumer: consumer_closed stored in every mailbox
   bool returns_final_ = false;   // consumer: returns_final stored in every mailbox
   std::atomic<bool> quiesced_{false};

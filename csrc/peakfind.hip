@@ -152,6 +152,10 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
   __shared__ unsigned char cand_f[kPfCandCap];
   int* counts = scratch != nullptr ? scratch->tickets : counts_out;
   float* summary = scratch != nullptr ? scratch->acc : summary_out;
+  // the running total: with a scratch block the last workgroup adds the launch's record count in
+  // ONE atomic (per-peak atomics on one address serialise, ~3 ns each: 1,800 per 32-frame launch
+  // kept the kernel's completion ~5 us behind its last wave); without one, one atomic per record
+  unsigned long long* const total_per_peak = scratch != nullptr ? nullptr : total;
   const int64_t hw = (int64_t)pp.rows * pp.cols;
   const int64_t n4 = (int64_t)pp.n_panels * hw / 4;
   const int ncpf = (int)((n4 + 256 * K - 1) / (256 * K));
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
           const int yy = y + dy, xx = x + dx;
           return (yy >= 0 && yy < pp.rows && xx >= 0 && xx < pp.cols) ? pim[(int64_t)yy * pp.cols + xx] : NaN;
         },
-        val, pp, f, panel, y, x, peaks, counts, total);
+        val, pp, f, panel, y, x, peaks, counts, total_per_peak);
   };
   // block-reduce this frame's statistics and add them (one atomic pair per workgroup and frame)
   auto flush = [&](int f, float s, int c) {
@@ -262,10 +266,22 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
   }
   __syncthreads();
   if (!is_last) return;
+  int written = 0;   // records written by this launch (slots below max_peaks)
   for (int i = threadIdx.x; i < nframes; i += blockDim.x) {
-    counts_out[i] = atomicExch(&scratch->tickets[i], 0);
+    const int c = atomicExch(&scratch->tickets[i], 0);
+    counts_out[i] = c;
+    written += min(c, pp.max_peaks);
     summary_out[2 * i] = atomicExch(&scratch->acc[2 * i], 0.0f);
     summary_out[2 * i + 1] = atomicExch(&scratch->acc[2 * i + 1], 0.0f);
+  }
+  if (total != nullptr) {
+    for (int o = 32; o > 0; o >>= 1) written += __shfl_down(written, o);
+    if (lane == 0) red_cnt[wave] = written;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int n = red_cnt[0] + red_cnt[1] + red_cnt[2] + red_cnt[3];
+      if (n > 0) atomicAdd(total, (unsigned long long)n);
+    }
   }
   if (threadIdx.x == 0) atomicExch(&scratch->done, 0u);
 }

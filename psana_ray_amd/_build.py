@@ -25,6 +25,7 @@ CSRC = REPO / "csrc"
 BUILD_DIR = REPO / "build" / "native"
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 TARGET = PKG_DIR / f"_C{EXT_SUFFIX}"
+STAMP = PKG_DIR / "_C.build-stamp"
 ARCH = os.environ.get("PSANA_RAY_AMD_ARCH", "gfx950")
 
 
@@ -69,7 +70,9 @@ def _stamp(srcs, inc, common) -> str:
     for p in srcs + sorted(CSRC.glob("*.h")):
         h.update(p.name.encode())
         h.update(p.read_bytes())
-    h.update(" ".join(inc + common + [ARCH]).encode())
+    # the tree's own location is not part of the build (a copy of the tree elsewhere -- a GPU box's
+    # scratch path, an A/B variant tree -- has the same extension)
+    h.update(" ".join([f.replace(str(CSRC), "<csrc>") for f in inc] + common + [ARCH]).encode())
     return h.hexdigest()
 
 
@@ -77,7 +80,9 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     srcs = _sources()
     inc, common = _flags()
     stamp = _stamp(srcs, inc, common)
-    stamp_file = BUILD_DIR / "stamp.txt"
+    # the stamp sits NEXT TO the extension, so the pair travels together (a snapshot of the tree
+    # without build/ -- a GPU box -- loads the extension as built instead of recompiling it)
+    stamp_file = STAMP
     if not force and TARGET.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
         return TARGET
     BUILD_DIR.mkdir(parents=True, exist_ok=True)

@@ -7,6 +7,7 @@ GPU box a missing/failed extension raises -- GPU ops never silently fall back to
 """
 from __future__ import annotations
 
+import atexit
 import importlib
 import os
 import threading
@@ -30,7 +31,11 @@ def load(build_if_missing: bool = True):
                 from .. import _build
 
                 _build.build()
-            _mod = importlib.import_module("psana_ray_amd._C")
+            mod = importlib.import_module("psana_ray_amd._C")
+            # native threads (queue fabric, producer engines) are stopped before the interpreter
+            # and the HIP runtime tear down (csrc/lifecycle.h)
+            atexit.register(mod.halt_native_threads)
+            _mod = mod
             return _mod
         except Exception as e:  # pragma: no cover - surfaced to the caller
             _err = e

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import collections
 import logging
+import threading
 import time
 from typing import List, Optional
 
@@ -281,22 +282,41 @@ class ProducerPipeline:
         return self.frames
 
 
+# Native streams with a hardware-queue placement, per (device, kind): created once, handed back
+# here when their torch wrapper is collected and handed out again -- never destroyed while the
+# process runs.  Tensors allocated on a stream keep its handle in torch's caching allocator after
+# the wrapper is gone, so destroying the native stream could leave the allocator a dangling handle;
+# and every CU-masked stream is a hardware queue of its own, so reuse also bounds their number.
+_STREAM_POOL: dict = {}
+_STREAM_POOL_LOCK = threading.Lock()
+
+
+def _return_stream(key, h: int):
+    with _STREAM_POOL_LOCK:
+        _STREAM_POOL.setdefault(key, []).append(h)
+
+
 def _make_streams(device, n: int, kind: str):
-    """n torch streams with the given hardware-queue placement (config.STREAM_KINDS); native
-    streams are destroyed when the last wrapper is collected (not at interpreter exit)."""
+    """n torch streams with the given hardware-queue placement (config.STREAM_KINDS), from the
+    process-wide pool of native streams (see _STREAM_POOL)."""
     if STREAM_KINDS[kind] == 0:
         return [torch.cuda.Stream(device=device) for _ in range(n)]
     import weakref
 
     C = _ext.load()
     dev = device.index if device.index is not None else torch.cuda.current_device()
+    key = (dev, STREAM_KINDS[kind])
     out = []
     for _ in range(n):
-        h = int(C.stream_create(dev, STREAM_KINDS[kind]))
+        with _STREAM_POOL_LOCK:
+            free = _STREAM_POOL.setdefault(key, [])
+            h = free.pop() if free else None
+        if h is None:
+            h = int(C.stream_create(dev, STREAM_KINDS[kind]))
         st = torch.cuda.ExternalStream(h, device=device)
-        fin = weakref.finalize(st, C.stream_destroy, dev, h)
-        fin.atexit = False   # at interpreter exit the HIP runtime may be torn down already; the
-        out.append(st)       # process exit releases the queue anyway
+        fin = weakref.finalize(st, _return_stream, key, h)
+        fin.atexit = False
+        out.append(st)
     return out
 
 

@@ -185,6 +185,31 @@ def test_peakfind_vs_reference(cuda_device, det, radius, scratch):
     assert torch.allclose(summary[:, 1].cpu(), ref_summary[:, 1], rtol=1e-4)
 
 
+@pytest.mark.parametrize("scratch", [False, True])
+def test_peakfind_total_counts_only_written_records(cuda_device, scratch):
+    """max_peaks below the frames' peak counts: counts report every accepted peak, the running
+    total only the records written (min(count, max_peaks) per frame) -- per peak without a scratch
+    block, in one atomic per launch from the last workgroup with one."""
+    spec, consts, raw = _setup("jungfrau05M", 5, seed=8, gain_config="AHL")
+    frames = reference.calibrate_reference(raw.to(torch.int32), consts, None, None)
+    params = PeakFinderParams(thr_peak=15.0, son_min=4.0, radius=1, max_peaks=3)
+    ref_peaks, _ = reference.peakfind_reference(frames, PeakFinderParams(thr_peak=15.0, son_min=4.0, radius=1))
+    F = frames.shape[0]
+    assert all(p.shape[0] > params.max_peaks for p in ref_peaks), "fixture must overflow max_peaks"
+    d = frames.to(cuda_device).contiguous()
+    peaks = torch.zeros((F, params.max_peaks, 8), dtype=torch.float32, device=cuda_device)
+    counts = torch.zeros(F, dtype=torch.int32, device=cuda_device)
+    summary = torch.zeros((F, 2), dtype=torch.float32, device=cuda_device)
+    total = torch.full((), 5, dtype=torch.int64, device=cuda_device)
+    scr = torch.zeros(kernels.PF_SCRATCH_WORDS, dtype=torch.int32, device=cuda_device) if scratch else None
+    for _ in range(3):
+        kernels.peakfind([d[i] for i in range(F)], spec.frame_shape, params, peaks, counts, summary, total=total,
+                         scratch=scr)
+    torch.cuda.synchronize()
+    assert [int(c) for c in counts.cpu()] == [p.shape[0] for p in ref_peaks]
+    assert int(total) == 5 + 3 * F * params.max_peaks
+
+
 @pytest.mark.parametrize("det,F", [("tiny_epix", kernels.MAX_FRAMES), ("jungfrau05M", 7)])
 def test_peakfind_full_batch(cuda_device, det, F):
     """A whole launch (64 frames) and an odd frame count: the balanced grid's contiguous chunk

@@ -37,6 +37,10 @@ PHASES = [
     ("bar3", 5, 6),
     ("p3_gain_out", 6, 7),
     ("flush(bar+stores)", 7, 8),
+    ("  out_barrier", 7, 9),
+    ("  place_or_flush", 9, 8),
+    ("  place", 9, 10),
+    ("  gaps", 10, 8),
 ]
 
 

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--thr", type=float, default=None, help="thr_peak (default: PeakFinderParams)")
     ap.add_argument("--frames", type=int, default=32)
+    ap.add_argument("--total", action="store_true", help="bump a running peak total (as the pipeline consumer does)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
     C = _ext.load()
@@ -42,12 +43,14 @@ def main():
     counts = torch.zeros(F, dtype=torch.int32, device=dev)
     summary = torch.zeros((F, 2), dtype=torch.float32, device=dev)
     scratch = torch.zeros(kernels.PF_SCRATCH_WORDS, dtype=torch.int32, device=dev)
+    total = torch.zeros((), dtype=torch.int64, device=dev)
+    total_ptr = int(total.data_ptr()) if a.total else 0
     ptrs = [int(f.data_ptr()) for f in frames]
 
     def launch(var):
         C.peakfind(ptrs, P, H, W, float(pp.thr_peak), float(pp.son_min), int(pp.radius),
                    int(pp.max_peaks), int(peaks.data_ptr()), int(counts.data_ptr()), int(summary.data_ptr()),
-                   _ext.stream_handle(), 0, int(scratch.data_ptr()))
+                   _ext.stream_handle(), total_ptr, int(scratch.data_ptr()))
 
     launch(0)
     torch.cuda.synchronize()
