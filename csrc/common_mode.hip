@@ -237,11 +237,12 @@ struct TileGeom {
 // desc[3p] + y * desc[3p+1] + x * desc[3p+2]; the corrected tile goes from LDS straight into the
 // assembled image instead of a frame-shaped scratch buffer that a second kernel re-reads
 // (saves a 2 x 8.65 MB HBM round trip per epix10k2M frame).  The gap pixels between panels are
-// zeroed by the same kernel: workgroup (tile t, frame f) takes its 1/n_tiles share of the gap
-// runs, read with scalar loads so no vector load sits between its stores.
+// zeroed by the same kernel from a gap table of image elements no panel covers: aligned 16-B chunks
+// (entry = first element, >= 0, a multiple of 4) first, then single elements (entry = -1 - element);
+// workgroup (tile t, frame f) takes its 1/n_tiles share.
 struct ImgOut {
   const int32_t* desc;    // [n_panels][3] (base, step per panel row, step per panel column); nullptr: frame layout
-  const int2* gaps;       // [n_gaps] (start, length) image runs no panel covers: zeroed by the kernel
+  const int32_t* gaps;    // [n_gaps] gap table (geometry.py gap_fill_table)
   int n_gaps;
 };
 
@@ -495,18 +496,41 @@ __device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C,
 
 // Image layout (fused K-05): every panel sits in the image by an integer rotation + translation,
 // so either tile rows or tile columns are contiguous image runs (step +-1).  Each run is cut into
-// 16-B aligned image chunks: whole chunks are 16-B stores, the (at most two) partial chunks at the
-// ends of a run 4-B stores.  The image mask is folded into the gain factors of this plan
-// (Calibrator), so no mask loads sit between the stores.
-__device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, int tile, int ntiles, PR_GLOBAL float* out) {
-  if (io.n_gaps <= 0) return;
-  const int r0 = (int)((int64_t)io.n_gaps * tile / ntiles), r1 = (int)((int64_t)io.n_gaps * (tile + 1) / ntiles);
-  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), nw = (int)blockDim.x >> 6;
-  const int lane = (int)threadIdx.x & 63;
-  for (int j = r0 + wave; j < r1; j += nw) {
-    const int2 rr = io.gaps[j];   // wave-uniform address: scalar load
-    for (int k = lane; k < rr.y; k += 64) out[(int64_t)rr.x + k] = 0.0f;
+// 16-B aligned image chunks.  Stores are issue-bound here (a 4-B-per-lane store costs the issue slot
+// of a 16-B one), so the FULL chunks go out first, one 16-B store per lane and no partial-chunk
+// branch in the loop, and the (at most 3 + 3) ragged elements of every run after them, one 4-B
+// store per element over all lanes.  (The round-2 form handled partial chunks inside the chunk loop:
+// every wave iteration that met one issued 1 + 4 store instructions.)  The image mask is folded
+// into the gain factors of this plan (Calibrator), so no mask loads sit between the stores.
+
+// Gap table share of this workgroup, preloaded into registers BEFORE the store phase's barrier (the
+// loads' latency hides behind the barrier and the placement; a load between stores would wait for
+// them).  kGapPre entries per thread cover the share; a larger share loops.
+constexpr int kGapPre = 4;
+struct GapPre {
+  int v[kGapPre];
+  int r0, r1;
+};
+__device__ __forceinline__ GapPre cm_gap_preload(const ImgOut& io, int tile, int ntiles) {
+  GapPre g;
+  g.r0 = io.n_gaps > 0 ? (int)((int64_t)io.n_gaps * tile / ntiles) : 0;
+  g.r1 = io.n_gaps > 0 ? (int)((int64_t)io.n_gaps * (tile + 1) / ntiles) : 0;
+#pragma unroll
+  for (int k = 0; k < kGapPre; ++k) {
+    const int e = g.r0 + (int)threadIdx.x + k * (int)blockDim.x;
+    g.v[k] = e < g.r1 ? io.gaps[e] : INT32_MIN;
   }
+  return g;
+}
+__device__ __forceinline__ void cm_gap_store(PR_GLOBAL float* out, int v) {
+  if (v >= 0) st_f4((PR_GLOBAL float4*)(out + v), make_float4(0.f, 0.f, 0.f, 0.f));
+  else if (v != INT32_MIN) out[-1 - (int64_t)v] = 0.0f;
+}
+__device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, const GapPre& g, PR_GLOBAL float* out) {
+#pragma unroll
+  for (int k = 0; k < kGapPre; ++k) cm_gap_store(out, g.v[k]);
+  for (int e = g.r0 + (int)threadIdx.x + kGapPre * (int)blockDim.x; e < g.r1; e += (int)blockDim.x)
+    cm_gap_store(out, io.gaps[e]);   // shares beyond kGapPre entries per thread (not the production shapes)
 }
 
 __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C, const ImgOut& io, int panel, int y0,
@@ -519,8 +543,9 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
   const int nruns = rows ? R : C;
   const int step = rows ? sx : sy;                  // +-1 along the run
   const int64_t outer = rows ? sy : sx;             // image step between runs
+  const int nb = (int)blockDim.x;
   if ((outer & 3) != 0) {                           // runs not equally aligned: 4-B stores
-    for (int e = threadIdx.x; e < R * C; e += blockDim.x) {
+    for (int e = threadIdx.x; e < R * C; e += nb) {
       const int a = e / len, t = e - a * len;
       const int r = rows ? a : t, c = rows ? t : a;
       out[b0 + (int64_t)r * sy + (int64_t)c * sx] = tile[r * P + c];
@@ -529,46 +554,51 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
   }
   const int64_t lo = step > 0 ? b0 : b0 - (len - 1);   // lowest image address of run 0
   const int head = (int)(lo & 3);                       // the same for every run
-  const int nch = (head + len + 3) >> 2;                // aligned chunks per run
-  // lanes -> (run, chunk): rows-case runs are tile rows (contiguous in LDS too), so consecutive
+  // full chunks ch in [ch_lo, ch_lo + nfull): chunk ch covers positions t = 4 ch - head .. + 3 in
+  // lowest-address order; positions [0, t_lo) and [t_hi, len) are ragged
+  const int ch_lo = (head + 3) >> 2;
+  const int nfull = max(0, ((len + head) >> 2) - ch_lo);
+  const int t_lo = nfull > 0 ? 4 * ch_lo - head : len;
+  const int t_hi = nfull > 0 ? t_lo + 4 * nfull : len;
+  const int rb_step = rows ? P : 1;                     // tile address of run `run`, element i:
+  const int ie = rows ? 1 : P;                          //   run * rb_step + i * ie
+  const int di = step > 0 ? ie : -ie;
+  auto tile_at = [&](int run, int t) { return tile + run * rb_step + (step > 0 ? t : len - 1 - t) * ie; };
+  // lanes -> (run, full chunk): rows-case runs are tile rows (contiguous in LDS too), so consecutive
   // lanes take consecutive chunks of one run; column-case runs are tile columns, so a wave takes 4
   // chunks (64 B of image) of 16 neighbouring columns -- LDS reads 2-way instead of 32-way
   // bank-conflicted, global stores 16 segments of 64 B.  The (run, chunk) walk is incremental (one
   // integer division per thread, not per chunk).
-  const int span = rows ? nch : ((nch + 3) >> 2) * 4;   // work items per run (column case: padded)
-  const int nb = (int)blockDim.x;
-  int a = (int)threadIdx.x / (rows ? nch : 4 * nruns), w = (int)threadIdx.x - a * (rows ? nch : 4 * nruns);
-  // rows: (a, w = chunk); columns: (a = chunk quad, w = 4 * run + chunk within the quad)
-  const int per = rows ? nch : 4 * nruns;
-  const int da = nb / per, dw = nb - da * per;
-  const int outer_n = rows ? nruns : (span >> 2);
-  for (; a < outer_n;) {
-    const int run = rows ? a : (w >> 2);
-    const int ch = rows ? w : 4 * a + (w & 3);
-    if (ch < nch) {
-      const int64_t sb = lo + (int64_t)run * outer;      // this run's lowest address
-      const int64_t base = (sb & ~(int64_t)3) + 4 * ch;
-      const int t0 = 4 * ch - head;                      // position of base in lowest-address order
-      const int rb = rows ? run * P : run;               // tile address of element i: rb + i * ie
-      const int ie = rows ? 1 : P;
-      if (t0 >= 0 && t0 + 3 < len) {
-        const int i0 = step > 0 ? t0 : len - 1 - t0;
-        const int di = step > 0 ? ie : -ie;
-        const float* tp = tile + rb + i0 * ie;
+  if (nfull > 0) {
+    const int span = rows ? nfull : ((nfull + 3) >> 2) * 4;   // work items per run (column case: padded)
+    const int per = rows ? nfull : 4 * nruns;
+    int a = (int)threadIdx.x / per, w = (int)threadIdx.x - a * per;
+    // rows: (a = run, w = chunk); columns: (a = chunk quad, w = 4 * run + chunk within the quad)
+    const int da = nb / per, dw = nb - da * per;
+    const int outer_n = rows ? nruns : (span >> 2);
+    for (; a < outer_n;) {
+      const int run = rows ? a : (w >> 2);
+      const int k = rows ? w : 4 * a + (w & 3);         // full chunk index from ch_lo
+      if (k < nfull) {
+        const int64_t base = (lo & ~(int64_t)3) + (int64_t)run * outer + 4 * (ch_lo + k);
+        const float* tp = tile_at(run, t_lo + 4 * k);
         st_f4((PR_GLOBAL float4*)(out + base), make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int t = t0 + k;
-          if (t >= 0 && t < len) out[base + k] = tile[rb + (step > 0 ? t : len - 1 - t) * ie];
-        }
+      }
+      a += da;
+      w += dw;
+      if (w >= per) {
+        w -= per;
+        ++a;
       }
     }
-    a += da;
-    w += dw;
-    if (w >= per) {
-      w -= per;
-      ++a;
+  }
+  // ragged elements: n_rag per run, the same for every run
+  const int n_head = t_lo, n_rag = t_lo + (len - t_hi);
+  if (n_rag > 0) {
+    for (int e = threadIdx.x; e < nruns * n_rag; e += nb) {
+      const int run = e / n_rag, j = e - run * n_rag;
+      const int t = j < n_head ? j : t_hi + (j - n_head);
+      out[lo + (int64_t)run * outer + t] = *tile_at(run, t);
     }
   }
 }
@@ -586,12 +616,14 @@ template <typename Mark = NoMark>
 __device__ __forceinline__ void cm_write_out(const float* tile, int P, int R, int C, const TileGeom& tg,
                                              const ImgOut& io, int tile_id, int panel, int y0, int x0, int64_t base,
                                              PR_GLOBAL float* out, const Mark& mark = Mark()) {
+  GapPre gp;
+  if (io.desc != nullptr) gp = cm_gap_preload(io, tile_id, (int)gridDim.x / ((tg.nframes + tg.fpw - 1) / tg.fpw));
   __syncthreads();
   mark(9);
   if (io.desc != nullptr) {
     cm_place(tile, P, R, C, io, panel, y0, x0, out);
     mark(10);
-    cm_fill_gaps(io, tile_id, (int)gridDim.x / ((tg.nframes + tg.fpw - 1) / tg.fpw), out);
+    cm_fill_gaps(io, gp, out);
   } else {
     cm_flush(tile, P, R, C, out, base, tg.panel_cols);
   }
@@ -958,6 +990,11 @@ __device__ __forceinline__ void cm_rows(float* tile, const int P, const int R, c
     constexpr int PA = (L & 1) ? (L - 1) / 2 : L / 2 - 1;
     constexpr int PB = PA + 1;
     select_regs<L, PA, PB>(x);
+#ifdef PR_CM_PROBE_ROWS_TWICE
+    // timing probe only (VALU sensitivity): the row network applied a second time -- the median
+    // positions are unchanged, the instruction count of the row phase doubles
+    select_regs<L, PA, PB>(x);
+#endif
     asm volatile("" ::: "memory");
     // toggle padding: L even -> odd count: x[L/2], even: mean of x[L/2-1], x[L/2];
     //                 L odd  -> odd count: x[(L-1)/2], even: mean of x[(L-1)/2], x[(L+1)/2]
@@ -1149,6 +1186,23 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
     // ---- phase 2a: rows by bank, one lane per segment ------------------------------------
     if (cp.flags & 1) {
       cm_rows<L>(tile, P, R, C, cp, tid, blockDim.x);
+#ifdef PR_CM_PROBE_W3_VALU
+      // timing probe only: the idle fourth wave issues ~800 VALU during the row phase.  Hidden if a
+      // workgroup's time is its own critical path; it costs if the SIMDs' VALU issue is the bound.
+      if (tid >= 192) {
+        float a[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] = tile[tid + q];
+        for (int it = 0; it < PR_CM_PROBE_W3_VALU; ++it) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) a[q] = fmaf(a[q], 1.0001f, 0.5f);
+        }
+        float z = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) z += a[q];
+        if (cp.flags & 64) tile[tid] = z;
+      }
+#endif
       PR_STAMP(3);
       __syncthreads();
       PR_STAMP(4);
@@ -1297,8 +1351,8 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   check(aligned16(ped) && aligned16(gf) && (planes & 3) == 0, "calib_cm: misaligned constant tables");
   for (int f = 0; f < nframes; ++f)
     check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_cm: frame buffers must be 16-B aligned");
-  check(n_gap_runs == 0 || (img_desc != 0 && gap_runs != 0 && gap_runs % 8 == 0), "calib_cm: bad gap run table");
-  const ImgOut io{reinterpret_cast<const int32_t*>(img_desc), reinterpret_cast<const int2*>(gap_runs),
+  check(n_gap_runs == 0 || (img_desc != 0 && gap_runs != 0 && gap_runs % 4 == 0), "calib_cm: bad gap table");
+  const ImgOut io{reinterpret_cast<const int32_t*>(img_desc), reinterpret_cast<const int32_t*>(gap_runs),
                   img_desc != 0 ? n_gap_runs : 0};
   // LDS budget of one workgroup: the epix10k2M 176x48 stripe runs PR_CM_EPIX_WG_PER_CU workgroups
   // per CU, the narrow compile-time kernels two, everything else one; what the tile leaves is side

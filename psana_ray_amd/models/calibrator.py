@@ -159,14 +159,14 @@ class Calibrator:
                 p.mode = 3
             elif place is not None:
                 # common mode writes the assembled image from its LDS tiles (no scratch round trip);
-                # a fill kernel zeroes the gaps between panels.  Every panel pixel lands on exactly
+                # the same kernel zeroes the gaps between panels (gap table).  Every panel pixel lands on exactly
                 # one image pixel, so the image mask folds into this plan's gain factors (the
                 # common-mode eligibility is unchanged: the reference masks after assembly)
                 p.mode = 5
                 self._img_desc = torch.from_numpy(place.ravel().copy()).to(self.device)
-                self._gap_runs = torch.from_numpy(self.geometry.gap_runs().ravel().copy()).to(self.device)
+                self._gap_runs = torch.from_numpy(self.geometry.gap_fill_table()).to(self.device)
                 p.img_desc, p.gap_runs = int(self._img_desc.data_ptr()), int(self._gap_runs.data_ptr())
-                p.n_gap_runs = int(self._gap_runs.numel() // 2)
+                p.n_gap_runs = int(self._gap_runs.numel())
                 if self.image_mask is not None:
                     imap = self.geometry.index_map().ravel()
                     keep = np.ones(spec.npix, dtype=np.float32)

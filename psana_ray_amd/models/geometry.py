@@ -79,6 +79,21 @@ class Geometry:
                 runs.append((s0, min(max_len, e - s0)))
         return np.asarray(runs, np.int32).reshape(-1, 2)
 
+    def gap_fill_table(self) -> np.ndarray:
+        """int32 gap table of the fused common-mode -> image kernel (csrc/common_mode.hip, ImgOut):
+        the image elements no panel pixel covers, as aligned 16-B chunks first (entry = first
+        element, a multiple of 4: all four elements are gaps) and the remaining gap elements after
+        them (entry = -1 - element)."""
+        gap = self.index_map() < 0
+        n = gap.size
+        n4 = n // 4
+        full = gap[: 4 * n4].reshape(n4, 4).all(axis=1)
+        chunks = 4 * np.nonzero(full)[0]
+        single = gap.copy()
+        single[: 4 * n4] &= ~np.repeat(full, 4)
+        singles = np.nonzero(single)[0]
+        return np.concatenate([chunks, -1 - singles]).astype(np.int32)
+
     def pixel_coords_um(self):
         """(x, y) pixel-centre coordinates in micrometres (psana-style geometry output)."""
         ps = self.spec.pixel_size_um

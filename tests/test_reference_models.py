@@ -83,6 +83,26 @@ def test_geometry_unique_and_epix_image_size():
     assert 1500 <= geo.image_shape[0] <= 1800   # "H,W ~ 1.7k" (SURVEY K-05)
 
 
+def test_gap_fill_table_covers_exactly_the_gaps():
+    """The fused CM -> image kernel zeroes the image through this table: aligned 16-B chunks
+    first (entry >= 0, a multiple of 4), single elements after (entry = -1 - element); together
+    they must cover every gap element once and no panel pixel."""
+    for det in list_detectors():
+        geo = make_geometry(get_detector(det))
+        gap = geo.index_map().ravel() < 0
+        t = geo.gap_fill_table()
+        assert t.dtype == np.int32
+        nch = int((t >= 0).sum())
+        assert (t[:nch] >= 0).all() and (t[nch:] < 0).all(), "chunks must precede singles"
+        ch, si = t[:nch], -1 - t[nch:]
+        assert (ch % 4 == 0).all()
+        hits = np.zeros(gap.size, np.int32)
+        for k in range(4):
+            np.add.at(hits, ch + k, 1)
+        np.add.at(hits, si, 1)
+        assert np.array_equal(hits, gap.astype(np.int32)), det
+
+
 def test_cpu_calibrator_image_mode_shape():
     spec, c, raw = _raw("tiny_epix", n=2)
     cal = Calibrator(c, "cpu", Mode.image)

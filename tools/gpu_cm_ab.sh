@@ -11,6 +11,7 @@ for v in $VS; do
   T=/tmp/tree_$v
   rm -rf $T && cp -r $R $T || exit 1
   [ $v = base ] || cp $R/variants/_C_$v.so $T/$SO || exit 1
+  case " ${NOTEST:-} " in *" $v "*) echo "$v: timing probe, no tests"; continue;; esac
   PYTHONPATH=$T timeout -k 10 300 python3 -u -m pytest $T/tests/test_kernels_gpu.py -x -q --timeout 180 --timeout-method thread -k "${TESTK:-common_mode}" > $O/tests_$v.log 2>&1; rc=$?; echo "$v tests: $(tail -1 $O/tests_$v.log)"; [ $rc -eq 0 ] || exit $rc
 done
 for r in 1 2 3; do
@@ -20,11 +21,13 @@ for r in 1 2 3; do
   done
 done
 if [ -n "${BENCH:-}" ]; then
-  for v in $VS; do
+  for br in $(seq 1 ${BENCH_ROUNDS:-1}); do
+  for v in ${BENCH_VARIANTS:-$VS}; do
     cd /tmp/tree_$v
     for m in calib image; do
-      PYTHONPATH=/tmp/tree_$v timeout -k 10 300 python3 bench.py --steps 200 --warmup 5 --source device --mode $m > $O/dev_${m}_$v.json 2> $O/dev_${m}_$v.err || exit $?
-      python3 -c "import json;d=json.load(open('$O/dev_${m}_$v.json'));print('$v dev $m', d['value'])"
+      PYTHONPATH=/tmp/tree_$v timeout -k 10 300 python3 bench.py --steps 200 --warmup 5 --source device --mode $m > $O/dev_${m}_${v}_$br.json 2> $O/dev_${m}_${v}_$br.err || exit $?
+      python3 -c "import json;d=json.load(open('$O/dev_${m}_${v}_$br.json'));print('$v dev $m r$br', d['value'])"
     done
+  done
   done
 fi
