@@ -60,6 +60,9 @@
 #ifndef PR_CM_RAW_NT
 #define PR_CM_RAW_NT 1
 #endif
+#ifndef PR_CM_SPREAD
+#define PR_CM_SPREAD 0
+#endif
 #ifndef PR_CM_EPIX_WG_PER_CU
 #define PR_CM_EPIX_WG_PER_CU ((PR_CM_FPW > 1 || PR_CM_GPRE) ? 3 : 4)
 #endif
@@ -1135,6 +1138,28 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
   // shapes prefetch frame k+1's raw words during frame k's medians)
   const int nf = min(tg.fpw, tg.nframes - t.f);
   uint4 rw[kNet ? NI : 1];
+  // Median-phase work -> lanes.  Packed (PR_CM_SPREAD 0): thread t takes segment / column-lane t,
+  // so the epix10k2M tile's 176 row segments fill waves 0-1 and 48 lanes of wave 2, its 192 column
+  // lanes waves 0-2, and wave 3 idles.  Spread (1): every wave takes an equal share (44 segments,
+  // 12 columns = 48 lanes; shares of whole quads), one item per lane.
+  int rows_t0 = tid, rows_nt = (int)blockDim.x, cols_t0 = tid, cols_nt = (int)blockDim.x;
+#if PR_CM_SPREAD
+  {
+    const int nw = (int)blockDim.x >> 6, wv = tid >> 6, ln = tid & 63;
+    const int nseg = R * (C / L);
+    const int rs = (nseg + nw - 1) / nw;
+    if (rs <= 64) {
+      rows_t0 = ln < rs ? wv * rs + ln : nseg;
+      rows_nt = nseg;
+    }
+    const int ncl = 4 * C;
+    const int cs = (((ncl + nw - 1) / nw) + 3) & ~3;
+    if (cs <= 64) {
+      cols_t0 = ln < cs ? wv * cs + ln : (1 << 20);
+      cols_nt = 1 << 20;
+    }
+  }
+#endif
 #if PR_CM_STAMPS
   uint64_t st_[12] = {};
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
@@ -1185,7 +1210,7 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
 
     // ---- phase 2a: rows by bank, one lane per segment ------------------------------------
     if (cp.flags & 1) {
-      cm_rows<L>(tile, P, R, C, cp, tid, blockDim.x);
+      cm_rows<L>(tile, P, R, C, cp, rows_t0, rows_nt);
 #ifdef PR_CM_PROBE_W3_VALU
       // timing probe only: the idle fourth wave issues ~800 VALU during the row phase.  Hidden if a
       // workgroup's time is its own critical path; it costs if the SIMDs' VALU issue is the bound.
@@ -1210,7 +1235,7 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void cal
 
     // ---- phase 2b: columns -----------------------------------------------------------------
     if (cp.flags & 2) {
-      cm_cols<M>(tile, P, R, C, cp, tid, blockDim.x);
+      cm_cols<M>(tile, P, R, C, cp, cols_t0, cols_nt);
       PR_STAMP(5);
       __syncthreads();
       PR_STAMP(6);
