@@ -60,6 +60,11 @@
 #ifndef PR_CM_RAW_NT
 #define PR_CM_RAW_NT 1
 #endif
+// Threads per workgroup of the epix10k2M production kernel (4 or 6 waves; the tile and four
+// workgroups per CU are unchanged: 6 waves leave each wave 80 VGPRs)
+#ifndef PR_CM_EPIX_BLOCK
+#define PR_CM_EPIX_BLOCK 256
+#endif
 #ifndef PR_CM_SPREAD
 #define PR_CM_SPREAD 0
 #endif
@@ -1118,7 +1123,7 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
 }
 
 template <int KIND, int L, int M, int BLOCK, int TR = 0, int TC = 0>
-__global__ __launch_bounds__(BLOCK, M <= 48 ? PR_CM_EPIX_WG_PER_CU : 2) void calib_cm_net_kernel(
+__global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_CU / 4 : 2) void calib_cm_net_kernel(
     const FramePtrs fp, const float* __restrict__ ped, const float* __restrict__ gf,
     const uint8_t* __restrict__ planes, const TileGeom tg, const CmParams cp, const ImgOut io) {
   constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
@@ -1409,7 +1414,8 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   const bool narrow = asic_cols <= 128;
   const size_t lds_all = lds + 32 * (size_t)side_slots;
   if (epix_prod && asic_cols == 48) {
-    cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, 256, 176, 48>, grid, 256, lds_all, s, fp, P, G, F, tg, cp, io);
+    cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, PR_CM_EPIX_BLOCK, 176, 48>, grid, PR_CM_EPIX_BLOCK, lds_all, s, fp, P,
+              G, F, tg, cp, io);
   } else if (jf_prod && asic_cols == 128) {
     cm_launch(calib_cm_net_kernel<kJungfrau, 64, 64, 512, 256, 128>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
   } else if (kind == kEpix10ka && bank_cols == 48 && M4 == 44 && narrow) {
