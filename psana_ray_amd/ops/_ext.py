@@ -11,6 +11,7 @@ import atexit
 import importlib
 import os
 import threading
+import weakref
 
 import torch  # noqa: F401  (must precede the extension: one HIP runtime per process)
 
@@ -32,14 +33,37 @@ def load(build_if_missing: bool = True):
 
                 _build.build()
             mod = importlib.import_module("psana_ray_amd._C")
-            # native threads (queue fabric, producer engines) are stopped before the interpreter
-            # and the HIP runtime tear down (csrc/lifecycle.h)
-            atexit.register(mod.halt_native_threads)
+            # at exit: Python threads that drive native objects (queue-session watchers) stop first,
+            # then every native thread (queue fabric, producer engines) -- all before the
+            # interpreter and the HIP runtime tear down (csrc/lifecycle.h)
+            atexit.register(_shutdown, mod)
             _mod = mod
             return _mod
         except Exception as e:  # pragma: no cover - surfaced to the caller
             _err = e
             raise RuntimeError(f"psana_ray_amd native extension unavailable: {e}") from e
+
+
+_exit_hooks: "weakref.WeakSet" = None
+
+
+def on_exit(obj) -> None:
+    """Call ``obj.stop_at_exit()`` at process exit, before the native threads halt (weakly held:
+    an object collected earlier is forgotten)."""
+    global _exit_hooks
+    with _lock:
+        if _exit_hooks is None:
+            _exit_hooks = weakref.WeakSet()
+        _exit_hooks.add(obj)
+
+
+def _shutdown(mod) -> None:
+    for obj in list(_exit_hooks or ()):
+        try:
+            obj.stop_at_exit()
+        except Exception:  # noqa: BLE001 - best effort at exit
+            pass
+    mod.halt_native_threads()
 
 
 def available() -> bool:

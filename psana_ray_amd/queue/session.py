@@ -228,7 +228,16 @@ class QueueSession:
         self.poll()   # members already present are linked before the first frame moves
         self._thread = threading.Thread(target=self._run, name=f"psana-ray-session-{self.mid}", daemon=True)
         self._thread.start()
+        from ..ops import _ext
+
+        _ext.on_exit(self)   # a session left open stops its watcher before the native threads halt
         return self
+
+    def stop_at_exit(self):
+        """Process exit: stop the watcher thread (its callbacks drive the native fabric)."""
+        self._stop.set()
+        if self._thread is not None and self._thread is not threading.current_thread():
+            self._thread.join(2)
 
     def _run(self):
         last_hb = 0.0

@@ -7,7 +7,8 @@ cd /tmp && export TMPDIR=/tmp
 export PYTHONPATH=$R
 O=$R/gpurun_out/r3_final
 mkdir -p $O
-timeout -k 10 900 python3 -u -m pytest $R/tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -1 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python3 ${PYFLAGS:-} -u -m pytest $R/tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -1 $O/tests.log
+[ $rc -eq 0 ] || { grep -n -A60 "Fatal Python error" $O/tests.log | head -150; exit $rc; }
 cd $R && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit $?
 tail -1 $O/smoke.log
 for s in 20 200; do

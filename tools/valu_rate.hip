@@ -12,20 +12,35 @@
 #include <cstdio>
 #include <vector>
 
-#define PR_V16(OPS)                                                                               \
-  asm volatile(OPS " %0, %0, %16, %0\n\t" OPS " %1, %1, %16, %1\n\t" OPS " %2, %2, %16, %2\n\t" OPS \
-               " %3, %3, %16, %3\n\t" OPS " %4, %4, %16, %4\n\t" OPS " %5, %5, %16, %5\n\t" OPS         \
-               " %6, %6, %16, %6\n\t" OPS " %7, %7, %16, %7\n\t" OPS " %8, %8, %16, %8\n\t" OPS         \
-               " %9, %9, %16, %9\n\t" OPS " %10, %10, %16, %10\n\t" OPS " %11, %11, %16, %11\n\t" OPS   \
-               " %12, %12, %16, %12\n\t" OPS " %13, %13, %16, %13\n\t" OPS " %14, %14, %16, %14\n\t" OPS \
-               " %15, %15, %16, %15"                                                                       \
-               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]),        \
-                 "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]), "+v"(r[13]),    \
-                 "+v"(r[14]), "+v"(r[15])                                                                   \
+// 16 independent chains of one instruction form: "%r" is the chain register, "%k" a constant VGPR
+#define PR_CHAIN(FMT) FMT
+#define PR_ASM16(T)                                                                                     \
+  asm volatile(T(0) "\n\t" T(1) "\n\t" T(2) "\n\t" T(3) "\n\t" T(4) "\n\t" T(5) "\n\t" T(6) "\n\t" T(7)  \
+               "\n\t" T(8) "\n\t" T(9) "\n\t" T(10) "\n\t" T(11) "\n\t" T(12) "\n\t" T(13) "\n\t" T(14)  \
+               "\n\t" T(15)                                                                             \
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]),    \
+                 "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]), "+v"(r[13]), \
+                 "+v"(r[14]), "+v"(r[15])                                                               \
                : "v"(k))
+#define S_(x) #x
+#define R_(i) "%" S_(i)
+#define T_MAXIMUM3(i) "v_maximum3_f32 " R_(i) ", " R_(i) ", %16, " R_(i)
+#define T_MAX3(i) "v_max3_f32 " R_(i) ", " R_(i) ", %16, " R_(i)
+#define T_MAX_E32(i) "v_max_f32_e32 " R_(i) ", %16, " R_(i)
+#define T_MAX_E64(i) "v_max_f32_e64 " R_(i) ", " R_(i) ", %16"
+#define T_FMA(i) "v_fma_f32 " R_(i) ", " R_(i) ", %16, " R_(i)
+#define T_ADD(i) "v_add_f32_e32 " R_(i) ", %16, " R_(i)
+#define T_MED3(i) "v_med3_f32 " R_(i) ", " R_(i) ", %16, " R_(i)
+#define T_MINIMUM3(i) "v_minimum3_f32 " R_(i) ", " R_(i) ", %16, " R_(i)
+#define T_BFI(i) "v_bfi_b32 " R_(i) ", " R_(i) ", %16, " R_(i)
+#define T_PKMAX16(i) "v_pk_max_f16 " R_(i) ", " R_(i) ", %16"
+#define T_MAXDPP(i) "v_max_f32_dpp " R_(i) ", %16, " R_(i) " quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
 
-// OP 0: v_maximum3_f32 (the networks' comparator half), 1: v_fma_f32; 16 independent chains, exactly
-// 16 VALU per iteration (inline asm: no compiler moves)
+constexpr int kOps = 11;
+static const char* kOpNames[kOps] = {"v_maximum3_f32", "v_minimum3_f32", "v_max3_f32", "v_med3_f32", "v_max_f32_e32",
+                                     "v_max_f32_e64", "v_max_f32_dpp", "v_fma_f32", "v_add_f32", "v_bfi_b32",
+                                     "v_pk_max_f16"};
+
 template <int OP>
 __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
   float r[16];
@@ -34,8 +49,17 @@ __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
   const float k = 0.5f + (float)(threadIdx.x & 1);
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int i = 0; i < iters; ++i) {
-    if constexpr (OP == 0) PR_V16("v_maximum3_f32");
-    else PR_V16("v_fma_f32");
+    if constexpr (OP == 0) PR_ASM16(T_MAXIMUM3);
+    else if constexpr (OP == 1) PR_ASM16(T_MINIMUM3);
+    else if constexpr (OP == 2) PR_ASM16(T_MAX3);
+    else if constexpr (OP == 3) PR_ASM16(T_MED3);
+    else if constexpr (OP == 4) PR_ASM16(T_MAX_E32);
+    else if constexpr (OP == 5) PR_ASM16(T_MAX_E64);
+    else if constexpr (OP == 6) PR_ASM16(T_MAXDPP);
+    else if constexpr (OP == 7) PR_ASM16(T_FMA);
+    else if constexpr (OP == 8) PR_ASM16(T_ADD);
+    else if constexpr (OP == 9) PR_ASM16(T_BFI);
+    else PR_ASM16(T_PKMAX16);
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   float z = 0.f;
@@ -43,6 +67,37 @@ __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
   for (int q = 0; q < 16; ++q) z += r[q];
   if (z == -12345.f) out[threadIdx.x] = z;
   if (threadIdx.x == 0 && blockIdx.x == 0) clk[0] = t1 - t0;
+}
+
+template <int OP>
+static void run_op(int cus, float* out, unsigned long long* clk, int iters, hipEvent_t e0, hipEvent_t e1) {
+  double us1 = 0;
+  for (int wps : {1, 2, 3, 4}) {
+    const int threads = 64 * 4 * wps;   // one workgroup per CU, wps waves per SIMD
+    std::vector<float> ts;
+    unsigned long long c = 0;
+    for (int r = 0; r < 5; ++r) {
+      (void)hipEventRecord(e0, 0);
+      hipLaunchKernelGGL(valu_kernel<OP>, dim3(cus), dim3(threads), 0, 0, out, clk, iters);
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      ts.push_back(ms);
+      (void)hipMemcpy(&c, clk, sizeof(c), hipMemcpyDeviceToHost);
+    }
+    if (hipGetLastError() != hipSuccess) {
+      printf("{\"op\": \"%s\", \"error\": true}\n", kOpNames[OP]);
+      return;
+    }
+    std::sort(ts.begin(), ts.end());
+    const double us = ts[2] * 1e3;
+    if (wps == 1) us1 = us;
+    // SIMD-level throughput relative to one wave alone: wps waves x the same work in `us`
+    printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"us\": %.1f, \"wave0_cycles_per_instr\": %.2f, "
+           "\"simd_throughput_vs_one_wave\": %.2f}\n",
+           kOpNames[OP], wps, us, (double)c / ((double)iters * 16), wps * us1 / us);
+  }
 }
 
 int main() {
@@ -57,30 +112,16 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  for (int op = 0; op < 2; ++op) {
-    for (int wps : {1, 2, 3, 4, 6, 8}) {
-      const int threads = 64 * 4 * wps;   // one workgroup per CU, wps waves per SIMD
-      auto k = op == 0 ? valu_kernel<0> : valu_kernel<1>;
-      std::vector<float> ts;
-      unsigned long long c = 0;
-      for (int r = 0; r < 5; ++r) {
-        (void)hipEventRecord(e0, 0);
-        hipLaunchKernelGGL(k, dim3(cus), dim3(threads), 0, 0, out, clk, iters);
-        (void)hipEventRecord(e1, 0);
-        (void)hipEventSynchronize(e1);
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, e0, e1);
-        ts.push_back(ms);
-        (void)hipMemcpy(&c, clk, sizeof(c), hipMemcpyDeviceToHost);
-      }
-      std::sort(ts.begin(), ts.end());
-      const double us = ts[2] * 1e3;
-      const double instr_per_wave = (double)iters * 16;   // 16 VALU per iteration
-      const double sclk_ghz = (double)c / (us * 1e3);     // shader cycles of wave 0 / wall us (approx)
-      const double cyc_per_simd_instr = (us * 1e3 * sclk_ghz) / (instr_per_wave * wps);
-      printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"us\": %.1f, \"sclk_ghz\": %.3f, \"cycles_per_wave_instr_at_simd\": %.2f}\n",
-             op == 0 ? "maximum3" : "fma", wps, us, sclk_ghz, cyc_per_simd_instr);
-    }
-  }
+  run_op<0>(cus, out, clk, iters, e0, e1);
+  run_op<1>(cus, out, clk, iters, e0, e1);
+  run_op<2>(cus, out, clk, iters, e0, e1);
+  run_op<3>(cus, out, clk, iters, e0, e1);
+  run_op<4>(cus, out, clk, iters, e0, e1);
+  run_op<5>(cus, out, clk, iters, e0, e1);
+  run_op<6>(cus, out, clk, iters, e0, e1);
+  run_op<7>(cus, out, clk, iters, e0, e1);
+  run_op<8>(cus, out, clk, iters, e0, e1);
+  run_op<9>(cus, out, clk, iters, e0, e1);
+  run_op<10>(cus, out, clk, iters, e0, e1);
   return 0;
 }
