@@ -1,6 +1,11 @@
 // pybind11 bindings of psana_ray_amd._C.  Device buffers and streams cross the boundary as
 // integers (tensor.data_ptr(), torch.cuda.current_stream().cuda_stream), so this module does
 // not depend on the torch C++ ABI; the Python layer validates shapes/dtypes/devices first.
+#include <execinfo.h>
+#include <signal.h>
+#include <stdlib.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <memory>
 
@@ -91,7 +96,31 @@ static FramePtrs make_ptrs(const std::vector<uint64_t>& in, const std::vector<ui
   return fp;
 }
 
+// Diagnostic (PSANA_RAY_AMD_SEGV_TRACE=1): a SIGSEGV prints the native stack first, then the
+// handler that was installed before (Python's faulthandler, or the default) runs on the re-fault.
+static struct sigaction g_prev_segv;
+static void segv_trace_handler(int sig, siginfo_t* info, void* uctx) {
+  (void)info;
+  (void)uctx;
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char hdr[] = "\n[psana_ray_amd] native stack at SIGSEGV:\n";
+  (void)!write(2, hdr, sizeof(hdr) - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  sigaction(sig, &g_prev_segv, nullptr);   // the faulting instruction re-runs into the old handler
+}
+static void maybe_install_segv_trace() {
+  const char* e = getenv("PSANA_RAY_AMD_SEGV_TRACE");
+  if (e == nullptr || e[0] != '1') return;
+  struct sigaction sa {};
+  sa.sa_sigaction = segv_trace_handler;
+  sa.sa_flags = SA_SIGINFO;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_prev_segv);
+}
+
 PYBIND11_MODULE(_C, m) {
+  maybe_install_segv_trace();
   m.doc() = "psana_ray_amd native extension: gfx950 HIP kernels + host runtime";
   m.attr("MAX_FRAMES_PER_LAUNCH") = pr::kMaxFrames;
   m.attr("KIND_EPIX10KA") = (int)pr::kEpix10ka;
