@@ -121,6 +121,7 @@ static void maybe_install_segv_trace() {
 
 PYBIND11_MODULE(_C, m) {
   maybe_install_segv_trace();
+  m.def("install_segv_trace", &maybe_install_segv_trace);
   m.doc() = "psana_ray_amd native extension: gfx950 HIP kernels + host runtime";
   m.attr("MAX_FRAMES_PER_LAUNCH") = pr::kMaxFrames;
   m.attr("KIND_EPIX10KA") = (int)pr::kEpix10ka;
@@ -251,13 +252,8 @@ PYBIND11_MODULE(_C, m) {
   // stop and join every fabric / engine thread still running (registered with atexit by the loader)
   m.def("halt_native_threads", &pr::halt_native_threads, py::call_guard<py::gil_scoped_release>());
   // streams with a chosen hardware-queue placement (streams.h); torch wraps them as ExternalStream
-  m.def("stream_create", [](int device, int kind) { return reinterpret_cast<uint64_t>(pr::make_stream(device, kind)); },
+  m.def("stream_create", [](int device, int kind) { return reinterpret_cast<uint64_t>(pr::acquire_stream(device, kind)); },
         py::arg("device"), py::arg("kind"));
-  m.def("stream_destroy", [](int device, uint64_t s) {
-        (void)hipSetDevice(device);
-        (void)hipStreamSynchronize(reinterpret_cast<hipStream_t>(s));
-        (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(s));
-      }, py::arg("device"), py::arg("stream"), py::call_guard<py::gil_scoped_release>());
   m.def("shm_remove", &pr::shm_remove, py::arg("name"));
   py::class_<pr::ShmRegion>(m, "ShmRegion", py::buffer_protocol())
       .def(py::init<const std::string&, int64_t, bool, double>(), py::arg("name"), py::arg("bytes"),

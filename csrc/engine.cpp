@@ -138,8 +138,8 @@ ProducerEngine::~ProducerEngine() {
   if (origin_) (void)hipEventDestroy(origin_);
   if (raw_bufs_) (void)hipFree(raw_bufs_);
   if (file_staging_) (void)hipHostFree(file_staging_);
-  if (h2d_) (void)hipStreamDestroy(h2d_);
-  for (auto cs : cstreams_) (void)hipStreamDestroy(cs);
+  release_stream(device_, stream_kind_, h2d_);
+  for (auto cs : cstreams_) release_stream(device_, stream_kind_, cs);
 }
 
 void ProducerEngine::set_compute_streams(int n, int kind) {
@@ -151,18 +151,16 @@ void ProducerEngine::set_compute_streams(int n, int kind) {
   }
   if (plan_.mode == kPlanImageScratch) n = 1;   // one scratch buffer: never two launches in flight
   hip_check(hipSetDevice(device_), "hipSetDevice");
-  for (auto cs : cstreams_) {
-    (void)hipStreamSynchronize(cs);
-    (void)hipStreamDestroy(cs);
-  }
+  for (auto cs : cstreams_) release_stream(device_, stream_kind_, cs);
   cstreams_.clear();
-  for (int i = 0; i < n; ++i) cstreams_.push_back(make_stream(device_, kind));
+  const int old_kind = stream_kind_;
+  stream_kind_ = kind;
+  for (int i = 0; i < n; ++i) cstreams_.push_back(acquire_stream(device_, kind));
   compute_ = cstreams_[0];
   // the staging copies get the same placement: a copy stream multiplexed onto a queue that runs
   // calibration or peak-finder kernels would wait behind them and idle the PCIe link
-  (void)hipStreamSynchronize(h2d_);
-  (void)hipStreamDestroy(h2d_);
-  h2d_ = make_stream(device_, kind);
+  release_stream(device_, old_kind, h2d_);
+  h2d_ = acquire_stream(device_, kind);
 }
 
 void ProducerEngine::set_cycled_source(const std::vector<uint64_t>& frames, const std::vector<double>& pe) {

@@ -137,6 +137,7 @@ class ProducerEngine {
   std::vector<std::vector<std::pair<int64_t, double>>> buf_meta_;   // per raw buffer: (gevt, pe)
   hipStream_t h2d_ = nullptr, compute_ = nullptr;   // compute_ == cstreams_[0]
   std::vector<hipStream_t> cstreams_;
+  int stream_kind_ = 0;   // placement of cstreams_ and h2d_ (streams.h): the constructor's are ordinary
   std::vector<hipEvent_t> buf_free_, h2d_done_;
   // optional GPU timing: start events per raw buffer, harvested (non-blocking) when the buffer is
   // reused or at the end of the run

@@ -1,5 +1,8 @@
 #include "streams.h"
 
+#include <map>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "common.h"
@@ -25,6 +28,42 @@ hipStream_t make_stream(int device, int kind) {
     hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   }
   return s;
+}
+
+namespace {
+std::mutex& pool_mu() {
+  static std::mutex* m = new std::mutex();   // leaked: used by destructors at process exit
+  return *m;
+}
+std::map<std::pair<int, int>, std::vector<hipStream_t>>& pool() {
+  static auto* p = new std::map<std::pair<int, int>, std::vector<hipStream_t>>();
+  return *p;
+}
+}  // namespace
+
+hipStream_t acquire_stream(int device, int kind) {
+  if (kind != kStreamShared) {
+    std::lock_guard<std::mutex> lk(pool_mu());
+    auto& v = pool()[{device, kind}];
+    if (!v.empty()) {
+      hipStream_t s = v.back();
+      v.pop_back();
+      return s;
+    }
+  }
+  return make_stream(device, kind);
+}
+
+void release_stream(int device, int kind, hipStream_t s) {
+  if (s == nullptr) return;
+  (void)hipSetDevice(device);
+  (void)hipStreamSynchronize(s);
+  if (kind == kStreamShared) {
+    (void)hipStreamDestroy(s);
+    return;
+  }
+  std::lock_guard<std::mutex> lk(pool_mu());
+  pool()[{device, kind}].push_back(s);
 }
 
 }  // namespace pr

@@ -16,5 +16,10 @@ namespace pr {
 
 enum StreamKind { kStreamShared = 0, kStreamDedicated = 1, kStreamHighPriority = 2 };
 hipStream_t make_stream(int device, int kind);
+// Streams with a placement (dedicated / high priority) come from a process-wide pool per (device,
+// kind) and go back to it: a hardware queue of its own is a scarce per-process resource, and such
+// streams are never destroyed while the process runs.  Ordinary streams are created and destroyed.
+hipStream_t acquire_stream(int device, int kind);
+void release_stream(int device, int kind, hipStream_t s);   // synchronises s first
 
 }  // namespace pr

@@ -58,6 +58,7 @@ def on_exit(obj) -> None:
 
 
 def _shutdown(mod) -> None:
+    mod.install_segv_trace()   # diagnostic (PSANA_RAY_AMD_SEGV_TRACE=1): after test runners restored theirs
     for obj in list(_exit_hooks or ()):
         try:
             obj.stop_at_exit()
