@@ -282,23 +282,27 @@ class ProducerPipeline:
         return self.frames
 
 
-# Native streams with a hardware-queue placement, per (device, kind): created once, handed back
-# here when their torch wrapper is collected and handed out again -- never destroyed while the
-# process runs.  Tensors allocated on a stream keep its handle in torch's caching allocator after
-# the wrapper is gone, so destroying the native stream could leave the allocator a dangling handle;
-# and every CU-masked stream is a hardware queue of its own, so reuse also bounds their number.
+# Native streams with a hardware-queue placement, per (device, kind): created once (a native pool,
+# csrc/streams.h), handed back here when their OWNER is collected and handed out again -- never
+# destroyed while the process runs.  Tensors allocated on a stream keep its handle in torch's
+# caching allocator after the wrapper is gone, so destroying the native stream could leave the
+# allocator a dangling handle; and every CU-masked stream is a hardware queue of its own, so reuse
+# also bounds their number.  No weak reference ever points at a torch stream object: torch's stream
+# type does not clear weak references when it is freed, and a weakref left behind crashed the
+# interpreter's final garbage collection (_PyWeakref_ClearRef, rc 139 after a passing GPU suite).
 _STREAM_POOL: dict = {}
 _STREAM_POOL_LOCK = threading.Lock()
 
 
-def _return_stream(key, h: int):
+def _return_streams(key, handles):
     with _STREAM_POOL_LOCK:
-        _STREAM_POOL.setdefault(key, []).append(h)
+        _STREAM_POOL.setdefault(key, []).extend(handles)
 
 
-def _make_streams(device, n: int, kind: str):
+def _make_streams(device, n: int, kind: str, owner=None):
     """n torch streams with the given hardware-queue placement (config.STREAM_KINDS), from the
-    process-wide pool of native streams (see _STREAM_POOL)."""
+    process-wide pool of native streams (see _STREAM_POOL); they go back to the pool when ``owner``
+    (a plain Python object) is collected."""
     if STREAM_KINDS[kind] == 0:
         return [torch.cuda.Stream(device=device) for _ in range(n)]
     import weakref
@@ -306,17 +310,18 @@ def _make_streams(device, n: int, kind: str):
     C = _ext.load()
     dev = device.index if device.index is not None else torch.cuda.current_device()
     key = (dev, STREAM_KINDS[kind])
-    out = []
+    out, handles = [], []
     for _ in range(n):
         with _STREAM_POOL_LOCK:
             free = _STREAM_POOL.setdefault(key, [])
             h = free.pop() if free else None
         if h is None:
             h = int(C.stream_create(dev, STREAM_KINDS[kind]))
-        st = torch.cuda.ExternalStream(h, device=device)
-        fin = weakref.finalize(st, _return_stream, key, h)
+        handles.append(h)
+        out.append(torch.cuda.ExternalStream(h, device=device))
+    if owner is not None:
+        fin = weakref.finalize(owner, _return_streams, key, handles)
         fin.atexit = False
-        out.append(st)
     return out
 
 
@@ -340,7 +345,7 @@ class PeakFinderConsumer:
         self.keep_results = keep_results
         self.results = []
         if self.gpu:
-            self.streams = _make_streams(self.device, 2, stream_kind)
+            self.streams = _make_streams(self.device, 2, stream_kind, owner=self)
             self.stream = self.streams[0]
             B = self.batch
             self._nbuf = 4   # even: buffer k % 4 is reused by launch k + 4, on the same stream as k
