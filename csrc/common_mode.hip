@@ -65,6 +65,11 @@
 #ifndef PR_CM_EPIX_BLOCK
 #define PR_CM_EPIX_BLOCK 256
 #endif
+// Fast paths for 8-pixel groups without a gain-switched pixel (epix10ka): decode and store skip
+// the per-pixel gain-bit masks and table selects (v_bfe / v_bfi: single-rate VALU on gfx950).
+#ifndef PR_CM_FASTDEC
+#define PR_CM_FASTDEC 0
+#endif
 #ifndef PR_CM_SPREAD
 #define PR_CM_SPREAD 0
 #endif
@@ -482,6 +487,13 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = xv[j] != xv[j] ? v[j] : xv[j];
   }
+#if PR_CM_FASTDEC
+  if (NT == 2 && cb == 0u) {   // no switched pixel: every gain factor from table 0, no selects
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = gmul(xv[j], ga[0][j]);
+    return;
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = gmul(xv[j], cm_gain<NT>(ga, cb, j));
 }
@@ -930,12 +942,26 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
     float v[8];
     uint32_t el = 0xFFu, cb = 0;
     if (act) {
-      float pa[NT][8];
+#if PR_CM_FASTDEC
+      if (KIND == kEpix10ka && ((rw[u].x | rw[u].y | rw[u].z | rw[u].w) & 0x40004000u) == 0u) {
+        // no pixel of the group switched gain (the common case: only bright pixels switch): every
+        // pixel is candidate 0 -- no gain-bit masks, no pedestal select, no second table
+        const uint32_t w4[4] = {rw[u].x, rw[u].y, rw[u].z, rw[u].w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pa[0][j] = pa0[u][0][j];
-      if constexpr (NT > 1)
-        load8<NT>(ped, tg.npix, base + (int64_t)r * tg.panel_cols + c, need_from_raw<NT>(rw[u]), pa, 1);
-      cm_decode8<KIND, NT>(rw[u], ep[u], pa, v, el, cb);
+        for (int j = 0; j < 8; ++j)
+          v[j] = (float)__builtin_amdgcn_ubfe(w4[j >> 1], 16 * (j & 1), 14) - pa0[u][0][j];
+        el = ep[u] & 0xFFu;
+        cb = 0;
+      } else
+#endif
+      {
+        float pa[NT][8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pa[0][j] = pa0[u][0][j];
+        if constexpr (NT > 1)
+          load8<NT>(ped, tg.npix, base + (int64_t)r * tg.panel_cols + c, need_from_raw<NT>(rw[u]), pa, 1);
+        cm_decode8<KIND, NT>(rw[u], ep[u], pa, v, el, cb);
+      }
       float x[8];
       cm_tile_values(v, el, x);
       float* trow = tile + r * P + c;

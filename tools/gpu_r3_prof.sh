@@ -21,3 +21,6 @@ for m in calib image; do
   tail -1 $O/prof_$m.log | cut -c1-150
 done
 du -sh $O
+timeout -k 10 120 $R/tools/valu_rate_bin > $O/valu_rate2.jsonl 2>&1 || exit $?
+cat $O/valu_rate2.jsonl | grep -E "cvt|bfe|and_or|cndmask|mul|mov|xor|sub|perm"
+VARIANTS="fastdec" TESTK="common_mode or image" BENCH=1 BENCH_ROUNDS=2 bash $R/tools/gpu_cm_ab.sh || exit $?

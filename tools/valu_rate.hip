@@ -34,12 +34,22 @@
 #define T_MINIMUM3(i) "v_minimum3_f32 " R_(i) ", " R_(i) ", %16, " R_(i)
 #define T_BFI(i) "v_bfi_b32 " R_(i) ", " R_(i) ", %16, " R_(i)
 #define T_PKMAX16(i) "v_pk_max_f16 " R_(i) ", " R_(i) ", %16"
+#define T_CVT(i) "v_cvt_f32_u32 " R_(i) ", " R_(i)
+#define T_BFE(i) "v_bfe_u32 " R_(i) ", " R_(i) ", 3, 14"
+#define T_ANDOR(i) "v_and_or_b32 " R_(i) ", " R_(i) ", %16, " R_(i)
+#define T_CNDMASK(i) "v_cndmask_b32 " R_(i) ", " R_(i) ", %16, vcc"
+#define T_MUL(i) "v_mul_f32 " R_(i) ", %16, " R_(i)
+#define T_MOV(i) "v_mov_b32 " R_(i) ", %16"
+#define T_XOR(i) "v_xor_b32 " R_(i) ", %16, " R_(i)
+#define T_SUB(i) "v_sub_f32 " R_(i) ", %16, " R_(i)
+#define T_PERM(i) "v_perm_b32 " R_(i) ", " R_(i) ", %16, %16"
 #define T_MAXDPP(i) "v_max_f32_dpp " R_(i) ", %16, " R_(i) " quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
 
-constexpr int kOps = 11;
+constexpr int kOps = 20;
 static const char* kOpNames[kOps] = {"v_maximum3_f32", "v_minimum3_f32", "v_max3_f32", "v_med3_f32", "v_max_f32_e32",
                                      "v_max_f32_e64", "v_max_f32_dpp", "v_fma_f32", "v_add_f32", "v_bfi_b32",
-                                     "v_pk_max_f16"};
+                                     "v_pk_max_f16", "v_cvt_f32_u32", "v_bfe_u32", "v_and_or_b32", "v_cndmask_b32",
+                                     "v_mul_f32", "v_mov_b32", "v_xor_b32", "v_sub_f32", "v_perm_b32"};
 
 template <int OP>
 __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
@@ -59,7 +69,16 @@ __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
     else if constexpr (OP == 7) PR_ASM16(T_FMA);
     else if constexpr (OP == 8) PR_ASM16(T_ADD);
     else if constexpr (OP == 9) PR_ASM16(T_BFI);
-    else PR_ASM16(T_PKMAX16);
+    else if constexpr (OP == 10) PR_ASM16(T_PKMAX16);
+    else if constexpr (OP == 11) PR_ASM16(T_CVT);
+    else if constexpr (OP == 12) PR_ASM16(T_BFE);
+    else if constexpr (OP == 13) PR_ASM16(T_ANDOR);
+    else if constexpr (OP == 14) PR_ASM16(T_CNDMASK);
+    else if constexpr (OP == 15) PR_ASM16(T_MUL);
+    else if constexpr (OP == 16) PR_ASM16(T_MOV);
+    else if constexpr (OP == 17) PR_ASM16(T_XOR);
+    else if constexpr (OP == 18) PR_ASM16(T_SUB);
+    else PR_ASM16(T_PERM);
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   float z = 0.f;
@@ -123,5 +142,14 @@ int main() {
   run_op<8>(cus, out, clk, iters, e0, e1);
   run_op<9>(cus, out, clk, iters, e0, e1);
   run_op<10>(cus, out, clk, iters, e0, e1);
+  run_op<11>(cus, out, clk, iters, e0, e1);
+  run_op<12>(cus, out, clk, iters, e0, e1);
+  run_op<13>(cus, out, clk, iters, e0, e1);
+  run_op<14>(cus, out, clk, iters, e0, e1);
+  run_op<15>(cus, out, clk, iters, e0, e1);
+  run_op<16>(cus, out, clk, iters, e0, e1);
+  run_op<17>(cus, out, clk, iters, e0, e1);
+  run_op<18>(cus, out, clk, iters, e0, e1);
+  run_op<19>(cus, out, clk, iters, e0, e1);
   return 0;
 }
