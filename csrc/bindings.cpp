@@ -254,6 +254,10 @@ PYBIND11_MODULE(_C, m) {
   // streams with a chosen hardware-queue placement (streams.h); torch wraps them as ExternalStream
   m.def("stream_create", [](int device, int kind) { return reinterpret_cast<uint64_t>(pr::acquire_stream(device, kind)); },
         py::arg("device"), py::arg("kind"));
+  m.def("stream_release", [](int device, int kind, uint64_t s) {
+        pr::release_stream(device, kind, reinterpret_cast<hipStream_t>(s)); },
+        py::arg("device"), py::arg("kind"), py::arg("stream"), py::call_guard<py::gil_scoped_release>());
+  m.def("close_stream_pool", &pr::close_stream_pool, py::call_guard<py::gil_scoped_release>());
   m.def("shm_remove", &pr::shm_remove, py::arg("name"));
   py::class_<pr::ShmRegion>(m, "ShmRegion", py::buffer_protocol())
       .def(py::init<const std::string&, int64_t, bool, double>(), py::arg("name"), py::arg("bytes"),

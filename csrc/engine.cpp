@@ -223,7 +223,8 @@ bool ProducerEngine::join(double timeout_s) {
     if (timeout_s >= 0 && std::chrono::steady_clock::now() >= t_end) return false;
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
-  thread_.join();
+  std::lock_guard<std::mutex> lk(halt_mu_);   // never two joins of one thread (halt() at exit)
+  if (thread_.joinable()) thread_.join();
   return true;
 }
 

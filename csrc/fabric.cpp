@@ -1356,7 +1356,8 @@ bool QueueFabric::join(double timeout_s) {
     if (timeout_s >= 0 && now_s() - t0 > timeout_s) return false;
     nap_ns(1000000);
   }
-  th_.join();
+  std::lock_guard<std::mutex> lk(halt_mu_);   // never two joins of one thread (halt() at exit)
+  if (th_.joinable()) th_.join();
   return true;
 }
 

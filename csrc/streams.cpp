@@ -54,16 +54,39 @@ hipStream_t acquire_stream(int device, int kind) {
   return make_stream(device, kind);
 }
 
+static bool& pool_closed() {
+  static bool* c = new bool(false);
+  return *c;
+}
+
 void release_stream(int device, int kind, hipStream_t s) {
   if (s == nullptr) return;
   (void)hipSetDevice(device);
   (void)hipStreamSynchronize(s);
-  if (kind == kStreamShared) {
-    (void)hipStreamDestroy(s);
-    return;
+  {
+    std::lock_guard<std::mutex> lk(pool_mu());
+    if (kind != kStreamShared && !pool_closed()) {
+      pool()[{device, kind}].push_back(s);
+      return;
+    }
   }
-  std::lock_guard<std::mutex> lk(pool_mu());
-  pool()[{device, kind}].push_back(s);
+  (void)hipStreamDestroy(s);
+}
+
+void close_stream_pool() {
+  std::map<std::pair<int, int>, std::vector<hipStream_t>> all;
+  {
+    std::lock_guard<std::mutex> lk(pool_mu());
+    pool_closed() = true;
+    all.swap(pool());
+  }
+  for (auto& kv : all) {
+    (void)hipSetDevice(kv.first.first);
+    for (hipStream_t s : kv.second) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+  }
 }
 
 }  // namespace pr

@@ -21,5 +21,9 @@ hipStream_t make_stream(int device, int kind);
 // streams are never destroyed while the process runs.  Ordinary streams are created and destroyed.
 hipStream_t acquire_stream(int device, int kind);
 void release_stream(int device, int kind, hipStream_t s);   // synchronises s first
+// Process exit (after the native threads halted): destroy the pooled streams; streams released
+// afterwards are destroyed at once.  Leaves no queue of ours to the runtime's static teardown, which
+// a profiler's own teardown (rocprofv3) does not survive.
+void close_stream_pool();
 
 }  // namespace pr

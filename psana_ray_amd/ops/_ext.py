@@ -65,6 +65,15 @@ def _shutdown(mod) -> None:
         except Exception:  # noqa: BLE001 - best effort at exit
             pass
     mod.halt_native_threads()
+    # pooled dedicated streams: Python's idle handles back to the native pool, then the pool is
+    # destroyed (no queue of ours is left for the runtime's static teardown)
+    try:
+        from .. import pipeline
+
+        pipeline._release_idle_streams(mod)
+    except Exception:  # noqa: BLE001 - best effort at exit
+        pass
+    mod.close_stream_pool()
 
 
 def available() -> bool:

@@ -299,6 +299,15 @@ def _return_streams(key, handles):
         _STREAM_POOL.setdefault(key, []).extend(handles)
 
 
+def _release_idle_streams(C):
+    """Process exit: the idle pooled handles go back to the native pool (csrc/streams.h)."""
+    with _STREAM_POOL_LOCK:
+        items = [(k, h) for k, hs in _STREAM_POOL.items() for h in hs]
+        _STREAM_POOL.clear()
+    for (dev, kind), h in items:
+        C.stream_release(dev, kind, h)
+
+
 def _make_streams(device, n: int, kind: str, owner=None):
     """n torch streams with the given hardware-queue placement (config.STREAM_KINDS), from the
     process-wide pool of native streams (see _STREAM_POOL); they go back to the pool when ``owner``
