@@ -67,6 +67,10 @@
 #endif
 // Fast paths for 8-pixel groups without a gain-switched pixel (epix10ka): decode and store skip
 // the per-pixel gain-bit masks and table selects (v_bfe / v_bfi: single-rate VALU on gfx950).
+// Lean fused-image placement loop (A/B build)
+#ifndef PR_CM_PLACE2
+#define PR_CM_PLACE2 0
+#endif
 #ifndef PR_CM_FASTDEC
 #define PR_CM_FASTDEC 0
 #endif
@@ -589,6 +593,51 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
   // chunks (64 B of image) of 16 neighbouring columns -- LDS reads 2-way instead of 32-way
   // bank-conflicted, global stores 16 segments of 64 B.  The (run, chunk) walk is incremental (one
   // integer division per thread, not per chunk).
+#if PR_CM_PLACE2
+  // Lean form: one loop per layout (no per-item selects on the uniform `rows`), tile and image
+  // addresses linear in (run, chunk) with the direction folded into a signed stride, 32-bit image
+  // offsets (the image is < 2^31 elements; Geometry.panel_placement).  Same (run, chunk) per thread
+  // sequence as the general form below.
+  if (nfull > 0) {
+    const float* tb = tile + (step > 0 ? t_lo : len - 1 - t_lo) * ie;   // element t_lo of run 0
+    const int32_t ob = (int32_t)((lo & ~(int64_t)3) + 4 * ch_lo);      // chunk 0 of run 0
+    const int32_t oo = (int32_t)outer;
+    if (rows) {
+      // items e = tid + nb * i over (run, chunk) run-major: consecutive lanes, consecutive chunks
+      int run = (int)threadIdx.x / nfull, k = (int)threadIdx.x - run * nfull;
+      const int drun = nb / nfull, dk = nb - drun * nfull;
+      for (; run < nruns;) {
+        const float* tp = tb + run * P + 4 * k * di;
+        st_f4((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)), make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
+        run += drun;
+        k += dk;
+        if (k >= nfull) {
+          k -= nfull;
+          ++run;
+        }
+      }
+    } else {
+      // a wave takes 4 chunks (64 B of image) of 16 neighbouring columns (see the general form)
+      const int per = 4 * nruns, nq = (nfull + 3) >> 2;
+      int a = (int)threadIdx.x / per, w = (int)threadIdx.x - a * per;
+      const int da = nb / per, dw = nb - da * per;
+      for (; a < nq;) {
+        const int run = w >> 2, k = 4 * a + (w & 3);
+        if (k < nfull) {
+          const float* tp = tb + run + 4 * k * di;
+          st_f4((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)),
+                make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
+        }
+        a += da;
+        w += dw;
+        if (w >= per) {
+          w -= per;
+          ++a;
+        }
+      }
+    }
+  }
+#else
   if (nfull > 0) {
     const int span = rows ? nfull : ((nfull + 3) >> 2) * 4;   // work items per run (column case: padded)
     const int per = rows ? nfull : 4 * nruns;
@@ -612,6 +661,7 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
       }
     }
   }
+#endif
   // ragged elements: n_rag per run, the same for every run
   const int n_head = t_lo, n_rag = t_lo + (len - t_hi);
   if (n_rag > 0) {
