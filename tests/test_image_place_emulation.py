@@ -52,6 +52,12 @@ def _place_tile(writes, P, R, C, desc, y0, x0, nb=256):
                 if k < nfull:
                     base = (lo & ~3) + run * outer + 4 * (ch_lo + k)
                     assert base % 4 == 0
+                    # the lean form (PR_CM_PLACE2): linear in (run, chunk), signed tile stride
+                    ob = (lo & ~3) + 4 * ch_lo
+                    assert ob + run * outer + 4 * k == base
+                    t0 = t_lo + 4 * k
+                    i_lean = (t_lo if step > 0 else ln - 1 - t_lo) + 4 * k * (1 if step > 0 else -1)
+                    assert i_lean == (t0 if step > 0 else ln - 1 - t0)
                     for q in range(4):
                         r, c = tile_rc(run, t_lo + 4 * k + q)
                         out.append((base + q, r, c, True))
