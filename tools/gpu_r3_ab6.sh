@@ -25,3 +25,9 @@ for r in 1 2; do
     python3 -c "import json;d=json.load(open('$O/dev_image_${v}_$r.json'));print('$v dev image r$r', d['value'])"
   done
 done
+# peak finder at rising candidate densities (thr_peak lowered): the overflow path's cost
+cd $R
+for t in 20 8 5 3; do
+  PYTHONPATH=$R timeout -k 10 200 python3 tools/pf_probe.py --repeat 1 --thr $t > $O/pf_thr$t.log 2>&1 || exit $?
+  tail -1 $O/pf_thr$t.log
+done

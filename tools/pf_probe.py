@@ -77,7 +77,10 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) / 8)
         ts.sort()
+        above = float(ref_sum[0, 0])
         res = {"run": var, "frames": F, "same_counts": same, "peaks_frame0": int(ref_counts[0]),
+               "thr_peak": float(pp.thr_peak), "above_thr_frame0": int(above),
+               "candidate_density": round(above / float(P * H * W), 5),
                "us_per_frame": round(1e3 * ts[len(ts) // 2] / F, 3)}
         line = json.dumps(res)
         print(line, flush=True)
