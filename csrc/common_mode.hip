@@ -69,7 +69,7 @@
 // the per-pixel gain-bit masks and table selects (v_bfe / v_bfi: single-rate VALU on gfx950).
 // Lean fused-image placement loop (A/B build)
 #ifndef PR_CM_PLACE2
-#define PR_CM_PLACE2 0
+#define PR_CM_PLACE2 1
 #endif
 #ifndef PR_CM_FASTDEC
 #define PR_CM_FASTDEC 0

@@ -51,55 +51,81 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
   for (int dy = -H; dy <= H; ++dy)
 #pragma unroll
     for (int dx = -H; dx <= H; ++dx) w[dy + H][dx + H] = (dy == 0 && dx == 0) ? v : at(dy, dx);
+  float bkg = 0.0f, noise = 0.0f, snr = 0.0f, inten = 0.0f;
+  auto accept = [&]() -> bool {
 #pragma unroll
-  for (int dy = -RAD; dy <= RAD; ++dy)
+    for (int dy = -RAD; dy <= RAD; ++dy)
 #pragma unroll
-    for (int dx = -RAD; dx <= RAD; ++dx) {
-      if (dy == 0 && dx == 0) continue;
-      const float n = w[dy + H][dx + H];
-      if (n != n) continue;
-      const bool before = (dy < 0) || (dy == 0 && dx < 0);
-      if (before ? !(v > n) : !(v >= n)) return;   // not the strict local max (ties: lower index wins)
+      for (int dx = -RAD; dx <= RAD; ++dx) {
+        if (dy == 0 && dx == 0) continue;
+        const float n = w[dy + H][dx + H];
+        if (n != n) continue;
+        const bool before = (dy < 0) || (dy == 0 && dx < 0);
+        if (before ? !(v > n) : !(v >= n)) return false;   // not the strict local max (ties: lower index wins)
+      }
+    float s = 0.0f, s2 = 0.0f;
+    int nr = 0;
+#pragma unroll
+    for (int dy = -H; dy <= H; ++dy)
+#pragma unroll
+      for (int dx = -H; dx <= H; ++dx) {
+        const int d = max(abs(dy), abs(dx));
+        if (d <= RAD) continue;
+        const float n = w[dy + H][dx + H];
+        if (n != n) continue;
+        s += n;
+        s2 += n * n;
+        ++nr;
+      }
+    bkg = nr > 0 ? s / nr : 0.0f;
+    const float var = nr > 0 ? fmaxf(s2 / nr - bkg * bkg, 0.0f) : 0.0f;
+    noise = sqrtf(var);
+    snr = (v - bkg) / fmaxf(noise, 1e-6f);
+    if (snr < pp.son_min) return false;
+#pragma unroll
+    for (int dy = -RAD; dy <= RAD; ++dy)
+#pragma unroll
+      for (int dx = -RAD; dx <= RAD; ++dx) {
+        const float n = w[dy + H][dx + H];
+        if (n == n) inten += n - bkg;
+      }
+    return true;
+  };
+  // Record slots: ONE atomic per (wave, frame) among the lanes here that accepted a peak, not one
+  // per peak -- same-address atomics serialise (~3 ns each), and a hit-rich frame (2 % of its
+  // pixels above threshold: ~32k peaks) spent ~90 us/frame in them.  Slot order within a frame is
+  // not part of the output contract (counts, and the records as a set).
+  bool pending = accept();
+  const int lane = (int)(threadIdx.x & 63);
+  for (;;) {
+    const uint64_t m = __ballot(pending);
+    if (m == 0) break;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const int f0 = __shfl(f, leader);
+    const uint64_t mf = __ballot(pending && f == f0);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counts + f0, __popcll(mf));
+    base = __shfl(base, leader);
+    int slot = 0;
+    if (pending && f == f0) {
+      slot = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf, 0u));
+      pending = false;
+      if (slot < pp.max_peaks) {
+        float* rec = peaks + ((int64_t)f * pp.max_peaks + slot) * 8;
+        rec[0] = (float)panel;
+        rec[1] = (float)gy;
+        rec[2] = (float)gx;
+        rec[3] = v;
+        rec[4] = inten;
+        rec[5] = bkg;
+        rec[6] = noise;
+        rec[7] = snr;
+      }
     }
-  float s = 0.0f, s2 = 0.0f;
-  int nr = 0;
-#pragma unroll
-  for (int dy = -H; dy <= H; ++dy)
-#pragma unroll
-    for (int dx = -H; dx <= H; ++dx) {
-      const int d = max(abs(dy), abs(dx));
-      if (d <= RAD) continue;
-      const float n = w[dy + H][dx + H];
-      if (n != n) continue;
-      s += n;
-      s2 += n * n;
-      ++nr;
+    if (total != nullptr) {   // records written by this group (slots below max_peaks)
+      const uint64_t wr = __ballot((mf >> lane) & 1ull && slot < pp.max_peaks);
+      if (lane == leader && wr != 0) atomicAdd(total, (unsigned long long)__popcll(wr));
     }
-  const float bkg = nr > 0 ? s / nr : 0.0f;
-  const float var = nr > 0 ? fmaxf(s2 / nr - bkg * bkg, 0.0f) : 0.0f;
-  const float noise = sqrtf(var);
-  const float snr = (v - bkg) / fmaxf(noise, 1e-6f);
-  if (snr < pp.son_min) return;
-  float inten = 0.0f;
-#pragma unroll
-  for (int dy = -RAD; dy <= RAD; ++dy)
-#pragma unroll
-    for (int dx = -RAD; dx <= RAD; ++dx) {
-      const float n = w[dy + H][dx + H];
-      if (n == n) inten += n - bkg;
-    }
-  const int slot = atomicAdd(counts + f, 1);
-  if (slot < pp.max_peaks) {
-    if (total != nullptr) atomicAdd(total, 1ull);
-    float* rec = peaks + ((int64_t)f * pp.max_peaks + slot) * 8;
-    rec[0] = (float)panel;
-    rec[1] = (float)gy;
-    rec[2] = (float)gx;
-    rec[3] = v;
-    rec[4] = inten;
-    rec[5] = bkg;
-    rec[6] = noise;
-    rec[7] = snr;
   }
 }
 
