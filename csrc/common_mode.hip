@@ -65,18 +65,6 @@
 #ifndef PR_CM_EPIX_BLOCK
 #define PR_CM_EPIX_BLOCK 256
 #endif
-// Fast paths for 8-pixel groups without a gain-switched pixel (epix10ka): decode and store skip
-// the per-pixel gain-bit masks and table selects (v_bfe / v_bfi: single-rate VALU on gfx950).
-// Lean fused-image placement loop (A/B build)
-#ifndef PR_CM_PLACE2
-#define PR_CM_PLACE2 1
-#endif
-#ifndef PR_CM_FASTDEC
-#define PR_CM_FASTDEC 0
-#endif
-#ifndef PR_CM_SPREAD
-#define PR_CM_SPREAD 0
-#endif
 #ifndef PR_CM_EPIX_WG_PER_CU
 #define PR_CM_EPIX_WG_PER_CU ((PR_CM_FPW > 1 || PR_CM_GPRE) ? 3 : 4)
 #endif
@@ -491,13 +479,6 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = xv[j] != xv[j] ? v[j] : xv[j];
   }
-#if PR_CM_FASTDEC
-  if (NT == 2 && cb == 0u) {   // no switched pixel: every gain factor from table 0, no selects
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = gmul(xv[j], ga[0][j]);
-    return;
-  }
-#endif
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = gmul(xv[j], cm_gain<NT>(ga, cb, j));
 }
@@ -593,11 +574,10 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
   // chunks (64 B of image) of 16 neighbouring columns -- LDS reads 2-way instead of 32-way
   // bank-conflicted, global stores 16 segments of 64 B.  The (run, chunk) walk is incremental (one
   // integer division per thread, not per chunk).
-#if PR_CM_PLACE2
-  // Lean form: one loop per layout (no per-item selects on the uniform `rows`), tile and image
-  // addresses linear in (run, chunk) with the direction folded into a signed stride, 32-bit image
-  // offsets (the image is < 2^31 elements; Geometry.panel_placement).  Same (run, chunk) per thread
-  // sequence as the general form below.
+  // One loop per layout (no per-item selects on the uniform `rows`), tile and image addresses
+  // linear in (run, chunk) with the direction folded into a signed stride, 32-bit image offsets
+  // (the image is < 2^31 elements; Geometry.panel_placement): 6.85-6.91 vs 7.04-7.07 us/frame for
+  // the round-2 loop with per-item selects (profiles/r3/image/place2_ab/).
   if (nfull > 0) {
     const float* tb = tile + (step > 0 ? t_lo : len - 1 - t_lo) * ie;   // element t_lo of run 0
     const int32_t ob = (int32_t)((lo & ~(int64_t)3) + 4 * ch_lo);      // chunk 0 of run 0
@@ -637,31 +617,6 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
       }
     }
   }
-#else
-  if (nfull > 0) {
-    const int span = rows ? nfull : ((nfull + 3) >> 2) * 4;   // work items per run (column case: padded)
-    const int per = rows ? nfull : 4 * nruns;
-    int a = (int)threadIdx.x / per, w = (int)threadIdx.x - a * per;
-    // rows: (a = run, w = chunk); columns: (a = chunk quad, w = 4 * run + chunk within the quad)
-    const int da = nb / per, dw = nb - da * per;
-    const int outer_n = rows ? nruns : (span >> 2);
-    for (; a < outer_n;) {
-      const int run = rows ? a : (w >> 2);
-      const int k = rows ? w : 4 * a + (w & 3);         // full chunk index from ch_lo
-      if (k < nfull) {
-        const int64_t base = (lo & ~(int64_t)3) + (int64_t)run * outer + 4 * (ch_lo + k);
-        const float* tp = tile_at(run, t_lo + 4 * k);
-        st_f4((PR_GLOBAL float4*)(out + base), make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
-      }
-      a += da;
-      w += dw;
-      if (w >= per) {
-        w -= per;
-        ++a;
-      }
-    }
-  }
-#endif
   // ragged elements: n_rag per run, the same for every run
   const int n_head = t_lo, n_rag = t_lo + (len - t_hi);
   if (n_rag > 0) {
@@ -992,18 +947,6 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
     float v[8];
     uint32_t el = 0xFFu, cb = 0;
     if (act) {
-#if PR_CM_FASTDEC
-      if (KIND == kEpix10ka && ((rw[u].x | rw[u].y | rw[u].z | rw[u].w) & 0x40004000u) == 0u) {
-        // no pixel of the group switched gain (the common case: only bright pixels switch): every
-        // pixel is candidate 0 -- no gain-bit masks, no pedestal select, no second table
-        const uint32_t w4[4] = {rw[u].x, rw[u].y, rw[u].z, rw[u].w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          v[j] = (float)__builtin_amdgcn_ubfe(w4[j >> 1], 16 * (j & 1), 14) - pa0[u][0][j];
-        el = ep[u] & 0xFFu;
-        cb = 0;
-      } else
-#endif
       {
         float pa[NT][8];
 #pragma unroll
@@ -1074,11 +1017,6 @@ __device__ __forceinline__ void cm_rows(float* tile, const int P, const int R, c
     constexpr int PA = (L & 1) ? (L - 1) / 2 : L / 2 - 1;
     constexpr int PB = PA + 1;
     select_regs<L, PA, PB>(x);
-#ifdef PR_CM_PROBE_ROWS_TWICE
-    // timing probe only (VALU sensitivity): the row network applied a second time -- the median
-    // positions are unchanged, the instruction count of the row phase doubles
-    select_regs<L, PA, PB>(x);
-#endif
     asm volatile("" ::: "memory");
     // toggle padding: L even -> odd count: x[L/2], even: mean of x[L/2-1], x[L/2];
     //                 L odd  -> odd count: x[(L-1)/2], even: mean of x[(L-1)/2], x[(L+1)/2]
@@ -1219,28 +1157,9 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
   // shapes prefetch frame k+1's raw words during frame k's medians)
   const int nf = min(tg.fpw, tg.nframes - t.f);
   uint4 rw[kNet ? NI : 1];
-  // Median-phase work -> lanes.  Packed (PR_CM_SPREAD 0): thread t takes segment / column-lane t,
-  // so the epix10k2M tile's 176 row segments fill waves 0-1 and 48 lanes of wave 2, its 192 column
-  // lanes waves 0-2, and wave 3 idles.  Spread (1): every wave takes an equal share (44 segments,
-  // 12 columns = 48 lanes; shares of whole quads), one item per lane.
-  int rows_t0 = tid, rows_nt = (int)blockDim.x, cols_t0 = tid, cols_nt = (int)blockDim.x;
-#if PR_CM_SPREAD
-  {
-    const int nw = (int)blockDim.x >> 6, wv = tid >> 6, ln = tid & 63;
-    const int nseg = R * (C / L);
-    const int rs = (nseg + nw - 1) / nw;
-    if (rs <= 64) {
-      rows_t0 = ln < rs ? wv * rs + ln : nseg;
-      rows_nt = nseg;
-    }
-    const int ncl = 4 * C;
-    const int cs = (((ncl + nw - 1) / nw) + 3) & ~3;
-    if (cs <= 64) {
-      cols_t0 = ln < cs ? wv * cs + ln : (1 << 20);
-      cols_nt = 1 << 20;
-    }
-  }
-#endif
+  // Median-phase work -> lanes: thread t takes row segment / column lane t (spreading the work
+  // evenly over the four waves measured neutral: the same instruction stream per wave either way)
+  const int rows_t0 = tid, rows_nt = (int)blockDim.x, cols_t0 = tid, cols_nt = (int)blockDim.x;
 #if PR_CM_STAMPS
   uint64_t st_[12] = {};
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
@@ -1292,23 +1211,6 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
     // ---- phase 2a: rows by bank, one lane per segment ------------------------------------
     if (cp.flags & 1) {
       cm_rows<L>(tile, P, R, C, cp, rows_t0, rows_nt);
-#ifdef PR_CM_PROBE_W3_VALU
-      // timing probe only: the idle fourth wave issues ~800 VALU during the row phase.  Hidden if a
-      // workgroup's time is its own critical path; it costs if the SIMDs' VALU issue is the bound.
-      if (tid >= 192) {
-        float a[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) a[q] = tile[tid + q];
-        for (int it = 0; it < PR_CM_PROBE_W3_VALU; ++it) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) a[q] = fmaf(a[q], 1.0001f, 0.5f);
-        }
-        float z = 0.f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) z += a[q];
-        if (cp.flags & 64) tile[tid] = z;
-      }
-#endif
       PR_STAMP(3);
       __syncthreads();
       PR_STAMP(4);
