@@ -44,7 +44,9 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=32, help="frames per rank per step (consumer batch)")
     ap.add_argument("--detector", default="epix10k2M")
     ap.add_argument("--mode", default="calib", choices=["calib", "image", "raw"])
-    ap.add_argument("--common-mode", default="default", help="off | default | flags,thr,maxcorr,npix_min[,bank]")
+    ap.add_argument("--common-mode", default="auto",
+                    help="auto (the producer CLI's default: on for epix10ka) | off | default | "
+                         "flags,thr,maxcorr,npix_min[,bank]")
     ap.add_argument("--consumer", default="peakfind", choices=["peakfind", "none"])
     ap.add_argument("--route", default="balanced", choices=["balanced", "local_first", "spread", "remote_only"],
                     help="routing policy of the headline window")
@@ -77,6 +79,12 @@ def parse(argv=None):
     ap.add_argument("--copy-engine", default="blit", choices=["blit", "sdma"],
                     help="runtime copies (HBM->HBM peer copies of the cross-GPU window): blit kernels "
                          "(HSA_ENABLE_SDMA=0) or the SDMA engines.  An HSA_ENABLE_SDMA already in the environment wins")
+    ap.add_argument("--fabric-copy", default=None, choices=["kernel", "runtime"],
+                    help="N > 1: how producers move frames into other ranks' rings: one copy_runs_kernel launch per "
+                         "fabric pass on its own hardware queue (default, config.FABRIC_COPY_ENGINE) or hipMemcpyAsync "
+                         "per run on one ordinary stream per link (round-3 path)")
+    ap.add_argument("--fabric-copy-wgs", type=int, default=None,
+                    help="workgroups of the fabric copy kernel (default config.FABRIC_COPY_WORKGROUPS)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: protocol rehearsal with gloo and the golden models (tests only; not a benchmark)")
     return ap.parse_args(argv)
@@ -106,6 +114,28 @@ def _wait_links(ep, n_members: int, expect_in: int, expect_out: int, timeout_s: 
         time.sleep(0.01)
 
 
+def _pct(v, q):
+    if not v:
+        return None
+    v = sorted(v)
+    return v[min(len(v) - 1, int(round(q * (len(v) - 1))))]
+
+
+def _copy_stats(samples) -> dict:
+    """p50 / p99 of a window's fabric copy dispatches (endpoint.copy_samples tuples)."""
+    if not samples:
+        return {"dispatches": 0}
+    dev = [s[0] for s in samples]
+    lat = [s[1] for s in samples]
+    byts = sum(s[2] for s in samples)
+    frames = [s[3] for s in samples]
+    return {"dispatches": len(samples), "frames_per_dispatch_mean": round(sum(frames) / len(frames), 1),
+            "dev_ms_p50": round(_pct(dev, 0.5), 4), "dev_ms_p99": round(_pct(dev, 0.99), 4),
+            "dev_GB_per_s": round(byts / max(1e-9, sum(dev) * 1e-3) / 1e9, 1),
+            "issue_to_done_ms_p50": round(_pct(lat, 0.5), 3), "issue_to_done_ms_p99": round(_pct(lat, 0.99), 3),
+            "ms_per_64_frames_dev_p50": round(64 * _pct([d / max(1, f) for d, f in zip(dev, frames)], 0.5), 4)}
+
+
 def main(argv=None):
     args = parse(argv)
     from psana_ray_amd.utils.runtime_env import select_copy_engine
@@ -115,8 +145,9 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
-    from psana_ray_amd.config import CONSUMER_STREAM_KIND, CommonModeParams, PeakFinderParams
-    from psana_ray_amd.models import Calibrator, Mode
+    from psana_ray_amd.config import CONSUMER_STREAM_KIND, PeakFinderParams
+    from psana_ray_amd.models import Mode
+    from psana_ray_amd.producer import build_calibrator
     from psana_ray_amd.parallel.launch import bind_numa_to_device, detect
     from psana_ray_amd.pipeline import PeakFinderConsumer, ProducerPipeline
     from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
@@ -162,7 +193,6 @@ def main(argv=None):
             dist.barrier(group=coord)
 
     mode = Mode(args.mode)
-    cm = CommonModeParams.parse(args.common_mode) if mode != Mode.raw else None
     n_prod = args.producers or world
     if not 1 <= n_prod <= world:
         print(f"bench.py: --producers must be in [1, {world}]", file=sys.stderr)
@@ -173,7 +203,8 @@ def main(argv=None):
     src = SyntheticRun("synthetic", 0, args.detector, rank=rank if is_prod else 0, size=n_prod,
                        pool_frames=args.pool_frames if is_prod else 1,
                        pinned=(args.source == "host" and gpu and is_prod), gen_device=str(device))
-    cal = Calibrator(src.consts, device, mode, common_mode=cm)
+    # the producer CLI's own construction (same mode / common-mode resolution as psana-ray-producer)
+    cal = build_calibrator(src, device, mode, None, args.common_mode)
     if args.queue_size is None:
         args.queue_size = 400 * world
     share = max(1, math.ceil(args.queue_size / world))
@@ -192,7 +223,8 @@ def main(argv=None):
                             device=device.index if gpu else -1, rank=rank)
     ring = FrameRing(cal.out_shape, cal.out_dtype, device, producer_slots, cslots,
                      shm_name=sess.ring_name() if (sess is not None and not gpu) else None)
-    ep = QueueEndpoint(ring, sess, is_producer=is_prod, is_consumer=True, route=args.route)
+    ep = QueueEndpoint(ring, sess, is_producer=is_prod, is_consumer=True, route=args.route,
+                       copy_engine=args.fabric_copy, copy_workgroups=args.fabric_copy_wgs)
     if args.source == "device":
         # raw pool resident in HBM: isolates the GPU pipeline from PCIe (secondary number)
         dev_pool = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(device)
@@ -348,6 +380,13 @@ def main(argv=None):
         fr_local = allsum(int(x1.get("frames_local", 0) - x0.get("frames_local", 0)))
         fr_recv = allsum(int(x1.get("frames_recv", 0) - x0.get("frames_recv", 0)))
         cms = allsum(round(float(x1.get("copy_ms_per_batch", 0.0)), 3))
+        # the window's copy dispatches: device time of the copy alone (timing events around it) and
+        # host issue -> completion (includes the wait for the frames' calibration)
+        n_new = int(x1.get("copy_launches", 0) - x0.get("copy_launches", 0))
+        smp = ep.copy_samples()[-n_new:] if n_new > 0 else []
+        copy_detail = allsum(_copy_stats(smp))
+        fb = ring.frame_bytes
+        per_link = allsum({str(int(l.peer)): round(int(l.frames) * fb / 1e9, 3) for l in ep.links() if l.outgoing})
         keys = ("grants_given", "grants_returned", "grants_reclaimed", "frames_recv", "frames_requeued")
         fab = allsum({k: int(x1.get(k, 0) - x0.get(k, 0)) for k in keys} |
                      {"credits": int(x1.get("credits", 0)), "ready": int(x1.get("ready", 0)),
@@ -361,8 +400,14 @@ def main(argv=None):
             "received_cross_per_consumed": round(sum(fr_recv) / max(1, world * cross_steps * B), 3),
             "bytes_sent_per_rank": sent, "frames_sent_per_rank": fr_sent, "frames_local_per_rank": fr_local,
             "copy_ms_per_batch_per_rank": cms,
+            "copy_dispatch_per_rank": copy_detail,
+            "link_GB_total_per_rank": per_link,
+            "fabric_copy": list(getattr(ep, "copy_engine", ("", 0))),
             "fabric_per_rank": fab,
-            "data_plane": "HIP IPC peer copies (hipMemcpyAsync D2D into the consumer's ring) over xGMI",
+            "data_plane": "HIP IPC peer writes into the consumer's ring over xGMI ("
+                          + ("one copy_runs_kernel launch per fabric pass, own hardware queue"
+                             if getattr(ep, "copy_engine", ("kernel",))[0] == "kernel"
+                             else "hipMemcpyAsync per run, one stream per link") + ")",
         }
         ep.set_route(args.route)
     stop.set()

@@ -112,6 +112,11 @@ static void segv_trace_handler(int sig, siginfo_t* info, void* uctx) {
 static void maybe_install_segv_trace() {
   const char* e = getenv("PSANA_RAY_AMD_SEGV_TRACE");
   if (e == nullptr || e[0] != '1') return;
+  // already ours (installed at import, called again at shutdown): keep the FIRST saved handler --
+  // saving our own as "previous" would make a SIGSEGV re-enter this handler forever
+  struct sigaction cur {};
+  if (sigaction(SIGSEGV, nullptr, &cur) == 0 && (cur.sa_flags & SA_SIGINFO) && cur.sa_sigaction == segv_trace_handler)
+    return;
   struct sigaction sa {};
   sa.sa_sigaction = segv_trace_handler;
   sa.sa_flags = SA_SIGINFO;
@@ -291,7 +296,16 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("frames_dropped", &pr::FabricStats::frames_dropped)
       .def_readonly("returns_rejected", &pr::FabricStats::returns_rejected)
       .def_readonly("readahead", &pr::FabricStats::readahead)
-      .def_readonly("copy_s", &pr::FabricStats::copy_s);
+      .def_readonly("copy_s", &pr::FabricStats::copy_s)
+      .def_readonly("copy_launches", &pr::FabricStats::copy_launches)
+      .def_readonly("copy_dev_ms", &pr::FabricStats::copy_dev_ms)
+      .def_readonly("copy_dev_bytes", &pr::FabricStats::copy_dev_bytes);
+  py::class_<pr::CopySample>(m, "CopySample")
+      .def_readonly("dev_ms", &pr::CopySample::dev_ms)
+      .def_readonly("issue_to_done_ms", &pr::CopySample::issue_to_done_ms)
+      .def_readonly("bytes", &pr::CopySample::bytes)
+      .def_readonly("frames", &pr::CopySample::frames)
+      .def_readonly("links", &pr::CopySample::links);
   py::class_<pr::LinkStatus>(m, "LinkStatus")
       .def_readonly("peer", &pr::LinkStatus::peer)
       .def_readonly("outgoing", &pr::LinkStatus::outgoing)
@@ -303,7 +317,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("keeper", &pr::LinkStatus::keeper)
       .def_readonly("taken", &pr::LinkStatus::taken)
       .def_readonly("outstanding", &pr::LinkStatus::outstanding)
-      .def_readonly("frames", &pr::LinkStatus::frames);
+      .def_readonly("frames", &pr::LinkStatus::frames)
+      .def_readonly("consumer_device", &pr::LinkStatus::consumer_device);
   py::class_<pr::QueueFabric>(m, "QueueFabric")
       .def(py::init<pr::SlotPool*, int64_t, int, bool, bool, int, int64_t>(), py::arg("pool"),
            py::arg("slot_bytes"), py::arg("device"), py::arg("is_producer"), py::arg("is_consumer"),
@@ -333,6 +348,10 @@ PYBIND11_MODULE(_C, m) {
       .def("set_keeper", &pr::QueueFabric::set_keeper, py::arg("on"))
       .def("set_peer_grantable", &pr::QueueFabric::set_peer_grantable, py::arg("mid"), py::arg("on"))
       .def("stats", &pr::QueueFabric::stats)
+      .def("set_copy_engine", &pr::QueueFabric::set_copy_engine, py::arg("engine"), py::arg("workgroups") = 0)
+      .def_property_readonly("copy_engine", &pr::QueueFabric::copy_engine)
+      .def_property_readonly("copy_workgroups", &pr::QueueFabric::copy_workgroups)
+      .def("copy_samples", &pr::QueueFabric::copy_samples)
       .def("links", &pr::QueueFabric::links);
 
   py::class_<pr::PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())
@@ -422,6 +441,7 @@ PYBIND11_MODULE(_C, m) {
       .def("complete_recv_batch", &SP::complete_recv_batch, py::arg("slots"), py::arg("headers"))
       .def("cancel_recv_batch", &SP::cancel_recv_batch, py::arg("slots"))
       .def("reoffer_batch", &SP::reoffer_batch, py::arg("slots"), py::arg("stream"))
+      .def("relay_ready", &SP::relay_ready, py::arg("max_n"))
       .def("set_external_held", &SP::set_external_held, py::arg("n"))
       .def("producer_room", &SP::producer_room)
       .def("set_track_origins", &SP::set_track_origins, py::arg("on"))

@@ -22,6 +22,17 @@ struct FramePtrs {
   uint64_t out[kMaxFrames];
 };
 
+// Runs of whole frames copied by one launch of copy_runs_kernel (queue fabric): run i moves n16[i]
+// 16-B words from src[i] to dst[i]; cstart is filled by the launcher (first chunk of each run).
+constexpr int kMaxCopyRuns = 64;
+struct CopyRuns {
+  uint64_t src[kMaxCopyRuns];
+  uint64_t dst[kMaxCopyRuns];
+  int64_t n16[kMaxCopyRuns];
+  int32_t cstart[kMaxCopyRuns + 1];
+  int32_t n;
+};
+
 // Gain decoding families (parameters, not verified psana facts).
 //  kEpix10ka: ADU = raw & 0x3FFF; bit 14 selects candidate table b (auto-ranging switched)
 //             vs a.  Candidates per pixel are pre-resolved from the pixel gain config on
@@ -63,6 +74,30 @@ inline void hip_check(hipError_t e, const char* what) {
 }
 
 inline bool aligned16(uint64_t p) { return (p & 15u) == 0; }
+
+// Switches the calling thread to `device` and restores the previous device on scope exit.  Every
+// native entry a Python thread can reach goes through this: a bare hipSetDevice would silently move
+// the caller's current device, and torch's next 'cuda' tensor would land on the wrong GPU in a
+// process that drives several.  device < 0: no-op.
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int device) {
+    if (device < 0) return;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) cur = -1;
+    if (cur == device) return;
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    prev_ = cur;
+  }
+  ~DeviceGuard() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+ private:
+  int prev_ = -1;
+};
 
 // Bijective XCD-aware block remap (guide T1): the hardware deals workgroups round-robin over the
 // 8 XCDs (block b and b+8 share an L2), so hand each XCD a CONTIGUOUS range of logical ids.

@@ -89,7 +89,7 @@ ProducerEngine::ProducerEngine(SlotPool* pool, int64_t slot_bytes, int device,
       size_(size), hdr_rank_(rank), gpu_timing_(gpu_timing), copy_workgroups_(std::max(0, copy_workgroups)) {
   check(pool != nullptr && device >= 0, "ProducerEngine needs a device SlotPool");
   check(plan.raw_frame_bytes > 0 && plan.raw_frame_bytes % 16 == 0, "ProducerEngine: bad raw frame size");
-  hip_check(hipSetDevice(device_), "hipSetDevice");
+  DeviceGuard dg(device_);
   hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
   hip_check(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate");
   cstreams_.push_back(compute_);
@@ -127,7 +127,7 @@ void ProducerEngine::halt() {
 ProducerEngine::~ProducerEngine() {
   unregister_native_thread_owner(this);
   halt();
-  (void)hipSetDevice(device_);
+  DeviceGuard dg(device_);
   if (h2d_) (void)hipStreamSynchronize(h2d_);
   for (auto cs : cstreams_) (void)hipStreamSynchronize(cs);
   for (auto e : buf_free_) (void)hipEventDestroy(e);
@@ -150,7 +150,7 @@ void ProducerEngine::set_compute_streams(int n, int kind) {
     check(!origin_recorded_, "ProducerEngine: set_compute_streams after the first start");
   }
   if (plan_.mode == kPlanImageScratch) n = 1;   // one scratch buffer: never two launches in flight
-  hip_check(hipSetDevice(device_), "hipSetDevice");
+  DeviceGuard dg(device_);
   for (auto cs : cstreams_) release_stream(device_, stream_kind_, cs);
   cstreams_.clear();
   const int old_kind = stream_kind_;
@@ -169,7 +169,7 @@ void ProducerEngine::set_cycled_source(const std::vector<uint64_t>& frames, cons
   src_frames_ = frames;
   src_pe_ = pe;
   // frames already resident in this GPU's memory are calibrated in place: no staging copy
-  hip_check(hipSetDevice(device_), "hipSetDevice");
+  DeviceGuard dg(device_);
   bool all_dev = true;
   for (uint64_t f : frames) {
     hipPointerAttribute_t a{};
@@ -187,7 +187,7 @@ void ProducerEngine::set_file_source(RawRunReader* reader) {
   check(!running_.load(), "ProducerEngine: cannot change the source while running");
   check(reader != nullptr, "ProducerEngine: null reader");
   check(reader->frame_bytes() == plan_.raw_frame_bytes, "ProducerEngine: file frame size != detector raw frame");
-  hip_check(hipSetDevice(device_), "hipSetDevice");
+  DeviceGuard dg(device_);
   if (file_staging_ == nullptr)
     hip_check(hipHostMalloc(&file_staging_, (size_t)n_raw_bufs_ * chunk_ * plan_.raw_frame_bytes, hipHostMallocDefault),
               "hipHostMalloc file staging");
@@ -207,7 +207,7 @@ void ProducerEngine::start(int64_t n_local_events, int64_t max_steps, int64_t k0
   {
     std::lock_guard<std::mutex> lk(done_mu_);
     if (!origin_recorded_) {   // the completion log's clock starts here
-      hip_check(hipSetDevice(device_), "hipSetDevice");
+      DeviceGuard dg(device_);
       hip_check(hipEventRecord(origin_, compute_), "record origin");
       origin_recorded_ = true;
     }
@@ -300,14 +300,14 @@ void ProducerEngine::record_chunk_done(int n, hipStream_t s) {
 
 int64_t ProducerEngine::completed() const {
   std::lock_guard<std::mutex> lk(done_mu_);
-  (void)hipSetDevice(device_);
+  DeviceGuard dg(device_);
   note_chunk_done_locked();
   return done_frames_;
 }
 
 std::vector<std::pair<int64_t, double>> ProducerEngine::completions(int64_t since, int64_t* first_index) const {
   std::lock_guard<std::mutex> lk(done_mu_);
-  (void)hipSetDevice(device_);
+  DeviceGuard dg(device_);
   note_chunk_done_locked();
   const int64_t a = std::max(since, done_base_);
   if (first_index != nullptr) *first_index = a;
@@ -322,7 +322,7 @@ double ProducerEngine::mark(uint64_t stream) const {
     std::lock_guard<std::mutex> lk(done_mu_);
     check(origin_recorded_, "ProducerEngine.mark: the engine has not started");
   }
-  hip_check(hipSetDevice(device_), "hipSetDevice");
+  DeviceGuard dg(device_);
   hip_check(hipEventCreate(&e), "hipEventCreate (mark)");
   float ms = 0.f;
   hipError_t err = hipEventRecord(e, reinterpret_cast<hipStream_t>(stream));

@@ -15,7 +15,9 @@
 #include <cstring>
 
 #include "common.h"
+#include "kernels.h"
 #include "lifecycle.h"
+#include "streams.h"
 #include "trace.h"
 
 namespace pr {
@@ -212,6 +214,8 @@ struct QueueFabric::Link {
   int n = 0;
   bool attached = false, dead = false, closed = false, eos = false, detached = false, named = true;
   bool keeper = false;                // the consumer end is a queue keeper
+  int consumer_device = -1;           // outgoing: GPU of the consumer ring (-1: host shared memory)
+  bool ipc = false;                   // outgoing: the consumer ring is IPC-mapped HBM
   double t_added = 0, last_check = 0;
   int64_t frames = 0;
   // producer side (outgoing)
@@ -252,8 +256,18 @@ struct QueueFabric::Link {
     s.outstanding = outgoing ? (int64_t)grants.size() : outstanding;
     s.frames = frames;
     s.taken = outgoing ? (int64_t)taken_seen : (int64_t)taken;
+    s.consumer_device = outgoing ? consumer_device : -1;
     return s;
   }
+};
+
+struct QueueFabric::CopyGroup {
+  hipEvent_t start = nullptr, end = nullptr;   // timing-enabled, on xstream_
+  int pending = 0;                             // batches of this dispatch not retired yet
+  bool timed = false;
+  double t_issue = 0;
+  int64_t bytes = 0;
+  int32_t frames = 0, links = 0;
 };
 
 struct QueueFabric::Batch {
@@ -261,7 +275,8 @@ struct QueueFabric::Batch {
   hipStream_t stream = nullptr;
   std::vector<int> slots, rslots;
   std::vector<SlotHeader> hdrs;
-  hipEvent_t ev = nullptr;
+  hipEvent_t ev = nullptr;                 // runtime engine / reclaims: this batch's own event
+  std::shared_ptr<CopyGroup> grp;          // kernel engine: the dispatch it rode in
   double t_issue = 0;
 };
 
@@ -275,7 +290,7 @@ QueueFabric::QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is
   check(is_producer || is_consumer, "QueueFabric: a member must produce or consume");
   if (is_consumer) pool_->set_track_origins(true);
   if (device_ >= 0) {
-    hip_check(hipSetDevice(device_), "hipSetDevice");
+    DeviceGuard dg(device_);
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate (fabric)");
   }
   if (!is_producer) drained_.store(true);
@@ -292,11 +307,21 @@ QueueFabric::~QueueFabric() {
   unregister_native_thread_owner(this);
   halt();
   try {
-    if (device_ >= 0) hip_check(hipSetDevice(device_), "hipSetDevice");
+    DeviceGuard dg(device_);
     // copies still in flight complete into memory we keep mapped until here
-    for (auto& b : inflight_)
+    std::vector<std::shared_ptr<CopyGroup>> groups;
+    for (auto& b : inflight_) {
       if (b.ev != nullptr) (void)hipEventSynchronize(b.ev);
+      if (b.grp != nullptr && std::find(groups.begin(), groups.end(), b.grp) == groups.end()) groups.push_back(b.grp);
+    }
+    for (auto& g : groups) {
+      (void)hipEventSynchronize(g->end);
+      free_timed_.push_back(g->start);
+      free_timed_.push_back(g->end);
+    }
     inflight_.clear();
+    if (xstream_ != nullptr) release_stream(device_, kStreamDedicated, xstream_);   // synchronises it
+    xstream_ = nullptr;
     for (auto& l : links_) {
       if (l->seg == nullptr) continue;
       if (l->outgoing) {
@@ -312,6 +337,7 @@ QueueFabric::~QueueFabric() {
     }
     links_.clear();
     for (auto e : all_events_) (void)hipEventDestroy(e);
+    for (auto e : free_timed_) (void)hipEventDestroy(e);
     if (stream_ != nullptr) (void)hipStreamDestroy(stream_);
   } catch (...) {
   }
@@ -356,7 +382,7 @@ void QueueFabric::export_host_ring(const std::string& shm_name) {
 
 void QueueFabric::export_ipc_ring() {
   check(is_consumer_ && device_ >= 0, "QueueFabric: IPC export needs a GPU consumer");
-  hip_check(hipSetDevice(device_), "hipSetDevice");
+  DeviceGuard dg(device_);
   segs_.clear();
   const int n = pool_->n_slots();
   uint64_t cur_base = 0, cur_first_ptr = 0;
@@ -415,6 +441,48 @@ void QueueFabric::set_policy(int policy) {
 void QueueFabric::set_peer_grantable(int64_t mid, bool on) {
   std::lock_guard<std::mutex> lk(ops_mu_);
   ops_.push_back(Op{on ? 3 : 4, mid, ""});
+}
+
+void QueueFabric::set_copy_engine(int engine, int workgroups) {
+  check(engine == kCopyKernel || engine == kCopyRuntime, "QueueFabric: unknown copy engine");
+  check(!running_.load(), "QueueFabric: set_copy_engine before start()");
+  copy_engine_ = engine;
+  if (workgroups > 0) copy_wgs_ = std::min(workgroups, 4096);
+}
+
+std::vector<CopySample> QueueFabric::copy_samples() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return std::vector<CopySample>(samples_.begin(), samples_.end());
+}
+
+hipEvent_t QueueFabric::take_timed_event() {
+  if (!free_timed_.empty()) {
+    hipEvent_t e = free_timed_.back();
+    free_timed_.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hip_check(hipEventCreate(&e), "hipEventCreate (fabric copy timing)");
+  return e;
+}
+
+// A dispatch whose end event completed: its device time becomes a sample (once).
+void QueueFabric::finish_group(const std::shared_ptr<CopyGroup>& g) {
+  if (g->timed) return;
+  g->timed = true;
+  float ms = 0.f;
+  CopySample cs;
+  if (hipEventElapsedTime(&ms, g->start, g->end) == hipSuccess) cs.dev_ms = ms;
+  (void)hipGetLastError();
+  cs.issue_to_done_ms = 1e3 * (now_s() - g->t_issue);
+  cs.bytes = g->bytes;
+  cs.frames = g->frames;
+  cs.links = g->links;
+  std::lock_guard<std::mutex> lk(mu_);
+  st_.copy_dev_ms += cs.dev_ms;
+  st_.copy_dev_bytes += cs.bytes;
+  samples_.push_back(cs);
+  while ((int)samples_.size() > kMaxSamples) samples_.pop_front();
 }
 
 hipEvent_t QueueFabric::take_event() {
@@ -583,7 +651,11 @@ bool QueueFabric::try_attach(Link& l, double now) {
     link_error_ = "link to consumer " + std::to_string(l.peer) + ": " + e.what();
     return false;
   }
-  if (device_ >= 0 && l.stream == nullptr) {
+  l.ipc = s->kind == 1;
+  l.consumer_device = l.ipc ? s->consumer_device : -1;
+  // a per-link copy stream only where the runtime copies: a host ring (pageable shared memory), or
+  // the runtime engine; the kernel engine moves every link's frames on xstream_
+  if (device_ >= 0 && l.stream == nullptr && (!l.ipc || copy_engine_ == kCopyRuntime)) {
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking), "hipStreamCreate (fabric link)");
   }
@@ -599,6 +671,8 @@ bool QueueFabric::try_attach(Link& l, double now) {
 
 void QueueFabric::release_out_link(Link& l) {
   if ((!l.ipc_ptrs.empty() || l.stream != nullptr) && device_ >= 0) (void)hipSetDevice(device_);
+  // kernel-engine copies towards this ring run on xstream_: none may still write it once unmapped
+  if (l.inflight > 0 && xstream_ != nullptr) (void)hipStreamSynchronize(xstream_);
   if (l.stream != nullptr) {
     (void)hipStreamSynchronize(l.stream);
     (void)hipStreamDestroy(l.stream);
@@ -1062,8 +1136,9 @@ int64_t QueueFabric::producer_pass(double now) {
       ++it;
       continue;
     }
-    if (b.ev != nullptr) {
-      const hipError_t q = hipEventQuery(b.ev);
+    hipEvent_t done_ev = b.grp != nullptr ? b.grp->end : b.ev;
+    if (done_ev != nullptr) {
+      const hipError_t q = hipEventQuery(done_ev);
       if (q == hipErrorNotReady) {
         blocked.push_back(b.link.get());
         ++it;
@@ -1071,13 +1146,17 @@ int64_t QueueFabric::producer_pass(double now) {
       }
       hip_check(q, "hipEventQuery (frame copy)");
     }
+    if (b.grp != nullptr) finish_group(b.grp);
     Link& l = *b.link;
     const int n = (int)b.slots.size();
     l.inflight -= n;
     if (l.attached && !l.dead && !l.closed) {
       for (int i = 0; i < n; ++i) post_notice(l, make_notice(b.rslots[i], 0, b.hdrs[i]));
       l.seg->n_head.store(l.n_head, std::memory_order_release);
-      pool_->end_send_batch(b.slots, reinterpret_cast<uint64_t>(b.stream != nullptr ? b.stream : stream_));
+      // the copy is complete (host-observed): free the slots with no device wait, and count the
+      // frames as consumer read-ahead in the same locked step (step 5 recomputes the exact value)
+      const bool ext = !l.acked_close;
+      pool_->end_send_completed(b.slots, ext);
       l.frames += n;
       l.noticed += n;
       std::lock_guard<std::mutex> lk(mu_);
@@ -1090,6 +1169,10 @@ int64_t QueueFabric::producer_pass(double now) {
       st_.frames_requeued += n;
     }
     if (b.ev != nullptr) free_events_.push_back(b.ev);
+    if (b.grp != nullptr && --b.grp->pending == 0) {
+      free_timed_.push_back(b.grp->start);
+      free_timed_.push_back(b.grp->end);
+    }
     it = inflight_.erase(it);
     work += n;
   }
@@ -1169,6 +1252,7 @@ int64_t QueueFabric::producer_pass(double now) {
       std::lock_guard<std::mutex> lk(mu_);
       st_.frames_local += (int64_t)local.size();
     }
+    std::vector<Batch> kbatches;   // kernel engine: one dispatch for every link of this pass
     for (size_t i = 0; i < cands.size(); ++i) {
       if (assign[i].empty()) continue;
       Link& l = *cands[i];
@@ -1182,6 +1266,12 @@ int64_t QueueFabric::producer_pass(double now) {
       b.rslots.assign(l.grants.begin(), l.grants.begin() + n);
       l.grants.erase(l.grants.begin(), l.grants.begin() + n);
       b.t_issue = now;
+      if (device_ >= 0 && l.ipc && copy_engine_ == kCopyKernel) {
+        l.inflight += n;
+        kbatches.push_back(std::move(b));
+        work += n;
+        continue;
+      }
       if (device_ >= 0) {
         trace::Range tr("fabric.copy_batch");
         b.stream = l.stream != nullptr ? l.stream : stream_;
@@ -1212,9 +1302,11 @@ int64_t QueueFabric::producer_pass(double now) {
       {
         std::lock_guard<std::mutex> lk(mu_);
         ++st_.batches;
+        ++st_.copy_launches;
       }
       work += n;
     }
+    if (!kbatches.empty()) issue_copies(kbatches, now);
   }
   // 5. read-ahead accounting (frames noticed and not taken still count against this producer's
   //    budget), demand hints, close acknowledgements, end of stream
@@ -1279,6 +1371,64 @@ int64_t QueueFabric::producer_pass(double now) {
   // links still being created by their consumer do not hold frames: EOS reaches them on attach
   drained_.store(drained);
   return work;
+}
+
+// Kernel engine: the frames of every link routed in this pass move in ONE copy_runs_kernel launch
+// on xstream_ (its own hardware queue), ordered after the frames' calibration by event waits on
+// that stream only.  Timing events bracket the copy itself, so each dispatch's device time is known.
+void QueueFabric::issue_copies(std::vector<Batch>& kb, double now) {
+  trace::Range tr("fabric.copy_dispatch");
+  if (xstream_ == nullptr) xstream_ = acquire_stream(device_, kStreamDedicated);
+  std::vector<int> all;
+  for (const Batch& b : kb) all.insert(all.end(), b.slots.begin(), b.slots.end());
+  pool_->begin_send_batch(all, reinterpret_cast<uint64_t>(xstream_));   // xstream_ waits for their data
+  auto g = std::make_shared<CopyGroup>();
+  g->start = take_timed_event();
+  g->end = take_timed_event();
+  g->t_issue = now;
+  g->links = (int32_t)kb.size();
+  hip_check(hipEventRecord(g->start, xstream_), "hipEventRecord (copy start)");
+  check(slot_bytes_ % 16 == 0, "QueueFabric: frame size must be a multiple of 16 B for the copy kernel");
+  CopyRuns cr{};
+  cr.n = 0;
+  const uint64_t sb = (uint64_t)slot_bytes_;
+  int launches = 0;
+  auto flush = [&] {
+    if (cr.n == 0) return;
+    launch_copy_runs(cr, copy_wgs_, reinterpret_cast<uint64_t>(xstream_));
+    cr.n = 0;
+    ++launches;
+  };
+  for (const Batch& b : kb) {
+    const Link& l = *b.link;
+    const int n = (int)b.slots.size();
+    int a = 0;
+    while (a < n) {   // coalesce runs contiguous on both sides
+      int e = a + 1;
+      while (e < n && pool_->slot_ptr(b.slots[e]) == pool_->slot_ptr(b.slots[e - 1]) + sb &&
+             l.remote[b.rslots[e]] == l.remote[b.rslots[e - 1]] + sb)
+        ++e;
+      if (cr.n == kMaxCopyRuns) flush();
+      cr.src[cr.n] = pool_->slot_ptr(b.slots[a]);
+      cr.dst[cr.n] = l.remote[b.rslots[a]];
+      cr.n16[cr.n] = (int64_t)(sb * (uint64_t)(e - a) / 16u);
+      ++cr.n;
+      a = e;
+    }
+    g->frames += n;
+    g->bytes += (int64_t)n * slot_bytes_;
+  }
+  flush();
+  hip_check(hipEventRecord(g->end, xstream_), "hipEventRecord (copy end)");
+  g->pending = (int)kb.size();
+  for (Batch& b : kb) {
+    b.stream = xstream_;
+    b.grp = g;
+    inflight_.push_back(std::move(b));
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  st_.batches += (int64_t)kb.size();
+  st_.copy_launches += launches;
 }
 
 void QueueFabric::publish_status() {

@@ -17,8 +17,9 @@
 //                                   or "grant s returned unused"
 //
 // The frame bytes never pass through the mailbox.  A GPU consumer exports its ring allocation as
-// a HIP IPC handle; the producer maps it and writes granted slots directly with a device-to-device
-// copy on its own stream -- over the point-to-point xGMI link when the two processes sit on
+// a HIP IPC handle; the producer maps it and writes granted slots directly -- every frame routed in
+// one fabric pass, to all its consumers, by ONE copy_runs_kernel launch on a stream that owns its
+// hardware queue (csrc/gather.hip) -- over the point-to-point xGMI links when the processes sit on
 // different GPUs (one hop, no staging, no rendezvous kernel on the receiver).  The notice is
 // posted only after that copy has completed, so the consumer needs no device-side wait.  Host
 // (CPU) consumers keep their ring in a named shared-memory region the producer maps and memcpy's
@@ -54,8 +55,9 @@
 // real consumers.
 //
 // Visibility of peer-written slots (SURVEY H-10; /opt/skills/guides/MI355X_MICROARCH.md:150-236):
-// the frame bytes are written by the PRODUCER's copy (hipMemcpyAsync D2D: a blit kernel or an SDMA
-// transfer writing the consumer's HBM through the IPC mapping, over xGMI when the GPUs differ).
+// the frame bytes are written by the PRODUCER's copy (copy_runs_kernel, or hipMemcpyAsync D2D with
+// the runtime engine: kernels or SDMA writing the consumer's HBM through the IPC mapping, over xGMI
+// when the GPUs differ).
 // The consumer is told only by a notice posted after hipEventQuery reported that copy complete,
 // i.e. after the copy's end-of-operation release (agent scope: buffer_wbl2 -- dirty lines,
 // including lines of peer memory, leave the producer GPU's L2).  The consumer reads a leased slot
@@ -123,7 +125,19 @@ struct FabricStats {
   int64_t frames_dropped = 0;    // consumer: read-ahead frames no live producer could take back
   int64_t returns_rejected = 0;  // consumer: returns refused (that producer had posted EOS) and re-routed
   int64_t readahead = 0;         // producer: frames in consumers' read-ahead not taken yet (gauge)
-  double copy_s = 0;             // sum over batches of issue -> completion observed
+  double copy_s = 0;             // sum over batches of issue -> completion observed (includes the wait
+                                 // for the frames' calibration, which the copy is ordered after)
+  int64_t copy_launches = 0;     // copy dispatches (kernel engine: one per fabric pass over all links)
+  double copy_dev_ms = 0;        // sum of device time of the copies themselves (timing events)
+  int64_t copy_dev_bytes = 0;    // bytes those timed copies moved
+};
+
+// One timed copy dispatch (fabric pass): device time of the copy, bytes, frames, host time from
+// issue to completion observed (the latter includes the wait for the frames' calibration).
+struct CopySample {
+  double dev_ms = 0, issue_to_done_ms = 0;
+  int64_t bytes = 0;
+  int32_t frames = 0, links = 0;
 };
 
 struct LinkStatus {
@@ -138,6 +152,7 @@ struct LinkStatus {
   int64_t outstanding = 0;   // grants not answered yet
   int64_t frames = 0;        // frames moved over the link
   int64_t taken = 0;         // frames of this link the consumer took (get)
+  int32_t consumer_device = -1;   // outgoing: the GPU of the consumer ring (-1 host)
 };
 
 class QueueFabric {
@@ -182,6 +197,20 @@ class QueueFabric {
   // consumer: true once no live producer can still be writing into this ring (every attached
   // producer acknowledged the close, detached or died) -- only then may the ring be freed
   bool consumer_quiesced() const { return quiesced_.load(); }
+  // producer (GPU): how frames move into GPU consumer rings.
+  //   kCopyKernel (default): every frame of one fabric pass, to all links, in ONE copy_runs_kernel
+  //     launch on a stream that owns its hardware queue (a copy waiting for its frames' calibration
+  //     blocks nothing else); `workgroups` bounds the CUs it takes from the pipeline.
+  //   kCopyRuntime: hipMemcpyAsync per contiguous run on one ordinary stream per link (blit kernels
+  //     or SDMA, HSA_ENABLE_SDMA) -- kept for A/B measurements.
+  // Before start().
+  static constexpr int kCopyKernel = 0, kCopyRuntime = 1;
+  void set_copy_engine(int engine, int workgroups);
+  int copy_engine() const { return copy_engine_; }
+  int copy_workgroups() const { return copy_wgs_; }
+  // the newest timed copy dispatches (bounded), oldest first
+  std::vector<CopySample> copy_samples() const;
+  static constexpr int kMaxSamples = 4096;
 
   void start();
   void request_stop() { stop_.store(true); }
@@ -204,6 +233,7 @@ class QueueFabric {
  private:
   struct Link;
   struct Batch;
+  struct CopyGroup;   // one timed copy dispatch shared by the per-link batches it carries
   void loop();
   void fail(const std::string& msg);
   void apply_ops();
@@ -216,6 +246,9 @@ class QueueFabric {
   void drop_returned(int slot);
   void publish_status();
   hipEvent_t take_event();
+  hipEvent_t take_timed_event();
+  void issue_copies(std::vector<Batch>& kb, double now);
+  void finish_group(const std::shared_ptr<CopyGroup>& g);
 
   SlotPool* pool_;
   int64_t slot_bytes_;
@@ -234,7 +267,12 @@ class QueueFabric {
   std::vector<SegExport> segs_;
 
   hipStream_t stream_ = nullptr;
+  hipStream_t xstream_ = nullptr;   // kernel engine: the copy stream (own hardware queue, pooled)
+  int copy_engine_ = kCopyKernel;
+  int copy_wgs_ = 128;
   std::vector<hipEvent_t> free_events_, all_events_;
+  std::vector<hipEvent_t> free_timed_;          // timing-enabled events (copy groups)
+  std::deque<CopySample> samples_;              // guarded by mu_
   std::vector<std::shared_ptr<Link>> links_;
   std::deque<Batch> inflight_;
   std::deque<Batch> reclaims_;   // producer: copies of returned frames back into this pool

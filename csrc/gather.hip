@@ -125,4 +125,59 @@ bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgro
   return true;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Queue-fabric frame copies (csrc/fabric.cpp): every frame a producer routes to OTHER processes in
+// one fabric pass -- to any number of consumer rings, each an IPC mapping of a peer's HBM (another
+// GPU over xGMI, or this GPU) -- moves in ONE launch on the fabric's own hardware queue.  The
+// runtime path was one blit launch per contiguous run per link, each on an ordinary stream
+// multiplexed with the staging and calibration streams.  Work unit: a 16-KB
+// chunk (256 lanes x U x 16 B in flight); the grid strides over the chunks of all runs, so the
+// writes to different consumers (different xGMI links) are in flight at the same time.  Loads are
+// nontemporal (the producer slot is freed right after); stores are plain (a same-GPU consumer reads
+// the slot next).  Visibility: the consumer is told only after this kernel's completion event
+// (end-of-kernel release), see csrc/fabric.h.
+// ---------------------------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(256) void copy_runs_kernel(const CopyRuns cr, const int total_chunks) {
+  constexpr int kChunk16 = 256 * U;
+  int e = 0;   // run of the current chunk: chunks ascend per workgroup, so the scan only moves forward
+  for (int c = blockIdx.x; c < total_chunks; c += gridDim.x) {
+    while (e + 1 < cr.n && cr.cstart[e + 1] <= c) ++e;
+    const PR_GLOBAL f32x4_t* src = gin<f32x4_t>(cr.src[e]);
+    PR_GLOBAL f32x4_t* dst = gout<f32x4_t>(cr.dst[e]);
+    const int64_t n16 = cr.n16[e];
+    const int64_t base = (int64_t)(c - cr.cstart[e]) * kChunk16 + threadIdx.x;
+    f32x4_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = base + 256 * u;
+      if (q < n16) v[u] = ld_nt_f4(src + q);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = base + 256 * u;
+      if (q < n16) dst[q] = v[u];
+    }
+  }
+}
+
+int launch_copy_runs(CopyRuns& cr, int workgroups, uint64_t stream) {
+  constexpr int U = 4;
+  constexpr int64_t kChunk16 = 256 * U;
+  check(cr.n >= 1 && cr.n <= kMaxCopyRuns, "copy_runs: 1..kMaxCopyRuns runs per launch");
+  int64_t total = 0;
+  for (int i = 0; i < cr.n; ++i) {
+    check(aligned16(cr.src[i]) && aligned16(cr.dst[i]) && cr.n16[i] > 0, "copy_runs: misaligned or empty run");
+    cr.cstart[i] = (int32_t)total;
+    total += (cr.n16[i] + kChunk16 - 1) / kChunk16;
+    check(total < (int64_t(1) << 30), "copy_runs: too many chunks in one launch");
+  }
+  cr.cstart[cr.n] = (int32_t)total;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(workgroups > 0 ? workgroups : 256, total));
+  hipLaunchKernelGGL(copy_runs_kernel<U>, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), cr,
+                     (int)total);
+  hip_check(hipGetLastError(), "copy_runs launch");
+  return grid;
+}
+
 }  // namespace pr

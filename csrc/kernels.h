@@ -33,6 +33,9 @@ void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_run
 void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool bf16, uint64_t stream);
 // host (pinned / registered) -> HBM copy by a kernel; false = not applicable, use hipMemcpyAsync
 bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgroups, uint64_t stream);
+// device -> device (incl. IPC-mapped peer HBM) copies of up to kMaxCopyRuns runs in ONE launch
+// (queue fabric); fills cr.cstart, returns the grid size used
+int launch_copy_runs(CopyRuns& cr, int workgroups, uint64_t stream);
 void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nout, uint64_t omask,
                      uint64_t stream);
 // scratch: 0, or a zero-initialised PfScratch block (kPfScratchBytes) reused by every launch on one

@@ -30,13 +30,13 @@ PinnedBuffer::~PinnedBuffer() {
 // ---------------------------------------------------------------------------------------
 DeviceBuffer::DeviceBuffer(int64_t bytes, int device) : bytes_(bytes), device_(device) {
   check(bytes > 0 && device >= 0, "DeviceBuffer: size must be > 0 on a device");
-  hip_check(hipSetDevice(device), "hipSetDevice");
+  DeviceGuard dg(device);
   hip_check(hipMalloc(&ptr_, (size_t)bytes), "hipMalloc (ring segment)");
 }
 
 DeviceBuffer::~DeviceBuffer() {
   if (ptr_ != nullptr) {
-    (void)hipSetDevice(device_);
+    DeviceGuard dg(device_);
     (void)hipFree(ptr_);
   }
 }
@@ -52,7 +52,7 @@ SlotPool::SlotPool(int producer_budget, int consumer_budget, int device)
   free_ref_.resize(n_);
   for (int i = 0; i < n_; ++i) free_list_.push_back(i);
   if (device_ >= 0) {
-    set_device();
+    DeviceGuard dg(device_);
     const int ne = std::max(256, 4 * n_);
     ev_.resize(ne);
     ev_gen_.assign(ne, 0);
@@ -63,7 +63,7 @@ SlotPool::SlotPool(int producer_budget, int consumer_budget, int device)
 
 SlotPool::~SlotPool() {
   if (device_ >= 0) {
-    set_device();
+    DeviceGuard dg(device_);
     for (auto e : ev_) (void)hipEventDestroy(e);
   }
 }
@@ -86,7 +86,7 @@ void SlotPool::check_slot(int slot) const {
 SlotPool::EvRef SlotPool::record_shared_locked(uint64_t stream) {
   EvRef r;
   if (device_ < 0) return r;
-  set_device();
+  DeviceGuard dg(device_);
   r.idx = ev_next_;
   ev_next_ = (ev_next_ + 1) % (int)ev_.size();
   r.gen = ++ev_gen_[r.idx];
@@ -305,7 +305,7 @@ void SlotPool::wait_ready_on(int slot, uint64_t stream) const {
     if (!ref_live_locked(ready_ref_[slot])) return;
     r = ready_ref_[slot];
   }
-  set_device();
+  DeviceGuard dg(device_);
   wait_ref(r, stream);
 }
 
@@ -318,7 +318,7 @@ void SlotPool::wait_free_on(int slot, uint64_t stream) const {
     if (!ref_live_locked(free_ref_[slot])) return;
     r = free_ref_[slot];
   }
-  set_device();
+  DeviceGuard dg(device_);
   wait_ref(r, stream);
 }
 
@@ -331,7 +331,7 @@ void SlotPool::sync_ready(int slot) const {
     if (!ref_live_locked(ready_ref_[slot])) return;
     e = ev_[ready_ref_[slot].idx];
   }
-  set_device();
+  DeviceGuard dg(device_);
   hip_check(hipEventSynchronize(e), "hipEventSynchronize");
 }
 
@@ -361,7 +361,7 @@ std::vector<int> SlotPool::acquire_batch(int n, double timeout_s, uint64_t strea
     }
   }
   if (device_ >= 0 && !waits.empty()) {
-    set_device();
+    DeviceGuard dg(device_);
     for (const auto& w : waits) wait_ref(w, stream);
   }
   return out;
@@ -405,7 +405,7 @@ void SlotPool::begin_send_batch(const std::vector<int>& slots, uint64_t stream) 
     }
   }
   if (device_ >= 0 && !waits.empty()) {
-    set_device();
+    DeviceGuard dg(device_);
     for (const auto& w : waits) wait_ref(w, stream);
   }
 }
@@ -431,7 +431,7 @@ std::vector<int> SlotPool::begin_recv_batch(int n, uint64_t stream) {
     }
   }
   if (device_ >= 0 && !waits.empty()) {
-    set_device();
+    DeviceGuard dg(device_);
     for (const auto& w : waits) wait_ref(w, stream);
   }
   return out;
@@ -452,6 +452,24 @@ void SlotPool::end_send_batch(const std::vector<int>& slots, uint64_t stream) {
     free_list_.push_back(s);
     ++st_.sent;
   }
+  cv_produce_.notify_all();
+}
+
+void SlotPool::end_send_completed(const std::vector<int>& slots, bool to_external) {
+  if (slots.empty()) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int s : slots) {
+    check_slot(s);
+    check(state_[s] == kSending, state_msg("end_send_completed", kSending, state_[s]));
+  }
+  for (int s : slots) {
+    free_ref_[s] = EvRef{};   // the host saw the copy complete: the next writer needs no device wait
+    state_[s] = kFree;
+    free_list_.push_back(s);
+    ++st_.sent;
+  }
+  producer_held_ -= (int)slots.size();
+  if (to_external) ext_held_ += (int)slots.size();
   cv_produce_.notify_all();
 }
 
@@ -607,7 +625,7 @@ std::vector<int> SlotPool::reclaim_batch(int n, uint64_t stream) {
     }
   }
   if (device_ >= 0 && !waits.empty()) {
-    set_device();
+    DeviceGuard dg(device_);
     for (const auto& w : waits) wait_ref(w, stream);
   }
   return out;
@@ -652,7 +670,7 @@ std::vector<int> SlotPool::get_batch(int max_n, double timeout_s, uint64_t strea
     }
   }
   if (device_ >= 0 && !waits.empty()) {
-    set_device();
+    DeviceGuard dg(device_);
     for (const auto& w : waits) wait_ref(w, stream);
   }
   return out;
@@ -681,7 +699,7 @@ std::vector<int> SlotPool::grant_batch(int max_n) {
   std::lock_guard<std::mutex> lk(mu_);
   const int n = std::min(max_n, cb_ - consumer_held_);
   if (n <= 0) return out;
-  if (device_ >= 0) set_device();
+  DeviceGuard dg(device_);
   for (auto it = free_list_.begin(); it != free_list_.end() && (int)out.size() < n;) {
     const int s = *it;
     const EvRef r = free_ref_[s];
@@ -764,6 +782,21 @@ int SlotPool::reoffer_batch(const std::vector<int>& slots, uint64_t stream) {
   }
   if (n > 0) cv_produce_.notify_one();
   return n;
+}
+
+int SlotPool::relay_ready(int max_n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  const int room = pb_ - producer_held_ - ext_held_;
+  int n = std::min<int>(std::min(max_n, room), (int)ready_fifo_.size());
+  for (int i = 0; i < n; ++i) {
+    const int s = pop_ready_locked();   // counts as taken: its producer learns it left the queue
+    state_[s] = kProduced;              // ready_ref_ (the frame's data) is kept
+    --consumer_held_;
+    ++producer_held_;
+    produced_fifo_.push_back(s);
+  }
+  if (n > 0) cv_produce_.notify_one();
+  return std::max(0, n);
 }
 
 std::vector<SlotHeader> SlotPool::headers(const std::vector<int>& slots) const {

@@ -160,6 +160,12 @@ class SlotPool {
   void begin_send_batch(const std::vector<int>& slots, uint64_t stream);   // + stream waits for their data
   std::vector<int> begin_recv_batch(int n, uint64_t stream);              // + stream waits for free slots
   void end_send_batch(const std::vector<int>& slots, uint64_t stream);
+  // queue fabric: copies the host has SEEN complete (event query) -- the slots are free with no
+  // device-side wait (end_send_batch would record a free event behind every copy queued since on
+  // that stream, each waiting for a later chunk's calibration).  to_external: the frames move from
+  // producer_held to the external read-ahead count in the same locked step, so producer_room()
+  // never reads high between the two (ADVICE r3 keeper race).
+  void end_send_completed(const std::vector<int>& slots, bool to_external);
   void end_recv_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream);
   int64_t event_records() const { return ev_records_; }
 
@@ -173,6 +179,11 @@ class SlotPool {
   // (LEASED -> PRODUCED, headers kept; consumer budget -> producer budget).  Returns how many
   // moved (stops when the producer budget is full).
   int reoffer_batch(const std::vector<int>& slots, uint64_t stream);
+  // queue keeper, atomically: up to max_n READY frames straight to PRODUCED (FIFO, headers and data
+  // references kept), bounded by the producer room read under the same lock -- no frame is ever
+  // leased without room to re-offer it (room read, lease and re-offer were three calls
+  // the fabric thread could interleave with).  Returns how many moved.
+  int relay_ready(int max_n);
   // Origins of consumed frames (elastic fabric): a received frame remembers the producer member it
   // came from (-1: routed locally); every frame a consumer takes (get / get_batch) appends its
   // origin to a log the fabric drains, so each producer learns how many of its frames were taken.

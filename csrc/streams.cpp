@@ -10,7 +10,7 @@
 namespace pr {
 
 hipStream_t make_stream(int device, int kind) {
-  hip_check(hipSetDevice(device), "hipSetDevice");
+  DeviceGuard dg(device);
   hipStream_t s = nullptr;
   if (kind == kStreamDedicated) {
     hipDeviceProp_t prop{};
@@ -61,7 +61,7 @@ static bool& pool_closed() {
 
 void release_stream(int device, int kind, hipStream_t s) {
   if (s == nullptr) return;
-  (void)hipSetDevice(device);
+  DeviceGuard dg(device);
   (void)hipStreamSynchronize(s);
   {
     std::lock_guard<std::mutex> lk(pool_mu());
@@ -81,7 +81,7 @@ void close_stream_pool() {
     all.swap(pool());
   }
   for (auto& kv : all) {
-    (void)hipSetDevice(kv.first.first);
+    DeviceGuard dg(kv.first.first);
     for (hipStream_t s : kv.second) {
       (void)hipStreamSynchronize(s);
       (void)hipStreamDestroy(s);

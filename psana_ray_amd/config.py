@@ -54,6 +54,26 @@ PRODUCER_STREAM_KIND = {"device": "dedicated", "staged": "shared"}
 # Consumer: the peak finder's two alternating streams, each on its own hardware queue (ordinary
 # streams landed both on ONE queue: rocprofv3 Queue_Id, profiles/r3/streams2/)
 CONSUMER_STREAM_KIND = "dedicated"
+# Queue fabric (csrc/fabric.h): how a producer moves frames into OTHER processes' GPU rings.
+# "kernel": every frame of one fabric pass, to all its consumers, in ONE copy_runs_kernel launch on
+# a stream with its own hardware queue, bounded to FABRIC_COPY_WORKGROUPS workgroups; "runtime":
+# hipMemcpyAsync per contiguous run on one ordinary stream per link (the round-3 path; A/B only).
+# Env override: PSANA_RAY_AMD_FABRIC_COPY=kernel|runtime[:workgroups].
+FABRIC_COPY_ENGINES = {"kernel": 0, "runtime": 1}
+FABRIC_COPY_ENGINE = "kernel"
+FABRIC_COPY_WORKGROUPS = 128
+
+
+def fabric_copy_setting(engine: Optional[str] = None, workgroups: Optional[int] = None) -> tuple[str, int]:
+    """(engine, workgroups) for a new fabric: explicit arguments, else the environment, else the
+    defaults above."""
+    env = os.environ.get("PSANA_RAY_AMD_FABRIC_COPY", "")
+    e_env, _, w_env = env.partition(":")
+    eng = engine or e_env or FABRIC_COPY_ENGINE
+    if eng not in FABRIC_COPY_ENGINES:
+        raise ValueError(f"unknown fabric copy engine {eng!r} ({' | '.join(FABRIC_COPY_ENGINES)})")
+    wgs = workgroups if workgroups else (int(w_env) if w_env else FABRIC_COPY_WORKGROUPS)
+    return eng, int(wgs)
 
 # --- rendezvous ---------------------------------------------------------------------------
 DEFAULT_STORE_PORT = 6379             # the Ray head port of README.md:15, reused for the store
@@ -110,6 +130,24 @@ class CommonModeParams:
         if len(parts) > 4:
             cm.bank_cols = int(parts[4])
         return cm
+
+
+# Common mode by detector family when the CLI says "auto" (the producer's default): psana's calib of
+# an ePix10ka includes common mode (SURVEY E-03 / Appendix B), Jungfrau has none by default.
+CM_AUTO_FAMILIES = ("epix10ka",)
+
+
+def resolve_common_mode(text: Optional[str], spec) -> Optional["CommonModeParams"]:
+    """``--common_mode`` value -> parameters for detector ``spec`` (models.detector.DetectorSpec):
+    ``auto`` = the defaults for families whose psana calibration applies common mode, else off;
+    anything else as :meth:`CommonModeParams.parse`.  The bank width comes from the detector."""
+    if text is not None and text.lower() == "auto":
+        cm = CommonModeParams() if spec.kind in CM_AUTO_FAMILIES else None
+    else:
+        cm = CommonModeParams.parse(text)
+    if cm is not None and cm.bank_cols is None:
+        cm.bank_cols = spec.bank_cols
+    return cm
 
 
 @dataclass

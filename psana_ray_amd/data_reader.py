@@ -146,14 +146,15 @@ class DataReader:
         from .source import open_source
 
         src = open_source(recipe["exp"], int(recipe["run"]), recipe["detector_name"], rank=0, size=1, pinned=False,
-                          pool_frames=1, data_dir=recipe.get("data_dir"))
+                          pool_frames=1, data_dir=recipe.get("data_dir"), mode=Mode.raw)
         if getattr(src, "calibrated", False) or not hasattr(src, "consts"):
             raise DataReaderError("calibrate_on_read: the producer's source has no calibration constants here")
         mask = load_masks(src, recipe.get("uses_bad_pixel_mask", False), recipe.get("manual_mask_path"))
         cm = recipe.get("common_mode")
         cm = None if cm is None else CommonModeParams(int(cm[0]), float(cm[1]), float(cm[2]), int(cm[3]),
                                                       None if cm[4] is None else int(cm[4]))
-        return Calibrator(src.consts, device, Mode(recipe["mode"]), mask=mask, common_mode=cm)
+        return Calibrator(src.consts, device, Mode(recipe["mode"]), mask=mask, common_mode=cm,
+                          geometry=getattr(src, "geometry", None))
 
     @property
     def calibrator(self):

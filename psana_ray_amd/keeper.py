@@ -13,7 +13,7 @@ for consumers to take them.  The keeper removes that wait: it is a session membe
     the keeper as they are produced and survive a producer crash, like puts into the detached
     actor; producers route to a keeper only when no real consumer has credit, so it never
     competes with live consumers (``QueueFabric.set_grant_filter`` / ``set_keeper``);
-  * every frame it receives goes straight back on offer (``SlotPool.reoffer_batch``: headers kept)
+  * every frame it receives goes straight back on offer (``SlotPool.relay_ready``: headers kept)
     and, as a PRODUCER with the ``relay`` policy (never to itself), it delivers them to any
     consumer that attaches, whenever that is;
   * once every other producer of the session is finished and it holds nothing, it posts EOS on
@@ -96,17 +96,13 @@ def run(args) -> int:
                 if mid not in granted and (sess.state(mid) == "draining" or sess.finished(mid)):
                     fab.set_peer_grantable(mid, True)
                     granted.add(mid)
-            # lease only what can go back on offer: a frame taken out of the receive side and not
-            # re-offered would be lost (the producer already counted it as delivered)
-            room = min(64, pool.producer_room())
-            slots = pool.get_batch(room, 0.05, 0) if room > 0 else []
-            if room <= 0:
-                time.sleep(0.05)   # every held frame is on offer: wait for consumers to take some
-            if slots:
-                moved = pool.reoffer_batch(slots, 0)
-                kept += moved
-                if moved != len(slots):
-                    raise RuntimeError(f"keeper: {len(slots) - moved} leased frames could not be re-offered")
+            # received frames go straight back on offer in ONE locked native step bounded by the
+            # producer room read under that lock (SlotPool.relay_ready): a frame is never taken out of
+            # the receive side without room to re-offer it, however the fabric thread interleaves
+            moved = pool.relay_ready(64)
+            kept += moved
+            if moved == 0:
+                time.sleep(0.005 if pool.n_ready() else 0.02)   # nothing received, or no room yet
             if ep.failed is not None:
                 raise RuntimeError(f"queue fabric failed: {ep.failed}")
             idle = pool.n_ready() == 0 and pool.n_produced() == 0 and pool.consumer_held() == 0 \

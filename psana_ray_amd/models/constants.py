@@ -102,8 +102,9 @@ class CalibConstants:
     def device_tables(self, mask: Optional[np.ndarray] = None):
         """Kernel tables: ``ped [NC, npix]``, ``gf [NC, npix]`` (mask folded) and the common-mode
         eligibility bit-planes ``elig [npix / 8, S]`` (uint8, S = 1, 2 or 4 for 1, 2 or 3 candidate
-        tables): bit j of byte k of group g is set when pixel 8g + j is CM-eligible (kept, status
-        good, gain in the CM set) if it decodes to candidate k (csrc/common_mode.hip cm_decode8).
+        tables): bit j of byte k of group g is set when pixel 8g + j is CM-eligible (status good,
+        gain in the CM set; the output mask does not enter) if it decodes to candidate k
+        (csrc/common_mode.hip cm_decode8).
 
         ``mask`` is the combined output mask (bad-pixel & manual, truthy = keep) in frame shape;
         None keeps every pixel (the reference applies masks only when asked, producer.py:92-95).
@@ -126,7 +127,9 @@ class CalibConstants:
         planes = np.zeros((npix // 8, stride), np.uint8)
         weights = (1 << np.arange(8)).astype(np.uint16)
         for c in range(nc):
-            elig = (keep & status_good & cm_set[cand[c]]).reshape(npix // 8, 8)
+            # common-mode eligibility ignores the output mask: the reference applies masks to psana's
+            # calibrated frames afterwards (producer.py:92-95), so they never change the median
+            elig = (status_good & cm_set[cand[c]]).reshape(npix // 8, 8)
             planes[:, c] = (elig.astype(np.uint16) * weights).sum(axis=1).astype(np.uint8)
         return (np.ascontiguousarray(ped.reshape(-1, npix)),
                 np.ascontiguousarray(gf.reshape(-1, npix)),

@@ -106,7 +106,10 @@ def calibrate_reference(raw: torch.Tensor, consts: CalibConstants, mask: Optiona
         cm_set = torch.zeros(max(s.n_gains, 1), dtype=torch.bool, device=raw.device)
         cm_set[list(consts.cm_gains)] = True
         status_good = torch.as_tensor(consts.status == 0, device=raw.device)
-        elig = valid & keep & status_good & cm_set[g]
+        # the output mask does NOT enter the estimate: the reference masks psana's calibrated frames
+        # afterwards (np.where(mask, data, 0), psana_ray/producer.py:92-95), psana's common mode sees
+        # only its own status constants
+        elig = valid & status_good & cm_set[g]
         v = common_mode_reference(v, elig, consts, cm)
     gf = 1.0 / gain                      # float32, same rounding as the packed device table
     out = v * gf

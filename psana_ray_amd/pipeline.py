@@ -39,13 +39,19 @@ class ProducerPipeline:
     def __init__(self, source, calibrator: Optional[Calibrator], endpoint: QueueEndpoint, rank: int = 0,
                  chunk: int = 32, n_raw_buffers: int = 6, acquire_timeout_s: float = 1.0,
                  log_every: int = 0, copy_workgroups: int = 32, gpu_timing: bool = False,
-                 compute_streams: Optional[int] = None, stream_kind: Optional[str] = None):
+                 compute_streams: Optional[int] = None, stream_kind: Optional[str] = None,
+                 mask: Optional[np.ndarray] = None, n_upload_buffers: int = 3):
         """copy_workgroups: host->HBM staging by copy_h2d_kernel with that many workgroups (0 = the
         runtime's hipMemcpyAsync); gpu_timing: event-time each chunk's copy and calibration;
         compute_streams: chunks alternate over that many HIP streams (native engine), so one chunk's
         calibration fills the CUs its predecessor's tail leaves idle; stream_kind: their
         hardware-queue placement (config.STREAM_KINDS).  None: config.PRODUCER_STREAMS /
-        PRODUCER_STREAM_KIND for the source (raw frames already in HBM or staged)."""
+        PRODUCER_STREAM_KIND for the source (raw frames already in HBM or staged).
+
+        Sources whose frames arrive calibrated (psana_wrapper without raw access): ``mask`` (truthy
+        keeps, producer.py:92-95) is applied on the device after the upload; frames move in
+        ``chunk``-frame batches through ``n_upload_buffers`` pinned staging buffers (one H2D copy per
+        frame, no host synchronisation except before a staging buffer is refilled)."""
         self.source = source
         self.cal = calibrator
         self.ep = endpoint
@@ -77,6 +83,9 @@ class ProducerPipeline:
             self.buf_used = [False] * n_raw_buffers
             self.h2d_done = [torch.cuda.Event() for _ in range(n_raw_buffers)]
         self._k = 0
+        self.mask = None
+        if self.calibrated_source:
+            self._init_upload(mask, n_upload_buffers)
         # completion log of the Python paths: (frames so far, perf_counter s) at commit -- the CPU
         # calibration is synchronous, so commit == completion (the native engine logs device events)
         self._done_log: List[tuple] = []
@@ -179,26 +188,92 @@ class ProducerPipeline:
                      tuple(self.ep.ring.frame_shape), evs[-1].photon_energy)
         return n
 
-    def _step_calibrated(self) -> int:
-        """psana path: frames arrive calibrated on the host; upload into the slot."""
-        if not hasattr(self, "_it"):
-            from .models.detector import Mode
-
-            self._it = enumerate(self.source.iter_events(self.cal.mode if self.cal else Mode.calib),
-                                 start=int(getattr(self.source, "_skip", 0)))
-        try:
-            idx, (data, pe) = next(self._it)
-        except StopIteration:
-            return 0
-        if data.ndim == 2:
-            data = data[None]
-        (s,) = self._acquire(1, None)
-        self.ep.slot_tensor(s).copy_(torch.from_numpy(np.ascontiguousarray(data, dtype=np.float32)))
+    def _init_upload(self, mask, n_bufs: int):
+        """Pinned staging for sources that deliver calibrated frames (psana_wrapper fallback path)."""
+        shape = tuple(self.ep.ring.frame_shape)
+        self._up_shape = shape
+        self._up_bufs, self._up_done, self._up_keep = [], [], []
+        if mask is not None:
+            m = np.asarray(mask).astype(bool)
+            if m.shape != shape:
+                if m.size != int(np.prod(shape)):
+                    raise ValueError(f"mask of shape {m.shape} does not match the frames {shape}")
+                m = m.reshape(shape)
+            self.mask = torch.from_numpy(~m).to(self.device)   # True = zero this pixel
         if self.gpu:
-            torch.cuda.current_stream(self.device).synchronize()
-        self.ep.commit(s, self.rank, idx, idx, pe)
-        self.frames += 1
-        return 1
+            C = _ext.load()
+            nbytes = self.chunk * int(np.prod(shape)) * 4
+            for _ in range(max(2, n_bufs)):
+                keep = C.PinnedBuffer(nbytes)
+                self._up_keep.append(keep)
+                self._up_bufs.append(np.frombuffer(keep, dtype=np.float32).reshape(self.chunk, *shape))
+                self._up_done.append(None)
+            self._up_stream = torch.cuda.Stream(device=self.device)
+        self._it = None
+
+    def _step_calibrated(self) -> int:
+        """psana path: frames arrive calibrated on the host in the producer's mode.  Up to ``chunk``
+        frames are gathered into a pinned staging buffer, copied into their ring slots on a side
+        stream (one H2D copy per frame), masked on the device and committed stream-ordered; the host
+        waits only before it refills a staging buffer whose copies are still running."""
+        if self._it is None:
+            self._it = self.source.iter_events(self.source.mode) if hasattr(self.source, "mode") \
+                else self.source.iter_events()
+            self._idx = int(getattr(self.source, "cursor", 0))
+        shape = self._up_shape
+        frames, pes = [], []
+        for _ in range(self.chunk):
+            try:
+                data, pe = next(self._it)
+            except StopIteration:
+                break
+            data = np.asarray(data)
+            if data.ndim == 2:
+                data = data[None]   # producer.py:96-97
+            if data.shape != shape:
+                raise ValueError(f"psana frame of shape {data.shape}; the queue was built for {shape}")
+            frames.append(data)
+            pes.append(pe)
+        n = len(frames)
+        if n == 0:
+            return 0
+        idx0 = self._idx
+        self._idx += n
+        if self.gpu:
+            C = _ext.load()
+            b = self._k % len(self._up_bufs)
+            self._k += 1
+            if self._up_done[b] is not None:
+                self._up_done[b].synchronize()   # this staging buffer's previous copies finished
+            buf = self._up_bufs[b]
+            for i, f in enumerate(frames):
+                np.copyto(buf[i], f, casting="same_kind")
+            st = self._up_stream
+            slots = self._acquire(n, st)
+            C.memcpy_h2d_batch([int(self.ep.slot_ptr(s)) for s in slots], [int(buf[i].ctypes.data) for i in range(n)],
+                               int(buf[0].nbytes), int(st.cuda_stream))
+            if self.mask is not None:
+                with torch.cuda.stream(st):
+                    for s in slots:
+                        self.ep.slot_tensor(s).masked_fill_(self.mask, 0.0)   # np.where(mask, data, 0)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            self._up_done[b] = ev
+            for i, s in enumerate(slots):
+                self.ep.commit(s, self.rank, idx0 + i, self.rank + (idx0 + i) * int(getattr(self.source, "size", 1)),
+                               pes[i], st)
+        else:
+            slots = self._acquire(n, None)
+            for i, s in enumerate(slots):
+                t = self.ep.slot_tensor(s)
+                t.copy_(torch.from_numpy(np.ascontiguousarray(frames[i], dtype=np.float32)).view(t.shape))
+                if self.mask is not None:
+                    t.masked_fill_(self.mask.view(t.shape), 0.0)
+                self.ep.commit(s, self.rank, idx0 + i, self.rank + (idx0 + i) * int(getattr(self.source, "size", 1)),
+                               pes[i])
+            self._done_log.append((self.frames + n, time.perf_counter()))
+        self.frames += n
+        return n
 
     @property
     def produced(self) -> int:
@@ -248,12 +323,14 @@ class ProducerPipeline:
             if max_steps is not None and self.frames >= max_steps:
                 log.info("Rank %d: Reached max_steps %d, terminating", self.rank, max_steps)
                 break
-            if max_steps is not None and not self.calibrated_source:
+            if max_steps is not None:
                 self.chunk = max(1, min(self.chunk, max_steps - self.frames))
             if self.step() == 0:
                 break
         if self.gpu and not self.calibrated_source:
             self.compute.synchronize()
+        if self.gpu and self.calibrated_source:
+            self._up_stream.synchronize()
         self.ep.finish()
         return self.frames
 

@@ -105,11 +105,13 @@ class FrameItem:
 
 class QueueEndpoint:
     def __init__(self, ring: FrameRing, session=None, is_producer: bool = True, is_consumer: bool = True,
-                 route: str = "balanced", prefetch: int = 0, keeper: bool = False):
+                 route: str = "balanced", prefetch: int = 0, keeper: bool = False,
+                 copy_engine: Optional[str] = None, copy_workgroups: Optional[int] = None):
         """``prefetch`` (consumer role, fabric mode): at most this many frames noticed-but-not-taken
         plus grants outstanding -- the read-ahead a crashed consumer can lose (0: the ring's free
         slots only).  ``keeper``: this member is a queue keeper (its links are marked so producers
-        use it only as the last resort)."""
+        use it only as the last resort).  ``copy_engine`` / ``copy_workgroups`` (producer role, GPU):
+        how frames move into other processes' rings (config.fabric_copy_setting)."""
         if route not in POLICIES:
             raise ValueError(f"unknown routing policy {route!r} ({' | '.join(POLICIES)})")
         self.ring = ring
@@ -140,6 +142,11 @@ class QueueEndpoint:
                                      POLICIES[route], session.mid)
         self._fabric.set_prefetch(int(prefetch))
         self._fabric.set_keeper(bool(keeper))
+        from ..config import FABRIC_COPY_ENGINES, fabric_copy_setting
+
+        eng, wgs = fabric_copy_setting(copy_engine, copy_workgroups)
+        self._fabric.set_copy_engine(FABRIC_COPY_ENGINES[eng], int(wgs))
+        self.copy_engine = (eng, int(wgs))
         if self.is_consumer:
             if self.gpu:
                 self._fabric.export_ipc_ring()
@@ -380,10 +387,20 @@ class QueueEndpoint:
                 "returns_rejected": st.returns_rejected, "readahead": st.readahead,
                 "links_opened": st.links_opened, "links_live": sum(1 for ls in links if ls.attached and not ls.dead),
                 "copy_ms_per_batch": 1e3 * st.copy_s / max(1, st.batches),
+                "copy_launches": st.copy_launches, "copy_dev_ms": st.copy_dev_ms,
+                "copy_dev_bytes": st.copy_dev_bytes,
                 "iterations": st.iterations, "idle_iterations": st.idle_iterations}
 
     def links(self) -> list:
         return [] if self._fabric is None else list(self._fabric.links())
+
+    def copy_samples(self) -> list:
+        """Timed copy dispatches of this producer (newest last): ``(device ms, issue->done ms, bytes,
+        frames, links)`` -- device ms is the copy alone, issue->done includes the wait for the
+        frames' calibration the copy is ordered after."""
+        if self._fabric is None:
+            return []
+        return [(c.dev_ms, c.issue_to_done_ms, c.bytes, c.frames, c.links) for c in self._fabric.copy_samples()]
 
     def metrics(self) -> dict:
         """Gauges + cumulative counters for utils.metrics."""

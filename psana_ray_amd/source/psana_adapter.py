@@ -1,19 +1,43 @@
-"""Optional adapter over the real ``psana_wrapper`` (E-01), used only when it is importable.
+"""Adapter over the real ``psana_wrapper`` (E-01), used when it is importable.
 
 The reference constructs ``PsanaWrapperSmd(exp=..., run=..., detector_name=...)`` and iterates
-``iter_events(mode=ImageRetrievalMode.calib|image)`` (psana_ray/producer.py:150-159).  psana
-calibrates on the CPU, so frames from this source are already calibrated: the producer
-uploads them (pinned -> hipMemcpyAsync) and skips the HIP calibration kernels.  Neither psana
-nor psana_wrapper exists in this environment: this path is import-gated and
-its parity is unpinned.
+``iter_events(mode=ImageRetrievalMode.calib|image)`` -> ``(data, photon_energy)``, with an
+optional ``create_bad_pixel_mask()`` (psana_ray/producer.py:11,81,88,150-159).  psana shards the
+run over the MPI ranks itself (SMD mode, P-01), so each rank's wrapper yields that rank's events.
+
+Two ways frames enter the GPU pipeline:
+
+* **raw** (preferred): when the wrapper offers ``ImageRetrievalMode.raw`` AND the run's
+  calibration constants (the adapter hook ``calib_constants()``, below), the source yields RAW
+  uint16 frames through pinned staging and the producer calibrates them with the gfx950 kernels
+  (K-01..K-05: gain decode, pedestal, gain, common mode, masks, geometry) -- the same path as the
+  synthetic and file sources.  psana's CPU calibration never runs.
+* **calibrated** (fallback): frames arrive calibrated by psana in the requested mode and are
+  uploaded in pinned batches (one H2D copy per chunk, no per-frame synchronisation); masks are
+  applied on the GPU.
+
+``calib_constants()`` hook -- a mapping with
+  ``pedestals`` [G, P, H, W] (ADU), ``gains`` [G, P, H, W] (ADU per keV),
+  optional ``status`` [P, H, W] (non-zero = bad), ``gain_config`` [P, H, W] (epix10ka: 0..4 =
+  FH FM FL AHL AML), ``pix_rows`` / ``pix_cols`` [P, H, W] (image-mode pixel indices; default: the
+  framework's geometry of the detector).
+The detector must be one the framework knows (``models/detector.py``) with matching shapes.
+
+Neither psana nor psana_wrapper exists in this environment: parity with real
+psana is unpinned; the contract is pinned by a stub ``psana_wrapper`` module in
+``tests/stubs/`` (tests/test_psana_wrapper.py).
 """
 from __future__ import annotations
 
-from typing import Iterator, Optional, Tuple
+import itertools
+import logging
+from typing import Iterator, List, Optional, Tuple
 
 import numpy as np
 
 from ..models.detector import Mode
+
+log = logging.getLogger(__name__)
 
 
 def psana_available() -> bool:
@@ -25,25 +49,182 @@ def psana_available() -> bool:
         return False
 
 
+def _normalise(data: np.ndarray) -> np.ndarray:
+    """The reference's ndim fix-up (producer.py:96-97): 2-D frames become (1, H, W)."""
+    data = np.asarray(data)
+    return data[None] if data.ndim == 2 else data
+
+
 class PsanaWrapperSource:
-    calibrated = True
+    """``(exp, run, detector_name)`` through psana_wrapper, for one producer rank.
 
-    def __init__(self, exp: str, run: int, detector_name: str):
-        from psana_wrapper import ImageRetrievalMode, PsanaWrapperSmd  # type: ignore
+    ``mode`` is the retrieval mode the producer serves (image by default, producer.py:156-159).
+    After construction ``calibrated`` tells which path applies: False -> ``spec`` / ``consts`` /
+    ``geometry`` describe the raw frames ``next_events`` stages; True -> ``frame_shape`` is the shape
+    of the calibrated frames ``iter_events`` yields (peeked from the first event)."""
 
-        self._mode_enum = ImageRetrievalMode
-        self.wrapper = PsanaWrapperSmd(exp=exp, run=run, detector_name=detector_name)
+    def __init__(self, exp: str, run: int, detector_name: str, mode: Mode = Mode.image, rank: int = 0,
+                 size: int = 1, pinned: bool = False, prefer_raw: bool = True, staging: int = 128,
+                 n_events: Optional[int] = None):
+        import psana_wrapper  # type: ignore
 
+        self.exp, self.run, self.detector_name = exp, int(run), detector_name
+        self.rank, self.size = int(rank), int(size)
+        self.mode = Mode(mode)
+        self.n_events = n_events
+        self._modes = psana_wrapper.ImageRetrievalMode
+        self.wrapper = psana_wrapper.PsanaWrapperSmd(exp=exp, run=run, detector_name=detector_name)
+        self._skip = 0
+        self._cursor = 0
+        self._it = None
+        self._peeked: Optional[Tuple[np.ndarray, Optional[float]]] = None
+        self.geometry = None
+        self.consts = None
+        why = self._try_raw(prefer_raw)
+        self.calibrated = why is not None
+        if self.calibrated:
+            if self.mode == Mode.raw:
+                raise RuntimeError(f"psana_wrapper source {exp}/{run}/{detector_name}: raw mode requested but {why}")
+            log.info("psana_wrapper %s/%d/%s: psana-calibrated %s frames uploaded in pinned batches (%s)", exp, run,
+                     detector_name, self.mode.value, why)
+            first = self._peek()
+            if first is None:
+                raise RuntimeError(f"psana_wrapper source {exp}/{run}/{detector_name}: the run has no events")
+            self.frame_shape = tuple(_normalise(first[0]).shape)
+            self.frame_dtype = np.float32
+        else:
+            log.info("psana_wrapper %s/%d/%s: RAW frames calibrated on the GPU (HIP kernels, %s mode)", exp, run,
+                     detector_name, self.mode.value)
+            self.frame_shape = tuple(self.spec.frame_shape)
+            if pinned:
+                from ..ops import _ext
+
+                self._buf = _ext.load().PinnedBuffer(staging * self.spec.raw_frame_bytes)
+                self.staging = np.frombuffer(self._buf, dtype=np.uint16).reshape(staging, *self.spec.frame_shape)
+            else:
+                self.staging = np.empty((staging, *self.spec.frame_shape), np.uint16)
+            self.n_staging = staging
+            self._slot = 0
+
+    # ---- capability probe ------------------------------------------------------------------
+    def _try_raw(self, prefer_raw: bool) -> Optional[str]:
+        """Set up the raw path; returns None when it applies, else why not."""
+        if not prefer_raw:
+            return "raw path disabled"
+        if not hasattr(self._modes, "raw"):
+            return "the wrapper has no ImageRetrievalMode.raw"
+        hook = getattr(self.wrapper, "calib_constants", None)
+        if hook is None:
+            return "the wrapper exposes no calib_constants()"
+        from ..models.constants import EPIX_CM_GAINS, JUNGFRAU_CM_GAINS, CalibConstants
+        from ..models.detector import get_detector
+        from ..models.geometry import Geometry, make_geometry
+
+        try:
+            spec = get_detector(self.detector_name)
+        except KeyError:
+            return f"detector {self.detector_name!r} has no kernel description"
+        c = hook()
+        ped = np.ascontiguousarray(c["pedestals"], dtype=np.float32)
+        gains = np.ascontiguousarray(c["gains"], dtype=np.float32)
+        want = (spec.n_gains, *spec.frame_shape)
+        if ped.shape != want or gains.shape != want:
+            return f"constants {ped.shape} / {gains.shape} do not match {spec.name} {want}"
+        status = np.asarray(c.get("status", np.zeros(spec.frame_shape, np.uint8))).astype(np.uint8)
+        cfg = c.get("gain_config")
+        if spec.kind == "epix10ka":
+            cfg = np.full(spec.frame_shape, 3, np.uint8) if cfg is None else np.asarray(cfg).astype(np.uint8)
+        cmg = {"epix10ka": EPIX_CM_GAINS, "jungfrau": JUNGFRAU_CM_GAINS}.get(spec.kind, (0,))
+        self.spec = spec
+        self.consts = CalibConstants(spec, ped, gains, status.reshape(spec.frame_shape), cfg, tuple(cmg))
+        rows, cols = c.get("pix_rows"), c.get("pix_cols")
+        if rows is not None and cols is not None:
+            rows = np.asarray(rows, np.int32).reshape(spec.frame_shape)
+            cols = np.asarray(cols, np.int32).reshape(spec.frame_shape)
+            self.geometry = Geometry(spec, (int(rows.max()) + 1, int(cols.max()) + 1), rows, cols)
+        else:
+            self.geometry = make_geometry(spec)
+        return None
+
+    # ---- reference surface -----------------------------------------------------------------
     def create_bad_pixel_mask(self) -> np.ndarray:
-        return self.wrapper.create_bad_pixel_mask()
+        return np.asarray(self.wrapper.create_bad_pixel_mask())
 
     def seek(self, start_event: int) -> int:
-        """Skip this rank's first ``start_event`` events (psana shards inside its SMD reader)."""
+        """Skip this rank's first ``start_event`` events (psana shards inside its SMD reader, so the
+        skip is rank-local: ``--start_event`` resumes each rank at the same local position)."""
+        if self._it is not None and self._cursor:
+            raise RuntimeError("PsanaWrapperSource.seek after events were read")
         self._skip = max(0, int(start_event))
+        self._cursor = self._skip
+        self._it = None
+        self._peeked = None
+        if self.calibrated and self._peek() is None:
+            log.warning("psana_wrapper source: nothing left after --start_event %d", start_event)
         return self._skip
 
-    def iter_events(self, mode: Mode) -> Iterator[Tuple[np.ndarray, Optional[float]]]:
-        import itertools
+    @property
+    def cursor(self) -> int:
+        return self._cursor
 
-        m = self._mode_enum.calib if Mode(mode) == Mode.calib else self._mode_enum.image
-        return itertools.islice(self.wrapper.iter_events(mode=m), getattr(self, "_skip", 0), None)
+    def _events(self):
+        if self._it is None:
+            m = getattr(self._modes, "raw" if not self.calibrated else
+                        ("calib" if self.mode == Mode.calib else "image"))
+            it = iter(self.wrapper.iter_events(mode=m))
+            self._it = itertools.islice(it, self._skip, None) if self._skip else it
+        return self._it
+
+    def _peek(self):
+        if self._peeked is None:
+            try:
+                self._peeked = next(self._events())
+            except StopIteration:
+                return None
+        return self._peeked
+
+    def _next(self):
+        if self._peeked is not None:
+            ev, self._peeked = self._peeked, None
+            return ev
+        return next(self._events())
+
+    def n_local_events(self) -> Optional[int]:
+        return None   # psana's SMD reader decides; the stream ends when the iterator does
+
+    def iter_events(self, mode: Optional[Mode] = None) -> Iterator[Tuple[np.ndarray, Optional[float]]]:
+        """Calibrated path: ``(data, photon_energy)`` in ``self.mode`` (the producer's requested mode;
+        a different ``mode`` argument is an error -- the source was opened for one mode)."""
+        if mode is not None and Mode(mode.value if hasattr(mode, "value") else mode) != self.mode:
+            raise ValueError(f"source opened for {self.mode.value} mode, asked for {mode}")
+        while True:
+            try:
+                data, pe = self._next()
+            except StopIteration:
+                return
+            self._cursor += 1
+            yield data, pe
+
+    def next_events(self, n: int) -> List:
+        """Raw path: up to ``n`` raw events staged into the (pinned) staging ring.  ``gevt`` is the
+        nominal ``rank + idx * size`` (psana's SMD batches do not expose a global index)."""
+        from .synthetic import RawEvent
+
+        out = []
+        n = min(n, self.n_staging)
+        for _ in range(n):
+            try:
+                data, pe = self._next()
+            except StopIteration:
+                break
+            s = self._slot
+            self._slot = (self._slot + 1) % self.n_staging
+            frame = np.asarray(data)
+            if frame.shape != self.spec.frame_shape:
+                frame = frame.reshape(self.spec.frame_shape)
+            np.copyto(self.staging[s], frame, casting="unsafe")
+            k = self._cursor
+            self._cursor += 1
+            out.append(RawEvent(self.rank + k * self.size, k, self.staging[s], self.staging[s].ctypes.data,
+                                None if pe is None else float(pe)))
+        return out

@@ -34,6 +34,7 @@ def main():
     import numpy as np
     import torch
 
+    from psana_ray_amd.config import resolve_common_mode
     from psana_ray_amd.data_reader import DataReader, EndOfStream
     from psana_ray_amd.ops import reference
     from psana_ray_amd.source import SyntheticRun
@@ -44,7 +45,10 @@ def main():
     def ref_frame(rank, idx):
         if rank not in refs:
             src = SyntheticRun(exp, int(run), det, rank=rank, size=int(size), pool_frames=32, gen_device=a.gen_device)
-            refs[rank] = reference.calibrate_reference(torch.from_numpy(src.pool.astype(np.int32)), src.consts)
+            # the producer CLI's default common mode (--common_mode auto: on for epix10ka)
+            cm = resolve_common_mode("auto", src.consts.spec)
+            refs[rank] = reference.calibrate_reference(torch.from_numpy(src.pool.astype(np.int32)), src.consts, None,
+                                                       cm)
         return refs[rank][idx % 32]
 
     out = open(a.out, "w", buffering=1)

@@ -28,6 +28,7 @@ def main():
     from psana_ray_amd.producer import initialize_queue
     from psana_ray_amd.queue import FrameRing, QueueEndpoint
     from psana_ray_amd.queue.session import QueueSession
+    from psana_ray_amd.producer import build_calibrator
     from psana_ray_amd.source import SyntheticRun
 
     device = torch.device(a.device)
@@ -36,7 +37,7 @@ def main():
         torch.cuda.set_device(device)
     # the same synthetic run as the producer CLI's (--exp synthetic --run 2, one rank)
     src = SyntheticRun("synthetic", 2, "tiny_epix", rank=0, size=1, pinned=gpu, gen_device="cuda" if gpu else "cpu")
-    cal = Calibrator(src.consts, device, Mode.calib)
+    cal = build_calibrator(src, device, Mode.calib, None, "auto")   # the producer CLI's default calibration
     store, meta = initialize_queue(a.address, "default", "my", a.queue_size, 0, 1, 1, cal.out_shape, "float32",
                                    device.type, timeout_s=30)
     sess = QueueSession(store, "default", "my", meta, "producer", device=device.index if gpu else -1, rank=0)

@@ -1,0 +1,102 @@
+"""Stub of the external ``psana_wrapper`` package (SURVEY E-01), for tests only.
+
+It has the surface psana-ray uses -- ``PsanaWrapperSmd(exp, run, detector_name)``,
+``.iter_events(mode)`` -> ``(data, photon_energy)``, ``.create_bad_pixel_mask()`` and
+``ImageRetrievalMode`` (psana_ray/producer.py:11,81,88,150-159) -- plus the adapter hook
+``calib_constants()`` (psana_ray_amd/source/psana_adapter.py).  Behind it sits the framework's
+synthetic detector; "psana's" calibrated / image frames are the fp32 golden model of the same raw
+frames, so a test can compare what reaches a consumer with what this stub says psana produces.
+
+Knobs (environment):
+  PSANA_STUB_RAW=0        no ImageRetrievalMode.raw / no calib_constants() (psana-calibrated path)
+  PSANA_STUB_EVENTS=N     events in the run (default 24)
+  PSANA_STUB_CM=text      common mode "psana" applies (default: "default"; "off" disables)
+SMD sharding: the rank / size come from the same launcher variables the producer reads, and rank
+r yields global events r, r + size, ... (psana's SMD mode distributes events over MPI ranks).
+"""
+from __future__ import annotations
+
+import enum
+import os
+
+import numpy as np
+
+RAW_OK = os.environ.get("PSANA_STUB_RAW", "1") != "0"
+
+if RAW_OK:
+    class ImageRetrievalMode(enum.Enum):
+        raw = "raw"
+        calib = "calib"
+        image = "image"
+else:
+    class ImageRetrievalMode(enum.Enum):
+        calib = "calib"
+        image = "image"
+
+
+def _rank_size():
+    from psana_ray_amd.parallel.launch import detect
+
+    li = detect()
+    return li.rank, li.size
+
+
+class PsanaWrapperSmd:
+    def __init__(self, exp, run, detector_name):
+        from psana_ray_amd.source.synthetic import SyntheticRun
+
+        self.exp, self.run, self.detector_name = exp, int(run), detector_name
+        self.rank, self.size = _rank_size()
+        self.n_events = int(os.environ.get("PSANA_STUB_EVENTS", "24"))
+        # one generator for the whole run (seeded by exp/run), sharded like SMD mode
+        self._syn = SyntheticRun(exp, run, detector_name, rank=0, size=1, pool_frames=8, gen_device="cpu")
+        self.consts = self._syn.consts
+
+    # ---- reference surface -------------------------------------------------------------------
+    def create_bad_pixel_mask(self):
+        return self.consts.create_bad_pixel_mask()
+
+    def raw_frame(self, gevt: int) -> np.ndarray:
+        return self._syn.pool[gevt % self._syn.pool_frames]
+
+    def photon_energy(self, gevt: int):
+        return None if gevt % 5 == 4 else float(self._syn.pool_pe[gevt % self._syn.pool_frames])
+
+    def local_events(self):
+        return range(self.rank, self.n_events, self.size)
+
+    def iter_events(self, mode):
+        name = mode.value if hasattr(mode, "value") else str(mode)
+        for g in self.local_events():
+            if name == "raw":
+                yield self.raw_frame(g).copy(), self.photon_energy(g)
+            else:
+                yield expected_frame(self, g, name), self.photon_energy(g)
+
+    # ---- adapter hook: the run's calibration constants ---------------------------------------
+    if RAW_OK:
+        def calib_constants(self):
+            c = self.consts
+            return {"pedestals": c.pedestals, "gains": c.gains, "status": c.status, "gain_config": c.gain_config}
+
+
+def stub_common_mode():
+    from psana_ray_amd.config import CommonModeParams
+
+    return CommonModeParams.parse(os.environ.get("PSANA_STUB_CM", "default"))
+
+
+def expected_frame(w: PsanaWrapperSmd, gevt: int, mode: str, mask=None) -> np.ndarray:
+    """What "psana" returns for event ``gevt`` in ``mode`` (calib: (P, H, W); image: 2-D), with an
+    optional output mask applied like the reference (np.where(mask, data, 0), producer.py:92-95)."""
+    import torch
+
+    from psana_ray_amd.models.calibrator import Calibrator
+    from psana_ray_amd.models.detector import Mode
+
+    cm = stub_common_mode()
+    if cm is not None and cm.bank_cols is None:
+        cm.bank_cols = w.consts.spec.bank_cols
+    cal = Calibrator(w.consts, "cpu", Mode(mode), mask=mask, common_mode=cm)
+    out = cal(torch.from_numpy(w.raw_frame(gevt).astype(np.int32)).to(torch.uint16)[None])[0].numpy()
+    return out[0] if mode == "image" else out

@@ -18,5 +18,6 @@ esac
 $CXX -x hip --offload-host-only --offload-arch=gfx950 -fno-gpu-sanitize -std=c++17 -O1 -g $FLAGS \
   -I"$R/csrc" \
   "$R/tests/cpp/slotpool_stress.cpp" "$R/csrc/runtime.cpp" "$R/csrc/fabric.cpp" "$R/csrc/lifecycle.cpp" "$R/csrc/trace.cpp" \
+  "$R/csrc/streams.cpp" "$R/tests/cpp/host_stubs.cpp" \
   -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64 -lpthread -lrt -o "$OUT"
 "$OUT" "$N"
