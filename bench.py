@@ -428,6 +428,13 @@ def main(argv=None):
     ep.join(timeout=60)
     peaks = consumer.synchronize() if consumer is not None else 0
     st = ep.stats()
+    # per rank over the whole run: the share of the frames it consumed that arrived from another
+    # process (consumer-only ranks of BASELINE config 3 receive every frame over the fabric)
+    recv_share = consumed_per_rank = None
+    if sess is not None:
+        got = int(st.get("got", 0))
+        consumed_per_rank = allsum(got)
+        recv_share = [round(x, 3) for x in allsum(int(st.get("frames_recv", 0)) / max(1, got))]
     copies = prod.engine.copy_stats() if (prod is not None and prod.engine is not None) else None
     if not gpu:
         staging = "host memory (CPU rehearsal)"
@@ -480,6 +487,8 @@ def main(argv=None):
             "peaks_found_rank0": peaks,
             "queue_full_waits_rank0": prod.full_waits if prod is not None else 0,
             "frames_local_rank0_headline": int(c1.get("frames_local", 0) - c0.get("frames_local", 0)),
+            "recv_cross_per_consumed_per_rank": recv_share,
+            "consumed_per_rank": consumed_per_rank,
             "frames_sent_rank0_headline": int(c1.get("frames_sent", 0) - c0.get("frames_sent", 0)),
             "bytes_sent_rank0": st.get("bytes_sent", 0),
             "xgmi_phase": cross,

@@ -25,6 +25,10 @@ def test_bench_multirank_cpu(native, nproc, route, producers):
            "--gpus", str(nproc), "--steps", "4", "--warmup", "2", "--batch", "4", "--detector", "tiny_epix",
            "--device", "cpu", "--queue-size", str(16 * nproc), "--chunk", "4", "--route", route,
            "--producers", str(producers)]
+    if producers:
+        # config 3 shape: the consumers only take frames (the CPU golden peak finder would be the
+        # bottleneck of a CPU rehearsal, not the queue), so the node must consume at the producers' rate
+        cmd += ["--consumer", "none"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -45,3 +49,11 @@ def test_bench_multirank_cpu(native, nproc, route, producers):
     # (the cross window must really cross; bench.py exits 4 below 0.9)
     assert x["cross_gpu_fraction"] >= 0.9, x
     assert all(b == 0 for b in x["bytes_sent_per_rank"][n_p:]), x
+    if producers:
+        # BASELINE config 3 shape: consumer-only ranks get every frame they consume
+        # from another process, and the node consumes at the producers' rate
+        share = d["extra"]["recv_cross_per_consumed_per_rank"]
+        assert all(v >= 0.9 for v in share[n_p:]), share
+        assert all(c > 0 for c in d["extra"]["consumed_per_rank"]), d["extra"]["consumed_per_rank"]
+        assert d["extra"]["consumer_frames_per_s"] >= 0.95 * d["extra"]["production_frames_per_s"] or \
+            d["value"] >= 0.95 * d["extra"]["production_frames_per_s"], d["extra"]
