@@ -40,7 +40,12 @@ void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nou
                      uint64_t stream);
 // scratch: 0, or a zero-initialised PfScratch block (kPfScratchBytes) reused by every launch on one
 // stream: counts / summary then need no zeroing before the launch (csrc/peakfind.hip)
-constexpr int kPfScratchBytes = 4 * (3 * kMaxFrames + 1);
+// The block also holds each workgroup's candidate SPILL list (hit-rich frames): candidates beyond the
+// kPfCandCap parked in LDS go to the workgroup's kPfSpillCap entries here and are tested after the
+// stream like the parked ones (only past both does a candidate get tested inline in the stream).
+constexpr int kPfScratchHeader = 1024;                 // PfScratch (counters), padded
+constexpr int kPfSpillWgs = 4096, kPfSpillCap = 1024;  // workgroups with a spill list, entries each
+constexpr int64_t kPfScratchBytes = kPfScratchHeader + (int64_t)kPfSpillWgs * kPfSpillCap * 4;
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
                      float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,
                      uint64_t summary, uint64_t total, uint64_t stream,

@@ -20,6 +20,7 @@
 // halo tiles 2.76-2.86, 64x16 tiles with scalar loads 5.88 (profiles/kernels_r1_peakfind_ab.jsonl;
 // the losing variants are retired).
 #include "common.h"
+#include "kernels.h"
 
 #include <map>
 #include <mutex>
@@ -157,6 +158,9 @@ struct PfScratch {
 };
 
 constexpr int kPfCandCap = 512;   // candidates parked per workgroup (2 KiB of LDS)
+static_assert(sizeof(PfScratch) <= kPfScratchHeader, "PfScratch outgrew its header");
+// spill entry: pixel | frame << 26 (frames of < 2^26 pixels; larger frames test overflow inline)
+constexpr int kPfSpillShift = 26;
 
 // Balanced grid: ONE resident wave of workgroups (CUs x occupancy) over the batch's (frame, chunk)
 // sequence, each taking a contiguous range of T / G chunks, so every workgroup ends within one
@@ -169,7 +173,8 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
                                                              float* __restrict__ peaks, int* __restrict__ counts_out,
                                                              float* __restrict__ summary_out,
                                                              unsigned long long* __restrict__ total,
-                                                             PfScratch* __restrict__ scratch, const int nframes) {
+                                                             PfScratch* __restrict__ scratch, const int nframes,
+                                                             const bool spill_ok) {
   __shared__ float red_sum[4];
   __shared__ int red_cnt[4];
   __shared__ int is_last;
@@ -189,6 +194,12 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
   const int64_t g0 = T * blockIdx.x / gridDim.x, g1 = T * (blockIdx.x + 1) / gridDim.x;
   const float NaN = __int_as_float(0x7fc00000);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // this workgroup's spill list (hit-rich frames; none without a scratch block or past kPfSpillWgs)
+  uint32_t* const spill = (scratch != nullptr && spill_ok && (int)blockIdx.x < kPfSpillWgs)
+                              ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + kPfScratchHeader) +
+                                    (int64_t)blockIdx.x * kPfSpillCap
+                              : nullptr;
+  const int cap = kPfCandCap + (spill != nullptr ? kPfSpillCap : 0);
   f32x4_t v[K];
   auto load = [&](int64_t g) {
     const int f = (int)(g / ncpf);
@@ -273,8 +284,10 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
         if (slot < kPfCandCap) {
           cand_p[slot] = (int)p;
           cand_f[slot] = (unsigned char)f;
+        } else if (slot < cap) {
+          spill[slot - kPfCandCap] = (uint32_t)p | ((uint32_t)f << kPfSpillShift);
         } else {
-          test(f, p);
+          test(f, p);   // past LDS and spill: tested in the stream (correct, slow)
         }
         ++slot;
       }
@@ -282,8 +295,17 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
   }
   if (g0 < g1) flush(fcur, above_sum, above_cnt);
   __syncthreads();
-  const int nc = min(cand_n, kPfCandCap);
-  for (int i = threadIdx.x; i < nc; i += blockDim.x) test(cand_f[i], cand_p[i]);
+  // parked, then spilled candidates, one per lane (the spill stores above are visible: the barrier
+  // orders them for the whole workgroup)
+  const int nc = min(cand_n, cap);
+  for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+    if (i < kPfCandCap) {
+      test(cand_f[i], cand_p[i]);
+    } else {
+      const uint32_t e = spill[i - kPfCandCap];
+      test((int)(e >> kPfSpillShift), (int64_t)(e & ((1u << kPfSpillShift) - 1u)));
+    }
+  }
   if (scratch == nullptr) return;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -355,7 +377,8 @@ void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, i
   const int64_t chunks = (n4 + 256 * K - 1) / (256 * K) * nframes;
   auto kern = radius == 1 ? peakfind_range_kernel<1, K> : peakfind_range_kernel<2, K>;
   const int g = (int)std::min<int64_t>(chunks, pf_resident_blocks(radius == 1 ? 0 : 1, kern));
-  hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, s, fp, pp, P, C, S, T, X, nframes);
+  const bool spill_ok = (int64_t)n_panels * rows * cols < ((int64_t)1 << kPfSpillShift) && nframes <= 64;
+  hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, s, fp, pp, P, C, S, T, X, nframes, spill_ok);
   hip_check(hipGetLastError(), "peakfind launch");
 }
 

@@ -14,7 +14,9 @@ from . import _ext
 
 MAX_FRAMES = 64
 # int32 words of the peak finder's self-resetting scratch (csrc/peakfind.hip PfScratch)
-PF_SCRATCH_WORDS = 3 * MAX_FRAMES + 1
+# peak-finder scratch block per consumer stream (csrc/kernels.h kPfScratchBytes): self-resetting
+# counters (1 KiB header) + every workgroup's candidate spill list for hit-rich frames (16 MiB)
+PF_SCRATCH_WORDS = (1024 + 4096 * 1024 * 4) // 4
 
 
 def _ptr(t: torch.Tensor) -> int:

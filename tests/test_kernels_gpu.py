@@ -171,7 +171,7 @@ def test_peakfind_vs_reference(cuda_device, det, radius, scratch):
     torch.cuda.synchronize()
     ref_peaks, ref_summary = reference.peakfind_reference(frames, params)
     if scratch:
-        assert int(scr.abs().sum()) == 0, "scratch not re-zeroed by the last workgroup"
+        assert int(scr[:256].abs().sum()) == 0, "scratch counters not re-zeroed by the last workgroup"
     assert int(total) == (2 if scratch else 1) * sum(min(int(c), params.max_peaks) for c in counts.cpu())
     for f in range(F):
         n = int(counts[f])
@@ -226,7 +226,7 @@ def test_peakfind_full_batch(cuda_device, det, F):
     kernels.peakfind([d[i] for i in range(F)], spec.frame_shape, params, peaks, counts, summary, scratch=scr)
     torch.cuda.synchronize()
     ref_peaks, ref_summary = reference.peakfind_reference(frames, params)
-    assert int(scr.abs().sum()) == 0
+    assert int(scr[:256].abs().sum()) == 0   # counters (the spill lists need not be zero)
     for f in range(F):
         n = int(counts[f])
         assert n == ref_peaks[f].shape[0], f"frame {f}: {n} peaks vs reference {ref_peaks[f].shape[0]}"

@@ -28,3 +28,11 @@ run dev_runtime 29714 --steps 100 --warmup 20 --source device --fabric-copy runt
 run host_kernel_b 29715 --steps 40 --warmup 10 --fabric-copy kernel && \
 run cfg3_host 29716 --steps 40 --warmup 10 --producers 1 && \
 run cfg3_dev 29717 --steps 100 --warmup 20 --source device --producers 1
+# peak finder: the spill path (hit-rich frames) against the golden model, then the probe at the
+# default threshold and at ~2 % candidate density
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_production_shapes_gpu.py -k peakfind > $O/pf_tests.log 2>&1 || { tail -30 $O/pf_tests.log; exit 1; }
+tail -2 $O/pf_tests.log
+timeout -k 10 200 python tools/pf_probe.py --repeat 3 --total > $O/pf_default.log 2>&1 || { tail -20 $O/pf_default.log; exit 1; }
+tail -2 $O/pf_default.log
+timeout -k 10 200 python tools/pf_probe.py --repeat 3 --thr 5 --total > $O/pf_thr5.log 2>&1 || { tail -20 $O/pf_thr5.log; exit 1; }
+tail -2 $O/pf_thr5.log
