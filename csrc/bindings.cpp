@@ -180,6 +180,24 @@ PYBIND11_MODULE(_C, m) {
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, int64_t nelem, bool bf16,
            uint64_t stream) { pr::launch_gather_frames(make_ptrs(in, out), (int)in.size(), nelem, bf16, stream); },
         py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("nelem"), py::arg("bf16"), py::arg("stream"));
+  m.def("copy_runs",
+        [](const std::vector<uint64_t>& src, const std::vector<uint64_t>& dst, const std::vector<int64_t>& bytes,
+           int workgroups, uint64_t stream) {
+          pr::check(src.size() == dst.size() && src.size() == bytes.size(), "copy_runs: list lengths differ");
+          pr::check(!src.empty() && (int)src.size() <= pr::kMaxCopyRuns, "copy_runs: 1..64 runs per launch");
+          pr::CopyRuns cr{};
+          cr.n = (int32_t)src.size();
+          for (size_t i = 0; i < src.size(); ++i) {
+            pr::check(src[i] != 0 && dst[i] != 0 && bytes[i] > 0 && bytes[i] % 16 == 0,
+                      "copy_runs: null pointer or a size that is not a positive multiple of 16 B");
+            cr.src[i] = src[i];
+            cr.dst[i] = dst[i];
+            cr.n16[i] = bytes[i] / 16;
+          }
+          return pr::launch_copy_runs(cr, workgroups, stream);
+        },
+        py::arg("src_ptrs"), py::arg("dst_ptrs"), py::arg("bytes"), py::arg("workgroups"), py::arg("stream"),
+        "the queue fabric's batched D2D copy kernel (copy_runs_kernel); returns the grid size");
   m.def("convert_u16_f32",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, int64_t npix, uint64_t stream) {
           pr::launch_convert_u16_f32(make_ptrs(in, out), (int)in.size(), npix, stream);

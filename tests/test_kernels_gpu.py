@@ -257,3 +257,27 @@ def test_common_mode_generic_kernel_bitwise(cuda_device, det):
     torch.cuda.synchronize()
     ref = reference.calibrate_reference(raw.to(torch.int32), consts, mask, cal.cm)
     _assert_equal(out, ref, f"generic cm {det}")
+
+
+@pytest.mark.parametrize("wgs", [1, 7, 128, 4096])
+def test_copy_runs_kernel_bitwise(cuda_device, native, wgs):
+    """The queue fabric's batched copy (csrc/gather.hip copy_runs_kernel): many runs of different
+    lengths (a 16-B word up to several 16-KB chunks, not chunk multiples) in ONE launch, with grids
+    smaller and larger than the chunk count -- every byte lands once, nothing outside the runs is
+    touched."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    sizes = [16, 48, 16384, 16400, 65536 + 32, 3 * 16384 - 16, 1 << 20, 8650752]
+    srcs = [torch.randint(-2 ** 31, 2 ** 31 - 1, (n // 4,), generator=g, dtype=torch.int32).to(cuda_device)
+            for n in sizes]
+    dst = torch.full((sum(n // 4 for n in sizes) + 64,), -7, dtype=torch.int32, device=cuda_device)
+    offs, o = [], 16
+    for n in sizes:
+        offs.append(o)
+        o += n // 4
+    grid = native.copy_runs([int(s.data_ptr()) for s in srcs], [int(dst[a:].data_ptr()) for a in offs], sizes,
+                            wgs, 0)
+    torch.cuda.synchronize()
+    assert 1 <= grid <= wgs
+    for s, a in zip(srcs, offs):
+        assert torch.equal(dst[a:a + s.numel()], s)
+    assert int((dst[:16] != -7).sum()) == 0 and int((dst[o:] != -7).sum()) == 0

@@ -9,6 +9,8 @@ O=$R/gpurun_out/r4_fabric
 mkdir -p $O
 timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_elastic_gpu.py tests/test_psana_wrapper.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
+timeout -k 10 200 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_kernels_gpu.py -k copy_runs > $O/copy_tests.log 2>&1 || { tail -30 $O/copy_tests.log; exit 1; }
+tail -2 $O/copy_tests.log
 run() {  # name, port, extra args
   timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $2 bench.py --gpus 2 ${@:3} > $O/$1.log 2>&1 || { tail -30 $O/$1.log; return 1; }
   grep '"metric"' $O/$1.log > $O/$1.json
