@@ -369,18 +369,27 @@ class ProducerPipeline:
 # interpreter's final garbage collection (_PyWeakref_ClearRef, rc 139 after a passing GPU suite).
 _STREAM_POOL: dict = {}
 _STREAM_POOL_LOCK = threading.Lock()
+# handles whose owner is still alive (token -> (key, handles)): at process exit they go back to the
+# native pool too, so close_stream_pool() synchronises and destroys every CU-masked queue of ours
+# (a PeakFinderConsumer alive at exit left its queues to the runtime's static teardown)
+_STREAMS_IN_USE: dict = {}
 
 
-def _return_streams(key, handles):
+def _return_streams(key, handles, token=None):
     with _STREAM_POOL_LOCK:
+        if token is not None and _STREAMS_IN_USE.pop(token, None) is None:
+            return   # already released at exit
         _STREAM_POOL.setdefault(key, []).extend(handles)
 
 
 def _release_idle_streams(C):
-    """Process exit: the idle pooled handles go back to the native pool (csrc/streams.h)."""
+    """Process exit: the idle pooled handles AND those of owners still alive go back to the native
+    pool (csrc/streams.h; release synchronises each stream first)."""
     with _STREAM_POOL_LOCK:
         items = [(k, h) for k, hs in _STREAM_POOL.items() for h in hs]
+        items += [(k, h) for k, hs in _STREAMS_IN_USE.values() for h in hs]
         _STREAM_POOL.clear()
+        _STREAMS_IN_USE.clear()
     for (dev, kind), h in items:
         C.stream_release(dev, kind, h)
 
@@ -406,7 +415,10 @@ def _make_streams(device, n: int, kind: str, owner=None):
         handles.append(h)
         out.append(torch.cuda.ExternalStream(h, device=device))
     if owner is not None:
-        fin = weakref.finalize(owner, _return_streams, key, handles)
+        token = object()
+        with _STREAM_POOL_LOCK:
+            _STREAMS_IN_USE[token] = (key, handles)
+        fin = weakref.finalize(owner, _return_streams, key, handles, token)
         fin.atexit = False
     return out
 
