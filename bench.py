@@ -83,6 +83,8 @@ def parse(argv=None):
                     help="N > 1: how producers move frames into other ranks' rings: one copy_runs_kernel launch per "
                          "fabric pass on its own hardware queue (default, config.FABRIC_COPY_ENGINE) or hipMemcpyAsync "
                          "per run on one ordinary stream per link (round-3 path)")
+    ap.add_argument("--fabric-copy-stream", default=None, choices=["shared", "dedicated", "high"],
+                    help="hardware-queue placement of the fabric copy stream (default config.FABRIC_COPY_STREAM)")
     ap.add_argument("--fabric-copy-wgs", type=int, default=None,
                     help="workgroups of the fabric copy kernel (default config.FABRIC_COPY_WORKGROUPS)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -224,7 +226,8 @@ def main(argv=None):
     ring = FrameRing(cal.out_shape, cal.out_dtype, device, producer_slots, cslots,
                      shm_name=sess.ring_name() if (sess is not None and not gpu) else None)
     ep = QueueEndpoint(ring, sess, is_producer=is_prod, is_consumer=True, route=args.route,
-                       copy_engine=args.fabric_copy, copy_workgroups=args.fabric_copy_wgs)
+                       copy_engine=args.fabric_copy, copy_workgroups=args.fabric_copy_wgs,
+                       copy_stream=args.fabric_copy_stream)
     if args.source == "device":
         # raw pool resident in HBM: isolates the GPU pipeline from PCIe (secondary number)
         dev_pool = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(device)
@@ -277,9 +280,13 @@ def main(argv=None):
                           name="producer", daemon=True)
     pt.start()
 
-    def consume(n_frames):
+    def consume(n_frames, stall_s=90.0):
+        """Take n_frames; a rank that receives nothing for stall_s fails loudly instead of hanging the
+        job (a starved consumer would block every barrier after it)."""
         got = 0
+        t_last = time.monotonic()
         while got < n_frames:
+            g0 = got
             if consumer is not None:
                 got += consumer.poll(timeout=0.05, max_items=n_frames - got)
             else:
@@ -289,6 +296,11 @@ def main(argv=None):
                     got += 1
             if ep.failed is not None:
                 raise RuntimeError(f"queue fabric failed: {ep.failed!r}")
+            if got > g0:
+                t_last = time.monotonic()
+            elif time.monotonic() - t_last > stall_s:
+                raise RuntimeError(f"bench.py rank {rank}: no frame for {stall_s:.0f} s ({got}/{n_frames} of this "
+                                   f"request; fabric {ep.metrics()})")
         return got
 
     def csync():

@@ -366,7 +366,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_keeper", &pr::QueueFabric::set_keeper, py::arg("on"))
       .def("set_peer_grantable", &pr::QueueFabric::set_peer_grantable, py::arg("mid"), py::arg("on"))
       .def("stats", &pr::QueueFabric::stats)
-      .def("set_copy_engine", &pr::QueueFabric::set_copy_engine, py::arg("engine"), py::arg("workgroups") = 0)
+      .def("set_copy_engine", &pr::QueueFabric::set_copy_engine, py::arg("engine"), py::arg("workgroups") = 0,
+           py::arg("stream_kind") = 1)
       .def_property_readonly("copy_engine", &pr::QueueFabric::copy_engine)
       .def_property_readonly("copy_workgroups", &pr::QueueFabric::copy_workgroups)
       .def("copy_samples", &pr::QueueFabric::copy_samples)

@@ -25,7 +25,7 @@ namespace pr {
 namespace {
 
 constexpr uint64_t kLinkMagic = 0x314B4E494C525350ull;  // "PSRLINK1"
-constexpr int32_t kLinkVersion = 2;
+constexpr int32_t kLinkVersion = 3;
 constexpr int32_t kNoticeReturned = 1;   // the grant comes back unused (producer finished / closing)
 constexpr int32_t kNoticeReclaimed = 2;  // a returned frame was copied out: its slot is free again
 constexpr int32_t kNoticeRejected = 4;   // a returned frame was refused (EOS posted): route it elsewhere
@@ -91,6 +91,7 @@ struct alignas(64) LinkSeg {
   std::atomic<int64_t> producer_budget;                // its pool budget (keeper watermark)
   std::atomic<int64_t> producer_other_credit;          // credit it holds from non-keeper consumers
   alignas(64) std::atomic<uint64_t> taken;             // consumer: frames of this link it took (get)
+  std::atomic<int64_t> consumer_ready;                 // consumer: frames ready to read in its whole shard
   std::atomic<uint32_t> returns_final;                 // consumer (closing): no return will follow
   std::atomic<uint32_t> producer_seen_closed;          // producer: no frame notice will follow
   alignas(64) std::atomic<uint64_t> r_head;            // consumer -> producer: returned frames
@@ -320,7 +321,7 @@ QueueFabric::~QueueFabric() {
       free_timed_.push_back(g->end);
     }
     inflight_.clear();
-    if (xstream_ != nullptr) release_stream(device_, kStreamDedicated, xstream_);   // synchronises it
+    if (xstream_ != nullptr) release_stream(device_, xstream_kind_, xstream_);   // synchronises it
     xstream_ = nullptr;
     for (auto& l : links_) {
       if (l->seg == nullptr) continue;
@@ -443,11 +444,14 @@ void QueueFabric::set_peer_grantable(int64_t mid, bool on) {
   ops_.push_back(Op{on ? 3 : 4, mid, ""});
 }
 
-void QueueFabric::set_copy_engine(int engine, int workgroups) {
+void QueueFabric::set_copy_engine(int engine, int workgroups, int stream_kind) {
   check(engine == kCopyKernel || engine == kCopyRuntime, "QueueFabric: unknown copy engine");
+  check(stream_kind == kStreamShared || stream_kind == kStreamDedicated || stream_kind == kStreamHighPriority,
+        "QueueFabric: unknown stream kind");
   check(!running_.load(), "QueueFabric: set_copy_engine before start()");
   copy_engine_ = engine;
   if (workgroups > 0) copy_wgs_ = std::min(workgroups, 4096);
+  xstream_kind_ = stream_kind;
 }
 
 std::vector<CopySample> QueueFabric::copy_samples() const {
@@ -730,8 +734,12 @@ int64_t QueueFabric::consumer_pass(double now) {
         break;
       }
   }
+  const int64_t ready_now = pool_->n_ready();   // demand signal for balanced producers (starving: 0)
   for (auto& lp : links_)
-    if (!lp->outgoing && lp->seg != nullptr) lp->seg->taken.store(lp->taken, std::memory_order_release);
+    if (!lp->outgoing && lp->seg != nullptr) {
+      lp->seg->consumer_ready.store(ready_now, std::memory_order_relaxed);
+      lp->seg->taken.store(lp->taken, std::memory_order_release);
+    }
   // 1. notices: frames (-> READY), unused grants, answers to returned frames.  n_tail is stored only
   //    after the returns of this pass were posted (a closing consumer hands back every frame noticed
   //    before a producer sees n_tail catch up and acknowledges the close)
@@ -1211,8 +1219,27 @@ int64_t QueueFabric::producer_pass(double now) {
     std::vector<std::vector<int>> assign(cands.size());
     std::vector<int> local;
     const int K = (int)cands.size() + 1;   // position K-1 = this process's own consumer
+    // balanced: a remote consumer with NOTHING to read (its published ready count is 0), credit
+    // here and no copy from us in flight is starving -- competing consumers pull from one queue in
+    // the reference (shared_queue.py:19-24), so it is fed first while our own consumer has frames
+    // ready (a consumer-only rank next to a fast co-located consumer would otherwise never see a
+    // frame; BASELINE config 3).  Consumers that are fed by their own producer are never starving,
+    // so the weak-scaling case stays local.
+    std::vector<int> starving;
+    if (policy == 0 && (local_credit <= 0 || pool_->n_ready() >= kFeedLocalReady))
+      for (size_t i = 0; i < cands.size(); ++i)
+        if (!cands[i]->keeper && avail[i] > 0 && cands[i]->inflight == 0 &&
+            cands[i]->seg->consumer_ready.load(std::memory_order_relaxed) == 0)
+          starving.push_back((int)i);
+    size_t sv = 0;
     for (int s : offers) {
       int pick = -2;   // -2 none, -1 local, >= 0 remote
+      while (sv < starving.size() && avail[starving[sv]] <= 0) ++sv;
+      if (sv < starving.size()) {
+        assign[starving[sv]].push_back(s);
+        --avail[starving[sv]];
+        continue;
+      }
       if (policy == 2) {
         for (int t = 0; t < K && pick == -2; ++t) {
           const int p = (rr_ + t) % K;
@@ -1378,7 +1405,7 @@ int64_t QueueFabric::producer_pass(double now) {
 // that stream only.  Timing events bracket the copy itself, so each dispatch's device time is known.
 void QueueFabric::issue_copies(std::vector<Batch>& kb, double now) {
   trace::Range tr("fabric.copy_dispatch");
-  if (xstream_ == nullptr) xstream_ = acquire_stream(device_, kStreamDedicated);
+  if (xstream_ == nullptr) xstream_ = acquire_stream(device_, xstream_kind_);
   std::vector<int> all;
   for (const Batch& b : kb) all.insert(all.end(), b.slots.begin(), b.slots.end());
   pool_->begin_send_batch(all, reinterpret_cast<uint64_t>(xstream_));   // xstream_ waits for their data

@@ -157,7 +157,8 @@ struct LinkStatus {
 
 class QueueFabric {
  public:
-  // policy: 0 balanced (local unless a remote consumer has kLocalSlack more free slots granted),
+  // policy: 0 balanced (local unless a remote consumer has kLocalSlack more free slots granted, or is
+  //           starving: nothing to read at all while this process's own consumer has frames ready),
   //         1 local_first, 2 spread (round-robin over every consumer with credit),
   //         3 relay (queue keeper: never to its own consumer side; most granted credit first),
   //         4 remote_only (never to its own consumer while a remote consumer link is attached:
@@ -205,7 +206,7 @@ class QueueFabric {
   //     or SDMA, HSA_ENABLE_SDMA) -- kept for A/B measurements.
   // Before start().
   static constexpr int kCopyKernel = 0, kCopyRuntime = 1;
-  void set_copy_engine(int engine, int workgroups);
+  void set_copy_engine(int engine, int workgroups, int stream_kind = 1);   // kind: csrc/streams.h
   int copy_engine() const { return copy_engine_; }
   int copy_workgroups() const { return copy_wgs_; }
   // the newest timed copy dispatches (bounded), oldest first
@@ -227,6 +228,7 @@ class QueueFabric {
   int policy() const { return policy_.load(); }
 
   static constexpr int kLocalSlack = 64;
+  static constexpr int kFeedLocalReady = 2;   // balanced: own consumer's ready frames before feeding a starving one
   static constexpr int kMinGrants = 4;      // grants kept at an idle producer (pipeline depth)
   static constexpr int kMaxDispatch = 64;   // produced frames routed per iteration
 
@@ -270,6 +272,7 @@ class QueueFabric {
   hipStream_t xstream_ = nullptr;   // kernel engine: the copy stream (own hardware queue, pooled)
   int copy_engine_ = kCopyKernel;
   int copy_wgs_ = 128;
+  int xstream_kind_ = 1;            // kStreamDedicated
   std::vector<hipEvent_t> free_events_, all_events_;
   std::vector<hipEvent_t> free_timed_;          // timing-enabled events (copy groups)
   std::deque<CopySample> samples_;              // guarded by mu_

@@ -58,22 +58,27 @@ CONSUMER_STREAM_KIND = "dedicated"
 # "kernel": every frame of one fabric pass, to all its consumers, in ONE copy_runs_kernel launch on
 # a stream with its own hardware queue, bounded to FABRIC_COPY_WORKGROUPS workgroups; "runtime":
 # hipMemcpyAsync per contiguous run on one ordinary stream per link (the round-3 path; A/B only).
-# Env override: PSANA_RAY_AMD_FABRIC_COPY=kernel|runtime[:workgroups].
+# FABRIC_COPY_STREAM: hardware-queue placement of the kernel engine's copy stream (STREAM_KINDS).
+# Env override: PSANA_RAY_AMD_FABRIC_COPY=kernel|runtime[:workgroups[:stream kind]].
 FABRIC_COPY_ENGINES = {"kernel": 0, "runtime": 1}
 FABRIC_COPY_ENGINE = "kernel"
 FABRIC_COPY_WORKGROUPS = 128
+FABRIC_COPY_STREAM = "dedicated"
 
 
-def fabric_copy_setting(engine: Optional[str] = None, workgroups: Optional[int] = None) -> tuple[str, int]:
-    """(engine, workgroups) for a new fabric: explicit arguments, else the environment, else the
-    defaults above."""
-    env = os.environ.get("PSANA_RAY_AMD_FABRIC_COPY", "")
-    e_env, _, w_env = env.partition(":")
-    eng = engine or e_env or FABRIC_COPY_ENGINE
+def fabric_copy_setting(engine: Optional[str] = None, workgroups: Optional[int] = None,
+                        stream: Optional[str] = None) -> tuple[str, int, str]:
+    """(engine, workgroups, stream kind) for a new fabric: explicit arguments, else the environment,
+    else the defaults above."""
+    parts = (os.environ.get("PSANA_RAY_AMD_FABRIC_COPY", "").split(":") + ["", "", ""])[:3]
+    eng = engine or parts[0] or FABRIC_COPY_ENGINE
     if eng not in FABRIC_COPY_ENGINES:
         raise ValueError(f"unknown fabric copy engine {eng!r} ({' | '.join(FABRIC_COPY_ENGINES)})")
-    wgs = workgroups if workgroups else (int(w_env) if w_env else FABRIC_COPY_WORKGROUPS)
-    return eng, int(wgs)
+    wgs = workgroups if workgroups else (int(parts[1]) if parts[1] else FABRIC_COPY_WORKGROUPS)
+    kind = stream or parts[2] or FABRIC_COPY_STREAM
+    if kind not in STREAM_KINDS:
+        raise ValueError(f"unknown stream kind {kind!r} ({' | '.join(STREAM_KINDS)})")
+    return eng, int(wgs), kind
 
 # --- rendezvous ---------------------------------------------------------------------------
 DEFAULT_STORE_PORT = 6379             # the Ray head port of README.md:15, reused for the store

@@ -106,7 +106,8 @@ class FrameItem:
 class QueueEndpoint:
     def __init__(self, ring: FrameRing, session=None, is_producer: bool = True, is_consumer: bool = True,
                  route: str = "balanced", prefetch: int = 0, keeper: bool = False,
-                 copy_engine: Optional[str] = None, copy_workgroups: Optional[int] = None):
+                 copy_engine: Optional[str] = None, copy_workgroups: Optional[int] = None,
+                 copy_stream: Optional[str] = None):
         """``prefetch`` (consumer role, fabric mode): at most this many frames noticed-but-not-taken
         plus grants outstanding -- the read-ahead a crashed consumer can lose (0: the ring's free
         slots only).  ``keeper``: this member is a queue keeper (its links are marked so producers
@@ -142,11 +143,11 @@ class QueueEndpoint:
                                      POLICIES[route], session.mid)
         self._fabric.set_prefetch(int(prefetch))
         self._fabric.set_keeper(bool(keeper))
-        from ..config import FABRIC_COPY_ENGINES, fabric_copy_setting
+        from ..config import FABRIC_COPY_ENGINES, STREAM_KINDS, fabric_copy_setting
 
-        eng, wgs = fabric_copy_setting(copy_engine, copy_workgroups)
-        self._fabric.set_copy_engine(FABRIC_COPY_ENGINES[eng], int(wgs))
-        self.copy_engine = (eng, int(wgs))
+        eng, wgs, kind = fabric_copy_setting(copy_engine, copy_workgroups, copy_stream)
+        self._fabric.set_copy_engine(FABRIC_COPY_ENGINES[eng], int(wgs), STREAM_KINDS[kind])
+        self.copy_engine = (eng, int(wgs), kind)
         if self.is_consumer:
             if self.gpu:
                 self._fabric.export_ipc_ring()

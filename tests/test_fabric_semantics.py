@@ -223,3 +223,37 @@ def test_keeper_links_are_the_last_resort(native, tok):
         assert kf.stats().frames_recv == 10
     finally:
         _stop(pf, cf, kf)
+
+
+def test_balanced_feeds_a_starving_consumer_only_rank(native, tok):
+    """BASELINE config 3 shape: a producer with its OWN fast consumer (prosumer) and a consumer-only
+    member.  balanced keeps frames local while every consumer has something to read, but a consumer
+    with nothing to read at all gets frames (the reference's competing consumers pull from one
+    queue, shared_queue.py:19-24) -- before, it starved forever next to a fast local consumer."""
+    C = native
+    sb = 128
+    pp, _pr, pf = _member(C, tok, 0, 32, 32, sb, 0)    # prosumer, balanced
+    cp, _cr, cf = _member(C, tok, 1, 0, 32, sb, 0)      # consumer only
+    _link(tok, pf, 0, cf, 1)
+    for f in (pf, cf):
+        f.start()
+    try:
+        produced = local = remote = 0
+        t0 = time.time()
+        while time.time() - t0 < 5.0 and remote < 20:
+            produced += _produce(C, pp, 8, produced)
+            for pool, is_local in ((pp, True), (cp, False)):
+                while True:   # both consumers take everything they have, at once (fast readers)
+                    s = pool.try_get()
+                    if s < 0:
+                        break
+                    pool.release(s, 0)
+                    if is_local:
+                        local += 1
+                    else:
+                        remote += 1
+            time.sleep(0.002)
+        assert remote >= 20, f"the consumer-only member got {remote} frames (local {local})"
+        assert local > 0
+    finally:
+        _stop(pf, cf)
