@@ -317,7 +317,7 @@ def main(argv=None):
     # consumer batch issued before it has (both streams were synchronised)
     cstream = (consumer.stream if consumer is not None else torch.cuda.current_stream(device)) if gpu else None
 
-    def window(steps):
+    def window(steps, takes=True, sit_out=False):
         """``steps`` timed steps between barriers, in steady state.  Returns (host seconds, max over
         ranks; sustained frames/s of the node = min(sum over producers of the production rate,
         frames consumed / seconds); frames completed by the producers inside the window (sum);
@@ -326,15 +326,19 @@ def main(argv=None):
         Production is counted at DEVICE COMPLETION (one timing event per producer chunk) and only
         for chunks that completed after t0: frames already READY when the window opened are
         excluded, and the rate runs between two chunk completions (utils.metrics.sustained_rate),
-        so a short window and a long one measure the same steady state."""
+        so a short window and a long one measure the same steady state.  ``takes=False``: this rank
+        consumes nothing in the window (a lone producer's own consumer in the remote_only window)."""
+        mine = steps * B if takes else 0
         csync()
         barrier()
         csync()
         c0 = ep.metrics()
         m0 = prod.clock(cstream) if prod is not None else None
         t0 = time.perf_counter()
-        consume(steps * B)
+        consume(mine)
         csync()
+        if sit_out:
+            barrier()   # some rank takes nothing: its window ends when the others' does (every rank calls it)
         t1 = time.perf_counter()
         m1 = prod.clock(cstream) if prod is not None else None
         c1 = ep.metrics()
@@ -353,12 +357,12 @@ def main(argv=None):
             t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=coord)
             dt = float(t[0])
-            v = torch.tensor([rate_p, float(fr_p)], dtype=torch.float64)
+            v = torch.tensor([rate_p, float(fr_p), float(mine)], dtype=torch.float64)
             dist.all_reduce(v, op=dist.ReduceOp.SUM, group=coord)
-            rate_sum, fr_sum = float(v[0]), int(v[1])
+            rate_sum, fr_sum, taken = float(v[0]), int(v[1]), int(v[2])
         else:
-            rate_sum, fr_sum = rate_p, fr_p
-        consumed_rate = world * steps * B / dt
+            rate_sum, fr_sum, taken = rate_p, fr_p, mine
+        consumed_rate = taken / dt
         value = min(rate_sum, consumed_rate)
         det = {"production_frames_per_s": round(rate_sum, 1), "consumer_frames_per_s": round(consumed_rate, 1),
                "produced_in_window": fr_sum, "produced_in_window_rank0": fr_p}
@@ -383,14 +387,20 @@ def main(argv=None):
     cross_steps = args.steps if args.cross_steps is None else args.cross_steps
     if world > 1 and cross_steps > 0:
         ep.set_route("remote_only")
+        # a LONE producer's own consumer receives nothing under remote_only (no other producer can
+        # feed it): it sits the window out and the consumer-only ranks take every frame (BASELINE
+        # config 3 with --producers 1)
+        takes = not (is_prod and n_prod == 1)
         # drain what the headline policy already put into this shard (FIFO), then warm up: the
         # window must see frames routed by the new policy, not the old backlog
-        consume(int(ep.metrics().get("ready", 0)) + max(2, args.warmup // 2) * B)
-        xdt, xval, xpw, xdet, x0, x1 = window(cross_steps)
+        consume(int(ep.metrics().get("ready", 0)) + (max(2, args.warmup // 2) * B if takes else 0))
+        xdt, xval, xpw, xdet, x0, x1 = window(cross_steps, takes, sit_out=n_prod == 1)
         sent = allsum(int(x1.get("bytes_sent", 0) - x0.get("bytes_sent", 0)))
         fr_sent = allsum(int(x1.get("frames_sent", 0) - x0.get("frames_sent", 0)))
         fr_local = allsum(int(x1.get("frames_local", 0) - x0.get("frames_local", 0)))
         fr_recv = allsum(int(x1.get("frames_recv", 0) - x0.get("frames_recv", 0)))
+        tk_rem = allsum(int(x1.get("taken_remote", 0) - x0.get("taken_remote", 0)))
+        tk_loc = allsum(int(x1.get("taken_local", 0) - x0.get("taken_local", 0)))
         cms = allsum(round(float(x1.get("copy_ms_per_batch", 0.0)), 3))
         # the window's copy dispatches: device time of the copy alone (timing events around it) and
         # host issue -> completion (includes the wait for the frames' calibration)
@@ -408,8 +418,14 @@ def main(argv=None):
             "route": "remote_only", "steps": cross_steps, "ms_per_step": round(1e3 * xdt / cross_steps, 4),
             "frames_per_s": round(xval, 2), **xdet,
             "cross_gpu_GB_per_s": round(sum(sent) / xdt / 1e9, 2),
-            "cross_gpu_fraction": round(sum(fr_sent) / max(1, sum(fr_sent) + sum(fr_local)), 3),
-            "received_cross_per_consumed": round(sum(fr_recv) / max(1, world * cross_steps * B), 3),
+            # of the frames consumers TOOK in the window, the share another process produced (a
+            # consumer's read-ahead at t0 counts where it came from; sends inside the window alone
+            # miss it when the window is short)
+            "cross_gpu_fraction": round(sum(tk_rem) / max(1, sum(tk_rem) + sum(tk_loc)), 3),
+            "sent_cross_fraction": round(sum(fr_sent) / max(1, sum(fr_sent) + sum(fr_local)), 3),
+            "taken_remote_per_rank": tk_rem, "taken_local_per_rank": tk_loc,
+            "received_cross_per_consumed": round(sum(fr_recv) / max(1, sum(allsum(cross_steps * B if takes else 0))),
+                                                 3),
             "bytes_sent_per_rank": sent, "frames_sent_per_rank": fr_sent, "frames_local_per_rank": fr_local,
             "copy_ms_per_batch_per_rank": cms,
             "copy_dispatch_per_rank": copy_detail,

@@ -317,7 +317,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("copy_s", &pr::FabricStats::copy_s)
       .def_readonly("copy_launches", &pr::FabricStats::copy_launches)
       .def_readonly("copy_dev_ms", &pr::FabricStats::copy_dev_ms)
-      .def_readonly("copy_dev_bytes", &pr::FabricStats::copy_dev_bytes);
+      .def_readonly("copy_dev_bytes", &pr::FabricStats::copy_dev_bytes)
+      .def_readonly("taken_local", &pr::FabricStats::taken_local)
+      .def_readonly("taken_remote", &pr::FabricStats::taken_remote);
   py::class_<pr::CopySample>(m, "CopySample")
       .def_readonly("dev_ms", &pr::CopySample::dev_ms)
       .def_readonly("issue_to_done_ms", &pr::CopySample::issue_to_done_ms)

@@ -726,13 +726,23 @@ int64_t QueueFabric::consumer_pass(double now) {
   const bool closing = consumer_closed_.load();
   // 0. frames the reader took since the last pass: tell each producer (its budget counts them
   //    until then -- queue_size is one logical bound)
+  int64_t tk_local = 0, tk_remote = 0;
   for (int64_t o : pool_->take_got_origins()) {
-    if (o < 0) continue;
+    if (o < 0) {
+      ++tk_local;
+      continue;
+    }
+    ++tk_remote;
     for (auto& lp : links_)
       if (!lp->outgoing && lp->peer == o) {
         ++lp->taken;
         break;
       }
+  }
+  if (tk_local + tk_remote > 0) {
+    std::lock_guard<std::mutex> lk(mu_);
+    st_.taken_local += tk_local;
+    st_.taken_remote += tk_remote;
   }
   const int64_t ready_now = pool_->n_ready();   // demand signal for balanced producers (starving: 0)
   for (auto& lp : links_)

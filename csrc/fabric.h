@@ -130,6 +130,8 @@ struct FabricStats {
   int64_t copy_launches = 0;     // copy dispatches (kernel engine: one per fabric pass over all links)
   double copy_dev_ms = 0;        // sum of device time of the copies themselves (timing events)
   int64_t copy_dev_bytes = 0;    // bytes those timed copies moved
+  int64_t taken_local = 0;       // consumer: frames taken (get) that its own process produced
+  int64_t taken_remote = 0;      // consumer: frames taken that another process produced
 };
 
 // One timed copy dispatch (fabric pass): device time of the copy, bytes, frames, host time from

@@ -389,7 +389,8 @@ class QueueEndpoint:
                 "links_opened": st.links_opened, "links_live": sum(1 for ls in links if ls.attached and not ls.dead),
                 "copy_ms_per_batch": 1e3 * st.copy_s / max(1, st.batches),
                 "copy_launches": st.copy_launches, "copy_dev_ms": st.copy_dev_ms,
-                "copy_dev_bytes": st.copy_dev_bytes,
+                "copy_dev_bytes": st.copy_dev_bytes, "taken_local": st.taken_local,
+                "taken_remote": st.taken_remote,
                 "iterations": st.iterations, "idle_iterations": st.idle_iterations}
 
     def links(self) -> list:

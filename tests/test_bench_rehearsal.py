@@ -15,14 +15,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.parametrize("nproc,route,producers", [(2, "balanced", 0), (4, "spread", 0), (4, "balanced", 2),
-                                                   (8, "balanced", 0), (8, "balanced", 4)])
+                                                   (8, "balanced", 0), (8, "balanced", 4), (2, "balanced", 1)])
 def test_bench_multirank_cpu(native, nproc, route, producers):
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     port = random.randint(30000, 45000)
+    # a lone producer: the consumer-only rank's read-ahead covers a 4-step window by itself, so the
+    # window must be long enough for frames to cross inside it
+    steps = 40 if producers == 1 else 4
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", str(nproc), "--steps", "4", "--warmup", "2", "--batch", "4", "--detector", "tiny_epix",
+           "--gpus", str(nproc), "--steps", str(steps), "--warmup", "2", "--batch", "4", "--detector", "tiny_epix",
            "--device", "cpu", "--queue-size", str(16 * nproc), "--chunk", "4", "--route", route,
            "--producers", str(producers)]
     if producers:
@@ -34,7 +37,7 @@ def test_bench_multirank_cpu(native, nproc, route, producers):
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == nproc and d["steps"] == 4 and d["value"] > 0
+    assert d["n_gpus"] == nproc and d["steps"] == steps and d["value"] > 0
     assert d["config"]["global_batch"] == 4 * nproc
     assert d["config"]["producer_ranks"] == (producers or nproc)
     x = d["extra"]["xgmi_phase"]
