@@ -60,8 +60,8 @@
 #ifndef PR_CM_RAW_NT
 #define PR_CM_RAW_NT 1
 #endif
-// Output stores of the production kernels: 1 = non-temporal (streaming: the frames bypass the L2
-// lines that hold the constant tables), 0 = plain.
+// Output stores of the production kernels: 0 = plain; 1 = non-temporal (streaming) for calib-mode
+// frames; 2 = non-temporal for the image placement too.
 #ifndef PR_CM_NT_STORE
 #define PR_CM_NT_STORE 0
 #endif
@@ -494,14 +494,15 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
 // no loads in this loop every store is fire-and-forget (the round-1 form that interleaved the
 // gain-factor loads with the stores serialised one store round trip per 8-pixel group).
 // Frame layout: 16 B per lane, consecutive lanes along tile rows.
+template <int LEVEL>
 __device__ __forceinline__ void st_out4(PR_GLOBAL float4* p, const float4 v) {
-#if PR_CM_NT_STORE
-  f32x4_t x;
-  x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
-  __builtin_nontemporal_store(x, (PR_GLOBAL f32x4_t*)p);
-#else
-  st_f4(p, v);
-#endif
+  if constexpr (PR_CM_NT_STORE >= LEVEL) {
+    f32x4_t x;
+    x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
+    __builtin_nontemporal_store(x, (PR_GLOBAL f32x4_t*)p);
+  } else {
+    st_f4(p, v);
+  }
 }
 
 __device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C, PR_GLOBAL float* out, int64_t base,
@@ -510,7 +511,7 @@ __device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C,
   for (int e = threadIdx.x; e < R * C4; e += blockDim.x) {
     const int r = e / C4, j = e - r * C4;
     const float4 v = *reinterpret_cast<const float4*>(tile + r * P + 4 * j);
-    st_out4((PR_GLOBAL float4*)(out + base + (int64_t)r * panel_cols + 4 * j), v);
+    st_out4<1>((PR_GLOBAL float4*)(out + base + (int64_t)r * panel_cols + 4 * j), v);
   }
 }
 
@@ -603,7 +604,7 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
       const int drun = nb / nfull, dk = nb - drun * nfull;
       for (; run < nruns;) {
         const float* tp = tb + run * P + 4 * k * di;
-        st_out4((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)), make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
+        st_out4<2>((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)), make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
         run += drun;
         k += dk;
         if (k >= nfull) {
@@ -620,8 +621,8 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
         const int run = w >> 2, k = 4 * a + (w & 3);
         if (k < nfull) {
           const float* tp = tb + run + 4 * k * di;
-          st_out4((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)),
-                  make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
+          st_out4<2>((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)),
+                     make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
         }
         a += da;
         w += dw;

@@ -157,6 +157,11 @@ struct PfScratch {
   unsigned int done;
 };
 
+// Frame loads of the stream: 1 = non-temporal (each pixel is read once; the frames do not push the
+// producer's common-mode tables out of L2 when both run on the GPU), 0 = plain.
+#ifndef PR_PF_NT_LOAD
+#define PR_PF_NT_LOAD 0
+#endif
 constexpr int kPfCandCap = 512;   // candidates parked per workgroup (2 KiB of LDS)
 static_assert(sizeof(PfScratch) <= kPfScratchHeader, "PfScratch outgrew its header");
 // spill entry: pixel | frame << 26 (frames of < 2^26 pixels; larger frames test overflow inline)
@@ -208,7 +213,11 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int64_t q = q0 + 256 * k;
+#if PR_PF_NT_LOAD
+      v[k] = q < n4 ? ld_nt_f4((const PR_GLOBAL f32x4_t*)(img + 4 * q)) : f32x4_t{NaN, NaN, NaN, NaN};
+#else
       v[k] = q < n4 ? *(const PR_GLOBAL f32x4_t*)(img + 4 * q) : f32x4_t{NaN, NaN, NaN, NaN};
+#endif
     }
   };
   auto test = [&](int f, int64_t p) {

@@ -16,7 +16,7 @@ from psana_ray_amd import _build  # noqa: E402
 def main():
     if len(sys.argv) < 3:
         raise SystemExit(__doc__)
-    name, src_name, extra = sys.argv[1], sys.argv[2], sys.argv[3:]
+    name, src_names, extra = sys.argv[1], set(sys.argv[2].split(",")), sys.argv[3:]   # sources: a,b,...
     _build.build()                      # the shipped objects are current
     inc, common = _build._flags()
     hipcc = _build._hipcc()
@@ -25,7 +25,7 @@ def main():
     objs = []
     for src in _build._sources():
         obj = _build.BUILD_DIR / (src.name + ".o")
-        if src.name == src_name:
+        if src.name in src_names:
             obj = out_dir / f"{src.name}.{name}.o"
             lang = ["-x", "hip"] if src.suffix == ".hip" else []
             cmd = [hipcc, *common, *extra, *inc, *lang, "-c", str(src), "-o", str(obj)]
