@@ -61,9 +61,13 @@
 #define PR_CM_RAW_NT 1
 #endif
 // Output stores of the production kernels: 0 = plain; 1 = non-temporal (streaming) for calib-mode
-// frames; 2 = non-temporal for the image placement too.
+// frames; 2 = non-temporal for the image placement too.  Same-box A/B, device-resident pipeline
+// (common mode + peak finder), two boxes (profiles/r4/cm_pass1, cm_pass2): level 1 calib 144.6k /
+// 145.0k / 144.9k / 143.6k vs plain 140.6k / 141.3k / 141.2k / 139.8k fr/s (+2.7 %), image mode
+// unchanged; level 2 costs image mode 13 % (100.9k vs 115.8k: partial-line image runs).  Kernel
+// alone: memory phases 4.14 vs 4.26 us/frame, full kernel within 0.5 %.
 #ifndef PR_CM_NT_STORE
-#define PR_CM_NT_STORE 0
+#define PR_CM_NT_STORE 1
 #endif
 // Threads per workgroup of the epix10k2M production kernel (4 or 6 waves; the tile and four
 // workgroups per CU are unchanged: 6 waves leave each wave 80 VGPRs)

@@ -147,7 +147,7 @@ __device__ void cols_hist(float* tile, int P, int R, int C, const CmParams& cp, 
         int mb = -1, mbelow = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          if (mb < 0 && k < pre + hv[j]) {
+          if (mb < 0 && k >= pre && k < pre + hv[j]) {   // only the lane whose bins hold rank k
             mb = 8 * q + j;
             mbelow = pre;
           }
