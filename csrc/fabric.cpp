@@ -92,6 +92,7 @@ struct alignas(64) LinkSeg {
   std::atomic<int64_t> producer_other_credit;          // credit it holds from non-keeper consumers
   alignas(64) std::atomic<uint64_t> taken;             // consumer: frames of this link it took (get)
   std::atomic<int64_t> consumer_ready;                 // consumer: frames ready to read in its whole shard
+  std::atomic<uint32_t> consumer_self_fed;             // consumer: its own process produces (and feeds it)
   std::atomic<uint32_t> returns_final;                 // consumer (closing): no return will follow
   std::atomic<uint32_t> producer_seen_closed;          // producer: no frame notice will follow
   alignas(64) std::atomic<uint64_t> r_head;            // consumer -> producer: returned frames
@@ -745,9 +746,11 @@ int64_t QueueFabric::consumer_pass(double now) {
     st_.taken_remote += tk_remote;
   }
   const int64_t ready_now = pool_->n_ready();   // demand signal for balanced producers (starving: 0)
+  const uint32_t self_fed = (is_producer_ && !finished_.load() && policy_.load() != 3) ? 1u : 0u;
   for (auto& lp : links_)
     if (!lp->outgoing && lp->seg != nullptr) {
       lp->seg->consumer_ready.store(ready_now, std::memory_order_relaxed);
+      lp->seg->consumer_self_fed.store(self_fed, std::memory_order_relaxed);
       lp->seg->taken.store(lp->taken, std::memory_order_release);
     }
   // 1. notices: frames (-> READY), unused grants, answers to returned frames.  n_tail is stored only
@@ -1229,16 +1232,17 @@ int64_t QueueFabric::producer_pass(double now) {
     std::vector<std::vector<int>> assign(cands.size());
     std::vector<int> local;
     const int K = (int)cands.size() + 1;   // position K-1 = this process's own consumer
-    // balanced: a remote consumer with NOTHING to read (its published ready count is 0), credit
-    // here and no copy from us in flight is starving -- competing consumers pull from one queue in
-    // the reference (shared_queue.py:19-24), so it is fed first while our own consumer has frames
-    // ready (a consumer-only rank next to a fast co-located consumer would otherwise never see a
-    // frame; BASELINE config 3).  Consumers that are fed by their own producer are never starving,
-    // so the weak-scaling case stays local.
+    // balanced: a remote consumer-ONLY member (no producer of its own feeds it) with NOTHING to
+    // read (its published ready count is 0), credit here and no copy from us in flight is starving --
+    // competing consumers pull from one queue in the reference (shared_queue.py:19-24), so it is fed
+    // first while our own consumer has frames ready (a consumer-only rank next to a fast co-located
+    // consumer would otherwise never see a frame; BASELINE config 3).  Consumers that produce for
+    // themselves are left to their own producer, so the weak-scaling case stays local.
     std::vector<int> starving;
     if (policy == 0 && (local_credit <= 0 || pool_->n_ready() >= kFeedLocalReady))
       for (size_t i = 0; i < cands.size(); ++i)
         if (!cands[i]->keeper && avail[i] > 0 && cands[i]->inflight == 0 &&
+            cands[i]->seg->consumer_self_fed.load(std::memory_order_relaxed) == 0 &&
             cands[i]->seg->consumer_ready.load(std::memory_order_relaxed) == 0)
           starving.push_back((int)i);
     size_t sv = 0;
@@ -1430,9 +1434,15 @@ void QueueFabric::issue_copies(std::vector<Batch>& kb, double now) {
   cr.n = 0;
   const uint64_t sb = (uint64_t)slot_bytes_;
   int launches = 0;
+  // grid: a copy inside this GPU's HBM (a consumer process on the same GPU) is bound by HBM and
+  // takes up to kLocalCopyWgs workgroups; copies over xGMI are bound by the links (~150 GB/s each,
+  // a few dozen workgroups keep one busy), so copy_wgs_ leaves the CUs to the calibration
+  bool all_local = true;
+  for (const Batch& b : kb) all_local &= b.link->consumer_device == device_;
+  const int wgs = all_local ? std::max(copy_wgs_, kLocalCopyWgs) : copy_wgs_;
   auto flush = [&] {
     if (cr.n == 0) return;
-    launch_copy_runs(cr, copy_wgs_, reinterpret_cast<uint64_t>(xstream_));
+    launch_copy_runs(cr, wgs, reinterpret_cast<uint64_t>(xstream_));
     cr.n = 0;
     ++launches;
   };
