@@ -111,16 +111,10 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
     if (pending && f == f0) {
       slot = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf, 0u));
       pending = false;
-      if (slot < pp.max_peaks) {
-        float* rec = peaks + ((int64_t)f * pp.max_peaks + slot) * 8;
-        rec[0] = (float)panel;
-        rec[1] = (float)gy;
-        rec[2] = (float)gx;
-        rec[3] = v;
-        rec[4] = inten;
-        rec[5] = bkg;
-        rec[6] = noise;
-        rec[7] = snr;
+      if (slot < pp.max_peaks) {   // one record = two 16-B stores (records are 32-B aligned)
+        f32x4_t* rec = reinterpret_cast<f32x4_t*>(peaks + ((int64_t)f * pp.max_peaks + slot) * 8);
+        rec[0] = f32x4_t{(float)panel, (float)gy, (float)gx, v};
+        rec[1] = f32x4_t{inten, bkg, noise, snr};
       }
     }
     if (total != nullptr) {   // records written by this group (slots below max_peaks)
@@ -220,19 +214,41 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
 #endif
     }
   };
+  // A candidate's (2H+1)^2 neighbourhood, H = RAD + 2, as THREE aligned 16-B loads per row (the
+  // 4-float groups holding columns x-H .. x+H; panels are a multiple of 4 wide, so a group is wholly
+  // inside or outside its row) instead of (2H+1) 4-B loads: 21 vector loads for RAD 1 where 49 scalar
+  // ones kept the texture units busy on hit-rich frames (tens of thousands of candidates per frame).
   auto test = [&](int f, int64_t p) {
+    constexpr int H = RAD + 2, D = 2 * H + 1;
+    static_assert(D <= 9, "three 4-float groups per row cover at most 9 columns at any alignment");
     const PR_GLOBAL float* img = gin<float>(fp.in[f]);
-    const float val = img[p];
     const int panel = (int)(p / hw);
     const int64_t rem = p - (int64_t)panel * hw;
     const int y = (int)(rem / pp.cols), x = (int)(rem - (int64_t)(rem / pp.cols) * pp.cols);
     const PR_GLOBAL float* pim = img + (int64_t)panel * hw;
-    pf_candidate<RAD>(
-        [&](int dy, int dx) {
-          const int yy = y + dy, xx = x + dx;
-          return (yy >= 0 && yy < pp.rows && xx >= 0 && xx < pp.cols) ? pim[(int64_t)yy * pp.cols + xx] : NaN;
-        },
-        val, pp, f, panel, y, x, peaks, counts, total_per_peak);
+    const int base = (x - H) & ~3;          // first group (may start left of the panel)
+    const int off = (x - H) - base;         // 0..3: column x-H inside it
+    float wv[D][D];
+#pragma unroll
+    for (int dy = -H; dy <= H; ++dy) {
+      const int yy = y + dy;
+      const bool row_ok = yy >= 0 && yy < pp.rows;
+      float e[12];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int c0 = base + 4 * k;
+        const f32x4_t q = (row_ok && c0 >= 0 && c0 < pp.cols)
+                              ? *(const PR_GLOBAL f32x4_t*)(pim + (int64_t)yy * pp.cols + c0)
+                              : f32x4_t{NaN, NaN, NaN, NaN};
+        e[4 * k] = q.x; e[4 * k + 1] = q.y; e[4 * k + 2] = q.z; e[4 * k + 3] = q.w;
+      }
+#pragma unroll
+      for (int dx = 0; dx < D; ++dx)   // register select on the run-time alignment (no indexed access)
+        wv[dy + H][dx] = off == 0 ? e[dx] : off == 1 ? e[dx + 1] : off == 2 ? e[dx + 2] : e[dx + 3];
+    }
+    const float val = wv[H][H];
+    pf_candidate<RAD>([&](int dy, int dx) { return wv[dy + H][dx + H]; }, val, pp, f, panel, y, x, peaks, counts,
+                      total_per_peak);
   };
   // block-reduce this frame's statistics and add them (one atomic pair per workgroup and frame)
   auto flush = [&](int f, float s, int c) {
