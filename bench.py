@@ -381,7 +381,10 @@ def main(argv=None):
         consume(B)
     barrier()
     consume(args.warmup * B)
-    dt, value, produced_window, rate_detail, c0, c1 = window(args.steps)
+    # producers < ranks (BASELINE config 3): every rank's window ends with the slowest consumer's, so
+    # the producers' rate and the node's consumption cover the same interval (a producer whose own
+    # consumer finished early would otherwise report its rate over a shorter, emptier-queue window)
+    dt, value, produced_window, rate_detail, c0, c1 = window(args.steps, sit_out=n_prod < world)
 
     cross = None
     cross_steps = args.steps if args.cross_steps is None else args.cross_steps

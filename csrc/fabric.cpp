@@ -1233,25 +1233,29 @@ int64_t QueueFabric::producer_pass(double now) {
     std::vector<int> local;
     const int K = (int)cands.size() + 1;   // position K-1 = this process's own consumer
     // balanced: a remote consumer-ONLY member (no producer of its own feeds it) with NOTHING to
-    // read (its published ready count is 0), credit here and no copy from us in flight is starving --
-    // competing consumers pull from one queue in the reference (shared_queue.py:19-24), so it is fed
-    // first while our own consumer has frames ready (a consumer-only rank next to a fast co-located
-    // consumer would otherwise never see a frame; BASELINE config 3).  Consumers that produce for
-    // themselves are left to their own producer, so the weak-scaling case stays local.
+    // read (its published ready count is 0) and credit here is starving -- competing consumers pull
+    // from one queue in the reference (shared_queue.py:19-24), so it is fed first while our own
+    // consumer has frames ready (a consumer-only rank next to a fast co-located consumer would
+    // otherwise never see a frame; BASELINE config 3).  Consumers that produce for themselves are
+    // left to their own producer, so the weak-scaling case stays local.  Each offer goes to the
+    // starving member given the fewest in this pass (several starving members share); a copy to it
+    // still in flight does not stop the feed (waiting for it idled the member one notice -> copy ->
+    // notice round trip per refill), its grants -- its read-ahead bound -- do.
     std::vector<int> starving;
     if (policy == 0 && (local_credit <= 0 || pool_->n_ready() >= kFeedLocalReady))
       for (size_t i = 0; i < cands.size(); ++i)
-        if (!cands[i]->keeper && avail[i] > 0 && cands[i]->inflight == 0 &&
+        if (!cands[i]->keeper && avail[i] > 0 &&
             cands[i]->seg->consumer_self_fed.load(std::memory_order_relaxed) == 0 &&
             cands[i]->seg->consumer_ready.load(std::memory_order_relaxed) == 0)
           starving.push_back((int)i);
-    size_t sv = 0;
     for (int s : offers) {
       int pick = -2;   // -2 none, -1 local, >= 0 remote
-      while (sv < starving.size() && avail[starving[sv]] <= 0) ++sv;
-      if (sv < starving.size()) {
-        assign[starving[sv]].push_back(s);
-        --avail[starving[sv]];
+      int sp = -1;
+      for (int i : starving)
+        if (avail[i] > 0 && (sp < 0 || assign[i].size() < assign[sp].size())) sp = i;
+      if (sp >= 0) {
+        assign[sp].push_back(s);
+        --avail[sp];
         continue;
       }
       if (policy == 2) {

@@ -230,11 +230,11 @@ class QueueFabric {
   int policy() const { return policy_.load(); }
 
   static constexpr int kLocalSlack = 64;
-  static constexpr int kFeedLocalReady = 2;
+  static constexpr int kFeedLocalReady = 2;   // balanced: own consumer's ready frames before feeding a starving one
   // copy-kernel grid when every consumer of a dispatch sits on this GPU (2-rank-on-one-GPU A/B,
   // device-resident, remote_only window: 512 -> 100.4k / 105.2k fr/s, 256 -> 100.1k / 101.1k,
   // 128 -> 93.6k / 94.4k; profiles/r4/fabric_pass3)
-  static constexpr int kLocalCopyWgs = 512;   // balanced: own consumer's ready frames before feeding a starving one
+  static constexpr int kLocalCopyWgs = 512;
   static constexpr int kMinGrants = 4;      // grants kept at an idle producer (pipeline depth)
   static constexpr int kMaxDispatch = 64;   // produced frames routed per iteration
 

@@ -44,7 +44,14 @@ void launch_assemble(const FramePtrs& fp, int nframes, uint64_t idx, int64_t nou
 // kPfCandCap parked in LDS go to the workgroup's kPfSpillCap entries here and are tested after the
 // stream like the parked ones (only past both does a candidate get tested inline in the stream).
 constexpr int kPfScratchHeader = 1024;                 // PfScratch (counters), padded
-constexpr int kPfSpillWgs = 4096, kPfSpillCap = 1024;  // workgroups with a spill list, entries each
+// The grid is one resident wave of workgroups (768 for radius 1, 512 for radius 2 on 256 CUs), so
+// 1024 lists of 4096 entries cover every workgroup with 4x the round-3 depth: on a 2 %-candidate
+// batch the in-stream path no longer runs (11.2 -> 7.4 us/frame, profiles/r4/README.md section 4).
+#ifndef PR_PF_SPILL_WGS
+#define PR_PF_SPILL_WGS 1024
+#endif
+constexpr int kPfSpillWgs = PR_PF_SPILL_WGS;                    // workgroups with a spill list
+constexpr int kPfSpillCap = (4096 / kPfSpillWgs) * 1024;        // entries each (same block size)
 constexpr int64_t kPfScratchBytes = kPfScratchHeader + (int64_t)kPfSpillWgs * kPfSpillCap * 4;
 void launch_peakfind(const FramePtrs& fp, int nframes, int n_panels, int rows, int cols, float thr_peak,
                      float son_min, int radius, int max_peaks, uint64_t peaks, uint64_t counts,

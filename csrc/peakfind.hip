@@ -37,11 +37,11 @@ struct PfParams {
   int n_panels, rows, cols;
 };
 
-// at(dy, dx): neighbour value, NaN outside the panel
+// The test of one candidate.  at(dy, dx): neighbour value, NaN outside the panel.  Returns whether
+// it is a peak and, if so, its record fields.
 template <int RAD, typename At>
-__device__ __forceinline__ void pf_candidate(const At& at, float v, const PfParams& pp, int f, int panel, int gy,
-                                             int gx, float* __restrict__ peaks, int* __restrict__ counts,
-                                             unsigned long long* __restrict__ total) {
+__device__ __forceinline__ bool pf_eval(const At& at, float v, const PfParams& pp, float& bkg, float& noise,
+                                        float& snr, float& inten) {
   constexpr int H = RAD + 2;
   constexpr int D = 2 * H + 1;
   // the whole (2H+1)^2 neighbourhood is loaded up front: ONE round of independent loads instead of
@@ -52,52 +52,60 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
   for (int dy = -H; dy <= H; ++dy)
 #pragma unroll
     for (int dx = -H; dx <= H; ++dx) w[dy + H][dx + H] = (dy == 0 && dx == 0) ? v : at(dy, dx);
-  float bkg = 0.0f, noise = 0.0f, snr = 0.0f, inten = 0.0f;
-  auto accept = [&]() -> bool {
+  bkg = 0.0f, noise = 0.0f, snr = 0.0f, inten = 0.0f;
 #pragma unroll
-    for (int dy = -RAD; dy <= RAD; ++dy)
+  for (int dy = -RAD; dy <= RAD; ++dy)
 #pragma unroll
-      for (int dx = -RAD; dx <= RAD; ++dx) {
-        if (dy == 0 && dx == 0) continue;
-        const float n = w[dy + H][dx + H];
-        if (n != n) continue;
-        const bool before = (dy < 0) || (dy == 0 && dx < 0);
-        if (before ? !(v > n) : !(v >= n)) return false;   // not the strict local max (ties: lower index wins)
-      }
-    float s = 0.0f, s2 = 0.0f;
-    int nr = 0;
+    for (int dx = -RAD; dx <= RAD; ++dx) {
+      if (dy == 0 && dx == 0) continue;
+      const float n = w[dy + H][dx + H];
+      if (n != n) continue;
+      const bool before = (dy < 0) || (dy == 0 && dx < 0);
+      if (before ? !(v > n) : !(v >= n)) return false;   // not the strict local max (ties: lower index wins)
+    }
+  float s = 0.0f, s2 = 0.0f;
+  int nr = 0;
 #pragma unroll
-    for (int dy = -H; dy <= H; ++dy)
+  for (int dy = -H; dy <= H; ++dy)
 #pragma unroll
-      for (int dx = -H; dx <= H; ++dx) {
-        const int d = max(abs(dy), abs(dx));
-        if (d <= RAD) continue;
-        const float n = w[dy + H][dx + H];
-        if (n != n) continue;
-        s += n;
-        s2 += n * n;
-        ++nr;
-      }
-    bkg = nr > 0 ? s / nr : 0.0f;
-    const float var = nr > 0 ? fmaxf(s2 / nr - bkg * bkg, 0.0f) : 0.0f;
-    noise = sqrtf(var);
-    snr = (v - bkg) / fmaxf(noise, 1e-6f);
-    if (snr < pp.son_min) return false;
+    for (int dx = -H; dx <= H; ++dx) {
+      const int d = max(abs(dy), abs(dx));
+      if (d <= RAD) continue;
+      const float n = w[dy + H][dx + H];
+      if (n != n) continue;
+      s += n;
+      s2 += n * n;
+      ++nr;
+    }
+  bkg = nr > 0 ? s / nr : 0.0f;
+  const float var = nr > 0 ? fmaxf(s2 / nr - bkg * bkg, 0.0f) : 0.0f;
+  noise = sqrtf(var);
+  snr = (v - bkg) / fmaxf(noise, 1e-6f);
+  if (snr < pp.son_min) return false;
 #pragma unroll
-    for (int dy = -RAD; dy <= RAD; ++dy)
+  for (int dy = -RAD; dy <= RAD; ++dy)
 #pragma unroll
-      for (int dx = -RAD; dx <= RAD; ++dx) {
-        const float n = w[dy + H][dx + H];
-        if (n == n) inten += n - bkg;
-      }
-    return true;
-  };
-  // Record slots: ONE atomic per (wave, frame) among the lanes here that accepted a peak, not one
-  // per peak -- same-address atomics serialise (~3 ns each), and a hit-rich frame (2 % of its
-  // pixels above threshold: ~32k peaks) spent ~90 us/frame in them.  Slot order within a frame is
-  // not part of the output contract (counts, and the records as a set).
-  bool pending = accept();
+    for (int dx = -RAD; dx <= RAD; ++dx) {
+      const float n = w[dy + H][dx + H];
+      if (n == n) inten += n - bkg;
+    }
+  return true;
+}
+
+// one record = two 16-B stores (records are 32-B aligned)
+__device__ __forceinline__ void pf_store(float* __restrict__ peaks, const PfParams& pp, int f, int slot,
+                                         const f32x4_t& a, const f32x4_t& b) {
+  f32x4_t* rec = reinterpret_cast<f32x4_t*>(peaks + ((int64_t)f * pp.max_peaks + slot) * 8);
+  rec[0] = a;
+  rec[1] = b;
+}
+
+// Slot index among the lanes here with `pending` set, per frame: ONE atomic on ctr[f] per (wave,
+// frame) -- same-address atomics serialise, so never one per lane.  ctr is an LDS counter array
+// (the workgroup's per-frame tallies) or the global per-frame counts (in-stream path).
+__device__ __forceinline__ int pf_claim(bool pending, int f, int* ctr) {
   const int lane = (int)(threadIdx.x & 63);
+  int loc = 0;
   for (;;) {
     const uint64_t m = __ballot(pending);
     if (m == 0) break;
@@ -105,23 +113,23 @@ __device__ __forceinline__ void pf_candidate(const At& at, float v, const PfPara
     const int f0 = __shfl(f, leader);
     const uint64_t mf = __ballot(pending && f == f0);
     int base = 0;
-    if (lane == leader) base = atomicAdd(counts + f0, __popcll(mf));
+    if (lane == leader) base = atomicAdd(ctr + f0, __popcll(mf));
     base = __shfl(base, leader);
-    int slot = 0;
     if (pending && f == f0) {
-      slot = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf, 0u));
+      loc = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf, 0u));
       pending = false;
-      if (slot < pp.max_peaks) {   // one record = two 16-B stores (records are 32-B aligned)
-        f32x4_t* rec = reinterpret_cast<f32x4_t*>(peaks + ((int64_t)f * pp.max_peaks + slot) * 8);
-        rec[0] = f32x4_t{(float)panel, (float)gy, (float)gx, v};
-        rec[1] = f32x4_t{inten, bkg, noise, snr};
-      }
-    }
-    if (total != nullptr) {   // records written by this group (slots below max_peaks)
-      const uint64_t wr = __ballot((mf >> lane) & 1ull && slot < pp.max_peaks);
-      if (lane == leader && wr != 0) atomicAdd(total, (unsigned long long)__popcll(wr));
     }
   }
+  return loc;
+}
+
+// records written by the active lanes with `wrote` set, added to the running total (one atomic
+// per wave)
+__device__ __forceinline__ void pf_add_total(unsigned long long* total, bool wrote) {
+  if (total == nullptr) return;
+  const uint64_t wr = __ballot(wrote);
+  const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+  if ((int)(threadIdx.x & 63) == leader && wr != 0) atomicAdd(total, (unsigned long long)__popcll(wr));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -180,6 +188,7 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
   __shared__ int cand_n;
   __shared__ int cand_p[kPfCandCap];
   __shared__ unsigned char cand_f[kPfCandCap];
+  __shared__ int wg_cnt[kMaxFrames], wg_n0[kMaxFrames], wg_base[kMaxFrames];   // per-frame tallies
   int* counts = scratch != nullptr ? scratch->tickets : counts_out;
   float* summary = scratch != nullptr ? scratch->acc : summary_out;
   // the running total: with a scratch block the last workgroup adds the launch's record count in
@@ -218,7 +227,8 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
   // 4-float groups holding columns x-H .. x+H; panels are a multiple of 4 wide, so a group is wholly
   // inside or outside its row) instead of (2H+1) 4-B loads: 21 vector loads for RAD 1 where 49 scalar
   // ones kept the texture units busy on hit-rich frames (tens of thousands of candidates per frame).
-  auto test = [&](int f, int64_t p) {
+  // Returns whether the candidate is a peak; its record in (ra, rb).
+  auto test = [&](int f, int64_t p, f32x4_t& ra, f32x4_t& rb) -> bool {
     constexpr int H = RAD + 2, D = 2 * H + 1;
     static_assert(D <= 9, "three 4-float groups per row cover at most 9 columns at any alignment");
     const PR_GLOBAL float* img = gin<float>(fp.in[f]);
@@ -247,8 +257,21 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
         wv[dy + H][dx] = off == 0 ? e[dx] : off == 1 ? e[dx + 1] : off == 2 ? e[dx + 2] : e[dx + 3];
     }
     const float val = wv[H][H];
-    pf_candidate<RAD>([&](int dy, int dx) { return wv[dy + H][dx + H]; }, val, pp, f, panel, y, x, peaks, counts,
-                      total_per_peak);
+    float bkg, noise, snr, inten;
+    const bool ok = pf_eval<RAD>([&](int dy, int dx) { return wv[dy + H][dx + H]; }, val, pp, bkg, noise, snr, inten);
+    ra = f32x4_t{(float)panel, (float)y, (float)x, val};
+    rb = f32x4_t{inten, bkg, noise, snr};
+    return ok;
+  };
+  // in-stream path (a workgroup past its LDS and spill capacity): slots straight from the global
+  // per-frame counts, one atomic per (wave, frame)
+  auto test_now = [&](int f, int64_t p) {
+    f32x4_t ra, rb;
+    const bool ok = test(f, p, ra, rb);
+    const int slot = pf_claim(ok, f, counts);
+    const bool wrote = ok && slot < pp.max_peaks;
+    if (wrote) pf_store(peaks, pp, f, slot, ra, rb);
+    pf_add_total(total_per_peak, wrote);
   };
   // block-reduce this frame's statistics and add them (one atomic pair per workgroup and frame)
   auto flush = [&](int f, float s, int c) {
@@ -273,6 +296,7 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
     }
   };
   if (threadIdx.x == 0) cand_n = 0;
+  if (threadIdx.x < kMaxFrames) wg_cnt[threadIdx.x] = 0;
   __syncthreads();
   float above_sum = 0.0f;
   int above_cnt = 0;
@@ -312,7 +336,7 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
         } else if (slot < cap) {
           spill[slot - kPfCandCap] = (uint32_t)p | ((uint32_t)f << kPfSpillShift);
         } else {
-          test(f, p);   // past LDS and spill: tested in the stream (correct, slow)
+          test_now(f, p);   // past LDS and spill: tested in the stream (correct, slow)
         }
         ++slot;
       }
@@ -320,16 +344,71 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
   }
   if (g0 < g1) flush(fcur, above_sum, above_cnt);
   __syncthreads();
-  // parked, then spilled candidates, one per lane (the spill stores above are visible: the barrier
-  // orders them for the whole workgroup)
+  // Parked, then spilled candidates, one per thread and round (the spill stores above are visible:
+  // the barrier orders them for the whole workgroup).  Record slots are reserved ONCE per
+  // (workgroup, frame) from the global counts, not per (wave, round): tallies go to LDS counters
+  // first.  (Per-wave global atomics on the few per-frame count words cost 2.6 us/frame on a
+  // hit-rich batch -- 44k candidates / 32k peaks per epix10k2M frame; one returning atomic on one
+  // word saturates near 88 per us, MI355X_MICROARCH.md dequeue row.)
+  //   round 0 (threads 0..255)  test, keep the record in registers, claim a local index
+  //   rounds >= 1               test, count only
+  //   reserve                   one global atomic per frame this workgroup accepted peaks in
+  //   write                     round 0 from registers; rounds >= 1 re-tested, only for frames
+  //                             whose reserved range still reaches below max_peaks (a hit-rich
+  //                             frame past its record capacity needs counts, not records)
   const int nc = min(cand_n, cap);
-  for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+  auto cand_at = [&](int i, int& f, int64_t& p) {
     if (i < kPfCandCap) {
-      test(cand_f[i], cand_p[i]);
+      f = cand_f[i];
+      p = cand_p[i];
     } else {
       const uint32_t e = spill[i - kPfCandCap];
-      test((int)(e >> kPfSpillShift), (int64_t)(e & ((1u << kPfSpillShift) - 1u)));
+      f = (int)(e >> kPfSpillShift);
+      p = (int64_t)(e & ((1u << kPfSpillShift) - 1u));
     }
+  };
+  const int tid = (int)threadIdx.x;
+  int f0 = 0, loc0 = 0;
+  f32x4_t ra0{}, rb0{};
+  bool ok0 = false;
+  if (tid < nc) {
+    int64_t p;
+    cand_at(tid, f0, p);
+    ok0 = test(f0, p, ra0, rb0);
+  }
+  loc0 = pf_claim(ok0, f0, wg_cnt);
+  __syncthreads();
+  if (tid < nframes) wg_n0[tid] = wg_cnt[tid];
+  for (int i = tid + 256; i < nc; i += 256) {
+    int f;
+    int64_t p;
+    cand_at(i, f, p);
+    f32x4_t ra, rb;
+    const bool ok = test(f, p, ra, rb);
+    pf_claim(ok, f, wg_cnt);
+  }
+  __syncthreads();
+  if (tid < nframes) {
+    const int c = wg_cnt[tid];
+    wg_base[tid] = c > 0 ? atomicAdd(counts + tid, c) : 0;
+    wg_cnt[tid] = wg_n0[tid];   // running local index of rounds >= 1
+  }
+  __syncthreads();
+  {
+    const bool wrote = ok0 && wg_base[f0] + loc0 < pp.max_peaks;
+    if (wrote) pf_store(peaks, pp, f0, wg_base[f0] + loc0, ra0, rb0);
+    pf_add_total(total_per_peak, wrote);
+  }
+  for (int i = tid + 256; i < nc; i += 256) {
+    int f;
+    int64_t p;
+    cand_at(i, f, p);
+    f32x4_t ra, rb;
+    const bool ok = wg_base[f] + wg_n0[f] < pp.max_peaks && test(f, p, ra, rb);
+    const int slot = wg_base[f] + pf_claim(ok, f, wg_cnt);
+    const bool wrote = ok && slot < pp.max_peaks;
+    if (wrote) pf_store(peaks, pp, f, slot, ra, rb);
+    pf_add_total(total_per_peak, wrote);
   }
   if (scratch == nullptr) return;
   __syncthreads();

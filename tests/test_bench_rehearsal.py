@@ -20,9 +20,10 @@ def test_bench_multirank_cpu(native, nproc, route, producers):
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     port = random.randint(30000, 45000)
-    # a lone producer: the consumer-only rank's read-ahead covers a 4-step window by itself, so the
-    # window must be long enough for frames to cross inside it
-    steps = 40 if producers == 1 else 4
+    # config-3 shapes (producers < ranks): a lone producer's consumer-only rank covers a 4-step
+    # window from its read-ahead alone, and the consumer vs producer rate comparison needs a window
+    # long against the queue slack -- 48 steps
+    steps = 48 if producers else 4
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
            "--gpus", str(nproc), "--steps", str(steps), "--warmup", "2", "--batch", "4", "--detector", "tiny_epix",
@@ -54,9 +55,10 @@ def test_bench_multirank_cpu(native, nproc, route, producers):
     assert all(b == 0 for b in x["bytes_sent_per_rank"][n_p:]), x
     if producers:
         # BASELINE config 3 shape: consumer-only ranks get every frame they consume
-        # from another process, and the node consumes at the producers' rate
+        # from another process, and the node consumes at the producers' rate -- to within the queue
+        # slack: production inside the window also refills the queue (queue_size 16 frames per rank
+        # against 192 consumed per rank in the window, i.e. up to ~8 %), and 8 ranks share 8 CPUs
         share = d["extra"]["recv_cross_per_consumed_per_rank"]
         assert all(v >= 0.9 for v in share[n_p:]), share
         assert all(c > 0 for c in d["extra"]["consumed_per_rank"]), d["extra"]["consumed_per_rank"]
-        assert d["extra"]["consumer_frames_per_s"] >= 0.95 * d["extra"]["production_frames_per_s"] or \
-            d["value"] >= 0.95 * d["extra"]["production_frames_per_s"], d["extra"]
+        assert d["extra"]["consumer_frames_per_s"] >= 0.90 * d["extra"]["production_frames_per_s"], d["extra"]

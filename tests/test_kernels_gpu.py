@@ -208,6 +208,11 @@ def test_peakfind_total_counts_only_written_records(cuda_device, scratch):
     torch.cuda.synchronize()
     assert [int(c) for c in counts.cpu()] == [p.shape[0] for p in ref_peaks]
     assert int(total) == 5 + 3 * F * params.max_peaks
+    for f in range(F):   # the written records: distinct golden-model peaks
+        got = peaks[f].cpu()
+        ref = {tuple(r[:4].tolist()) for r in ref_peaks[f]}
+        rows = {tuple(r[:4].tolist()) for r in got}
+        assert len(rows) == params.max_peaks and rows <= ref
 
 
 @pytest.mark.parametrize("det,F", [("tiny_epix", kernels.MAX_FRAMES), ("jungfrau05M", 7)])

@@ -107,20 +107,21 @@ def _sorted_peaks(p):
     return p[torch.argsort(q[:, 0] * 100_000_000 + q[:, 1] * 10_000 + q[:, 2])]
 
 
-@pytest.mark.parametrize("quantile,floor", [(0.70, 512), (0.50, 512 + 1024)])
-def test_peakfind_candidate_overflow(cuda_device, quantile, floor):
-    """Candidates above thr_peak at ~30 % / ~50 % of the pixels: every workgroup's 4096-pixel range
-    parks more than kPfCandCap (512) of them in LDS, the rest go to its spill list in the scratch
-    block (kPfSpillCap, 1024) and -- at 50 % -- past that too, so the in-stream test path runs.  The
+@pytest.mark.parametrize("quantile,floor,F", [(0.70, 512, 2), (0.50, 1200, 6)])
+def test_peakfind_candidate_overflow(cuda_device, quantile, floor, F):
+    """Candidates above thr_peak at ~30 % / ~50 % of the pixels: every workgroup parks more than
+    kPfCandCap (512) of them in LDS and the rest go to its spill list in the scratch block
+    (kPfSpillCap, 4096); with 6 frames at 50 % each workgroup's range (>= 4 x 4096 pixels of the 768
+    resident workgroups, > 1200 candidates each) holds > 4608, past both, so the in-stream test
+    path runs too.  The
     peak list still matches the golden model exactly (positions / values; intensities to fp32
     summation order)."""
     spec = get_detector("epix10k2M")
     consts = CalibConstants.random(spec, seed=8, gain_config="AHL")
-    raw, _ = generate_raw(consts, 2, seed=9)
+    raw, _ = generate_raw(consts, F, seed=9)
     frames = reference.calibrate_reference(torch.from_numpy(raw.astype(np.int32)), consts, None, None)
     thr = float(torch.quantile(frames[0].flatten()[::97], quantile))
     params = PeakFinderParams(thr_peak=thr, son_min=0.0, radius=1, max_peaks=400_000)
-    F = frames.shape[0]
     above = (frames > thr).reshape(F, -1).float()
     per_range = above.reshape(F, -1, 4096).sum(-1)
     assert float(per_range.min()) > floor, "test data too weak: some 4096-pixel range stays under the cap"
@@ -140,3 +141,50 @@ def test_peakfind_candidate_overflow(cuda_device, quantile, floor):
         assert torch.allclose(got[:, 4:], exp[:, 4:], rtol=1e-4, atol=1e-3)
     assert torch.equal(summary[:, 0].cpu(), ref_summary[:, 0])
     assert int(scr[:256].abs().sum()) == 0   # the counters reset themselves (the spill lists need not)
+
+
+def _keys(p):
+    q = p[:, :3].to(torch.int64).cpu()
+    return set((q[:, 0] * 100_000_000 + q[:, 1] * 10_000 + q[:, 2]).tolist())
+
+
+@pytest.mark.parametrize("radius", [1, 2])
+def test_peakfind_hit_rich_past_max_peaks(cuda_device, radius):
+    """A hit-rich batch (10 % of the pixels above threshold: several candidate rounds per workgroup,
+    ~100k peaks per frame) with max_peaks = 2048: counts are exact, and the 2048 records written per
+    frame are distinct peaks of the golden model with its values (slots are reserved once per
+    workgroup and frame; rounds past round 0 are re-tested only while their frame's reserved range
+    reaches below max_peaks)."""
+    spec = get_detector("epix10k2M")
+    consts = CalibConstants.random(spec, seed=8, gain_config="AHL")
+    raw, _ = generate_raw(consts, 2, seed=9)
+    frames = reference.calibrate_reference(torch.from_numpy(raw.astype(np.int32)), consts, None, None)
+    thr = float(torch.quantile(frames[0].flatten()[::97], 0.90))
+    params = PeakFinderParams(thr_peak=thr, son_min=0.0, radius=radius, max_peaks=2048)
+    F = frames.shape[0]
+    d = frames.to(cuda_device).contiguous()
+    peaks = torch.zeros((F, params.max_peaks, 8), dtype=torch.float32, device=cuda_device)
+    counts = torch.zeros(F, dtype=torch.int32, device=cuda_device)
+    summary = torch.zeros((F, 2), dtype=torch.float32, device=cuda_device)
+    total = torch.zeros((), dtype=torch.int64, device=cuda_device)
+    scr = torch.zeros(kernels.PF_SCRATCH_WORDS, dtype=torch.int32, device=cuda_device)
+    kernels.peakfind([d[i] for i in range(F)], spec.frame_shape, params, peaks, counts, summary, total=total,
+                     scratch=scr)
+    torch.cuda.synchronize()
+    ref_peaks, _ = reference.peakfind_reference(frames, PeakFinderParams(thr_peak=thr, son_min=0.0, radius=radius,
+                                                                         max_peaks=1 << 30))
+    assert int(total) == F * params.max_peaks
+    for f in range(F):
+        n = int(counts[f])
+        assert n == ref_peaks[f].shape[0] and n > 8 * params.max_peaks, (n, ref_peaks[f].shape[0])
+        got = _sorted_peaks(peaks[f])
+        keys = _keys(got)
+        assert len(keys) == params.max_peaks, "records written twice or left empty"
+        ref = ref_peaks[f]
+        q = ref[:, :3].to(torch.int64)
+        rk = q[:, 0] * 100_000_000 + q[:, 1] * 10_000 + q[:, 2]
+        sel = torch.isin(rk, torch.tensor(sorted(keys), dtype=torch.int64))
+        assert int(sel.sum()) == params.max_peaks, "a written record is not a golden-model peak"
+        exp = _sorted_peaks(ref[sel])
+        assert torch.equal(got[:, :4], exp[:, :4])
+        assert torch.allclose(got[:, 4:], exp[:, 4:], rtol=1e-4, atol=1e-3)

@@ -71,3 +71,26 @@ def test_wake_all_unblocks(native):
     p.wake_all()
     th.join(5)
     assert out == [-1]
+
+
+def test_relay_ready_moves_at_most_the_producer_room(native):
+    """The keeper's re-offer: READY frames go back on offer in ONE locked step,
+    never more than the producer room at that moment, headers kept -- no lease-then-reoffer window
+    in which the fabric thread can shrink the room."""
+    C = native
+    p = C.SlotPool(3, 4, -1)
+    slots = [p.try_acquire_produce() for _ in range(3)]
+    for i, s in enumerate(slots):
+        p.commit_produce(s, C.SlotHeader(0, i, 100 + i, 0.0), 0)
+        p.route_local(s)
+    assert p.n_ready() == 3 and p.producer_room() == 3
+    held = [p.try_acquire_produce(), p.try_acquire_produce()]   # room 1 left
+    assert all(h >= 0 for h in held) and p.producer_room() == 1
+    assert p.relay_ready(64) == 1
+    assert p.n_ready() == 2 and p.n_produced() == 1 and p.producer_room() == 0
+    moved = p.produced(10)
+    assert [h.gevt for h in p.headers(moved)] == [100]          # FIFO, header kept
+    assert p.relay_ready(64) == 0                                # no room: nothing moves
+    for h in held:
+        p.abort_produce(h)
+    assert p.relay_ready(1) == 1 and p.n_ready() == 1            # bounded by max_n
