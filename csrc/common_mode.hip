@@ -1156,8 +1156,18 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
   }
 }
 
+// PR_CM_MAX_VGPR > 0: cap the net kernel's VGPRs (diagnostic builds: leave room on each SIMD for
+// a co-resident consumer kernel's wave)
+#ifndef PR_CM_MAX_VGPR
+#define PR_CM_MAX_VGPR 0
+#endif
+#if PR_CM_MAX_VGPR > 0
+#define PR_CM_VGPR_ATTR __attribute__((amdgpu_num_vgpr(PR_CM_MAX_VGPR / 2)))   // gfx950: the request counts twice (VGPR + AGPR file)
+#else
+#define PR_CM_VGPR_ATTR
+#endif
 template <int KIND, int L, int M, int BLOCK, int TR = 0, int TC = 0>
-__global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_CU / 4 : 2) void calib_cm_net_kernel(
+__global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_CU / 4 : 2) PR_CM_VGPR_ATTR void calib_cm_net_kernel(
     const FramePtrs fp, const float* __restrict__ ped, const float* __restrict__ gf,
     const uint8_t* __restrict__ planes, const TileGeom tg, const CmParams cp, const ImgOut io) {
   constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);

@@ -175,8 +175,18 @@ constexpr int kPfSpillShift = 26;
 // 528 chunks -- gave 16 of every 64 a ninth chunk: 1.92-1.99 vs 1.88-1.89 us/frame for this form,
 // 32 epix10k2M frames, tools/pf_probe.py; K = 8 / 16 float4 per lane: 2.19 / 2.25, lower occupancy.)
 // A range crosses at most a couple of frame boundaries; the hit statistics are flushed at each.
+// PR_PF_WAVES_PER_EU > 0: VGPR budget 512 / N (diagnostic builds: co-residency with the
+// common-mode kernel's waves, which leave 64 VGPRs per SIMD lane free)
+#ifndef PR_PF_WAVES_PER_EU
+#define PR_PF_WAVES_PER_EU 0
+#endif
+#if PR_PF_WAVES_PER_EU > 0
+#define PR_PF_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(PR_PF_WAVES_PER_EU, PR_PF_WAVES_PER_EU)))
+#else
+#define PR_PF_WAVES_ATTR
+#endif
 template <int RAD, int K>
-__global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp, const PfParams pp,
+__global__ __launch_bounds__(256) PR_PF_WAVES_ATTR void peakfind_range_kernel(const FramePtrs fp, const PfParams pp,
                                                              float* __restrict__ peaks, int* __restrict__ counts_out,
                                                              float* __restrict__ summary_out,
                                                              unsigned long long* __restrict__ total,
@@ -324,6 +334,9 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
     }
     const int64_t q0 = (g - (int64_t)f * ncpf) * 256 * K + threadIdx.x;
     if (g + 1 < g1) load(g + 1);
+#ifdef PR_PF_DIAG_STREAM_ONLY
+    cand = 0;   // diagnostic builds only: the stream without any candidate handling
+#endif
     if (cand) {
       int slot = atomicAdd(&cand_n, __popcll(cand));
       while (cand) {
@@ -356,7 +369,11 @@ __global__ __launch_bounds__(256) void peakfind_range_kernel(const FramePtrs fp,
   //   write                     round 0 from registers; rounds >= 1 re-tested, only for frames
   //                             whose reserved range still reaches below max_peaks (a hit-rich
   //                             frame past its record capacity needs counts, not records)
+#ifdef PR_PF_DIAG_STREAM_ONLY
+  const int nc = 0;
+#else
   const int nc = min(cand_n, cap);
+#endif
   auto cand_at = [&](int i, int& f, int64_t& p) {
     if (i < kPfCandCap) {
       f = cand_f[i];
