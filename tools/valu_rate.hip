@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <vector>
 
@@ -44,12 +45,21 @@
 #define T_SUB(i) "v_sub_f32 " R_(i) ", %16, " R_(i)
 #define T_PERM(i) "v_perm_b32 " R_(i) ", " R_(i) ", %16, %16"
 #define T_MAXDPP(i) "v_max_f32_dpp " R_(i) ", %16, " R_(i) " quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+#define T_MAXI32(i) "v_max_i32 " R_(i) ", %16, " R_(i)
+#define T_MINU32(i) "v_min_u32 " R_(i) ", %16, " R_(i)
+#define T_MAX3I32(i) "v_max3_i32 " R_(i) ", " R_(i) ", %16, " R_(i)
+#define T_MED3I32(i) "v_med3_i32 " R_(i) ", " R_(i) ", %16, " R_(i)
+#define T_ADDU32(i) "v_add_u32 " R_(i) ", %16, " R_(i)
+#define T_PKMAXI16(i) "v_pk_max_i16 " R_(i) ", " R_(i) ", %16"
+#define T_MINF32(i) "v_min_f32_e32 " R_(i) ", %16, " R_(i)
 
-constexpr int kOps = 20;
+constexpr int kOps = 27;
 static const char* kOpNames[kOps] = {"v_maximum3_f32", "v_minimum3_f32", "v_max3_f32", "v_med3_f32", "v_max_f32_e32",
                                      "v_max_f32_e64", "v_max_f32_dpp", "v_fma_f32", "v_add_f32", "v_bfi_b32",
                                      "v_pk_max_f16", "v_cvt_f32_u32", "v_bfe_u32", "v_and_or_b32", "v_cndmask_b32",
-                                     "v_mul_f32", "v_mov_b32", "v_xor_b32", "v_sub_f32", "v_perm_b32"};
+                                     "v_mul_f32", "v_mov_b32", "v_xor_b32", "v_sub_f32", "v_perm_b32",
+                                     "v_max_i32", "v_min_u32", "v_max3_i32", "v_med3_i32", "v_add_u32",
+                                     "v_pk_max_i16", "v_min_f32_e32"};
 
 template <int OP>
 __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
@@ -78,7 +88,14 @@ __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
     else if constexpr (OP == 16) PR_ASM16(T_MOV);
     else if constexpr (OP == 17) PR_ASM16(T_XOR);
     else if constexpr (OP == 18) PR_ASM16(T_SUB);
-    else PR_ASM16(T_PERM);
+    else if constexpr (OP == 19) PR_ASM16(T_PERM);
+    else if constexpr (OP == 20) PR_ASM16(T_MAXI32);
+    else if constexpr (OP == 21) PR_ASM16(T_MINU32);
+    else if constexpr (OP == 22) PR_ASM16(T_MAX3I32);
+    else if constexpr (OP == 23) PR_ASM16(T_MED3I32);
+    else if constexpr (OP == 24) PR_ASM16(T_ADDU32);
+    else if constexpr (OP == 25) PR_ASM16(T_PKMAXI16);
+    else PR_ASM16(T_MINF32);
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   float z = 0.f;
@@ -119,7 +136,8 @@ static void run_op(int cus, float* out, unsigned long long* clk, int iters, hipE
   }
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const int first = argc > 1 ? atoi(argv[1]) : 0;   // run ops [first, kOps)
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -131,25 +149,32 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  run_op<0>(cus, out, clk, iters, e0, e1);
-  run_op<1>(cus, out, clk, iters, e0, e1);
-  run_op<2>(cus, out, clk, iters, e0, e1);
-  run_op<3>(cus, out, clk, iters, e0, e1);
-  run_op<4>(cus, out, clk, iters, e0, e1);
-  run_op<5>(cus, out, clk, iters, e0, e1);
-  run_op<6>(cus, out, clk, iters, e0, e1);
-  run_op<7>(cus, out, clk, iters, e0, e1);
-  run_op<8>(cus, out, clk, iters, e0, e1);
-  run_op<9>(cus, out, clk, iters, e0, e1);
-  run_op<10>(cus, out, clk, iters, e0, e1);
-  run_op<11>(cus, out, clk, iters, e0, e1);
-  run_op<12>(cus, out, clk, iters, e0, e1);
-  run_op<13>(cus, out, clk, iters, e0, e1);
-  run_op<14>(cus, out, clk, iters, e0, e1);
-  run_op<15>(cus, out, clk, iters, e0, e1);
-  run_op<16>(cus, out, clk, iters, e0, e1);
-  run_op<17>(cus, out, clk, iters, e0, e1);
-  run_op<18>(cus, out, clk, iters, e0, e1);
-  run_op<19>(cus, out, clk, iters, e0, e1);
+  if (0 >= first) run_op<0>(cus, out, clk, iters, e0, e1);
+  if (1 >= first) run_op<1>(cus, out, clk, iters, e0, e1);
+  if (2 >= first) run_op<2>(cus, out, clk, iters, e0, e1);
+  if (3 >= first) run_op<3>(cus, out, clk, iters, e0, e1);
+  if (4 >= first) run_op<4>(cus, out, clk, iters, e0, e1);
+  if (5 >= first) run_op<5>(cus, out, clk, iters, e0, e1);
+  if (6 >= first) run_op<6>(cus, out, clk, iters, e0, e1);
+  if (7 >= first) run_op<7>(cus, out, clk, iters, e0, e1);
+  if (8 >= first) run_op<8>(cus, out, clk, iters, e0, e1);
+  if (9 >= first) run_op<9>(cus, out, clk, iters, e0, e1);
+  if (10 >= first) run_op<10>(cus, out, clk, iters, e0, e1);
+  if (11 >= first) run_op<11>(cus, out, clk, iters, e0, e1);
+  if (12 >= first) run_op<12>(cus, out, clk, iters, e0, e1);
+  if (13 >= first) run_op<13>(cus, out, clk, iters, e0, e1);
+  if (14 >= first) run_op<14>(cus, out, clk, iters, e0, e1);
+  if (15 >= first) run_op<15>(cus, out, clk, iters, e0, e1);
+  if (16 >= first) run_op<16>(cus, out, clk, iters, e0, e1);
+  if (17 >= first) run_op<17>(cus, out, clk, iters, e0, e1);
+  if (18 >= first) run_op<18>(cus, out, clk, iters, e0, e1);
+  if (19 >= first) run_op<19>(cus, out, clk, iters, e0, e1);
+  if (20 >= first) run_op<20>(cus, out, clk, iters, e0, e1);
+  if (21 >= first) run_op<21>(cus, out, clk, iters, e0, e1);
+  if (22 >= first) run_op<22>(cus, out, clk, iters, e0, e1);
+  if (23 >= first) run_op<23>(cus, out, clk, iters, e0, e1);
+  if (24 >= first) run_op<24>(cus, out, clk, iters, e0, e1);
+  if (25 >= first) run_op<25>(cus, out, clk, iters, e0, e1);
+  if (26 >= first) run_op<26>(cus, out, clk, iters, e0, e1);
   return 0;
 }
