@@ -257,3 +257,35 @@ def test_balanced_feeds_a_starving_consumer_only_rank(native, tok):
         assert local > 0
     finally:
         _stop(pf, cf)
+
+
+def test_balanced_shares_between_two_starving_consumer_only_members(native, tok):
+    """Two consumer-only members next to a prosumer: every offer goes to the starving member given
+    the fewest in the pass, so neither starves (the first-listed member used to take every offer
+    while it had grants)."""
+    C = native
+    sb = 128
+    pp, _pr, pf = _member(C, tok, 0, 32, 32, sb, 0)    # prosumer, balanced
+    ap, _ar, af = _member(C, tok, 1, 0, 32, sb, 0)      # consumer only
+    bp, _br, bf = _member(C, tok, 2, 0, 32, sb, 0)      # consumer only
+    _link(tok, pf, 0, af, 1)
+    _link(tok, pf, 0, bf, 2)
+    for f in (pf, af, bf):
+        f.start()
+    try:
+        produced = 0
+        got = {"local": 0, "a": 0, "b": 0}
+        t0 = time.time()
+        while time.time() - t0 < 5.0 and min(got["a"], got["b"]) < 20:
+            produced += _produce(C, pp, 8, produced)
+            for pool, key in ((pp, "local"), (ap, "a"), (bp, "b")):
+                while True:
+                    s = pool.try_get()
+                    if s < 0:
+                        break
+                    pool.release(s, 0)
+                    got[key] += 1
+            time.sleep(0.002)
+        assert got["a"] >= 20 and got["b"] >= 20, got
+    finally:
+        _stop(pf, af, bf)
