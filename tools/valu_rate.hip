@@ -22,7 +22,7 @@
                : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]),    \
                  "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]), "+v"(r[13]), \
                  "+v"(r[14]), "+v"(r[15])                                                               \
-               : "v"(k))
+               : "v"(k), "s"(ks), "s"(km))
 #define S_(x) #x
 #define R_(i) "%" S_(i)
 #define T_MAXIMUM3(i) "v_maximum3_f32 " R_(i) ", " R_(i) ", %16, " R_(i)
@@ -52,14 +52,20 @@
 #define T_ADDU32(i) "v_add_u32 " R_(i) ", %16, " R_(i)
 #define T_PKMAXI16(i) "v_pk_max_i16 " R_(i) ", " R_(i) ", %16"
 #define T_MINF32(i) "v_min_f32_e32 " R_(i) ", %16, " R_(i)
+#define T_CND64(i) "v_cndmask_b32_e64 " R_(i) ", " R_(i) ", %16, %18"
+#define T_MAXS(i) "v_max_f32_e64 " R_(i) ", " R_(i) ", %17"
+#define T_ADDS(i) "v_add_f32_e64 " R_(i) ", " R_(i) ", %17"
+#define T_CMPCND(i) "v_cmp_lt_f32_e64 s[40:41], " R_(i) ", %16\n\tv_cndmask_b32_e64 " R_(i) ", " R_(i) ", %16, s[40:41]"
 
-constexpr int kOps = 27;
+constexpr int kOps = 31;
 static const char* kOpNames[kOps] = {"v_maximum3_f32", "v_minimum3_f32", "v_max3_f32", "v_med3_f32", "v_max_f32_e32",
                                      "v_max_f32_e64", "v_max_f32_dpp", "v_fma_f32", "v_add_f32", "v_bfi_b32",
                                      "v_pk_max_f16", "v_cvt_f32_u32", "v_bfe_u32", "v_and_or_b32", "v_cndmask_b32",
                                      "v_mul_f32", "v_mov_b32", "v_xor_b32", "v_sub_f32", "v_perm_b32",
                                      "v_max_i32", "v_min_u32", "v_max3_i32", "v_med3_i32", "v_add_u32",
-                                     "v_pk_max_i16", "v_min_f32_e32"};
+                                     "v_pk_max_i16", "v_min_f32_e32", "v_cndmask_b32_e64_sgpr_mask",
+                                     "v_max_f32_e64_sgpr_operand", "v_add_f32_e64_sgpr_operand",
+                                     "v_cmp_lt_f32+v_cndmask (pair, per 2 instr)"};
 
 template <int OP>
 __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
@@ -67,6 +73,9 @@ __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
 #pragma unroll
   for (int q = 0; q < 16; ++q) r[q] = (float)threadIdx.x * 1e-3f + q;
   const float k = 0.5f + (float)(threadIdx.x & 1);
+  // wave-uniform operands for the SGPR-operand forms
+  const float ks = __builtin_amdgcn_readfirstlane(__float_as_int(k)) == 0 ? 1.0f : 0.75f;
+  const unsigned long long km = (unsigned long long)__builtin_amdgcn_read_exec() & 0x5555555555555555ull;
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int i = 0; i < iters; ++i) {
     if constexpr (OP == 0) PR_ASM16(T_MAXIMUM3);
@@ -95,7 +104,11 @@ __global__ void valu_kernel(float* out, unsigned long long* clk, int iters) {
     else if constexpr (OP == 23) PR_ASM16(T_MED3I32);
     else if constexpr (OP == 24) PR_ASM16(T_ADDU32);
     else if constexpr (OP == 25) PR_ASM16(T_PKMAXI16);
-    else PR_ASM16(T_MINF32);
+    else if constexpr (OP == 26) PR_ASM16(T_MINF32);
+    else if constexpr (OP == 27) PR_ASM16(T_CND64);
+    else if constexpr (OP == 28) PR_ASM16(T_MAXS);
+    else if constexpr (OP == 29) PR_ASM16(T_ADDS);
+    else PR_ASM16(T_CMPCND);
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   float z = 0.f;
@@ -176,5 +189,9 @@ int main(int argc, char** argv) {
   if (24 >= first) run_op<24>(cus, out, clk, iters, e0, e1);
   if (25 >= first) run_op<25>(cus, out, clk, iters, e0, e1);
   if (26 >= first) run_op<26>(cus, out, clk, iters, e0, e1);
+  if (27 >= first) run_op<27>(cus, out, clk, iters, e0, e1);
+  if (28 >= first) run_op<28>(cus, out, clk, iters, e0, e1);
+  if (29 >= first) run_op<29>(cus, out, clk, iters, e0, e1);
+  if (30 >= first) run_op<30>(cus, out, clk, iters, e0, e1);
   return 0;
 }
