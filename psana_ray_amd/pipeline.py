@@ -40,13 +40,16 @@ class ProducerPipeline:
                  chunk: int = 32, n_raw_buffers: int = 6, acquire_timeout_s: float = 1.0,
                  log_every: int = 0, copy_workgroups: int = 32, gpu_timing: bool = False,
                  compute_streams: Optional[int] = None, stream_kind: Optional[str] = None,
-                 mask: Optional[np.ndarray] = None, n_upload_buffers: int = 3):
+                 mask: Optional[np.ndarray] = None, n_upload_buffers: int = 3, gap_fill: Optional[bool] = None):
         """copy_workgroups: host->HBM staging by copy_h2d_kernel with that many workgroups (0 = the
         runtime's hipMemcpyAsync); gpu_timing: event-time each chunk's copy and calibration;
         compute_streams: chunks alternate over that many HIP streams (native engine), so one chunk's
         calibration fills the CUs its predecessor's tail leaves idle; stream_kind: their
         hardware-queue placement (config.STREAM_KINDS).  None: config.PRODUCER_STREAMS /
         PRODUCER_STREAM_KIND for the source (raw frames already in HBM or staged).
+
+        gap_fill: image mode, zero the panel gaps of every frame (None: only when the ring was not
+        zero-filled at creation -- ``FrameRing.zero_filled`` -- since a zeroed ring's gaps stay 0).
 
         Sources whose frames arrive calibrated (psana_wrapper without raw access): ``mask`` (truthy
         keeps, producer.py:92-95) is applied on the device after the upload; frames move in
@@ -92,6 +95,7 @@ class ProducerPipeline:
         self._inflight = collections.deque()
         self._reuses = hasattr(source, "n_staging")
         self.engine = None
+        self.gap_fill = None        # image mode, native engine: kernels zero the panel gaps per frame
         self.stream_config = None   # (compute streams, kind) of the native engine
         if use_engine:
             # native hot loop: no Python (and no GIL) per frame or per chunk
@@ -100,11 +104,19 @@ class ProducerPipeline:
             dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
             # gevt = event_rank + k * size; a panel-sharded source (source/shard.py) shards events
             # over rank GROUPS, while the headers keep this rank (its panel shard)
-            self.engine = C.ProducerEngine(ring.pool, ring.frame_bytes, dev_index,
-                                           calibrator.plan, self.chunk, n_raw_buffers,
-                                           int(getattr(source, "event_rank", rank)),
-                                           int(getattr(source, "size", 1)),
-                                           copy_workgroups=int(copy_workgroups), gpu_timing=bool(gpu_timing))
+            plan = calibrator.plan
+            n_gaps = plan.n_gap_runs
+            self.gap_fill = bool(n_gaps) and (not ring.zero_filled if gap_fill is None else bool(gap_fill))
+            if n_gaps and not self.gap_fill:
+                plan.n_gap_runs = 0   # the engine keeps its own copy of the plan
+            try:
+                self.engine = C.ProducerEngine(ring.pool, ring.frame_bytes, dev_index,
+                                               plan, self.chunk, n_raw_buffers,
+                                               int(getattr(source, "event_rank", rank)),
+                                               int(getattr(source, "size", 1)),
+                                               copy_workgroups=int(copy_workgroups), gpu_timing=bool(gpu_timing))
+            finally:
+                plan.n_gap_runs = n_gaps
             self.engine.set_header_rank(int(rank))
             if zero_copy is not None:
                 ptrs, pe = zero_copy

@@ -87,6 +87,15 @@ class FrameRing:
                 self._buffers.append(buf)
                 t = torch.from_dlpack(buf).view(dtype).view(k, *self.frame_shape)
                 self.segments.append((t, first, k))
+        # HBM rings start zeroed: slots only ever receive whole frames of the session's shape, so
+        # pixels no kernel writes (the panel gaps of an assembled image) stay 0 in every slot and the
+        # producer engine skips their per-frame fill (``zero_filled``; ProducerPipeline)
+        self.zero_filled = False
+        if self.device.type == "cuda":
+            for t, _, _ in self.segments:
+                t.view(torch.uint8).zero_()
+            torch.cuda.synchronize(self.device)
+            self.zero_filled = True
         self.views = [v for t, _, _ in self.segments for v in t.unbind(0)]
         self.slot_ptrs = [int(v.data_ptr()) for v in self.views]
         self.pool = C.SlotPool(producer_slots, consumer_slots, dev_index)

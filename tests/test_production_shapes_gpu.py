@@ -188,3 +188,47 @@ def test_peakfind_hit_rich_past_max_peaks(cuda_device, radius):
         exp = _sorted_peaks(ref[sel])
         assert torch.equal(got[:, :4], exp[:, :4])
         assert torch.allclose(got[:, 4:], exp[:, 4:], rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("gap_fill", [None, True])
+def test_image_pipeline_zero_filled_ring_exact(cuda_device, gap_fill):
+    """Image mode through the producer engine at chunk 64 with a small ring (every slot reused
+    several times): the ring starts zero-filled, so by default the kernels skip the per-frame gap
+    fill (the gaps of every slot stay 0); with and without the skip every assembled frame is
+    bit-exact against the golden assembly, gaps included."""
+    from psana_ray_amd.pipeline import ProducerPipeline
+    from psana_ray_amd.queue import EndOfStream, FrameRing, QueueEndpoint
+    from psana_ray_amd.source import SyntheticRun
+
+    n_events, chunk = 320, 64
+    src = SyntheticRun("synthetic", 5, "epix10k2M", n_events=n_events, pool_frames=8, pinned=True,
+                       gen_device="cuda")
+    cal = Calibrator(src.consts, cuda_device, Mode.image, common_mode=CommonModeParams())
+    assert cal.plan.n_gap_runs > 0
+    ring = FrameRing(cal.out_shape, cal.out_dtype, cuda_device, 2 * chunk, 32)
+    assert ring.zero_filled
+    ep = QueueEndpoint(ring)
+    prod = ProducerPipeline(src, cal, ep, chunk=chunk, gap_fill=gap_fill)
+    assert prod.gap_fill == (gap_fill is True)
+    assert cal.plan.n_gap_runs > 0                  # the calibrator's own plan is untouched
+    t = threading.Thread(target=prod.run)
+    t.start()
+    geo = cal.geometry
+    ref = reference.calibrate_reference(torch.from_numpy(src.pool.astype(np.int32)).to(cuda_device), src.consts,
+                                        None, cal.cm)
+    ref = reference.assemble_reference(ref, geo.rows, geo.cols, geo.image_shape, None)
+    seen = []
+    while True:
+        try:
+            it = ep.get(timeout=0.5)
+        except EndOfStream:
+            break
+        if it is None:
+            continue
+        with it:
+            got = it.data.clone()
+        torch.cuda.synchronize()
+        _bitwise(got.view(-1), ref[it.idx % 8].reshape(-1), f"image frame {it.idx}")
+        seen.append(it.idx)
+    t.join()
+    assert seen == list(range(n_events))
