@@ -5,7 +5,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 export PYTHONPATH=$R
-O=$R/gpurun_out/r4_checkpoint
+O=$R/gpurun_out/${OUT:-r4_checkpoint}
 mkdir -p $O
 timeout -k 10 900 python3 ${PYFLAGS:-} -u -m pytest $R/tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -1 $O/tests.log
 [ $rc -eq 0 ] || { grep -n -A60 "Fatal Python error" $O/tests.log | head -150; exit $rc; }
