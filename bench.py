@@ -37,11 +37,13 @@ METRIC = "detector frames/sec (whole node) through SharedQueue, epix10k2M at 1/2
 
 
 def parse(argv=None):
+    from psana_ray_amd.config import CONSUMER_BATCH
+
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=32, help="frames per rank per step (consumer batch)")
+    ap.add_argument("--batch", type=int, default=CONSUMER_BATCH, help="frames per rank per step (consumer batch)")
     ap.add_argument("--detector", default="epix10k2M")
     ap.add_argument("--mode", default="calib", choices=["calib", "image", "raw"])
     ap.add_argument("--common-mode", default="auto",

@@ -49,11 +49,18 @@ STREAM_KINDS = {"shared": 0, "dedicated": 1, "high": 2}
 # chunk's calibration fills the CUs its predecessor's tail leaves, and the peak finder no longer
 # queues behind it); host-staged (PCIe-bound) -> one ordinary stream (13,064-13,069 vs
 # 12,852-12,858 with 3: concurrent calibrations delay the staging copy kernel).
-PRODUCER_STREAMS = {"device": 3, "staged": 1}
+# Round 4 (profiles/r4/sweep3/, interleaved, 4 rounds): 4 streams with 64-frame consumer batches
+# 151.2-153.9k vs 142.9-144.7k for 3 streams / 32 (4 streams alone 145.8-147.9k, batch 64 alone
+# 144.8-147.6k); image mode 128.8-129.0k vs 124.6-125.1k (sweep4/); 4 is the engine's maximum.
+PRODUCER_STREAMS = {"device": 4, "staged": 1}
 PRODUCER_STREAM_KIND = {"device": "dedicated", "staged": "shared"}
 # Consumer: the peak finder's two alternating streams, each on its own hardware queue (ordinary
 # streams landed both on ONE queue: rocprofv3 Queue_Id, profiles/r3/streams2/)
 CONSUMER_STREAM_KIND = "dedicated"
+# Frames per peak-finder launch of the in-process consumer (bench.py --batch, the producer CLI's
+# co-consumer): one full launch (kernels.MAX_FRAMES) -- half as many launch ramps and drains per
+# frame as 32 (host-staged headline unchanged: 13.01-13.04k either way, PCIe-bound)
+CONSUMER_BATCH = 64
 # Queue fabric (csrc/fabric.h): how a producer moves frames into OTHER processes' GPU rings.
 # "kernel": every frame of one fabric pass, to all its consumers, in ONE copy_runs_kernel launch on
 # a stream with its own hardware queue, bounded to FABRIC_COPY_WORKGROUPS workgroups; "runtime":

@@ -327,7 +327,7 @@ def main(argv=None) -> int:
         registry.register("producer", pipe.metrics)
         registry.register("queue", ep.metrics)
         if co_consumer:
-            cons = PeakFinderConsumer(ep, frame_shape, PeakFinderParams())
+            cons = PeakFinderConsumer(ep, frame_shape, PeakFinderParams(), batch=CONSUMER_BATCH)
             registry.register("consumer", cons.metrics)
 
             def consume():
