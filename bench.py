@@ -50,6 +50,8 @@ def parse(argv=None):
                     help="auto (the producer CLI's default: on for epix10ka) | off | default | "
                          "flags,thr,maxcorr,npix_min[,bank]")
     ap.add_argument("--consumer", default="peakfind", choices=["peakfind", "none"])
+    ap.add_argument("--consumer-streams", type=int, default=None,
+                    help="peak-finder consumer streams (default config.CONSUMER_STREAMS)")
     ap.add_argument("--gap-fill", action="store_true",
                     help="image mode: zero the panel gaps of every frame even in a zero-filled ring (A/B)")
     ap.add_argument("--route", default="balanced", choices=["balanced", "local_first", "spread", "remote_only"],
@@ -267,6 +269,8 @@ def main(argv=None):
     if args.stream_kind is not None:
         cs_kw["stream_kind"] = args.stream_kind
     sk_kw = {} if args.consumer_stream_kind is None else {"stream_kind": args.consumer_stream_kind}
+    if args.consumer_streams is not None:
+        sk_kw["streams"] = args.consumer_streams
     if args.gap_fill:
         cs_kw["gap_fill"] = True
     prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk, **cs_kw) if is_prod else None

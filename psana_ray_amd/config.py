@@ -57,6 +57,7 @@ PRODUCER_STREAM_KIND = {"device": "dedicated", "staged": "shared"}
 # Consumer: the peak finder's two alternating streams, each on its own hardware queue (ordinary
 # streams landed both on ONE queue: rocprofv3 Queue_Id, profiles/r3/streams2/)
 CONSUMER_STREAM_KIND = "dedicated"
+CONSUMER_STREAMS = 2
 # Frames per peak-finder launch of the in-process consumer (bench.py --batch, the producer CLI's
 # co-consumer): one full launch (kernels.MAX_FRAMES) -- half as many launch ramps and drains per
 # frame as 32 (host-staged headline unchanged: 13.01-13.04k either way, PCIe-bound)

@@ -25,7 +25,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from .config import (CONSUMER_STREAM_KIND, PRODUCER_STREAM_KIND, PRODUCER_STREAMS, STREAM_KINDS,
+from .config import (CONSUMER_STREAM_KIND, CONSUMER_STREAMS, PRODUCER_STREAM_KIND, PRODUCER_STREAMS, STREAM_KINDS,
                      PeakFinderParams)
 from .models.calibrator import Calibrator
 from .ops import _ext, kernels
@@ -443,7 +443,8 @@ class PeakFinderConsumer:
     its stream of reads) overlaps the next launch's streaming reads instead of idling HBM."""
 
     def __init__(self, endpoint: QueueEndpoint, frame_shape, params: Optional[PeakFinderParams] = None,
-                 batch: int = 16, keep_results: bool = False, stream_kind: str = CONSUMER_STREAM_KIND):
+                 batch: int = 16, keep_results: bool = False, stream_kind: str = CONSUMER_STREAM_KIND,
+                 streams: int = CONSUMER_STREAMS):
         self.ep = endpoint
         self.params = params or PeakFinderParams()
         self.batch = min(batch, kernels.MAX_FRAMES)
@@ -455,10 +456,11 @@ class PeakFinderConsumer:
         self.keep_results = keep_results
         self.results = []
         if self.gpu:
-            self.streams = _make_streams(self.device, 2, stream_kind, owner=self)
+            self.streams = _make_streams(self.device, int(streams), stream_kind, owner=self)
             self.stream = self.streams[0]
             B = self.batch
-            self._nbuf = 4   # even: buffer k % 4 is reused by launch k + 4, on the same stream as k
+            # buffer k % nbuf is reused by launch k + nbuf, on the same stream as k
+            self._nbuf = 2 * len(self.streams)
             self.peaks = torch.empty((self._nbuf, B, self.params.max_peaks, 8), dtype=torch.float32, device=self.device)
             # counts [B] int32 and summary [B, 2] f32 of a batch share one row; the peak finder
             # writes them whole from its self-resetting scratch (no per-batch fill)

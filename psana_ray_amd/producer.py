@@ -26,7 +26,8 @@ from typing import Optional
 
 import numpy as np
 
-from .config import (BACKOFF_BASE_S, BACKOFF_JITTER_S, BACKOFF_MAX_S, DEFAULT_LOG_LEVEL, DEFAULT_NUM_CONSUMERS,
+from .config import (BACKOFF_BASE_S, BACKOFF_JITTER_S, BACKOFF_MAX_S, CONSUMER_BATCH, DEFAULT_LOG_LEVEL,
+                     DEFAULT_NUM_CONSUMERS,
                      DEFAULT_QUEUE_NAME, DEFAULT_QUEUE_SIZE, DEFAULT_RAY_ADDRESS, DEFAULT_RAY_NAMESPACE, LOG_LEVELS,
                      QUEUE_LOOKUP_DELAY_S, QUEUE_LOOKUP_RETRIES, CommonModeParams, PeakFinderParams,
                      resolve_common_mode)
