@@ -144,7 +144,7 @@ ProducerEngine::~ProducerEngine() {
 
 void ProducerEngine::set_compute_streams(int n, int kind) {
   check(!running_.load() && !thread_.joinable(), "ProducerEngine: set_compute_streams before start");
-  check(n >= 1 && n <= 4, "ProducerEngine: compute streams must be 1..4");
+  check(n >= 1 && n <= 8, "ProducerEngine: compute streams must be 1..8");
   {
     std::lock_guard<std::mutex> lk(done_mu_);
     check(!origin_recorded_, "ProducerEngine: set_compute_streams after the first start");

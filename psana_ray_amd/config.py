@@ -51,7 +51,8 @@ STREAM_KINDS = {"shared": 0, "dedicated": 1, "high": 2}
 # 12,852-12,858 with 3: concurrent calibrations delay the staging copy kernel).
 # Round 4 (profiles/r4/sweep3/, interleaved, 4 rounds): 4 streams with 64-frame consumer batches
 # 151.2-153.9k vs 142.9-144.7k for 3 streams / 32 (4 streams alone 145.8-147.9k, batch 64 alone
-# 144.8-147.6k); image mode 128.8-129.0k vs 124.6-125.1k (sweep4/); 4 is the engine's maximum.
+# 144.8-147.6k); image mode 128.8-129.0k vs 124.6-125.1k (sweep4/).  5 streams 152.3-153.2k vs
+# 151.1-154.1k for 4, 6 streams 146.8-148.4k (sweep6/).
 PRODUCER_STREAMS = {"device": 4, "staged": 1}
 PRODUCER_STREAM_KIND = {"device": "dedicated", "staged": "shared"}
 # Consumer: the peak finder's two alternating streams, each on its own hardware queue (ordinary
