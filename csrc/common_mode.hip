@@ -430,6 +430,40 @@ __device__ __forceinline__ void load8(const float* __restrict__ t, int64_t npix,
   }
 }
 
+// PR_CM_OFF32: the production kernel's per-item loads address a per-frame uniform global base (SGPR)
+// plus a 32-bit element offset within the tile, instead of a 64-bit per-item pointer (64-bit VALU
+// adds per load; generic-pointer flat loads for the tables).  Same-box A/B (profiles/r4/off32/):
+// kernel 5.39-5.43 vs 5.48-5.50 us/frame (flags 0: 4.05-4.07 vs 4.15-4.17), 120 -> 109 VGPRs,
+// device-resident pipeline 151.0-153.8k vs 149.2-151.7k.
+#ifndef PR_CM_OFF32
+#define PR_CM_OFF32 1
+#endif
+// tables[k] = base of candidate table k at the tile origin (uniform); o = element offset in the tile
+template <int NT>
+__device__ __forceinline__ void load8o(const PR_GLOBAL float* const (&tb)[NT], uint32_t o, uint32_t need,
+                                       float (&a)[NT][8], int k0 = 0) {
+#pragma unroll
+  for (int k = k0; k < NT; ++k) {
+    f32x4_t u, w;
+    if ((need >> k) & 1u) {
+      u = *reinterpret_cast<const PR_GLOBAL f32x4_t*>(tb[k] + o);
+      w = *reinterpret_cast<const PR_GLOBAL f32x4_t*>(tb[k] + o + 4);
+    } else {
+      asm("" : "=v"(u));
+      asm("" : "=v"(w));
+    }
+    a[k][0] = u.x; a[k][1] = u.y; a[k][2] = u.z; a[k][3] = u.w;
+    a[k][4] = w.x; a[k][5] = w.y; a[k][6] = w.z; a[k][7] = w.w;
+  }
+}
+template <int NT>
+__device__ __forceinline__ uint32_t load_planes_o(const PR_GLOBAL uint8_t* planes_tile, uint32_t o) {
+  const uint32_t g = o >> 3;   // o is a multiple of 8 (8-pixel groups, 8-aligned tiles and rows)
+  if constexpr (NT == 1) return planes_tile[g];
+  else if constexpr (NT == 2) return *reinterpret_cast<const PR_GLOBAL uint16_t*>(planes_tile + 2 * g);
+  else return *reinterpret_cast<const PR_GLOBAL uint32_t*>(planes_tile + 4 * g);
+}
+
 template <int NT>
 __device__ __forceinline__ uint32_t load_planes(const uint8_t* __restrict__ planes, int64_t pix) {
   const int64_t g = pix >> 3;
@@ -948,15 +982,30 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
   constexpr int C8 = TC / 8;
   uint32_t ep[NI];
   float pa0[NI][1][8];
+#if PR_CM_OFF32
+  // uniform (SGPR) bases at the tile origin; per item one 32-bit offset
+  const PR_GLOBAL uint16_t* raw_t = raw + base;
+  const PR_GLOBAL uint8_t* pl_t = (const PR_GLOBAL uint8_t*)planes + CmLayout<NT>::kPlaneBytes * (base >> 3);
+  const PR_GLOBAL float* ped_t[NT];
+#pragma unroll
+  for (int k = 0; k < NT; ++k) ped_t[k] = (const PR_GLOBAL float*)ped + k * tg.npix + base;
+#endif
 #pragma unroll
   for (int u = 0; u < NI; ++u) {
     const int i = tid + u * BLOCK;
     if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
       const int r = i / C8, c = (i % C8) * 8;
+#if PR_CM_OFF32
+      const uint32_t o = (uint32_t)(r * tg.panel_cols + c);
+      if constexpr (!RAW_IN) rw[u] = ld_raw_u4((const PR_GLOBAL uint4*)(raw_t + o));
+      ep[u] = load_planes_o<NT>(pl_t, o);
+      load8o<1>(reinterpret_cast<const PR_GLOBAL float* const(&)[1]>(ped_t), o, 1u, pa0[u]);
+#else
       const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
       if constexpr (!RAW_IN) rw[u] = ld_raw_u4((const PR_GLOBAL uint4*)(raw + pix));
       ep[u] = load_planes<NT>(planes, pix);
       load8<1>(ped, tg.npix, pix, 1u, pa0[u]);
+#endif
     }
   }
 #pragma unroll
@@ -971,8 +1020,13 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
         float pa[NT][8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) pa[0][j] = pa0[u][0][j];
-        if constexpr (NT > 1)
+        if constexpr (NT > 1) {
+#if PR_CM_OFF32
+          load8o<NT>(ped_t, (uint32_t)(r * tg.panel_cols + c), need_from_raw<NT>(rw[u]), pa, 1);
+#else
           load8<NT>(ped, tg.npix, base + (int64_t)r * tg.panel_cols + c, need_from_raw<NT>(rw[u]), pa, 1);
+#endif
+        }
         cm_decode8<KIND, NT>(rw[u], ep[u], pa, v, el, cb);
       }
       float x[8];
@@ -1261,13 +1315,24 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
       // (the first gain table of every item up front; the switched-gain tables are rare and are
       // loaded per item, which keeps the production kernel within 128 VGPRs)
       uint32_t cbs[NI], slots[NI];
+#if PR_CM_OFF32
+      const PR_GLOBAL float* gf_t[NT];
+#pragma unroll
+      for (int k = 0; k < NT; ++k) gf_t[k] = (const PR_GLOBAL float*)gfp + k * tg.npix + tb;
+#endif
 #pragma unroll
       for (int u = 0; u < NI; ++u) {
         const int i = tid + u * BLOCK;
         if ((u + 1) * BLOCK <= NITEMS || i < NITEMS) {
           const int r = i / C8, k = i % C8, c = k * 8;
           cm_get_meta<NT>(reinterpret_cast<const uint8_t*>(tile + r * P + C), C, k, cbs[u], slots[u]);
+#if PR_CM_OFF32
+          if constexpr (!PR_CM_GPRE)
+            load8o<1>(reinterpret_cast<const PR_GLOBAL float* const(&)[1]>(gf_t), (uint32_t)(r * tg.panel_cols + c), 1u,
+                      g0[u]);
+#else
           if constexpr (!PR_CM_GPRE) load8<1>(gfp, tg.npix, tb + (int64_t)r * tg.panel_cols + c, 1u, g0[u]);
+#endif
         }
       }
 #pragma unroll
@@ -1279,7 +1344,11 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
           float ga[NT][8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) ga[0][j] = g0[u][0][j];
+#if PR_CM_OFF32
+          if constexpr (NT > 1) load8o<NT>(gf_t, (uint32_t)(r * tg.panel_cols + c), cm_need<NT>(cbs[u]), ga, 1);
+#else
           if constexpr (NT > 1) load8<NT>(gfp, tg.npix, pix, cm_need<NT>(cbs[u]), ga, 1);
+#endif
           float o[8];
           cm_out8<KIND, NT>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, pedp, tg.npix, pix, o);
           cm_put8(tile + r * P + c, o);
