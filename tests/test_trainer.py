@@ -141,7 +141,7 @@ def test_trainer_gpu_overfits_ring_batch(native, cuda_device):
     batch = collate_items(items, torch.float32)
     # miopen=False: MIOpen JIT-compiles every convolution shape on a fresh node (~80 s for this
     # net); the HIP gather / peak-finder path under test is the same
-    torch.manual_seed(0)   # random init: the 25-step loss drop ranged 0.64-0.5 x unseeded
+    torch.manual_seed(0)   # random init: unseeded, 25 steps once ended at 0.74 x the first loss
     tr = OnlinePeakNetTrainer(cal.out_shape, cuda_device, width=8, lr=3e-3, miopen=False)
     first = tr.step(batch.data)
     for _ in range(40):
