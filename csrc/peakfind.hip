@@ -219,18 +219,36 @@ __global__ __launch_bounds__(256) PR_PF_WAVES_ATTR void peakfind_range_kernel(co
                               : nullptr;
   const int cap = kPfCandCap + (spill != nullptr ? kPfSpillCap : 0);
   f32x4_t v[K];
+  #ifndef PR_PF_FASTLOAD
+#define PR_PF_FASTLOAD 1
+#endif
+// chunk g's float4s: a uniform base (SGPR) + a 32-bit lane offset; interior chunks (all but a
+  // frame's last) load without per-load bounds checks (each cost a 64-bit compare, an exec-mask
+  // branch and four NaN moves: ~1/3 of the stream loop's VALU)
   auto load = [&](int64_t g) {
     const int f = (int)(g / ncpf);
-    const PR_GLOBAL float* img = gin<float>(fp.in[f]);
-    const int64_t q0 = (g - (int64_t)f * ncpf) * 256 * K + threadIdx.x;
+    const int64_t c0 = (g - (int64_t)f * ncpf) * 256 * K;   // first float4 of the chunk (uniform)
+    const PR_GLOBAL f32x4_t* cp = reinterpret_cast<const PR_GLOBAL f32x4_t*>(gin<float>(fp.in[f])) + c0;
+    const uint32_t t = threadIdx.x;
+    if (PR_PF_FASTLOAD && c0 + 256 * K <= n4) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int64_t q = q0 + 256 * k;
+      for (int k = 0; k < K; ++k) {
 #if PR_PF_NT_LOAD
-      v[k] = q < n4 ? ld_nt_f4((const PR_GLOBAL f32x4_t*)(img + 4 * q)) : f32x4_t{NaN, NaN, NaN, NaN};
+        v[k] = ld_nt_f4(cp + t + 256 * k);
 #else
-      v[k] = q < n4 ? *(const PR_GLOBAL f32x4_t*)(img + 4 * q) : f32x4_t{NaN, NaN, NaN, NaN};
+        v[k] = cp[t + 256 * k];
 #endif
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const bool in = c0 + t + 256 * k < n4;
+#if PR_PF_NT_LOAD
+        v[k] = in ? ld_nt_f4(cp + t + 256 * k) : f32x4_t{NaN, NaN, NaN, NaN};
+#else
+        v[k] = in ? cp[t + 256 * k] : f32x4_t{NaN, NaN, NaN, NaN};
+#endif
+      }
     }
   };
   // A candidate's (2H+1)^2 neighbourhood, H = RAD + 2, as THREE aligned 16-B loads per row (the
