@@ -546,11 +546,23 @@ __device__ __forceinline__ void st_out4(PR_GLOBAL float4* p, const float4 v) {
 __device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C, PR_GLOBAL float* out, int64_t base,
                                          int panel_cols) {
   const int C4 = C >> 2;
+#ifndef PR_CM_FLUSH32
+#define PR_CM_FLUSH32 PR_CM_OFF32
+#endif
+#if PR_CM_FLUSH32
+  PR_GLOBAL float* const ob = out + base;   // uniform tile origin; 32-bit offsets per store
+  for (int e = threadIdx.x; e < R * C4; e += blockDim.x) {
+    const int r = e / C4, j = e - r * C4;
+    const float4 v = *reinterpret_cast<const float4*>(tile + r * P + 4 * j);
+    st_out4<1>((PR_GLOBAL float4*)(ob + (uint32_t)(r * panel_cols + 4 * j)), v);
+  }
+#else
   for (int e = threadIdx.x; e < R * C4; e += blockDim.x) {
     const int r = e / C4, j = e - r * C4;
     const float4 v = *reinterpret_cast<const float4*>(tile + r * P + 4 * j);
     st_out4<1>((PR_GLOBAL float4*)(out + base + (int64_t)r * panel_cols + 4 * j), v);
   }
+#endif
 }
 
 // Image layout (fused K-05): every panel sits in the image by an integer rotation + translation,
