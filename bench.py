@@ -43,7 +43,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=CONSUMER_BATCH, help="frames per rank per step (consumer batch)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help=f"frames per rank per step (consumer batch; default {CONSUMER_BATCH}, 32 when ranks share a GPU)")
     ap.add_argument("--detector", default="epix10k2M")
     ap.add_argument("--mode", default="calib", choices=["calib", "image", "raw"])
     ap.add_argument("--common-mode", default="auto",
@@ -153,7 +154,7 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
-    from psana_ray_amd.config import CONSUMER_STREAM_KIND, PeakFinderParams
+    from psana_ray_amd.config import CONSUMER_BATCH, CONSUMER_STREAM_KIND, PeakFinderParams
     from psana_ray_amd.models import Mode
     from psana_ray_amd.producer import build_calibrator
     from psana_ray_amd.parallel.launch import bind_numa_to_device, detect
@@ -182,6 +183,15 @@ def main(argv=None):
         torch.cuda.set_device(device)
         numa = bind_numa_to_device(device)
     gpu = device.type == "cuda"
+    # ranks sharing one GPU (rehearsals of an N-rank launch on fewer GPUs): every process's
+    # dedicated streams are hardware queues of that one GPU, so the pipeline takes the round-3
+    # shape there -- 3 producer compute streams, 32-frame consumer batches.  2 ranks on one GPU,
+    # device-resident: 142.8k fr/s with it, 83.6k with the 1-rank-per-GPU shape (4 streams, 64)
+    # (profiles/r4/n2final/)
+    lws = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    gpu_share = max(1, -(-lws // max(1, torch.cuda.device_count()))) if gpu else 1
+    if args.batch is None:
+        args.batch = CONSUMER_BATCH if gpu_share == 1 else 32
 
     coord = None
     store = None
@@ -273,6 +283,8 @@ def main(argv=None):
         sk_kw["streams"] = args.consumer_streams
     if args.gap_fill:
         cs_kw["gap_fill"] = True
+    if gpu_share > 1 and args.source == "device" and args.compute_streams is None:
+        cs_kw["compute_streams"] = 3
     prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk, **cs_kw) if is_prod else None
     consumer = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=args.batch, **sk_kw) \
         if args.consumer == "peakfind" else None
@@ -513,6 +525,7 @@ def main(argv=None):
             "queue_size": args.queue_size,
             "source": args.source,
             "chunk": args.chunk,
+            "ranks_per_gpu": gpu_share,
             "producer_ranks": n_prod,
             "queue": "local (single process)" if sess is None else "elastic fabric session",
         },
