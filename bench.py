@@ -93,7 +93,7 @@ def parse(argv=None):
     ap.add_argument("--fabric-copy-stream", default=None, choices=["shared", "dedicated", "high"],
                     help="hardware-queue placement of the fabric copy stream (default config.FABRIC_COPY_STREAM)")
     ap.add_argument("--fabric-copy-wgs", type=int, default=None,
-                    help="workgroups of the fabric copy kernel (default config.FABRIC_COPY_WORKGROUPS)")
+                    help="fabric copy kernel workgroups per peer GPU link (default config.FABRIC_COPY_WORKGROUPS)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: protocol rehearsal with gloo and the golden models (tests only; not a benchmark)")
     return ap.parse_args(argv)

@@ -124,8 +124,54 @@ static void maybe_install_segv_trace() {
   sigaction(SIGSEGV, &sa, &g_prev_segv);
 }
 
+// Peer-access / link topology of every GPU this process sees (bench topology record):
+// {"n", "can_access"[i][j], "link_type"[i][j], "hops"[i][j]} (diagonal: -1)
+static py::dict device_topology() {
+  int n = 0;
+  py::dict d;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  py::list acc, typ, hop;
+  for (int i = 0; i < n; ++i) {
+    py::list ra, rt, rh;
+    for (int j = 0; j < n; ++j) {
+      int can = -1;
+      uint32_t lt = 0, hc = 0;
+      int t = -1, h = -1;
+      if (i != j) {
+        if (hipDeviceCanAccessPeer(&can, i, j) != hipSuccess) {
+          (void)hipGetLastError();
+          can = -1;
+        }
+        if (hipExtGetLinkTypeAndHopCount(i, j, &lt, &hc) == hipSuccess) {
+          t = (int)lt;
+          h = (int)hc;
+        } else {
+          (void)hipGetLastError();
+        }
+      }
+      ra.append(can);
+      rt.append(t);
+      rh.append(h);
+    }
+    acc.append(ra);
+    typ.append(rt);
+    hop.append(rh);
+  }
+  d["n"] = n;
+  d["can_access"] = acc;
+  d["link_type"] = typ;
+  d["hops"] = hop;
+  return d;
+}
+
 PYBIND11_MODULE(_C, m) {
   maybe_install_segv_trace();
+  m.def("device_topology", &device_topology,
+        "peer access (hipDeviceCanAccessPeer) and link type / hop count (hipExtGetLinkTypeAndHopCount) "
+        "between every pair of visible GPUs");
   m.def("install_segv_trace", &maybe_install_segv_trace);
   m.doc() = "psana_ray_amd native extension: gfx950 HIP kernels + host runtime";
   m.attr("MAX_FRAMES_PER_LAUNCH") = pr::kMaxFrames;
@@ -180,6 +226,12 @@ PYBIND11_MODULE(_C, m) {
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, int64_t nelem, bool bf16,
            uint64_t stream) { pr::launch_gather_frames(make_ptrs(in, out), (int)in.size(), nelem, bf16, stream); },
         py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("nelem"), py::arg("bf16"), py::arg("stream"));
+  m.def("mask_frames",
+        [](const std::vector<uint64_t>& frames, uint64_t zero, int64_t npix, uint64_t stream) {
+          pr::launch_mask_frames(make_ptrs(frames, frames), (int)frames.size(), zero, npix, stream);
+        },
+        py::arg("frame_ptrs"), py::arg("zero_mask"), py::arg("npix"), py::arg("stream"),
+        "in place: pixel i of every frame -> 0 where zero_mask[i] != 0 (u8), one launch for <= 64 frames");
   m.def("copy_runs",
         [](const std::vector<uint64_t>& src, const std::vector<uint64_t>& dst, const std::vector<int64_t>& bytes,
            int workgroups, uint64_t stream) {
@@ -338,7 +390,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("taken", &pr::LinkStatus::taken)
       .def_readonly("outstanding", &pr::LinkStatus::outstanding)
       .def_readonly("frames", &pr::LinkStatus::frames)
-      .def_readonly("consumer_device", &pr::LinkStatus::consumer_device);
+      .def_readonly("consumer_device", &pr::LinkStatus::consumer_device)
+      .def_readonly("kernel_copy", &pr::LinkStatus::kernel_copy)
+      .def_readonly("peer_access", &pr::LinkStatus::peer_access)
+      .def_readonly("link_type", &pr::LinkStatus::link_type)
+      .def_readonly("hops", &pr::LinkStatus::hops);
   py::class_<pr::QueueFabric>(m, "QueueFabric")
       .def(py::init<pr::SlotPool*, int64_t, int, bool, bool, int, int64_t>(), py::arg("pool"),
            py::arg("slot_bytes"), py::arg("device"), py::arg("is_producer"), py::arg("is_consumer"),
@@ -373,6 +429,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("copy_engine", &pr::QueueFabric::copy_engine)
       .def_property_readonly("copy_workgroups", &pr::QueueFabric::copy_workgroups)
       .def("copy_samples", &pr::QueueFabric::copy_samples)
+      .def_static("copy_grid_for", &pr::QueueFabric::copy_grid_for, py::arg("consumer_devices"), py::arg("device"),
+                  py::arg("per_peer"))
       .def("links", &pr::QueueFabric::links);
 
   py::class_<pr::PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())

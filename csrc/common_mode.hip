@@ -1191,12 +1191,13 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
       if ((i & 15) == 15) asm volatile("" ::: "memory");
     }
     asm volatile("" ::: "memory");
-    sort_regs<M>(x);
+    sort_regs3<M>(x);
     // level 1: merge-split with lane q^1, both lanes V-shaped
     float z[M];
 #pragma unroll
     for (int i = 0; i < M; ++i) z[i] = max_dpp<0xB1, false, true>(x[i], x[i]);
-    bitonic_merge_vpad<M>(z);
+    if constexpr (have_vmerge3<M>()) vmerge_regs3<M>(z);
+    else bitonic_merge_vpad<M>(z);
     asm volatile("" ::: "memory");
     // level 2: merge path with lane q^3 (lanes 1 and 3 hold the terms)
     float kh = INF, kl = INF;

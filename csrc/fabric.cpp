@@ -25,7 +25,7 @@ namespace pr {
 namespace {
 
 constexpr uint64_t kLinkMagic = 0x314B4E494C525350ull;  // "PSRLINK1"
-constexpr int32_t kLinkVersion = 3;
+constexpr int32_t kLinkVersion = 4;
 constexpr int32_t kNoticeReturned = 1;   // the grant comes back unused (producer finished / closing)
 constexpr int32_t kNoticeReclaimed = 2;  // a returned frame was copied out: its slot is free again
 constexpr int32_t kNoticeRejected = 4;   // a returned frame was refused (EOS posted): route it elsewhere
@@ -93,6 +93,7 @@ struct alignas(64) LinkSeg {
   alignas(64) std::atomic<uint64_t> taken;             // consumer: frames of this link it took (get)
   std::atomic<int64_t> consumer_ready;                 // consumer: frames ready to read in its whole shard
   std::atomic<uint32_t> consumer_self_fed;             // consumer: its own process produces (and feeds it)
+  std::atomic<uint32_t> consumer_published;            // consumer: the two above hold real values (first pass)
   std::atomic<uint32_t> returns_final;                 // consumer (closing): no return will follow
   std::atomic<uint32_t> producer_seen_closed;          // producer: no frame notice will follow
   alignas(64) std::atomic<uint64_t> r_head;            // consumer -> producer: returned frames
@@ -218,6 +219,9 @@ struct QueueFabric::Link {
   bool keeper = false;                // the consumer end is a queue keeper
   int consumer_device = -1;           // outgoing: GPU of the consumer ring (-1: host shared memory)
   bool ipc = false;                   // outgoing: the consumer ring is IPC-mapped HBM
+  bool kcopy = false;                 // outgoing: frames move by the copy kernel (kCopyKernel, 16-B frames)
+  int peer_access = -1;               // outgoing, cross-GPU: hipDeviceCanAccessPeer (-1: same GPU / host)
+  int link_type = -1, hops = -1;      // outgoing, cross-GPU: hipExtGetLinkTypeAndHopCount
   double t_added = 0, last_check = 0;
   int64_t frames = 0;
   // producer side (outgoing)
@@ -259,6 +263,10 @@ struct QueueFabric::Link {
     s.frames = frames;
     s.taken = outgoing ? (int64_t)taken_seen : (int64_t)taken;
     s.consumer_device = outgoing ? consumer_device : -1;
+    s.kernel_copy = outgoing && kcopy;
+    s.peer_access = outgoing ? peer_access : -1;
+    s.link_type = outgoing ? link_type : -1;
+    s.hops = outgoing ? hops : -1;
     return s;
   }
 };
@@ -631,6 +639,14 @@ bool QueueFabric::try_attach(Link& l, double now) {
         // the copy engine / blit kernels of THIS GPU write the consumer GPU's HBM over xGMI
         int can = 0;
         hip_check(hipDeviceCanAccessPeer(&can, device_, cdev), "hipDeviceCanAccessPeer");
+        l.peer_access = can;
+        uint32_t lt = 0, hc = 0;   // topology record (bench extra.links_rank0): 4 = xGMI, hops 1 = direct
+        if (hipExtGetLinkTypeAndHopCount(device_, cdev, &lt, &hc) == hipSuccess) {
+          l.link_type = (int)lt;
+          l.hops = (int)hc;
+        } else {
+          (void)hipGetLastError();
+        }
         check(can != 0, "GPU " + std::to_string(device_) + " has no peer access to GPU " + std::to_string(cdev) +
                             " (hipDeviceCanAccessPeer = 0)");
       }
@@ -658,9 +674,15 @@ bool QueueFabric::try_attach(Link& l, double now) {
   }
   l.ipc = s->kind == 1;
   l.consumer_device = l.ipc ? s->consumer_device : -1;
+  // the copy kernel moves 16-B words between 16-B aligned slots; a frame size that is not a multiple
+  // of 16 B (an image whose H * W is not a multiple of 4) or a misaligned ring takes the runtime
+  // engine on this link instead -- decided here, once, never after frames were handed to a copy
+  l.kcopy = device_ >= 0 && l.ipc && copy_engine_ == kCopyKernel && slot_bytes_ % 16 == 0;
+  for (int k = 0; l.kcopy && k < l.n; ++k) l.kcopy = l.remote[k] % 16 == 0;
+  for (uint64_t p : pool_->slot_ptrs()) l.kcopy = l.kcopy && p % 16 == 0;
   // a per-link copy stream only where the runtime copies: a host ring (pageable shared memory), or
   // the runtime engine; the kernel engine moves every link's frames on xstream_
-  if (device_ >= 0 && l.stream == nullptr && (!l.ipc || copy_engine_ == kCopyRuntime)) {
+  if (device_ >= 0 && l.stream == nullptr && !l.kcopy) {
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking), "hipStreamCreate (fabric link)");
   }
@@ -752,6 +774,7 @@ int64_t QueueFabric::consumer_pass(double now) {
       lp->seg->consumer_ready.store(ready_now, std::memory_order_relaxed);
       lp->seg->consumer_self_fed.store(self_fed, std::memory_order_relaxed);
       lp->seg->taken.store(lp->taken, std::memory_order_release);
+      lp->seg->consumer_published.store(1, std::memory_order_release);
     }
   // 1. notices: frames (-> READY), unused grants, answers to returned frames.  n_tail is stored only
   //    after the returns of this pass were posted (a closing consumer hands back every frame noticed
@@ -1244,7 +1267,9 @@ int64_t QueueFabric::producer_pass(double now) {
     std::vector<int> starving;
     if (policy == 0 && (local_credit <= 0 || pool_->n_ready() >= kFeedLocalReady))
       for (size_t i = 0; i < cands.size(); ++i)
-        if (!cands[i]->keeper && avail[i] > 0 &&
+        // (a link whose consumer has not published its demand yet -- every field still the zero of a
+        // fresh mailbox -- is not starving: a self-fed prosumer would look like one)
+        if (!cands[i]->keeper && avail[i] > 0 && cands[i]->seg->consumer_published.load(std::memory_order_acquire) != 0 &&
             cands[i]->seg->consumer_self_fed.load(std::memory_order_relaxed) == 0 &&
             cands[i]->seg->consumer_ready.load(std::memory_order_relaxed) == 0)
           starving.push_back((int)i);
@@ -1311,7 +1336,7 @@ int64_t QueueFabric::producer_pass(double now) {
       b.rslots.assign(l.grants.begin(), l.grants.begin() + n);
       l.grants.erase(l.grants.begin(), l.grants.begin() + n);
       b.t_issue = now;
-      if (device_ >= 0 && l.ipc && copy_engine_ == kCopyKernel) {
+      if (l.kcopy) {
         l.inflight += n;
         kbatches.push_back(std::move(b));
         work += n;
@@ -1418,12 +1443,31 @@ int64_t QueueFabric::producer_pass(double now) {
   return work;
 }
 
+int QueueFabric::copy_grid_for(const std::vector<int>& consumer_devices, int device, int per_peer) {
+  bool local = false;
+  std::vector<int> peers;
+  for (int d : consumer_devices) {
+    if (d == device) local = true;
+    else if (std::find(peers.begin(), peers.end(), d) == peers.end()) peers.push_back(d);
+  }
+  const int w = (local ? kLocalCopyWgs : 0) + per_peer * (int)peers.size();
+  return std::min(std::max(w, std::max(per_peer, 1)), kMaxCopyWgs);
+}
+
+int QueueFabric::copy_grid(const std::vector<Batch>& kb) const {
+  std::vector<int> devs;
+  devs.reserve(kb.size());
+  for (const Batch& b : kb) devs.push_back(b.link->consumer_device);
+  return copy_grid_for(devs, device_, copy_wgs_);
+}
+
 // Kernel engine: the frames of every link routed in this pass move in ONE copy_runs_kernel launch
 // on xstream_ (its own hardware queue), ordered after the frames' calibration by event waits on
 // that stream only.  Timing events bracket the copy itself, so each dispatch's device time is known.
 void QueueFabric::issue_copies(std::vector<Batch>& kb, double now) {
   trace::Range tr("fabric.copy_dispatch");
   if (xstream_ == nullptr) xstream_ = acquire_stream(device_, xstream_kind_);
+  check(slot_bytes_ % 16 == 0, "QueueFabric: frame size must be a multiple of 16 B for the copy kernel");
   std::vector<int> all;
   for (const Batch& b : kb) all.insert(all.end(), b.slots.begin(), b.slots.end());
   pool_->begin_send_batch(all, reinterpret_cast<uint64_t>(xstream_));   // xstream_ waits for their data
@@ -1433,17 +1477,15 @@ void QueueFabric::issue_copies(std::vector<Batch>& kb, double now) {
   g->t_issue = now;
   g->links = (int32_t)kb.size();
   hip_check(hipEventRecord(g->start, xstream_), "hipEventRecord (copy start)");
-  check(slot_bytes_ % 16 == 0, "QueueFabric: frame size must be a multiple of 16 B for the copy kernel");
   CopyRuns cr{};
   cr.n = 0;
   const uint64_t sb = (uint64_t)slot_bytes_;
   int launches = 0;
   // grid: a copy inside this GPU's HBM (a consumer process on the same GPU) is bound by HBM and
-  // takes up to kLocalCopyWgs workgroups; copies over xGMI are bound by the links (~150 GB/s each,
-  // a few dozen workgroups keep one busy), so copy_wgs_ leaves the CUs to the calibration
-  bool all_local = true;
-  for (const Batch& b : kb) all_local &= b.link->consumer_device == device_;
-  const int wgs = all_local ? std::max(copy_wgs_, kLocalCopyWgs) : copy_wgs_;
+  // takes kLocalCopyWgs workgroups; a copy over xGMI is bound by its point-to-point link (~150 GB/s),
+  // so the grid grows by copy_wgs_ workgroups per distinct peer GPU this dispatch writes (7 links
+  // out of an MI355X run concurrently) and leaves the other CUs to the calibration
+  const int wgs = copy_grid(kb);
   auto flush = [&] {
     if (cr.n == 0) return;
     launch_copy_runs(cr, wgs, reinterpret_cast<uint64_t>(xstream_));

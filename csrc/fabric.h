@@ -155,6 +155,10 @@ struct LinkStatus {
   int64_t frames = 0;        // frames moved over the link
   int64_t taken = 0;         // frames of this link the consumer took (get)
   int32_t consumer_device = -1;   // outgoing: the GPU of the consumer ring (-1 host)
+  bool kernel_copy = false;       // outgoing: frames move by the copy kernel (else the runtime's copies)
+  int32_t peer_access = -1;       // outgoing, other GPU: hipDeviceCanAccessPeer(this, consumer) (-1: n/a)
+  int32_t link_type = -1;         // outgoing, other GPU: hipExtGetLinkTypeAndHopCount type (4 = xGMI)
+  int32_t hops = -1;              //   and hop count (1 = a direct link)
 };
 
 class QueueFabric {
@@ -235,6 +239,11 @@ class QueueFabric {
   // device-resident, remote_only window: 512 -> 100.4k / 105.2k fr/s, 256 -> 100.1k / 101.1k,
   // 128 -> 93.6k / 94.4k; profiles/r4/fabric_pass3)
   static constexpr int kLocalCopyWgs = 512;
+  static constexpr int kMaxCopyWgs = 4096;
+  // workgroups of one copy dispatch writing the rings on `consumer_devices` from GPU `device`:
+  // kLocalCopyWgs if one of them is this GPU, plus `per_peer` per distinct other GPU (each is its
+  // own xGMI link), capped at kMaxCopyWgs
+  static int copy_grid_for(const std::vector<int>& consumer_devices, int device, int per_peer);
   static constexpr int kMinGrants = 4;      // grants kept at an idle producer (pipeline depth)
   static constexpr int kMaxDispatch = 64;   // produced frames routed per iteration
 
@@ -256,6 +265,7 @@ class QueueFabric {
   hipEvent_t take_event();
   hipEvent_t take_timed_event();
   void issue_copies(std::vector<Batch>& kb, double now);
+  int copy_grid(const std::vector<Batch>& kb) const;
   void finish_group(const std::shared_ptr<CopyGroup>& g);
 
   SlotPool* pool_;

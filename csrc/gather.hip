@@ -56,6 +56,44 @@ void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool 
   hip_check(hipGetLastError(), "gather_frames launch");
 }
 
+// Output mask of psana-calibrated frames (psana_wrapper fallback path, R-05: np.where(mask, data, 0),
+// psana_ray/producer.py:92-95) over a whole uploaded chunk in ONE launch, in place: frame f's pixel
+// i becomes 0 where zero[i] != 0.  Each lane owns 4 pixels (one 32-bit load of mask bytes, one
+// 16-B frame load) and stores only when one of them is masked; a frame size that is not a multiple
+// of 4 pixels leaves a scalar tail to lane 0 of the last workgroup.
+__global__ __launch_bounds__(256) void mask_frames_kernel(const FramePtrs fp, const uint8_t* __restrict__ zero,
+                                                          const int64_t npix) {
+  const int f = blockIdx.y;
+  PR_GLOBAL float* out = gout<float>(fp.out[f]);
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n4 = npix >> 2;
+  if (q < n4) {
+    const uint32_t m = reinterpret_cast<const uint32_t*>(zero)[q];
+    if (m != 0u) {
+      f32x4_t v = reinterpret_cast<PR_GLOBAL f32x4_t*>(out)[q];
+      if (m & 0x000000FFu) v.x = 0.0f;
+      if (m & 0x0000FF00u) v.y = 0.0f;
+      if (m & 0x00FF0000u) v.z = 0.0f;
+      if (m & 0xFF000000u) v.w = 0.0f;
+      reinterpret_cast<PR_GLOBAL f32x4_t*>(out)[q] = v;
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+    for (int64_t i = n4 * 4; i < npix; ++i)
+      if (zero[i]) out[i] = 0.0f;
+}
+
+void launch_mask_frames(const FramePtrs& fp, int nframes, uint64_t zero, int64_t npix, uint64_t stream) {
+  check(nframes >= 1 && nframes <= kMaxFrames, "mask_frames: 1..kMaxFrames frames per launch");
+  check(npix > 0 && zero != 0 && zero % 4 == 0, "mask_frames: needs a 4-B aligned byte mask of npix entries");
+  for (int i = 0; i < nframes; ++i) check(aligned16(fp.out[i]), "mask_frames: frames must be 16-B aligned");
+  const int64_t n4 = npix / 4;
+  const dim3 grid((unsigned)std::max<int64_t>(1, (n4 + 255) / 256), (unsigned)nframes);
+  hipLaunchKernelGGL(mask_frames_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), fp,
+                     reinterpret_cast<const uint8_t*>(zero), npix);
+  hip_check(hipGetLastError(), "mask_frames launch");
+}
+
 // Zero fill of fixed element runs in every output frame (the gaps between panels of an image
 // written by the fused common-mode kernel).  One wave per run (host splits runs to <= 1024
 // elements so the waves are balanced), consecutive lanes on consecutive elements.

@@ -30,6 +30,7 @@ void launch_xor_selftest(uint64_t out, uint64_t stream);
 // diagnostic builds only (-DPR_CM_STAMPS=1): per-wave phase stamps of the epix10k2M CM kernel
 void cm_set_stamp_buffer(uint64_t p);
 void launch_fill_runs(const FramePtrs& fp, int nframes, uint64_t runs, int n_runs, uint64_t stream);
+void launch_mask_frames(const FramePtrs& fp, int nframes, uint64_t zero, int64_t npix, uint64_t stream);
 void launch_gather_frames(const FramePtrs& fp, int nframes, int64_t nelem, bool bf16, uint64_t stream);
 // host (pinned / registered) -> HBM copy by a kernel; false = not applicable, use hipMemcpyAsync
 bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgroups, uint64_t stream);

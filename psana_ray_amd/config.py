@@ -65,13 +65,15 @@ CONSUMER_STREAMS = 2
 CONSUMER_BATCH = 64
 # Queue fabric (csrc/fabric.h): how a producer moves frames into OTHER processes' GPU rings.
 # "kernel": every frame of one fabric pass, to all its consumers, in ONE copy_runs_kernel launch on
-# a stream with its own hardware queue, bounded to FABRIC_COPY_WORKGROUPS workgroups; "runtime":
+# a stream with its own hardware queue: 512 workgroups when a consumer sits on the same GPU (HBM ->
+# HBM), plus FABRIC_COPY_WORKGROUPS per distinct peer GPU written (one xGMI link each,
+# QueueFabric::copy_grid_for); a link whose frames are not 16-B multiples copies by "runtime":
 # hipMemcpyAsync per contiguous run on one ordinary stream per link (the round-3 path; A/B only).
 # FABRIC_COPY_STREAM: hardware-queue placement of the kernel engine's copy stream (STREAM_KINDS).
 # Env override: PSANA_RAY_AMD_FABRIC_COPY=kernel|runtime[:workgroups[:stream kind]].
 FABRIC_COPY_ENGINES = {"kernel": 0, "runtime": 1}
 FABRIC_COPY_ENGINE = "kernel"
-FABRIC_COPY_WORKGROUPS = 128
+FABRIC_COPY_WORKGROUPS = 32
 FABRIC_COPY_STREAM = "dedicated"
 
 

@@ -147,6 +147,9 @@ def peakfind(frames: Sequence[torch.Tensor], shape, params, peaks: torch.Tensor,
         raise ValueError("peakfind: radius must be 1 or 2")
     if total is not None and (total.dtype != torch.int64 or total.numel() != 1 or total.device != dev):
         raise ValueError("peakfind: total must be an int64 scalar on the frames' device")
+    if C.PF_SCRATCH_BYTES != 4 * PF_SCRATCH_WORDS:   # the kernel's spill lists would overrun the block
+        raise RuntimeError(f"peakfind: PF_SCRATCH_WORDS {PF_SCRATCH_WORDS} disagrees with the extension's "
+                           f"kPfScratchBytes {C.PF_SCRATCH_BYTES}")
     if scratch is not None and (scratch.dtype != torch.int32 or scratch.numel() < PF_SCRATCH_WORDS
                                 or scratch.device != dev or not scratch.is_contiguous()):
         raise ValueError(f"peakfind: scratch must be a contiguous int32 [{PF_SCRATCH_WORDS}] tensor on the frames' device")
@@ -159,6 +162,24 @@ def peakfind(frames: Sequence[torch.Tensor], shape, params, peaks: torch.Tensor,
         C.peakfind([_ptr(t) for t in frames[a:b]], P, H, W, float(params.thr_peak), float(params.son_min),
                    int(params.radius), int(params.max_peaks), _ptr(peaks[a]), _ptr(counts[a:]), _ptr(summary[a]), s,
                    0 if total is None else _ptr(total), 0 if scratch is None else _ptr(scratch))
+
+
+def mask_frames(frames: Sequence[torch.Tensor], zero: torch.Tensor, stream=None):
+    """In place, ``np.where(mask, data, 0)`` (psana_ray/producer.py:92-95) over F float32 frames:
+    pixel i of every frame becomes 0 where ``zero[i]`` (uint8, 1 = masked) is non-zero.  ONE launch
+    per 64 frames (csrc/gather.hip mask_frames_kernel) -- the psana-calibrated upload path."""
+    C = _ext.load()
+    if not frames:
+        return
+    dev = frames[0].device
+    n = frames[0].numel()
+    _check_frames(frames, torch.float32, n, dev, "mask_frames")
+    if zero.dtype != torch.uint8 or zero.numel() != n or zero.device != dev or not zero.is_contiguous() \
+            or _ptr(zero) % 4:
+        raise ValueError(f"mask_frames: zero must be a contiguous, 4-B aligned uint8 [{n}] tensor on {dev}")
+    s = _ext.stream_handle(stream)
+    for a, b in _chunks(len(frames)):
+        C.mask_frames([_ptr(t) for t in frames[a:b]], _ptr(zero), n, s)
 
 
 def gather_frames(frames: Sequence[torch.Tensor], out, stream=None):

@@ -68,6 +68,9 @@ class ProducerPipeline:
         self.full_waits = 0
         self.t_first = None
         self.calibrated_source = getattr(source, "calibrated", False)
+        # which calibration runs (metrics "producer.source_path"): the HIP kernels on raw frames,
+        # psana's CPU calibration (psana_wrapper fallback), or the fp32 golden model (CPU rehearsal)
+        self.source_path = "psana_cpu" if self.calibrated_source else ("raw_hip" if self.gpu else "raw_cpu")
         spec = getattr(source, "spec", None)
         file_source = getattr(source, "reader", None)   # RawFileRun: native RawRunReader
         # file sources: DMA straight out of the registered file mapping when possible
@@ -212,6 +215,8 @@ class ProducerPipeline:
                     raise ValueError(f"mask of shape {m.shape} does not match the frames {shape}")
                 m = m.reshape(shape)
             self.mask = torch.from_numpy(~m).to(self.device)   # True = zero this pixel
+            # the GPU path masks a whole uploaded chunk in one kernel launch (ops.kernels.mask_frames)
+            self._mask_u8 = self.mask.reshape(-1).to(torch.uint8).contiguous() if self.gpu else None
         if self.gpu:
             C = _ext.load()
             nbytes = self.chunk * int(np.prod(shape)) * 4
@@ -264,10 +269,8 @@ class ProducerPipeline:
             slots = self._acquire(n, st)
             C.memcpy_h2d_batch([int(self.ep.slot_ptr(s)) for s in slots], [int(buf[i].ctypes.data) for i in range(n)],
                                int(buf[0].nbytes), int(st.cuda_stream))
-            if self.mask is not None:
-                with torch.cuda.stream(st):
-                    for s in slots:
-                        self.ep.slot_tensor(s).masked_fill_(self.mask, 0.0)   # np.where(mask, data, 0)
+            if self.mask is not None:   # np.where(mask, data, 0): one launch for the chunk
+                kernels.mask_frames([self.ep.slot_tensor(s) for s in slots], self._mask_u8, st)
             ev = torch.cuda.Event()
             ev.record(st)
             self._up_done[b] = ev
@@ -317,7 +320,8 @@ class ProducerPipeline:
     def metrics(self) -> dict:
         """Cumulative counters for utils.metrics (sampled, nothing runs per frame)."""
         d = {"frames_produced": self.produced,
-             "full_waits": int(self.engine.full_waits) if self.engine is not None else self.full_waits}
+             "full_waits": int(self.engine.full_waits) if self.engine is not None else self.full_waits,
+             "source_path": self.source_path}
         if self.engine is not None:
             st, acq, launch, commit, total = self.engine.timing()
             d.update(host_stage_s=st, host_acquire_s=acq, host_launch_s=launch, host_commit_s=commit)

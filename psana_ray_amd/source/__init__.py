@@ -4,7 +4,8 @@ from __future__ import annotations
 import os
 from typing import Optional
 
-from .psana_adapter import PsanaWrapperSource, psana_available
+from .errors import NoSourceError
+from .psana_adapter import PsanaWrapperSource, RawUnavailable, psana_available
 from .rawfile import RawFileRun, make_synthetic_run, run_path, write_run
 from .synthetic import RawEvent, SyntheticRun, generate_raw
 from .xtc2 import find_xtc2_run, make_synthetic_xtc2_run, open_xtc2_run, write_xtc2_run, xtc2_paths
@@ -13,11 +14,6 @@ ENV_DATA_DIR = "PSANA_RAY_DATA"
 
 
 SYNTHETIC_EXPS = ("synthetic",)
-
-
-class NoSourceError(RuntimeError):
-    """No event source exists for ``(exp, run, detector_name)`` (the reference fails at import
-    when psana_wrapper is missing, psana_ray/producer.py:11)."""
 
 
 def open_source(exp: str, run: int, detector_name: str, rank: int = 0, size: int = 1,
@@ -58,6 +54,6 @@ def open_source(exp: str, run: int, detector_name: str, rank: int = 0, size: int
                         f"(random-init constants), or psana-ray-mkrun to write a run file.")
 
 
-__all__ = ["NoSourceError", "SYNTHETIC_EXPS", "RawEvent", "SyntheticRun", "RawFileRun", "PsanaWrapperSource", "open_source", "generate_raw",
+__all__ = ["NoSourceError", "RawUnavailable", "SYNTHETIC_EXPS", "RawEvent", "SyntheticRun", "RawFileRun", "PsanaWrapperSource", "open_source", "generate_raw",
            "write_run", "make_synthetic_run", "run_path", "psana_available", "find_xtc2_run", "open_xtc2_run",
            "write_xtc2_run", "make_synthetic_xtc2_run", "xtc2_paths"]

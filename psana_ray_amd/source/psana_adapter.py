@@ -7,20 +7,29 @@ run over the MPI ranks itself (SMD mode, P-01), so each rank's wrapper yields th
 
 Two ways frames enter the GPU pipeline:
 
-* **raw** (preferred): when the wrapper offers ``ImageRetrievalMode.raw`` AND the run's
-  calibration constants (the adapter hook ``calib_constants()``, below), the source yields RAW
-  uint16 frames through pinned staging and the producer calibrates them with the gfx950 kernels
-  (K-01..K-05: gain decode, pedestal, gain, common mode, masks, geometry) -- the same path as the
-  synthetic and file sources.  psana's CPU calibration never runs.
-* **calibrated** (fallback): frames arrive calibrated by psana in the requested mode and are
-  uploaded in pinned batches (one H2D copy per chunk, no per-frame synchronisation); masks are
-  applied on the GPU.
+* **raw** (preferred, ``source_path = "raw_hip"``): raw uint16 frames go through pinned staging and
+  the producer calibrates them with the gfx950 kernels (K-01..K-05: gain decode, pedestal, gain,
+  common mode, masks, geometry) -- the same path as the synthetic and file sources; psana's CPU
+  calibration never runs.  It needs raw frames AND the run's calibration constants, probed by
+  attribute (nothing is fetched, nothing guessed over a network):
+    raw frames  1. the wrapper's own ``ImageRetrievalMode.raw`` through ``iter_events`` (keeps its
+                   photon energies), else
+                2. the psana detector handle the wrapper holds (``det`` / ``detector`` / ...):
+                   psana2 ``det.raw.raw(evt)`` or psana1 ``det.raw(evt)``, over the events of the
+                   run it holds (``run.events()`` / ``ds.events()``; photon energy from a wrapper
+                   ``get_photon_energy(evt)`` when it has one);
+    constants   1. an adapter hook ``calib_constants()`` on the wrapper (mapping below), else
+                2. the detector handle's constant accessors: psana2 ``det.raw._pedestals()``,
+                   ``_gain()`` (ADU/keV), ``_status()``, ``_pixel_coord_indexes()``; psana1
+                   ``det.pedestals(run)``, ``gain(run)``, ``status(run)``, ``indexes_xy(run)``.
+* **calibrated** (fallback, ``source_path = "psana_cpu"``, logged once at WARNING): frames arrive
+  calibrated by psana in the requested mode and are uploaded in pinned batches (one H2D copy per
+  frame of a chunk, no per-frame synchronisation); masks are applied by one kernel per chunk.
 
-``calib_constants()`` hook -- a mapping with
-  ``pedestals`` [G, P, H, W] (ADU), ``gains`` [G, P, H, W] (ADU per keV),
-  optional ``status`` [P, H, W] (non-zero = bad), ``gain_config`` [P, H, W] (epix10ka: 0..4 =
-  FH FM FL AHL AML), ``pix_rows`` / ``pix_cols`` [P, H, W] (image-mode pixel indices; default: the
-  framework's geometry of the detector).
+``calib_constants()`` mapping -- ``pedestals`` [G, P, H, W] (ADU), ``gains`` [G, P, H, W] (ADU per
+keV), optional ``status`` [P, H, W] or [G, P, H, W] (non-zero = bad), ``gain_config`` [P, H, W]
+(epix10ka: 0..4 = FH FM FL AHL AML; default AHL), ``pix_rows`` / ``pix_cols`` [P, H, W] (image-mode
+pixel indices; default: the framework's geometry of the detector).
 The detector must be one the framework knows (``models/detector.py``) with matching shapes.
 
 Neither psana nor psana_wrapper exists in this environment: parity with real
@@ -36,8 +45,93 @@ from typing import Iterator, List, Optional, Tuple
 import numpy as np
 
 from ..models.detector import Mode
+from .errors import NoSourceError
 
 log = logging.getLogger(__name__)
+
+
+_DET_ATTRS = ("det", "detector", "psana_det", "psana_detector", "_det", "_detector")
+_EVENT_ATTRS = ("run", "psana_run", "_run", "ds", "datasource", "_ds")
+_PE_ATTRS = ("get_photon_energy", "photon_energy", "_photon_energy")
+_warned_cpu = False
+
+
+def _find_detector(wrapper):
+    """(attribute name, psana detector handle) the wrapper holds, or (None, None): a handle is an
+    object with a ``raw`` member (psana2: an object with ``raw(evt)``; psana1: a method)."""
+    for a in _DET_ATTRS:
+        d = getattr(wrapper, a, None)
+        if d is not None and getattr(d, "raw", None) is not None:
+            return a, d
+    return None, None
+
+
+def _raw_accessor(det):
+    """evt -> raw frame of a detector handle: psana2 ``det.raw.raw``, psana1 ``det.raw``."""
+    r = getattr(det, "raw", None)
+    if r is not None and callable(getattr(r, "raw", None)):
+        return r.raw
+    return r if callable(r) else None
+
+
+def _find_events(wrapper):
+    """The run's event iterator factory the wrapper holds (``run.events`` / ``ds.events``)."""
+    for a in _EVENT_ATTRS:
+        o = getattr(wrapper, a, None)
+        if o is not None and callable(getattr(o, "events", None)):
+            return o.events
+    return None
+
+
+def _call(fn, *alts):
+    """fn(), else fn(alt) for the first alternative argument it accepts (psana1 accessors take the
+    run or an event)."""
+    try:
+        return fn()
+    except TypeError:
+        if not alts:
+            raise
+    err = None
+    for a in alts:
+        try:
+            return fn(a)
+        except TypeError as e:
+            err = e
+    raise err
+
+
+def _constants_from_detector(det, run: int):
+    """The calib_constants() mapping from a psana detector handle, or (None, why)."""
+    r = getattr(det, "raw", None)
+    if r is not None and hasattr(r, "_pedestals"):        # psana2 AreaDetector (det.raw.*)
+        acc = {"pedestals": "_pedestals", "gains": "_gain", "status": "_status", "coords": "_pixel_coord_indexes",
+               "gain_config": "_gain_config"}
+        obj, style = r, "psana2"
+    elif hasattr(det, "pedestals"):                       # psana1 Detector
+        acc = {"pedestals": "pedestals", "gains": "gain", "status": "status", "coords": "indexes_xy",
+               "gain_config": "gain_config"}
+        obj, style = det, "psana1"
+    else:
+        return None, "the psana detector handle exposes no calibration constants"
+    out = {}
+    for key in ("pedestals", "gains"):
+        fn = getattr(obj, acc[key], None)
+        v = _call(fn, run) if callable(fn) else None
+        if v is None:
+            return None, f"the {style} detector handle gives no {key} ({acc[key]})"
+        out[key] = np.asarray(v)
+    for key in ("status", "gain_config"):
+        fn = getattr(obj, acc[key], None)
+        if callable(fn):
+            v = _call(fn, run)
+            if v is not None:
+                out[key] = np.asarray(v)
+    fn = getattr(obj, acc["coords"], None)
+    if callable(fn):
+        rc = _call(fn, run)
+        if rc is not None and len(rc) >= 2:
+            out["pix_rows"], out["pix_cols"] = np.asarray(rc[0]), np.asarray(rc[1])
+    return out, style
 
 
 def psana_available() -> bool:
@@ -53,6 +147,11 @@ def _normalise(data: np.ndarray) -> np.ndarray:
     """The reference's ndim fix-up (producer.py:96-97): 2-D frames become (1, H, W)."""
     data = np.asarray(data)
     return data[None] if data.ndim == 2 else data
+
+
+class RawUnavailable(NoSourceError):
+    """Raw frames were requested (``--mode raw`` / ``calibrate_on_read``) from a psana_wrapper that
+    cannot provide them; a :class:`~psana_ray_amd.source.NoSourceError` too (the CLI's clean exit 2)."""
 
 
 class PsanaWrapperSource:
@@ -80,21 +179,31 @@ class PsanaWrapperSource:
         self._peeked: Optional[Tuple[np.ndarray, Optional[float]]] = None
         self.geometry = None
         self.consts = None
+        self.raw_via = self.constants_via = None
+        self._raw_fn = self._events_fn = self._pe_fn = None
         why = self._try_raw(prefer_raw)
         self.calibrated = why is not None
+        self.source_path = "psana_cpu" if self.calibrated else "raw_hip"
         if self.calibrated:
             if self.mode == Mode.raw:
-                raise RuntimeError(f"psana_wrapper source {exp}/{run}/{detector_name}: raw mode requested but {why}")
-            log.info("psana_wrapper %s/%d/%s: psana-calibrated %s frames uploaded in pinned batches (%s)", exp, run,
-                     detector_name, self.mode.value, why)
+                raise RawUnavailable(f"psana_wrapper source {exp}/{run}/{detector_name}: raw mode requested but {why}")
+            global _warned_cpu
+            if not _warned_cpu and prefer_raw:
+                log.warning("psana_wrapper %s/%d/%s: the HIP calibration kernels cannot run (%s); psana calibrates on "
+                            "the CPU and its %s frames are uploaded in pinned batches", exp, run, detector_name, why,
+                            self.mode.value)
+                _warned_cpu = True
+            else:
+                log.info("psana_wrapper %s/%d/%s: psana-calibrated %s frames uploaded in pinned batches (%s)", exp, run,
+                         detector_name, self.mode.value, why)
             first = self._peek()
             if first is None:
-                raise RuntimeError(f"psana_wrapper source {exp}/{run}/{detector_name}: the run has no events")
+                raise NoSourceError(f"psana_wrapper source {exp}/{run}/{detector_name}: the run has no events")
             self.frame_shape = tuple(_normalise(first[0]).shape)
             self.frame_dtype = np.float32
         else:
-            log.info("psana_wrapper %s/%d/%s: RAW frames calibrated on the GPU (HIP kernels, %s mode)", exp, run,
-                     detector_name, self.mode.value)
+            log.info("psana_wrapper %s/%d/%s: RAW frames (%s) calibrated on the GPU with constants from the %s "
+                     "(HIP kernels, %s mode)", exp, run, detector_name, self.raw_via, self.constants_via, self.mode.value)
             self.frame_shape = tuple(self.spec.frame_shape)
             if pinned:
                 from ..ops import _ext
@@ -110,12 +219,32 @@ class PsanaWrapperSource:
     def _try_raw(self, prefer_raw: bool) -> Optional[str]:
         """Set up the raw path; returns None when it applies, else why not."""
         if not prefer_raw:
-            return "raw path disabled"
-        if not hasattr(self._modes, "raw"):
-            return "the wrapper has no ImageRetrievalMode.raw"
+            return "raw path disabled (--psana_calibrated)"
+        det_attr, det = _find_detector(self.wrapper)
+        # raw frames: the wrapper's raw retrieval mode, else the detector handle over the run's events
+        if hasattr(self._modes, "raw"):
+            self.raw_via = "iter_events(raw)"
+        elif det is not None and _raw_accessor(det) is not None and _find_events(self.wrapper) is not None:
+            self.raw_via = f"{det_attr}.raw(evt)"
+            self._raw_fn = _raw_accessor(det)
+            self._events_fn = _find_events(self.wrapper)
+            self._pe_fn = next((getattr(self.wrapper, a) for a in _PE_ATTRS if callable(getattr(self.wrapper, a, None))),
+                               None)
+        else:
+            return ("the wrapper has no ImageRetrievalMode.raw and no psana detector handle with raw frames and a "
+                    "run event loop")
+        # calibration constants: the adapter hook, else the detector handle's accessors
         hook = getattr(self.wrapper, "calib_constants", None)
-        if hook is None:
-            return "the wrapper exposes no calib_constants()"
+        if callable(hook):
+            c = hook()
+            self.constants_via = "calib_constants() hook"
+        elif det is not None:
+            c, style = _constants_from_detector(det, self.run)
+            if c is None:
+                return style
+            self.constants_via = f"{style} detector handle ({det_attr})"
+        else:
+            return "no calibration constants: no calib_constants() hook and no psana detector handle"
         from ..models.constants import EPIX_CM_GAINS, JUNGFRAU_CM_GAINS, CalibConstants
         from ..models.detector import get_detector
         from ..models.geometry import Geometry, make_geometry
@@ -124,16 +253,22 @@ class PsanaWrapperSource:
             spec = get_detector(self.detector_name)
         except KeyError:
             return f"detector {self.detector_name!r} has no kernel description"
-        c = hook()
         ped = np.ascontiguousarray(c["pedestals"], dtype=np.float32)
         gains = np.ascontiguousarray(c["gains"], dtype=np.float32)
         want = (spec.n_gains, *spec.frame_shape)
         if ped.shape != want or gains.shape != want:
             return f"constants {ped.shape} / {gains.shape} do not match {spec.name} {want}"
-        status = np.asarray(c.get("status", np.zeros(spec.frame_shape, np.uint8))).astype(np.uint8)
+        status = np.asarray(c.get("status", np.zeros(spec.frame_shape, np.uint8)))
+        if status.ndim == len(spec.frame_shape) + 1:   # per gain mode (psana2 _status()): bad in any
+            status = (status != 0).any(axis=0)
+        status = status.astype(np.uint8)
         cfg = c.get("gain_config")
         if spec.kind == "epix10ka":
-            cfg = np.full(spec.frame_shape, 3, np.uint8) if cfg is None else np.asarray(cfg).astype(np.uint8)
+            if cfg is None:
+                log.warning("psana_wrapper %s: no per-pixel gain configuration among the constants; assuming AHL "
+                            "(auto high-to-low) for every pixel", self.detector_name)
+            cfg = np.full(spec.frame_shape, 3, np.uint8) if cfg is None else \
+                np.asarray(cfg).astype(np.uint8).reshape(spec.frame_shape)
         cmg = {"epix10ka": EPIX_CM_GAINS, "jungfrau": JUNGFRAU_CM_GAINS}.get(spec.kind, (0,))
         self.spec = spec
         self.consts = CalibConstants(spec, ped, gains, status.reshape(spec.frame_shape), cfg, tuple(cmg))
@@ -167,12 +302,26 @@ class PsanaWrapperSource:
     def cursor(self) -> int:
         return self._cursor
 
+    def _raw_from_handle(self):
+        """(raw frame, photon energy) per event of the run through the psana detector handle."""
+        for evt in self._events_fn():
+            data = self._raw_fn(evt)
+            if data is None:   # the detector is not in this event (psana returns None)
+                continue
+            pe = self._pe_fn(evt) if self._pe_fn is not None else None
+            yield data, pe
+
     def _events(self):
         if self._it is None:
-            m = getattr(self._modes, "raw" if not self.calibrated else
-                        ("calib" if self.mode == Mode.calib else "image"))
-            it = iter(self.wrapper.iter_events(mode=m))
-            self._it = itertools.islice(it, self._skip, None) if self._skip else it
+            if not self.calibrated and self._raw_fn is not None:
+                it = self._raw_from_handle()
+            else:
+                m = getattr(self._modes, "raw" if not self.calibrated else
+                            ("calib" if self.mode == Mode.calib else "image"))
+                it = iter(self.wrapper.iter_events(mode=m))
+            # --num_events: this rank's events after --start_event (ADVICE r4: it was ignored)
+            stop = None if self.n_events is None else self._skip + int(self.n_events)
+            self._it = itertools.islice(it, self._skip, stop) if (self._skip or stop is not None) else it
         return self._it
 
     def _peek(self):

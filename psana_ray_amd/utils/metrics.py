@@ -87,6 +87,8 @@ class Registry:
                     v = int(v)
                 if isinstance(v, (int, float)):
                     out[f"{name}.{k}"] = float(v)
+                elif isinstance(v, str):   # a label (e.g. producer.source_path): JSON as is, Prometheus as info
+                    out[f"{name}.{k}"] = v
         return out
 
 
@@ -157,6 +159,13 @@ class Reporter:
         if self._prom is not None:
             for k, v in rec.items():
                 name = "psana_ray_" + k.replace(".", "_").replace("-", "_")
+                if isinstance(v, str):   # info-style gauge: the label carries the value
+                    name += "_info"
+                    g = self._gauges.get(name)
+                    if g is None:
+                        g = self._gauges[name] = self._prom.Gauge(name, k, ["rank", "value"])
+                    g.labels(rank=str(self.rank), value=v).set(1)
+                    continue
                 g = self._gauges.get(name)
                 if g is None:
                     g = self._gauges[name] = self._prom.Gauge(name, k, ["rank"])

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--verify", default="synthetic:2:tiny_epix:1", help="exp:run:detector:n_producers")
     ap.add_argument("--timeout", type=float, default=60.0)
     ap.add_argument("--gen_device", default="cpu", help="device the producer generated its synthetic pool on")
+    ap.add_argument("--mode", default="calib", choices=["calib", "image"], help="the producer's retrieval mode")
     a = ap.parse_args()
 
     import numpy as np
@@ -47,8 +48,13 @@ def main():
             src = SyntheticRun(exp, int(run), det, rank=rank, size=int(size), pool_frames=32, gen_device=a.gen_device)
             # the producer CLI's default common mode (--common_mode auto: on for epix10ka)
             cm = resolve_common_mode("auto", src.consts.spec)
-            refs[rank] = reference.calibrate_reference(torch.from_numpy(src.pool.astype(np.int32)), src.consts, None,
-                                                       cm)
+            ref = reference.calibrate_reference(torch.from_numpy(src.pool.astype(np.int32)), src.consts, None, cm)
+            if a.mode == "image":
+                from psana_ray_amd.models.geometry import make_geometry
+
+                geo = make_geometry(src.consts.spec)
+                ref = reference.assemble_reference(ref, geo.rows, geo.cols, geo.image_shape)
+            refs[rank] = ref
         return refs[rank][idx % 32]
 
     out = open(a.out, "w", buffering=1)

@@ -8,7 +8,19 @@ synthetic detector; "psana's" calibrated / image frames are the fp32 golden mode
 frames, so a test can compare what reaches a consumer with what this stub says psana produces.
 
 Knobs (environment):
-  PSANA_STUB_RAW=0        no ImageRetrievalMode.raw / no calib_constants() (psana-calibrated path)
+  PSANA_STUB_RAW=0        no ImageRetrievalMode.raw / no calib_constants() / no detector handle
+                          (psana-calibrated path)
+  PSANA_STUB_STYLE=...    how raw frames and constants can be reached (the adapter's probes):
+                          hook (default): ImageRetrievalMode.raw + the calib_constants() hook;
+                          psana2: ImageRetrievalMode.raw, constants only on a psana2-style detector
+                            handle ``wrapper.det`` (det.raw._pedestals() / _gain() / per-gain
+                            _status() / _pixel_coord_indexes());
+                          psana2_events: no raw retrieval mode at all -- raw frames through
+                            ``wrapper.det.raw.raw(evt)`` over ``wrapper.run.events()``, photon
+                            energy from ``wrapper.get_photon_energy(evt)``;
+                          psana1: no raw retrieval mode; a psana1-style handle ``wrapper.detector``
+                            (detector.raw(evt), pedestals(run), gain(run), status(run)) over
+                            ``wrapper.ds.events()``
   PSANA_STUB_EVENTS=N     events in the run (default 24)
   PSANA_STUB_CM=text      common mode "psana" applies (default: "default"; "off" disables)
 SMD sharding: the rank / size come from the same launcher variables the producer reads, and rank
@@ -22,8 +34,9 @@ import os
 import numpy as np
 
 RAW_OK = os.environ.get("PSANA_STUB_RAW", "1") != "0"
+STYLE = os.environ.get("PSANA_STUB_STYLE", "hook") if RAW_OK else "none"
 
-if RAW_OK:
+if STYLE in ("hook", "psana2"):
     class ImageRetrievalMode(enum.Enum):
         raw = "raw"
         calib = "calib"
@@ -46,11 +59,23 @@ class PsanaWrapperSmd:
         from psana_ray_amd.source.synthetic import SyntheticRun
 
         self.exp, self.run, self.detector_name = exp, int(run), detector_name
+        self.runnum = int(run)
         self.rank, self.size = _rank_size()
         self.n_events = int(os.environ.get("PSANA_STUB_EVENTS", "24"))
         # one generator for the whole run (seeded by exp/run), sharded like SMD mode
         self._syn = SyntheticRun(exp, run, detector_name, rank=0, size=1, pool_frames=8, gen_device="cpu")
         self.consts = self._syn.consts
+        if STYLE in ("psana2", "psana2_events"):
+            self.det = _Psana2Det(self)
+        if STYLE == "psana2_events":
+            self.run_obj = _Run(self)
+            self.run = self.run_obj          # psana2: the wrapper holds the run (``run.events()``)
+        if STYLE == "psana1":
+            self.detector = _Psana1Det(self)
+            self.ds = _Run(self)             # psana1: the DataSource (``ds.events()``)
+
+    def get_photon_energy(self, evt):
+        return self.photon_energy(evt.gevt)
 
     # ---- reference surface -------------------------------------------------------------------
     def create_bad_pixel_mask(self):
@@ -74,10 +99,77 @@ class PsanaWrapperSmd:
                 yield expected_frame(self, g, name), self.photon_energy(g)
 
     # ---- adapter hook: the run's calibration constants ---------------------------------------
-    if RAW_OK:
+    if STYLE == "hook":
         def calib_constants(self):
             c = self.consts
             return {"pedestals": c.pedestals, "gains": c.gains, "status": c.status, "gain_config": c.gain_config}
+
+
+class _Evt:
+    def __init__(self, gevt):
+        self.gevt = gevt
+
+
+class _Run:
+    """psana2 run / psana1 DataSource: this rank's events (SMD sharding)."""
+
+    def __init__(self, w):
+        self._w = w
+
+    def events(self):
+        for g in self._w.local_events():
+            yield _Evt(g)
+
+
+class _Psana2Raw:
+    """psana2 ``det.raw``: raw(evt) and the run's constants (per gain mode, as psana2 keeps them)."""
+
+    def __init__(self, w):
+        self._w = w
+
+    def raw(self, evt):
+        return self._w.raw_frame(evt.gevt).copy()
+
+    def _pedestals(self):
+        return self._w.consts.pedestals
+
+    def _gain(self):
+        return self._w.consts.gains
+
+    def _status(self):
+        st = self._w.consts.status
+        return np.broadcast_to(st, (self._w.consts.pedestals.shape[0], *st.shape)).copy()
+
+    def _pixel_coord_indexes(self):
+        from psana_ray_amd.models.geometry import make_geometry
+
+        g = make_geometry(self._w.consts.spec)
+        return g.rows, g.cols
+
+
+class _Psana2Det:
+    def __init__(self, w):
+        self.raw = _Psana2Raw(w)
+
+
+class _Psana1Det:
+    """psana1 ``Detector``: raw(evt) and constants that take the run number."""
+
+    def __init__(self, w):
+        self._w = w
+
+    def raw(self, evt):
+        return self._w.raw_frame(evt.gevt).copy()
+
+    def pedestals(self, run):
+        assert run == self._w.runnum, "psana1 constants are looked up by run number"
+        return self._w.consts.pedestals
+
+    def gain(self, run):
+        return self._w.consts.gains
+
+    def status(self, run):
+        return self._w.consts.status
 
 
 def stub_common_mode():

@@ -140,3 +140,21 @@ def test_gpu_keeper_holds_frames_after_the_producer_exits(store_port, tmp_path):
     assert sorted(frames(recs)) == list(range(40))
     assert recs[-1].get("eos") is True
     assert "keeper done: kept=40" in out_k, out_k[-2000:]
+
+
+def test_gpu_odd_sized_image_frames_cross_processes(store_port, tmp_path):  # noqa: F811
+    """Image frames of 612 B (9 x 17 pixels: not a multiple of 16 B) between two GPU processes: the
+    producer's fabric decides at link attach that its copy kernel (16-B words) cannot move them and
+    copies that link with the runtime engine instead -- every frame bit-exact, then EOS."""
+    from tests.test_elastic_queue import producer
+
+    prod = producer(store_port, 30, "--device", "cuda:0", queue_size=16, detector="tiny_odd", mode="image")
+    c = consumer(store_port, tmp_path / "c.jsonl", "--device", "cuda:0", "--gen_device", "cuda", "--mode", "image",
+                 "--verify", "synthetic:2:tiny_odd:1")
+    rc_c, out_c = finish(c, 120)
+    rc_p, out_p = finish(prod, 120)
+    assert rc_c == 0, out_c[-3000:]
+    assert rc_p == 0, out_p[-3000:]
+    recs = records(tmp_path / "c.jsonl")
+    assert sorted(frames(recs)) == list(range(30))
+    assert recs[-1].get("eos") is True

@@ -52,9 +52,10 @@ def store_port():
         p.kill()
 
 
-def producer(port, n_events, *extra, queue_size=16, chunk=4, timeout=60):
+def producer(port, n_events, *extra, queue_size=16, chunk=4, timeout=60, detector="tiny_epix", mode="calib"):
     cmd = [sys.executable, "-m", "psana_ray_amd.producer", "--exp", "synthetic", "--run", "2", "--detector_name",
-           "tiny_epix", "--calib", "--device", "cpu", "--ray_address", f"127.0.0.1:{port}", "--num_events",
+           detector, *(("--calib",) if mode == "calib" else ()), "--device", "cpu", "--ray_address", f"127.0.0.1:{port}",
+           "--num_events",
            str(n_events), "--queue_size", str(queue_size), "--chunk", str(chunk), "--timeout", str(timeout),
            "--metrics_interval", "0", "--log_level", "INFO", *extra]
     return subprocess.Popen(cmd, env=ENV, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
@@ -100,6 +101,19 @@ def test_producer_first_consumer_ten_seconds_later(store_port, tmp_path):
     assert rc_p == 0, out_p
     recs = records(tmp_path / "c.jsonl")
     assert sorted(frames(recs)) == list(range(24))
+    assert recs[-1].get("eos") is True
+
+
+def test_odd_sized_image_frames_cross_processes(store_port, tmp_path):
+    """Image frames of 612 B (tiny_odd: 9 x 17 pixels, not a multiple of 16 B) through host rings."""
+    prod = producer(store_port, 20, detector="tiny_odd", mode="image")
+    c = consumer(store_port, tmp_path / "c.jsonl", "--mode", "image", "--verify", "synthetic:2:tiny_odd:1")
+    rc_c, out_c = finish(c)
+    rc_p, out_p = finish(prod)
+    assert rc_c == 0, out_c
+    assert rc_p == 0, out_p
+    recs = records(tmp_path / "c.jsonl")
+    assert sorted(frames(recs)) == list(range(20))
     assert recs[-1].get("eos") is True
 
 

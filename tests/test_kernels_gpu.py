@@ -286,3 +286,17 @@ def test_copy_runs_kernel_bitwise(cuda_device, native, wgs):
     for s, a in zip(srcs, offs):
         assert torch.equal(dst[a:a + s.numel()], s)
     assert int((dst[:16] != -7).sum()) == 0 and int((dst[o:] != -7).sum()) == 0
+
+
+@pytest.mark.parametrize("shape,n", [((16, 352, 384), 40), ((1, 9, 17), 3), ((1, 5, 7), 70)])
+def test_mask_frames_kernel_matches_where(cuda_device, shape, n):
+    """psana-calibrated upload path: one mask_frames launch per <= 64 frames equals
+    np.where(mask, data, 0) (psana_ray/producer.py:92-95) bit for bit, 4-pixel body and scalar tail."""
+    g = torch.Generator().manual_seed(5)
+    frames = torch.randn((n, *shape), generator=g).to(cuda_device)
+    keep = torch.rand(shape, generator=g) > 0.3
+    zero = (~keep).reshape(-1).to(torch.uint8).to(cuda_device)
+    ref = torch.where(keep.to(cuda_device), frames, torch.zeros_like(frames))
+    kernels.mask_frames([frames[i] for i in range(n)], zero)
+    torch.cuda.synchronize()
+    _assert_equal(frames, ref, f"mask_frames {shape}")

@@ -23,3 +23,28 @@ def test_extension_links_no_rccl(native):
     needed = [l.split("[")[1].rstrip("]") for l in out.splitlines() if "(NEEDED)" in l]
     assert not any("rccl" in n or "nccl" in n for n in needed), needed
     assert any(n.startswith("libamdhip64.so") for n in needed), needed
+
+
+def test_pf_scratch_words_match_the_extension(native):
+    """The Python size of the peak finder's scratch block is the kernel's (ADVICE r4)."""
+    from psana_ray_amd.ops import kernels
+
+    assert native.PF_SCRATCH_BYTES == 4 * kernels.PF_SCRATCH_WORDS
+
+
+def test_copy_grid_grows_per_peer_gpu(native):
+    """Fabric copy dispatch grid: 512 workgroups for consumers on this GPU, plus the per-peer count
+    for every DISTINCT other GPU written (one xGMI link each), capped (VERDICT r4 next #2)."""
+    g = native.QueueFabric.copy_grid_for
+    assert g([0, 0, 0], 0, 32) == 512
+    assert g([1], 0, 32) == 32
+    assert g([1, 1, 2, 3, 3], 0, 32) == 96
+    assert g([0, 1, 2, 3, 4, 5, 6, 7], 0, 32) == 512 + 7 * 32
+    assert g([], 0, 32) == 32
+    assert g(list(range(1, 300)), 0, 64) == 4096
+
+
+def test_device_topology_on_a_cpu_box(native):
+    t = native.device_topology()
+    assert set(t) == {"n", "can_access", "link_type", "hops"}
+    assert len(t["can_access"]) == t["n"]
