@@ -76,9 +76,13 @@ def parse(argv=None):
     ap.add_argument("--consumer-stream-kind", default=None, choices=["shared", "dedicated", "high"],
                     help="placement of the peak finder's streams (default: config.CONSUMER_STREAM_KIND)")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--preroll-s", type=float, default=0.5,
-                    help="untimed streaming before the warmup steps: the queue fills and the GPU clocks settle, so "
-                         "a 20-step window measures the same steady state as a 200-step one")
+    ap.add_argument("--preroll-s", type=float, default=0.0,
+                    help="fixed untimed streaming before the steady-state gate (the gate alone is the default)")
+    ap.add_argument("--gate-tol", type=float, default=0.03,
+                    help="steady-state gate: untimed windows of --gate-window-s until two consecutive ones agree within "
+                         "this fraction on EVERY rank (then the --warmup steps, then the timed window); 0 disables")
+    ap.add_argument("--gate-window-s", type=float, default=0.25, help="target length of one gate window")
+    ap.add_argument("--gate-max-s", type=float, default=10.0, help="bound of the gate (the run goes on unconverged)")
     ap.add_argument("--producers", type=int, default=0,
                     help="producer ranks P (ranks < P produce, every rank consumes; 0 = all).  BASELINE config 3: "
                          "--gpus 8 --producers 4")
@@ -123,6 +127,24 @@ def _wait_links(ep, n_members: int, expect_in: int, expect_out: int, timeout_s: 
         time.sleep(0.01)
 
 
+def _topology(ep, device, allsum) -> dict:
+    """Per-rank topology evidence for the result line: every rank's GPU and its
+    outgoing fabric links (consumer GPU, copy engine, hipDeviceCanAccessPeer, hipExtGetLinkType-
+    AndHopCount type / hops -- 4 = xGMI, hops 1 = a direct link), plus rank 0's view of the peer
+    access / link-type / hop matrices of every visible GPU."""
+    links = [{"peer": int(x.peer), "consumer_device": int(x.consumer_device), "attached": bool(x.attached),
+              "kernel_copy": bool(getattr(x, "kernel_copy", False)), "peer_access": int(getattr(x, "peer_access", -1)),
+              "link_type": int(getattr(x, "link_type", -1)), "hops": int(getattr(x, "hops", -1))}
+             for x in ep.links() if x.outgoing]
+    out = {"device_per_rank": allsum(device.index if device.type == "cuda" else -1),
+           "outgoing_links_per_rank": allsum(links)}
+    if device.type == "cuda":
+        from psana_ray_amd.ops import _ext
+
+        out["rank0_view"] = _ext.load().device_topology()
+    return out
+
+
 def _pct(v, q):
     if not v:
         return None
@@ -145,6 +167,17 @@ def _copy_stats(samples) -> dict:
             "ms_per_64_frames_dev_p50": round(64 * _pct([d / max(1, f) for d, f in zip(dev, frames)], 0.5), 4)}
 
 
+def resolve_shape(args, gpu: bool):
+    """(ranks per GPU, consumer batch, producer compute streams) of this launch: explicit flags, else
+    the library's resolution (pipeline.resolve_consumer_batch / resolve_producer_streams)."""
+    from psana_ray_amd.parallel.launch import ranks_per_gpu
+    from psana_ray_amd.pipeline import resolve_consumer_batch, resolve_producer_streams
+
+    share = ranks_per_gpu() if gpu else 1
+    where = "device" if args.source == "device" else "staged"
+    return share, resolve_consumer_batch(args.batch, share), resolve_producer_streams(where, args.compute_streams, share)
+
+
 def main(argv=None):
     args = parse(argv)
     from psana_ray_amd.utils.runtime_env import select_copy_engine
@@ -154,7 +187,7 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
-    from psana_ray_amd.config import CONSUMER_BATCH, CONSUMER_STREAM_KIND, PeakFinderParams
+    from psana_ray_amd.config import CONSUMER_STREAM_KIND, PeakFinderParams
     from psana_ray_amd.models import Mode
     from psana_ray_amd.producer import build_calibrator
     from psana_ray_amd.parallel.launch import bind_numa_to_device, detect
@@ -183,15 +216,10 @@ def main(argv=None):
         torch.cuda.set_device(device)
         numa = bind_numa_to_device(device)
     gpu = device.type == "cuda"
-    # ranks sharing one GPU (rehearsals of an N-rank launch on fewer GPUs): every process's
-    # dedicated streams are hardware queues of that one GPU, so the pipeline takes the round-3
-    # shape there -- 3 producer compute streams, 32-frame consumer batches.  2 ranks on one GPU,
-    # device-resident: 142.8k fr/s with it, 83.6k with the 1-rank-per-GPU shape (4 streams, 64)
-    # (profiles/r4/n2final/)
-    lws = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-    gpu_share = max(1, -(-lws // max(1, torch.cuda.device_count()))) if gpu else 1
-    if args.batch is None:
-        args.batch = CONSUMER_BATCH if gpu_share == 1 else 32
+    # ranks sharing one GPU (rehearsals of an N-rank launch on fewer GPUs): the library's pipeline
+    # shape (config.pipeline_shape: 3 producer streams and 32-frame batches there), the same
+    # resolution psana-ray-producer / psana-ray-consumer make
+    gpu_share, args.batch, compute_streams = resolve_shape(args, gpu)
 
     coord = None
     store = None
@@ -283,11 +311,11 @@ def main(argv=None):
         sk_kw["streams"] = args.consumer_streams
     if args.gap_fill:
         cs_kw["gap_fill"] = True
-    if gpu_share > 1 and args.source == "device" and args.compute_streams is None:
-        cs_kw["compute_streams"] = 3
-    prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk, **cs_kw) if is_prod else None
-    consumer = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=args.batch, **sk_kw) \
-        if args.consumer == "peakfind" else None
+    cs_kw["compute_streams"] = compute_streams
+    prod = ProducerPipeline(source, cal, ep, rank=rank, chunk=args.chunk, ranks_per_gpu=gpu_share, **cs_kw) \
+        if is_prod else None
+    consumer = PeakFinderConsumer(ep, cal.out_shape, PeakFinderParams(), batch=args.batch, ranks_per_gpu=gpu_share,
+                                  **sk_kw) if args.consumer == "peakfind" else None
 
     stop = threading.Event()
     ep.start()
@@ -397,10 +425,44 @@ def main(argv=None):
         dist.all_gather_object(out, x, group=coord)
         return out
 
+    def steady_gate():
+        """Untimed windows until two consecutive ones agree within --gate-tol on every rank (the
+        queue's start-up backlog drained, clocks and the routing settled), bounded by --gate-max-s.
+        Each window takes ~--gate-window-s worth of frames at the last measured rate; the decision
+        is collective (all-reduce), so every rank leaves the gate after the same window."""
+        t_start = time.perf_counter()
+        n = max(4, args.warmup) * B
+        prev, rates, it, converged = None, [], 0, False
+        while True:
+            csync()
+            barrier()
+            t0 = time.perf_counter()
+            consume(n)
+            csync()
+            r = n / max(1e-9, time.perf_counter() - t0)
+            it += 1
+            rates.append(round(r, 1))
+            agree = prev is not None and abs(r - prev) <= args.gate_tol * prev
+            prev = r
+            n = max(B, int(round(r * args.gate_window_s / B)) * B)
+            flags = [0.0 if agree else 1.0, time.perf_counter() - t_start]
+            if coord is not None:
+                t = torch.tensor(flags, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=coord)
+                flags = [float(t[0]), float(t[1])]
+            if flags[0] == 0.0:
+                converged = True
+                break
+            if flags[1] > args.gate_max_s:
+                break
+        return {"tol": args.gate_tol, "iterations": it, "converged": converged,
+                "seconds": round(time.perf_counter() - t_start, 3), "window_rates": rates[-8:]}
+
     B = args.batch
     t_pre = time.perf_counter()
     while time.perf_counter() - t_pre < args.preroll_s:
         consume(B)
+    gate = steady_gate() if args.gate_tol > 0 else None
     barrier()
     consume(args.warmup * B)
     # producers < ranks (BASELINE config 3): every rank's window ends with the slowest consumer's, so
@@ -479,6 +541,7 @@ def main(argv=None):
             break
     pt.join(timeout=60)
     ep.join(timeout=60)
+    topology = _topology(ep, device, allsum) if sess is not None or gpu else None
     peaks = consumer.synchronize() if consumer is not None else 0
     st = ep.stats()
     # per rank over the whole run: the share of the frames it consumed that arrived from another
@@ -547,6 +610,8 @@ def main(argv=None):
             "bytes_sent_rank0": st.get("bytes_sent", 0),
             "xgmi_phase": cross,
             "links_rank0": linking,
+            "topology": topology,
+            "steady_gate": gate,
             "staging": staging,
             "staging_copies_span_frame_kernel": copies,
             "numa_node": numa,

@@ -55,6 +55,27 @@ STREAM_KINDS = {"shared": 0, "dedicated": 1, "high": 2}
 # 151.1-154.1k for 4, 6 streams 146.8-148.4k (sweep6/).
 PRODUCER_STREAMS = {"device": 4, "staged": 1}
 PRODUCER_STREAM_KIND = {"device": "dedicated", "staged": "shared"}
+# Ranks sharing ONE GPU (an N-rank launch on fewer GPUs, e.g. `mpirun -n 4` on a one-GPU box,
+# README.md:20): every process's dedicated streams are hardware queues of that one GPU, so the
+# pipeline takes the round-3 shape there -- 3 producer compute streams (raw frames in HBM) and
+# 32-frame consumer batches.  2 ranks on one GPU, device-resident: 142.8k fr/s with it, 83.6k
+# with the one-rank-per-GPU shape (4 streams, 64) (profiles/r4/n2final/).
+SHARED_GPU_PRODUCER_STREAMS = {"device": 3, "staged": 1}
+SHARED_GPU_CONSUMER_BATCH = 32
+
+
+def pipeline_shape(where: str, ranks_per_gpu: int = 1) -> dict:
+    """Producer compute streams and consumer batch for a producer whose raw frames are ``where``
+    ("device": already in HBM; "staged": pinned host memory) on a GPU shared by ``ranks_per_gpu``
+    ranks (parallel.launch.ranks_per_gpu).  The one resolution the producer / consumer CLIs,
+    ProducerPipeline, PeakFinderConsumer and bench.py all use."""
+    if where not in PRODUCER_STREAMS:
+        raise ValueError(f"pipeline_shape: where must be one of {sorted(PRODUCER_STREAMS)}, not {where!r}")
+    shared = int(ranks_per_gpu) > 1
+    return {"producer_streams": (SHARED_GPU_PRODUCER_STREAMS if shared else PRODUCER_STREAMS)[where],
+            "consumer_batch": SHARED_GPU_CONSUMER_BATCH if shared else CONSUMER_BATCH}
+
+
 # Consumer: the peak finder's two alternating streams, each on its own hardware queue (ordinary
 # streams landed both on ONE queue: rocprofv3 Queue_Id, profiles/r3/streams2/)
 CONSUMER_STREAM_KIND = "dedicated"

@@ -39,7 +39,9 @@ def build_parser():
     ap.add_argument("--ddp", action="store_true",
                     help="--task train: data-parallel training over the consumer processes of a torchrun launch "
                          "(gradients all-reduced by RCCL on GPUs, gloo on the CPU)")
-    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per peak-finder / training batch (default: config.pipeline_shape -- 64, or 32 when "
+                         "the launch puts more ranks than GPUs on this node)")
     ap.add_argument("--prefetch", type=int, default=None,
                     help=f"read-ahead bound: frames delivered but not read yet + grants outstanding (default "
                          f"max({DEFAULT_PREFETCH}, 2 x --batch)); what a crashed consumer can lose")
@@ -70,6 +72,14 @@ def _init_data_parallel(device) -> int:
     return dist.get_rank()
 
 
+def resolve_batch(batch=None) -> int:
+    """--batch, else the library's pipeline shape for the ranks sharing this GPU (the producer CLI's
+    co-consumer and bench.py resolve the same way)."""
+    from .pipeline import resolve_consumer_batch
+
+    return resolve_consumer_batch(batch)
+
+
 def main(argv=None) -> int:
     args = build_parser().parse_args(argv)
     logging.basicConfig(level=getattr(logging, args.log_level), format="%(asctime)s - %(levelname)s - %(message)s")
@@ -78,6 +88,8 @@ def main(argv=None) -> int:
 
     from .config import PeakFinderParams
     from .data_reader import DataReader, DataReaderError, EndOfStream
+
+    args.batch = resolve_batch(args.batch)
 
     stop = {"flag": False}
 

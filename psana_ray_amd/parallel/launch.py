@@ -14,6 +14,8 @@ from typing import Optional
 _RANK = ("RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK", "SLURM_PROCID")
 _SIZE = ("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS")
 _LOCAL = ("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "PMI_LOCAL_RANK", "SLURM_LOCALID")
+_LOCAL_SIZE = ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "PMI_LOCAL_SIZE",
+               "SLURM_NTASKS_PER_NODE")
 
 
 def _first_int(names, default: Optional[int] = None) -> Optional[int]:
@@ -33,6 +35,7 @@ class LaunchInfo:
     size: int
     local_rank: int
     launcher: str
+    local_size: int = 1   # ranks of this launch on this node
 
     @property
     def distributed(self) -> bool:
@@ -55,7 +58,23 @@ def detect() -> LaunchInfo:
         launcher = "slurm"
     else:
         launcher = "single"
-    return LaunchInfo(rank, size, local, launcher)
+    local_size = _first_int(_LOCAL_SIZE, None)
+    if local_size is None:
+        local_size = size if launcher != "slurm" else 1
+    return LaunchInfo(rank, size, local, launcher, max(1, local_size))
+
+
+def ranks_per_gpu(n_gpus: Optional[int] = None, local_size: Optional[int] = None) -> int:
+    """How many ranks of this launch share one GPU of this node: ceil(local ranks / GPUs) (1 on a
+    node with a GPU per rank; `mpirun -n 4` on a one-GPU box: 4).  ``n_gpus`` default: the visible
+    GPUs (counting them does not initialise the HIP runtime); 1 without a GPU."""
+    if local_size is None:
+        local_size = detect().local_size
+    if n_gpus is None:
+        import torch
+
+        n_gpus = torch.cuda.device_count()
+    return max(1, -(-int(local_size) // max(1, int(n_gpus))))
 
 
 def device_for(local_rank: int, requested: Optional[str] = None):

@@ -25,8 +25,8 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from .config import (CONSUMER_STREAM_KIND, CONSUMER_STREAMS, PRODUCER_STREAM_KIND, PRODUCER_STREAMS, STREAM_KINDS,
-                     PeakFinderParams)
+from .config import (CONSUMER_STREAM_KIND, CONSUMER_STREAMS, PRODUCER_STREAM_KIND, STREAM_KINDS, PeakFinderParams,
+                     pipeline_shape)
 from .models.calibrator import Calibrator
 from .ops import _ext, kernels
 from .queue.endpoint import EndOfStream, FrameItem, QueueEndpoint
@@ -35,18 +35,46 @@ from .utils.tracing import trace_range
 log = logging.getLogger(__name__)
 
 
+def resolve_producer_streams(where: str, compute_streams: Optional[int] = None,
+                             ranks_per_gpu: Optional[int] = None) -> int:
+    """Producer compute streams: ``compute_streams``, else config.pipeline_shape for raw frames
+    ``where`` ("device" / "staged") on a GPU shared by ``ranks_per_gpu`` ranks (None: the launch's,
+    parallel.launch.ranks_per_gpu).  ProducerPipeline, the producer CLI and bench.py all use it."""
+    if compute_streams is not None:
+        return int(compute_streams)
+    if ranks_per_gpu is None:
+        from .parallel.launch import ranks_per_gpu as _rpg
+
+        ranks_per_gpu = _rpg()
+    return pipeline_shape(where, int(ranks_per_gpu))["producer_streams"]
+
+
+def resolve_consumer_batch(batch: Optional[int] = None, ranks_per_gpu: Optional[int] = None) -> int:
+    """Frames per peak-finder launch: ``batch``, else config.pipeline_shape for the ranks sharing
+    this GPU (PeakFinderConsumer, the producer's co-consumer, psana-ray-consumer, bench.py)."""
+    if batch is not None:
+        return int(batch)
+    if ranks_per_gpu is None:
+        from .parallel.launch import ranks_per_gpu as _rpg
+
+        ranks_per_gpu = _rpg()
+    return pipeline_shape("device", int(ranks_per_gpu))["consumer_batch"]
+
+
 class ProducerPipeline:
     def __init__(self, source, calibrator: Optional[Calibrator], endpoint: QueueEndpoint, rank: int = 0,
                  chunk: int = 32, n_raw_buffers: int = 6, acquire_timeout_s: float = 1.0,
                  log_every: int = 0, copy_workgroups: int = 32, gpu_timing: bool = False,
                  compute_streams: Optional[int] = None, stream_kind: Optional[str] = None,
-                 mask: Optional[np.ndarray] = None, n_upload_buffers: int = 3, gap_fill: Optional[bool] = None):
+                 mask: Optional[np.ndarray] = None, n_upload_buffers: int = 3, gap_fill: Optional[bool] = None,
+                 ranks_per_gpu: Optional[int] = None):
         """copy_workgroups: host->HBM staging by copy_h2d_kernel with that many workgroups (0 = the
         runtime's hipMemcpyAsync); gpu_timing: event-time each chunk's copy and calibration;
         compute_streams: chunks alternate over that many HIP streams (native engine), so one chunk's
         calibration fills the CUs its predecessor's tail leaves idle; stream_kind: their
-        hardware-queue placement (config.STREAM_KINDS).  None: config.PRODUCER_STREAMS /
-        PRODUCER_STREAM_KIND for the source (raw frames already in HBM or staged).
+        hardware-queue placement (config.STREAM_KINDS).  None: config.pipeline_shape /
+        PRODUCER_STREAM_KIND for the source (raw frames already in HBM or staged) and the number of
+        ranks sharing this GPU (``ranks_per_gpu``; None: parallel.launch.ranks_per_gpu()).
 
         gap_fill: image mode, zero the panel gaps of every frame (None: only when the ring was not
         zero-filled at creation -- ``FrameRing.zero_filled`` -- since a zeroed ring's gaps stay 0).
@@ -132,7 +160,7 @@ class ProducerPipeline:
                 self.engine.set_cycled_source([int(x) for x in ptrs],
                                               [float("nan") if v is None else float(v) for v in pe])
             where = "device" if self.engine.device_resident else "staged"
-            n_cs = PRODUCER_STREAMS[where] if compute_streams is None else int(compute_streams)
+            n_cs = resolve_producer_streams(where, compute_streams, ranks_per_gpu)
             kind = PRODUCER_STREAM_KIND[where] if stream_kind is None else stream_kind
             self.engine.set_compute_streams(n_cs, STREAM_KINDS[kind])
             self.stream_config = (n_cs, kind)
@@ -447,11 +475,13 @@ class PeakFinderConsumer:
     its stream of reads) overlaps the next launch's streaming reads instead of idling HBM."""
 
     def __init__(self, endpoint: QueueEndpoint, frame_shape, params: Optional[PeakFinderParams] = None,
-                 batch: int = 16, keep_results: bool = False, stream_kind: str = CONSUMER_STREAM_KIND,
-                 streams: int = CONSUMER_STREAMS):
+                 batch: Optional[int] = None, keep_results: bool = False, stream_kind: str = CONSUMER_STREAM_KIND,
+                 streams: int = CONSUMER_STREAMS, ranks_per_gpu: Optional[int] = None):
+        """batch: frames per peak-finder launch; None -> config.pipeline_shape for the ranks sharing
+        this GPU (``ranks_per_gpu``; None: parallel.launch.ranks_per_gpu())."""
         self.ep = endpoint
         self.params = params or PeakFinderParams()
-        self.batch = min(batch, kernels.MAX_FRAMES)
+        self.batch = min(resolve_consumer_batch(batch, ranks_per_gpu), kernels.MAX_FRAMES)
         self.device = endpoint.ring.device
         self.gpu = self.device.type == "cuda"
         self.shape = tuple(frame_shape)

@@ -26,7 +26,7 @@ from typing import Optional
 
 import numpy as np
 
-from .config import (BACKOFF_BASE_S, BACKOFF_JITTER_S, BACKOFF_MAX_S, CONSUMER_BATCH, DEFAULT_LOG_LEVEL,
+from .config import (BACKOFF_BASE_S, BACKOFF_JITTER_S, BACKOFF_MAX_S, DEFAULT_LOG_LEVEL,
                      DEFAULT_NUM_CONSUMERS,
                      DEFAULT_QUEUE_NAME, DEFAULT_QUEUE_SIZE, DEFAULT_RAY_ADDRESS, DEFAULT_RAY_NAMESPACE, LOG_LEVELS,
                      QUEUE_LOOKUP_DELAY_S, QUEUE_LOOKUP_RETRIES, CommonModeParams, PeakFinderParams,
@@ -328,7 +328,9 @@ def main(argv=None) -> int:
         registry.register("producer", pipe.metrics)
         registry.register("queue", ep.metrics)
         if co_consumer:
-            cons = PeakFinderConsumer(ep, frame_shape, PeakFinderParams(), batch=CONSUMER_BATCH)
+            # batch: config.pipeline_shape for the ranks sharing this GPU (mpirun -n 4 on fewer GPUs
+            # takes the shared-GPU shape, like bench.py)
+            cons = PeakFinderConsumer(ep, frame_shape, PeakFinderParams())
             registry.register("consumer", cons.metrics)
 
             def consume():

@@ -62,3 +62,16 @@ def test_bench_multirank_cpu(native, nproc, route, producers):
         assert all(v >= 0.9 for v in share[n_p:]), share
         assert all(c > 0 for c in d["extra"]["consumed_per_rank"]), d["extra"]["consumed_per_rank"]
         assert d["extra"]["consumer_frames_per_s"] >= 0.90 * d["extra"]["production_frames_per_s"], d["extra"]
+    # the steady-state gate replaced the fixed pre-roll (collective decision,
+    # bounded), and the line carries per-rank topology evidence of every link
+    g = d["extra"]["steady_gate"]
+    assert g is not None and g["iterations"] >= 2 and g["tol"] == 0.03, g
+    assert g["converged"] or g["seconds"] >= 10.0, g
+    t = d["extra"]["topology"]
+    assert len(t["device_per_rank"]) == nproc and len(t["outgoing_links_per_rank"]) == nproc
+    for r, links in enumerate(t["outgoing_links_per_rank"]):
+        want = (nproc - 1) if r < n_p else 0
+        assert len(links) == want, (r, links)
+        for lk in links:
+            assert set(lk) == {"peer", "consumer_device", "attached", "kernel_copy", "peer_access", "link_type", "hops"}
+            assert lk["attached"] and lk["consumer_device"] == -1 and not lk["kernel_copy"]   # host rings (CPU)

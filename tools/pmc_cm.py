@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-phase counters of the common-mode kernel from one ``cm_probe.py --pmc-pass`` rocprofv3 run.
 
-The probe launches calib_cm 3 times per flags value, in the order 0 (memory phases only),
+After one correctness launch, the probe launches calib_cm 3 times per flags value, in the order 0 (memory phases only),
 1 (+ row medians), 2 (+ column medians), 3 (both), on 32 epix10k2M frames; this prints, per flags
 value, the mean per-frame value of every counter (summed over the dispatch's instances), and the
 row / column phase deltas (flags 1 - 0, 2 - 0).
@@ -30,6 +30,7 @@ def main():
     names = sorted({k[1] for k in agg})
     if len(disp) < 12:
         raise SystemExit(f"expected 12 calib_cm dispatches, found {len(disp)}")
+    disp = disp[-12:]   # the probe's correctness launch (flags 3) comes first
     per = {}
     for flags in range(4):
         ds = disp[3 * flags:3 * flags + 3]
