@@ -6,7 +6,8 @@
 #   2. PROBE rounds interleaved across variants (base, v1, ..., base, v1, ...) so clock / thermal
 #      drift hits every build alike (PROBE default tools/cm_probe.py, ROUNDS default 3);
 #   3. PMC=1: one counter pass per variant over `cm_probe.py --pmc-pass` (VALU / LDS / conflicts);
-#   4. BENCH=1: device-resident calib + image pipelines per variant (BENCH_ROUNDS rounds).
+#   4. PMCW=1: WRITE_SIZE and FETCH_SIZE passes per variant (HBM bytes per phase);
+#   5. BENCH=1: device-resident calib + image pipelines per variant (BENCH_ROUNDS rounds).
 # Outputs: gpurun_out/${OUT:-ab}/.  Every GPU step has its own timeout; a failure ends the script.
 #   VARIANTS="net0" PMC=1 BENCH=1 gpurun -- bash tools/gpu_ab.sh
 set -o pipefail
@@ -37,6 +38,15 @@ if [ -n "${PMC:-}" ]; then
       --output-format csv -d $O/pmc_$v -o run -- python3 /tmp/tree_$v/tools/cm_probe.py --pmc-pass > $O/pmc_$v.log 2>&1 || { tail -5 $O/pmc_$v.log; exit 1; }
     python3 $R/tools/pmc_cm.py $O/pmc_$v > $O/pmc_$v.txt 2>&1 || { cat $O/pmc_$v.txt; exit 1; }
     echo "$v pmc:"; cat $O/pmc_$v.txt
+  done
+fi
+if [ -n "${PMCW:-}" ]; then   # HBM traffic per phase: WRITE_SIZE (2 TCC slots) and FETCH_SIZE (3) in separate passes
+  for v in $VS; do
+    for c in WRITE_SIZE FETCH_SIZE; do
+      timeout -s KILL 90 rocprofv3 --pmc $c GRBM_GUI_ACTIVE --output-format csv -d $O/pmc${c}_$v -o run -- python3 /tmp/tree_$v/tools/cm_probe.py --pmc-pass > $O/pmc${c}_$v.log 2>&1 || { tail -5 $O/pmc${c}_$v.log; exit 1; }
+      python3 $R/tools/pmc_cm.py $O/pmc${c}_$v > $O/pmc${c}_$v.txt 2>&1 || { cat $O/pmc${c}_$v.txt; exit 1; }
+      echo "$v $c:"; grep -v GRBM $O/pmc${c}_$v.txt
+    done
   done
 fi
 if [ -n "${BENCH:-}" ]; then
