@@ -499,12 +499,25 @@ __device__ __forceinline__ float cm_gain(const float (&ga)[NT][8], uint32_t cb, 
 // their raw value comes from the group's side slot (or, on slot overflow, is recomputed from raw
 // + pedestal in global memory); masked pixels have a zero gain factor, Jungfrau's invalid gain
 // code a zero value, so both come out 0.
+// PR_CM_LDS_PROBE = 1 (diagnostic, WRONG results): the store phase's tile reads and the flush's reads
+// use bank-conflict-free addresses instead of the tile layout's -- the timing bound of removing the
+// memory phases' LDS read conflicts (tools/lds_bank_model.py attributes all 660 conflict cycles per
+// tile to those phases: phase-1 / phase-3 b128 writes 176 + 176, phase-3 b128 reads 176, flush 132).
+#ifndef PR_CM_LDS_PROBE
+#define PR_CM_LDS_PROBE 0
+#endif
 template <int KIND, int NT>
 __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side, uint32_t cb, uint32_t slot,
                                         const float (&ga)[NT][8], const PR_GLOBAL uint16_t* raw,
                                         const float* __restrict__ ped, int64_t npix, int64_t pix, float (&o)[8]) {
+#if PR_CM_LDS_PROBE
+  tile_row = side - 8 * 1024 + 4 * (int)threadIdx.x;   // the tile base is side - R * P; 4 dwords per lane
+  const float4 t0 = *reinterpret_cast<const float4*>(tile_row);
+  const float4 t1 = *reinterpret_cast<const float4*>(tile_row + 1024);
+#else
   const float4 t0 = *reinterpret_cast<const float4*>(tile_row);
   const float4 t1 = *reinterpret_cast<const float4*>(tile_row + 4);
+#endif
   float xv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
   if (slot < kSideOverflow) {
     const float4 s0 = *reinterpret_cast<const float4*>(side + 8 * slot);
@@ -553,7 +566,11 @@ __device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C,
   PR_GLOBAL float* const ob = out + base;   // uniform tile origin; 32-bit offsets per store
   for (int e = threadIdx.x; e < R * C4; e += blockDim.x) {
     const int r = e / C4, j = e - r * C4;
+#if PR_CM_LDS_PROBE
+    const float4 v = *reinterpret_cast<const float4*>(tile + 4 * e);
+#else
     const float4 v = *reinterpret_cast<const float4*>(tile + r * P + 4 * j);
+#endif
     st_out4<1>((PR_GLOBAL float4*)(ob + (uint32_t)(r * panel_cols + 4 * j)), v);
   }
 #else

@@ -674,9 +674,10 @@ bool QueueFabric::try_attach(Link& l, double now) {
   }
   l.ipc = s->kind == 1;
   l.consumer_device = l.ipc ? s->consumer_device : -1;
-  // the copy kernel moves 16-B words between 16-B aligned slots; a frame size that is not a multiple
-  // of 16 B (an image whose H * W is not a multiple of 4) or a misaligned ring takes the runtime
-  // engine on this link instead -- decided here, once, never after frames were handed to a copy
+  // the copy kernel moves 16-B words between 16-B aligned slots; a slot size that is not a multiple
+  // of 16 B or a misaligned ring takes the runtime engine on this link instead -- decided here, once,
+  // never after frames were handed to a copy (FrameRing pads its slots to 256 B, so its rings always
+  // qualify; the check guards rings built by other code)
   l.kcopy = device_ >= 0 && l.ipc && copy_engine_ == kCopyKernel && slot_bytes_ % 16 == 0;
   for (int k = 0; l.kcopy && k < l.n; ++k) l.kcopy = l.remote[k] % 16 == 0;
   for (uint64_t p : pool_->slot_ptrs()) l.kcopy = l.kcopy && p % 16 == 0;

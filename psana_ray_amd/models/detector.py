@@ -130,7 +130,7 @@ TINY_EPIX = register(DetectorSpec("tiny_epix", "epix10ka", 2, 32, 48, 16, 24, 8,
 TINY_JUNGFRAU = register(DetectorSpec("tiny_jungfrau", "jungfrau", 2, 16, 32, 8, 16, 8, 75.0, panel_gap_px=2))
 TINY_PLAIN = register(DetectorSpec("tiny_plain", "plain", 1, 16, 16, 8, 8, 8, 100.0, panel_gap_px=2))
 # image frames of 9 x 17 pixels = 612 B, not a multiple of 16 B (like the psana raw path's
-# pix_rows.max() + 1 geometries): the fabric copies such frames with the runtime engine
+# pix_rows.max() + 1 geometries): ring slots are padded to 256 B (queue/ring.py SLOT_ALIGN)
 TINY_ODD = register(DetectorSpec("tiny_odd", "plain", 2, 9, 8, 9, 8, 8, 100.0, panel_gap_px=1))
 
 

@@ -124,7 +124,7 @@ class QueueEndpoint:
         self._producer_finished = not is_producer
         self._consumer_closed = not is_consumer
         self._views = ring.views                  # per-slot tensor views, built once
-        self._slot_bytes = ring.frame_bytes
+        self._slot_bytes = ring.slot_bytes   # the ring's slot stride (>= frame_bytes): what the fabric moves
         self._fabric = None
         self._final: dict = {}
         self._started = False

@@ -31,7 +31,7 @@ def physical_slots(logical_share: int, frame_bytes: int, device: torch.device, h
     if device.type != "cuda":
         return max(1, logical_share)
     free, _total = torch.cuda.mem_get_info(device)
-    fit = int(free * hbm_fraction) // max(1, frame_bytes) - reserve_slots
+    fit = int(free * hbm_fraction) // max(1, slot_stride(frame_bytes)) - reserve_slots
     if fit < 1:
         raise MemoryError(f"not even one {frame_bytes}-byte frame slot fits in device memory")
     if fit < logical_share:
@@ -41,6 +41,14 @@ def physical_slots(logical_share: int, frame_bytes: int, device: torch.device, h
 
 
 SEGMENT_BYTES = 1 << 30   # HBM rings are built from allocations of at most 1 GiB (HIP IPC limit, see below)
+# Slot stride alignment: every slot starts on a 256-B boundary whatever the frame size (the kernels
+# and the fabric's copy kernel move 16-B words; an assembled image of H * W pixels with H * W not a
+# multiple of 4 -- psana's pix_rows.max() + 1 geometries -- would otherwise misalign every other slot).
+SLOT_ALIGN = 256
+
+
+def slot_stride(frame_bytes: int) -> int:
+    return -(-int(frame_bytes) // SLOT_ALIGN) * SLOT_ALIGN
 
 
 class FrameRing:
@@ -65,38 +73,42 @@ class FrameRing:
             raise ValueError("ring needs at least one slot")
         esz = torch.empty((), dtype=dtype).element_size()
         self.frame_bytes = int(math.prod(self.frame_shape)) * esz
+        # slot stride (SLOT_ALIGN): the frame is a prefix of its slot; the fabric moves whole slots
+        self.slot_bytes = slot_stride(self.frame_bytes)
+        sb = self.slot_bytes
         self.shm_name = shm_name if self.device.type == "cpu" else None
         self._region = None
         self._buffers = []
-        self.segments = []     # (tensor [k, *frame_shape], first slot, k)
+        self.segments = []     # (flat uint8 tensor [k * slot_bytes], first slot, k)
         dev_index = -1
         if self.device.type == "cpu":
             if self.shm_name is not None:
                 # a host consumer's shard lives in named shared memory so producer processes write into it
-                self._region = C.ShmRegion(self.shm_name, n * self.frame_bytes, True)
+                self._region = C.ShmRegion(self.shm_name, n * sb, True)
                 flat = torch.frombuffer(self._region, dtype=torch.uint8)
             else:
-                flat = torch.empty(n * self.frame_bytes, dtype=torch.uint8)
-            self.segments.append((flat.view(dtype).view(n, *self.frame_shape), 0, n))
+                flat = torch.empty(n * sb, dtype=torch.uint8)
+            self.segments.append((flat, 0, n))
         else:
             dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
-            per = max(1, int(segment_bytes) // self.frame_bytes)
+            per = max(1, int(segment_bytes) // sb)
             for first in range(0, n, per):
                 k = min(per, n - first)
-                buf = C.DeviceBuffer(k * self.frame_bytes, dev_index)
+                buf = C.DeviceBuffer(k * sb, dev_index)
                 self._buffers.append(buf)
-                t = torch.from_dlpack(buf).view(dtype).view(k, *self.frame_shape)
-                self.segments.append((t, first, k))
+                self.segments.append((torch.from_dlpack(buf), first, k))
         # HBM rings start zeroed: slots only ever receive whole frames of the session's shape, so
         # pixels no kernel writes (the panel gaps of an assembled image) stay 0 in every slot and the
         # producer engine skips their per-frame fill (``zero_filled``; ProducerPipeline)
         self.zero_filled = False
         if self.device.type == "cuda":
             for t, _, _ in self.segments:
-                t.view(torch.uint8).zero_()
+                t.zero_()
             torch.cuda.synchronize(self.device)
             self.zero_filled = True
-        self.views = [v for t, _, _ in self.segments for v in t.unbind(0)]
+        fb = self.frame_bytes
+        self.views = [t[j * sb:j * sb + fb].view(dtype).view(self.frame_shape)
+                      for t, _, k in self.segments for j in range(k)]
         self.slot_ptrs = [int(v.data_ptr()) for v in self.views]
         self.pool = C.SlotPool(producer_slots, consumer_slots, dev_index)
         self.pool.set_slot_ptrs(self.slot_ptrs)
@@ -107,7 +119,7 @@ class FrameRing:
 
     @property
     def nbytes(self) -> int:
-        return self.n_slots * self.frame_bytes
+        return self.n_slots * self.slot_bytes
 
     def slot(self, i: int) -> torch.Tensor:
         return self.views[i]

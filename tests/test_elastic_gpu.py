@@ -143,9 +143,11 @@ def test_gpu_keeper_holds_frames_after_the_producer_exits(store_port, tmp_path):
 
 
 def test_gpu_odd_sized_image_frames_cross_processes(store_port, tmp_path):  # noqa: F811
-    """Image frames of 612 B (9 x 17 pixels: not a multiple of 16 B) between two GPU processes: the
-    producer's fabric decides at link attach that its copy kernel (16-B words) cannot move them and
-    copies that link with the runtime engine instead -- every frame bit-exact, then EOS."""
+    """Image frames of 612 B (9 x 17 pixels: not a multiple of 16 B) between two GPU processes
+    (ADVICE r4): ring slots are 256-B strided (FrameRing.slot_bytes), so every slot stays aligned for
+    the calibration kernels and the fabric's copy kernel moves whole slots -- every frame bit-exact,
+    then EOS.  (A ring whose slots are not 16-B multiples is copied by the runtime engine instead:
+    the engine is chosen per link at attach, csrc/fabric.cpp.)"""
     from tests.test_elastic_queue import producer
 
     prod = producer(store_port, 30, "--device", "cuda:0", queue_size=16, detector="tiny_odd", mode="image")

@@ -72,3 +72,22 @@ def test_backpressure_blocks_until_consumed(native):
             got += 1
     t.join(5)
     assert got == 12 and prod.full_waits > 0
+
+
+def test_ring_slots_are_256_byte_strided_for_odd_frames(native):
+    """a 9 x 17 float32 image is 612 B; its ring slots start 256-B aligned (768-B stride)
+    so the 16-B-vector kernels and the fabric's copy kernel can use every slot."""
+    import torch
+
+    from psana_ray_amd.queue import FrameRing
+
+    ring = FrameRing((1, 9, 17), torch.float32, torch.device("cpu"), 3, 4)
+    assert ring.frame_bytes == 612 and ring.slot_bytes == 768
+    ptrs = ring.slot_ptrs
+    assert all(b - a == 768 for a, b in zip(ptrs, ptrs[1:]))
+    assert all(p % 16 == 0 for p in ptrs)
+    for i in range(ring.n_slots):
+        v = ring.slot(i)
+        assert v.shape == (1, 9, 17) and v.is_contiguous() and v.data_ptr() == ptrs[i]
+    ring.slot(1).fill_(7.0)
+    assert float(ring.slot(0).sum()) == 0.0 and float(ring.slot(2).sum()) == 0.0

@@ -292,11 +292,20 @@ def test_copy_runs_kernel_bitwise(cuda_device, native, wgs):
 def test_mask_frames_kernel_matches_where(cuda_device, shape, n):
     """psana-calibrated upload path: one mask_frames launch per <= 64 frames equals
     np.where(mask, data, 0) (psana_ray/producer.py:92-95) bit for bit, 4-pixel body and scalar tail."""
+    from psana_ray_amd.queue.ring import slot_stride
+
     g = torch.Generator().manual_seed(5)
-    frames = torch.randn((n, *shape), generator=g).to(cuda_device)
+    data = torch.randn((n, *shape), generator=g).to(cuda_device)
     keep = torch.rand(shape, generator=g) > 0.3
     zero = (~keep).reshape(-1).to(torch.uint8).to(cuda_device)
-    ref = torch.where(keep.to(cuda_device), frames, torch.zeros_like(frames))
-    kernels.mask_frames([frames[i] for i in range(n)], zero)
+    ref = torch.where(keep.to(cuda_device), data, torch.zeros_like(data))
+    # frames in ring-like slots: 256-B aligned starts whatever the frame size (FrameRing.slot_bytes)
+    fb = data[0].numel() * 4
+    sb = slot_stride(fb)
+    buf = torch.zeros(n * sb, dtype=torch.uint8, device=cuda_device)
+    frames = [buf[i * sb:i * sb + fb].view(torch.float32).view(shape) for i in range(n)]
+    for i in range(n):
+        frames[i].copy_(data[i])
+    kernels.mask_frames(frames, zero)
     torch.cuda.synchronize()
-    _assert_equal(frames, ref, f"mask_frames {shape}")
+    _assert_equal(torch.stack(frames), ref, f"mask_frames {shape}")
