@@ -36,7 +36,7 @@ if [ -n "${PMC:-}" ]; then
   for v in $VS; do
     timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE \
       --output-format csv -d $O/pmc_$v -o run -- python3 /tmp/tree_$v/tools/cm_probe.py --pmc-pass > $O/pmc_$v.log 2>&1 || { tail -5 $O/pmc_$v.log; exit 1; }
-    python3 $R/tools/pmc_cm.py $O/pmc_$v > $O/pmc_$v.txt 2>&1 || { cat $O/pmc_$v.txt; exit 1; }
+    python3 $R/tools/pmc_table.py --cm-phases $O/pmc_$v > $O/pmc_$v.txt 2>&1 || { cat $O/pmc_$v.txt; exit 1; }
     echo "$v pmc:"; cat $O/pmc_$v.txt
   done
 fi
@@ -44,7 +44,7 @@ if [ -n "${PMCW:-}" ]; then   # HBM traffic per phase: WRITE_SIZE (2 TCC slots) 
   for v in $VS; do
     for c in WRITE_SIZE FETCH_SIZE; do
       timeout -s KILL 90 rocprofv3 --pmc $c GRBM_GUI_ACTIVE --output-format csv -d $O/pmc${c}_$v -o run -- python3 /tmp/tree_$v/tools/cm_probe.py --pmc-pass > $O/pmc${c}_$v.log 2>&1 || { tail -5 $O/pmc${c}_$v.log; exit 1; }
-      python3 $R/tools/pmc_cm.py $O/pmc${c}_$v > $O/pmc${c}_$v.txt 2>&1 || { cat $O/pmc${c}_$v.txt; exit 1; }
+      python3 $R/tools/pmc_table.py --cm-phases $O/pmc${c}_$v > $O/pmc${c}_$v.txt 2>&1 || { cat $O/pmc${c}_$v.txt; exit 1; }
       echo "$v $c:"; grep -v GRBM $O/pmc${c}_$v.txt
     done
   done

@@ -1,10 +1,10 @@
 # Phase stamps of the epix10k2M common-mode kernel: the stamps build (variants/_C_stamps.so, built
-# beforehand with tools/build_variant.py stamps common_mode.hip -DPR_CM_STAMPS=1) in a copy of the
-# tree, its CM tests, then tools/cm_stamps.py
+# beforehand: python tools/build_variant.py stamps common_mode.hip -DPR_CM_STAMPS=1) in a copy of
+# the tree, its bit-exact CM tests, then tools/cm_stamps.py (per-wave phase durations).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
-O=$R/gpurun_out/cm_stamps
+O=$R/gpurun_out/${OUT:-cm_stamps}
 mkdir -p $O
 SO=psana_ray_amd/_C.cpython-310-x86_64-linux-gnu.so
 T=/tmp/tree_stamps

@@ -1,18 +1,21 @@
 #!/usr/bin/env python3
-"""Per-kernel counter table of tools/pmc_r4.py runs.
+"""Per-kernel counter table of tools/pmc_workload.py runs.
 
-    python tools/pmc_r4_summary.py PHASES.json TRACE_DIR PASS_DIR [PASS_DIR ...] > table.md
+    python tools/pmc_table.py PHASES.json TRACE_DIR PASS_DIR [PASS_DIR ...] > table.md
+    python tools/pmc_table.py --cm-phases PASS_DIR [FRAMES]      (per-phase common-mode counters)
 
 TRACE_DIR: a ``--kernel-trace`` run (durations); PASS_DIRs: ``--pmc`` runs.  Dispatches are
-labelled by the phase list pmc_r4.py wrote (the LAST dispatches of each kernel family, in phase
+labelled by the phase list pmc_workload.py wrote (the LAST dispatches of each kernel family, in phase
 order).  Bytes: FETCH_SIZE x 2 (gfx950 tallies a wide coalesced stream's 128-B requests at 64 B,
 /opt/skills/guides/MI355X_MICROARCH.md:297-299), WRITE_SIZE as reported; both in KB per dispatch.
 Mean waves per SIMD = 4 x SQ_WAVE_CYCLES (quad-cycles) / (cycles x 1024 SIMDs), cycles =
 GRBM_GUI_ACTIVE / 8 XCDs."""
+import argparse
 import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 FAMILY = {"cm": "calib_cm_net_kernel", "cm_image": "calib_cm_net_kernel", "peakfind": "peakfind_range_kernel",
@@ -97,5 +100,35 @@ def main():
     print("```")
 
 
+def cm_phases(argv):
+    """One ``cm_probe.py --pmc-pass`` run: after its correctness launch the probe launches calib_cm 3
+    times per flags value, in the order 0 (memory phases only), 1 (+ row medians), 2 (+ column
+    medians), 3 (both), on 32 epix10k2M frames; prints per flags value the mean per-frame value of
+    every counter (summed over the dispatch's instances) and the row / column phase deltas."""
+    a = argparse.Namespace(dir=argv[0], frames=int(argv[1]) if len(argv) > 1 else 32)
+    agg = collections.defaultdict(float)
+    for f in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "calib_cm" not in r.get("Kernel_Name", ""):
+                continue
+            agg[(int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])
+    disp = sorted({k[0] for k in agg})
+    names = sorted({k[1] for k in agg})
+    if len(disp) < 12:
+        raise SystemExit(f"expected 12 calib_cm dispatches, found {len(disp)}")
+    disp = disp[-12:]   # the probe's correctness launch (flags 3) comes first
+    per = {}
+    for flags in range(4):
+        ds = disp[3 * flags:3 * flags + 3]
+        per[flags] = {n: sum(agg[(d, n)] for d in ds) / len(ds) / a.frames for n in names}
+    print("counter (per frame) | flags0 | flags1 | flags2 | flags3 | rows (1-0) | cols (2-0)")
+    for n in names:
+        v = [per[f][n] for f in range(4)]
+        print(f"{n} | " + " | ".join(f"{x:,.0f}" for x in v) + f" | {v[1] - v[0]:,.0f} | {v[2] - v[0]:,.0f}")
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--cm-phases":
+        cm_phases(sys.argv[2:])
+        sys.exit(0)
     main()

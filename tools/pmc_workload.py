@@ -9,7 +9,7 @@ its kernel REPEAT times on 64 epix10k2M frames (the producer's chunk), in this o
   xcopy     copy_runs_kernel: 64 calibrated frames HBM -> HBM in one launch (the fabric's copy)
 
 Run it under rocprofv3 (--pmc passes, and --kernel-trace --stats for durations);
-tools/pmc_r4_summary.py turns the CSVs into the per-kernel table.  Writes the phase list to
+tools/pmc_table.py turns the CSVs into the per-kernel table.  Writes the phase list to
 ``--phases`` (JSON) so the summary can label dispatches."""
 import argparse
 import json
