@@ -7,8 +7,11 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
 Behind it, every producer rank streams raw epix10k2M frames from a pinned host pool into HBM
 (our copy kernel on a side stream), calibrates them with the HIP kernels (pedestal + gain
 switching + common mode + mask) directly into its ring slots, and the queue routes them to the
-consumer shards.  W untimed warmup steps, then exactly K timed steps bracketed by a barrier +
-device synchronisation; the time is the MAX over ranks; rank 0 prints ONE JSON line.  ``value``
+consumer shards.  A steady-state gate (untimed windows of ~0.25 s until two consecutive ones agree
+within 3 % on every rank, bounded at 10 s; ``extra.steady_gate``), then W untimed warmup steps,
+then exactly K timed steps bracketed by a barrier + device synchronisation; the time is the MAX
+over ranks; rank 0 prints ONE JSON line (with every rank's GPU and fabric links, peer access and
+xGMI link type / hops, under ``extra.topology``).  ``value``
 = total frames/s of the node (headline phase: ``--route``, default balanced -- frames stay on the
 GPU that produced them unless another shard is starving).
 
