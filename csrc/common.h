@@ -141,6 +141,7 @@ __device__ __forceinline__ uint4 ld_nt_u4(const PR_GLOBAL uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 // 16-B global store (HIP_vector_type has no address-space-qualified operator=)
 __device__ __forceinline__ void st_f4(PR_GLOBAL float4* p, const float4 v) {
   f32x4_t x;

@@ -61,7 +61,8 @@
 #define PR_CM_RAW_NT 1
 #endif
 // Output stores of the production kernels: 0 = plain; 1 = non-temporal (streaming) for calib-mode
-// frames; 2 = non-temporal for the image placement too.  Same-box A/B, device-resident pipeline
+// frames; 2 = non-temporal for the image placement too; 3 = calib-mode frames non-temporal for the
+// 128-B lines a tile row owns, plain for the lines it shares with its neighbour tile (cm_flush).  Same-box A/B, device-resident pipeline
 // (common mode + peak finder), two boxes (profiles/r4/cm_pass1, cm_pass2): level 1 calib 144.6k /
 // 145.0k / 144.9k / 143.6k vs plain 140.6k / 141.3k / 141.2k / 139.8k fr/s (+2.7 %), image mode
 // unchanged; level 2 costs image mode 13 % (100.9k vs 115.8k: partial-line image runs).  Kernel
@@ -495,6 +496,22 @@ __device__ __forceinline__ float cm_gain(const float (&ga)[NT][8], uint32_t cb, 
   }
 }
 
+// NaN-fill: x if x is a number, else s -- ONE v_med3_f32 instead of v_cmp_u + v_cndmask.  With no
+// NaN operand med3(x, s, x) = x; with a NaN operand v_med3_f32 returns v_min3_f32 of its operands,
+// whose minNum semantics drop the NaNs: med3(NaN, s, NaN) = s (s is never NaN: a raw value or a
+// recomputed ADU - pedestal).  The third operand is an opaque copy of x, so the compiler cannot fold
+// med3(x, s, x) to x.
+#ifndef PR_CM_MED3_FILL
+#define PR_CM_MED3_FILL 1
+#endif
+__device__ __forceinline__ float nan_fill(float x, float s) {
+#if PR_CM_MED3_FILL
+  return __builtin_amdgcn_fmed3f(x, s, x);
+#else
+  return x != x ? s : x;
+#endif
+}
+
 // Store-phase output of one 8-pixel group.  NaN tile entries are pixels that were not CM-eligible:
 // their raw value comes from the group's side slot (or, on slot overflow, is recomputed from raw
 // + pedestal in global memory); masked pixels have a zero gain factor, Jungfrau's invalid gain
@@ -524,7 +541,7 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
     const float4 s1 = *reinterpret_cast<const float4*>(side + 8 * slot + 4);
     const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xv[j] = xv[j] != xv[j] ? sv[j] : xv[j];
+    for (int j = 0; j < 8; ++j) xv[j] = nan_fill(xv[j], sv[j]);
   } else if (slot == kSideOverflow) {
     const uint4 rw = ld_nt_u4((const PR_GLOBAL uint4*)(raw + pix));
     float pa[NT][8];
@@ -533,7 +550,7 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
     uint32_t el, cb2;
     cm_decode8<KIND, NT>(rw, 0u, pa, v, el, cb2);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xv[j] = xv[j] != xv[j] ? v[j] : xv[j];
+    for (int j = 0; j < 8; ++j) xv[j] = nan_fill(xv[j], v[j]);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = gmul(xv[j], cm_gain<NT>(ga, cb, j));
@@ -547,7 +564,7 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
 // Frame layout: 16 B per lane, consecutive lanes along tile rows.
 template <int LEVEL>
 __device__ __forceinline__ void st_out4(PR_GLOBAL float4* p, const float4 v) {
-  if constexpr (PR_CM_NT_STORE >= LEVEL) {
+  if constexpr (LEVEL == 1 ? PR_CM_NT_STORE >= 1 : PR_CM_NT_STORE == 2) {
     f32x4_t x;
     x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
     __builtin_nontemporal_store(x, (PR_GLOBAL f32x4_t*)p);
@@ -556,22 +573,71 @@ __device__ __forceinline__ void st_out4(PR_GLOBAL float4* p, const float4 v) {
   }
 }
 
+// Flush of the float4 chunks [j0, j0 + nj) of every tile row; NT: streaming (non-temporal) stores.
+template <bool NT>
+__device__ __forceinline__ void cm_flush_cols(const float* tile, int P, int R, PR_GLOBAL float* ob, int panel_cols,
+                                              int j0, int nj) {
+  if (nj <= 0) return;
+  // (row, chunk) advance incrementally by blockDim.x chunks per iteration (one division per thread)
+  const int dr = (int)blockDim.x / nj, dj = (int)blockDim.x - dr * nj;
+  int r = (int)threadIdx.x / nj, j = (int)threadIdx.x - r * nj;
+  for (int e = threadIdx.x; e < R * nj; e += blockDim.x) {
+    const float4 v = *reinterpret_cast<const float4*>(tile + r * P + 4 * (j0 + j));
+    PR_GLOBAL float4* d = (PR_GLOBAL float4*)(ob + (uint32_t)(r * panel_cols + 4 * (j0 + j)));
+    if constexpr (NT) st_out4<1>(d, v);
+    else st_f4(d, v);
+    r += dr;
+    j += dj;
+    if (j >= nj) {
+      j -= nj;
+      ++r;
+    }
+  }
+}
+
+// PR_CM_NT_STORE = 3 (calib mode): non-temporal stores for the 128-B lines a tile row owns whole, plain
+// stores for the lines it shares with its neighbour tile (a 48-float stripe row is 192 B: every other
+// line is half this tile's, half the next one's).  A streaming store evicts its partial line before the
+// neighbour's half arrives, so the L2 writes it back twice: +9 % WRITE_SIZE per frame with every store
+// non-temporal (profiles/r5/README.md); the neighbour tile of the same frame runs on the same XCD
+// (table-major order, 64 frames per launch), so a plain store's half line waits in L2 for its partner.
 __device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C, PR_GLOBAL float* out, int64_t base,
                                          int panel_cols) {
   const int C4 = C >> 2;
+#if PR_CM_NT_STORE == 3 && !PR_CM_LDS_PROBE
+  if ((panel_cols & 31) == 0) {   // every tile row starts at the same offset within its 128-B line
+    PR_GLOBAL float* const ob = out + base;
+    const int s = (int)(reinterpret_cast<uintptr_t>(ob) & 127);        // byte offset of the rows in their lines
+    const int jlo = min(C4, ((128 - s) & 127) >> 4);                    // first chunk of a whole line
+    const int jhi = max(jlo, (((s + 16 * C4) & ~127) - s) >> 4);        // end of the last whole line
+    cm_flush_cols<true>(tile, P, R, ob, panel_cols, jlo, jhi - jlo);
+    cm_flush_cols<false>(tile, P, R, ob, panel_cols, 0, jlo);
+    cm_flush_cols<false>(tile, P, R, ob, panel_cols, jhi, C4 - jhi);
+    return;
+  }
+#endif
 #ifndef PR_CM_FLUSH32
 #define PR_CM_FLUSH32 PR_CM_OFF32
 #endif
 #if PR_CM_FLUSH32
   PR_GLOBAL float* const ob = out + base;   // uniform tile origin; 32-bit offsets per store
+  // (row, float4 column) of element e advance incrementally by blockDim.x elements per iteration:
+  // one integer division per thread instead of one per element
+  const int dr = (int)blockDim.x / C4, dj = (int)blockDim.x - dr * C4;
+  int r = (int)threadIdx.x / C4, j = (int)threadIdx.x - r * C4;
   for (int e = threadIdx.x; e < R * C4; e += blockDim.x) {
-    const int r = e / C4, j = e - r * C4;
 #if PR_CM_LDS_PROBE
     const float4 v = *reinterpret_cast<const float4*>(tile + 4 * e);
 #else
     const float4 v = *reinterpret_cast<const float4*>(tile + r * P + 4 * j);
 #endif
     st_out4<1>((PR_GLOBAL float4*)(ob + (uint32_t)(r * panel_cols + 4 * j)), v);
+    r += dr;
+    j += dj;
+    if (j >= C4) {
+      j -= C4;
+      ++r;
+    }
   }
 #else
   for (int e = threadIdx.x; e < R * C4; e += blockDim.x) {
@@ -1143,6 +1209,10 @@ __device__ __forceinline__ void cm_rows(float* tile, const int P, const int R, c
   }
 }
 
+// PR_CM_PK_COLSUB = 0: the column correction one v_sub_f32 per row (A/B of the packed form)
+#ifndef PR_CM_PK_COLSUB
+#define PR_CM_PK_COLSUB 1
+#endif
 // Column medians, FOUR lanes (a quad) per column, M rows each (t0 a multiple of 4).
 //  Sign domain: the odd lane of each pair (q = 1, 3) holds its values NEGATED, so both lanes of a
 //  pair run identical instructions where the classic merge-split needs lane-dependent min / max:
@@ -1231,10 +1301,21 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
     const float med = (k_lo + ((cnt & 1) ? k_lo : k_hi)) * 0.5f;
     asm volatile("" ::: "memory");
     if (act && cnt >= cp.npix_min && cnt > 0 && fabsf(med) <= cp.maxcorr) {
+      // every element minus the median (NaN -- non-eligible -- stays NaN), two rows per v_pk_add_f32:
+      // rows 2j and 2j + 1 of a lane are one ds_read2_b32 / ds_write2_b32 pair
+      const f32x2_t m2 = {med, med};
 #pragma unroll
-      for (int i = 0; i < M; ++i) {
-        if (row_of(i) < R) colp[off_of(i)] -= med;   // NaN (non-eligible) stays NaN
-        if ((i & 15) == 15) asm volatile("" ::: "memory");
+      for (int i = 0; i < M; i += 2) {
+        if (PR_CM_PK_COLSUB && row_of(i + 1) < R) {
+          f32x2_t v = {colp[off_of(i)], colp[off_of(i + 1)]};
+          v -= m2;
+          colp[off_of(i)] = v.x;
+          colp[off_of(i + 1)] = v.y;
+        } else {
+          if (row_of(i) < R) colp[off_of(i)] -= med;
+          if (!PR_CM_PK_COLSUB && row_of(i + 1) < R) colp[off_of(i + 1)] -= med;
+        }
+        if ((i & 14) == 14) asm volatile("" ::: "memory");
       }
     }
   }
