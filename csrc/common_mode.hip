@@ -370,6 +370,33 @@ __device__ __forceinline__ void cm_decode8(const uint4 rw, const uint32_t ep, co
   }
 }
 
+// PR_CM_BASE_FAST = 1: wave-uniform fast paths for items in which no pixel of the whole wave left the
+// first candidate table (no gain switch: epix10ka bit 14 / Jungfrau bits 14-15 clear everywhere) --
+// in the decode (v = ADU - table-0 pedestal, no per-pixel mask / select, no candidate bits) and in
+// the store phase (table-0 gain factor, no per-pixel select).  Gain switching marks bright pixels
+// only (synthetic epix10k2M: 2e-5 of the 8-pixel groups), so nearly every item takes them; a wave
+// that meets one switched pixel runs the general path for that item.
+#ifndef PR_CM_BASE_FAST
+#define PR_CM_BASE_FAST 1
+#endif
+template <int KIND>
+__device__ __forceinline__ bool cm_base_only(const uint4 rw) {
+  const uint32_t b = rw.x | rw.y | rw.z | rw.w;
+  if constexpr (KIND == kEpix10ka) return (b & 0x40004000u) == 0u;
+  else if constexpr (KIND == kJungfrau) return (b & 0xC000C000u) == 0u;
+  else return true;
+}
+// cm_decode8 for a group whose pixels all decode to candidate 0 (cm_base_only)
+template <int KIND>
+__device__ __forceinline__ void cm_decode8_base(const uint4 rw, const uint32_t ep, const float (&pa0)[8], float (&v)[8],
+                                                uint32_t& el) {
+  const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    v[j] = (float)__builtin_amdgcn_ubfe(w[j >> 1], 16 * (j & 1), KIND == kPlain ? 16 : 14) - pa0[j];
+  el = ep & 0xFFu;
+}
+
 // tile value: v where eligible, NaN elsewhere
 __device__ __forceinline__ void cm_tile_values(const float (&v)[8], uint32_t el, float (&x)[8]) {
   const uint32_t qnan = 0x7fc00000u;
@@ -523,7 +550,7 @@ __device__ __forceinline__ float nan_fill(float x, float s) {
 #ifndef PR_CM_LDS_PROBE
 #define PR_CM_LDS_PROBE 0
 #endif
-template <int KIND, int NT>
+template <int KIND, int NT, bool BASE = false>
 __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side, uint32_t cb, uint32_t slot,
                                         const float (&ga)[NT][8], const PR_GLOBAL uint16_t* raw,
                                         const float* __restrict__ ped, int64_t npix, int64_t pix, float (&o)[8]) {
@@ -553,7 +580,7 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
     for (int j = 0; j < 8; ++j) xv[j] = nan_fill(xv[j], v[j]);
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = gmul(xv[j], cm_gain<NT>(ga, cb, j));
+  for (int j = 0; j < 8; ++j) o[j] = gmul(xv[j], BASE ? ga[0][j] : cm_gain<NT>(ga, cb, j));
 }
 
 // Store phase, part 2.  Part 1 leaves the finished output tile in LDS; part 2 only reads LDS
@@ -1111,7 +1138,9 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
     float v[8];
     uint32_t el = 0xFFu, cb = 0;
     if (act) {
-      {
+      if (PR_CM_BASE_FAST && NT > 1 && __builtin_amdgcn_ballot_w64(!cm_base_only<KIND>(rw[u])) == 0) {
+        cm_decode8_base<KIND>(rw[u], ep[u], pa0[u][0], v, el);   // wave-uniform: no switched pixel
+      } else {
         float pa[NT][8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) pa[0][j] = pa0[u][0][j];
@@ -1455,13 +1484,18 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
           float ga[NT][8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) ga[0][j] = g0[u][0][j];
-#if PR_CM_OFF32
-          if constexpr (NT > 1) load8o<NT>(gf_t, (uint32_t)(r * tg.panel_cols + c), cm_need<NT>(cbs[u]), ga, 1);
-#else
-          if constexpr (NT > 1) load8<NT>(gfp, tg.npix, pix, cm_need<NT>(cbs[u]), ga, 1);
-#endif
           float o[8];
-          cm_out8<KIND, NT>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, pedp, tg.npix, pix, o);
+          if (PR_CM_BASE_FAST && NT > 1 && __builtin_amdgcn_ballot_w64(cbs[u] != 0u) == 0) {
+            // wave-uniform: every pixel of the item takes the table-0 gain factor
+            cm_out8<KIND, NT, true>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, pedp, tg.npix, pix, o);
+          } else {
+#if PR_CM_OFF32
+            if constexpr (NT > 1) load8o<NT>(gf_t, (uint32_t)(r * tg.panel_cols + c), cm_need<NT>(cbs[u]), ga, 1);
+#else
+            if constexpr (NT > 1) load8<NT>(gfp, tg.npix, pix, cm_need<NT>(cbs[u]), ga, 1);
+#endif
+            cm_out8<KIND, NT>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, pedp, tg.npix, pix, o);
+          }
           cm_put8(tile + r * P + c, o);
         }
       }

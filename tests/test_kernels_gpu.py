@@ -74,6 +74,38 @@ def test_common_mode_bitwise(cuda_device, det, flags):
     _assert_equal(out, ref, f"cm{flags} {det}")
 
 
+@pytest.mark.parametrize("det", ["epix10k2M", "jungfrau4M", "tiny_epix"])
+def test_common_mode_switched_and_unswitched_waves_bitwise(cuda_device, det):
+    """The decode / store phases take a wave-uniform fast path for items with no gain-switched pixel
+    (PR_CM_BASE_FAST) and the general path otherwise: frames whose left half has a gain-switch bit on
+    ~7 % of the pixels (every wave there takes the general path) and whose right half has none (every
+    wave takes the fast path), Jungfrau also with its invalid gain code, bitwise against the golden."""
+    spec = get_detector(det)
+    consts = CalibConstants.random(spec, seed=9, gain_config="mixed", bad_fraction=0.02)
+    n = 2
+    raw, _ = generate_raw(consts, n, seed=4)
+    raw = raw.astype(np.int32)
+    rng = np.random.default_rng(2)
+    P, H, W = spec.frame_shape
+    left = np.zeros((n, P, H, W), bool)
+    left[..., : W // 2] = True
+    sw = left & (rng.random((n, P, H, W)) < 0.07)
+    raw = np.where(sw, (raw & 0x3FFF) | (1 << 14), raw & 0x3FFF if spec.kind != "plain" else raw)
+    if spec.kind == "jungfrau":   # some gain code 3 (G2) and code 2 (invalid) pixels in the left half too
+        g2 = left & (rng.random((n, P, H, W)) < 0.02)
+        bad = left & (rng.random((n, P, H, W)) < 0.01)
+        raw = np.where(g2, raw | (3 << 14), raw)
+        raw = np.where(bad, (raw & 0x3FFF) | (2 << 14), raw)
+    raw = torch.from_numpy(raw.astype(np.uint16).view(np.int16)).view(torch.uint16)
+    cm = CommonModeParams(flags=3, thr=30.0, maxcorr=50.0, npix_min=5)
+    mask = _mask(spec)
+    cal = Calibrator(consts, cuda_device, Mode.calib, mask=mask, common_mode=cm)
+    out = cal(raw.to(cuda_device))
+    torch.cuda.synchronize()
+    ref = reference.calibrate_reference(raw.to(torch.int32), consts, mask, cal.cm)
+    _assert_equal(out, ref, f"switched / unswitched waves {det}")
+
+
 def test_common_mode_even_odd_and_empty_segments(cuda_device):
     """Hand-built tile: even/odd participant counts, all-masked rows, |median| > maxcorr."""
     spec = get_detector("tiny_epix")
