@@ -11,6 +11,8 @@
 #   prof       rocprofv3 --kernel-trace --stats of both device-resident pipelines (stats CSVs kept)
 #   configs    BASELINE config 4 (Jungfrau-16M, queue_size 400000; host-staged / device-resident,
 #              rocprofv3 stats) and config 1 (256x256, in-process CPU queue)
+#   jfcm       Jungfrau-16M device-resident with common mode ON (the Jungfrau CM kernel) + its stats
+#   rehearsal4 4 ranks on the one GPU (the shared-GPU pipeline shape; `mpirun -n 4` on fewer GPUs)
 # Outputs: gpurun_out/${OUT:-checkpoint}/
 #   OUT=r5_cp STAGES="tests smoke bench" gpurun -- bash tools/gpu_checkpoint.sh
 set -o pipefail
@@ -67,6 +69,18 @@ if has configs; then
   head -4 $O/prof_jf16m/run_kernel_stats.csv | cut -c1-160
   timeout -k 10 300 python3 bench/config1_cpu_queue.py > $O/config1.json 2> $O/config1.err || { tail $O/config1.err; exit 1; }
   cut -c1-200 $O/config1.json
+fi
+if has jfcm; then
+  timeout -k 10 300 python3 bench.py --detector jungfrau16M --queue-size 400000 --batch 8 --chunk 8 --steps 150 --warmup 40 --source device --pool-frames 16 --common-mode default > $O/jf16m_cm_device.json 2> $O/jf16m_cm_device.err || { tail $O/jf16m_cm_device.err; exit 1; }
+  line $O/jf16m_cm_device.json "jf16m cm device"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_jf16m_cm -o run -- python3 bench.py --detector jungfrau16M --queue-size 400000 --batch 8 --chunk 8 --steps 150 --warmup 40 --source device --pool-frames 16 --common-mode default > $O/prof_jf16m_cm.log 2>&1 || { tail $O/prof_jf16m_cm.log; exit 1; }
+  head -4 $O/prof_jf16m_cm/run_kernel_stats.csv | cut -c1-160
+fi
+if has rehearsal4; then
+  timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) \
+    bench.py --gpus 4 --steps 40 --warmup 10 --source device > $O/n4_device.log 2>&1 || { tail -30 $O/n4_device.log; exit 1; }
+  grep '"metric"' $O/n4_device.log > $O/n4_device.json
+  python3 -c "import json;d=json.load(open('$O/n4_device.json'));x=d['extra'];c=x['xgmi_phase'];print('n4 device', d['value'], 'rpg', d['config']['ranks_per_gpu'], 'batch', d['config']['global_batch'], 'streams', x['producer_streams'], 'cross', c['frames_per_s'], c['cross_gpu_fraction'], 'gate', x['steady_gate']['iterations'], x['steady_gate']['converged'])"
 fi
 find $O -path "*prof_*" -type f ! -name "*stats.csv" ! -name "*.log" -delete 2>/dev/null
 du -sh $O
