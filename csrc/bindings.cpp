@@ -196,14 +196,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("calib_cm",
         [](const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, uint64_t ped, uint64_t gf,
            uint64_t elig, int kind, int n_panels, int panel_rows, int panel_cols, int asic_rows,
-           int asic_cols, float thr, float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream) {
+           int asic_cols, float thr, float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream,
+           uint64_t ped_sg) {
           pr::launch_calib_cm(make_ptrs(in, out), (int)in.size(), ped, gf, elig, kind, n_panels, panel_rows,
-                              panel_cols, asic_rows, asic_cols, thr, maxcorr, npix_min, flags, bank_cols, stream);
+                              panel_cols, asic_rows, asic_cols, thr, maxcorr, npix_min, flags, bank_cols, stream, 0, 0,
+                              0, ped_sg);
         },
         py::arg("raw_ptrs"), py::arg("out_ptrs"), py::arg("ped"), py::arg("gf"), py::arg("elig"),
         py::arg("kind"), py::arg("n_panels"), py::arg("panel_rows"), py::arg("panel_cols"),
         py::arg("asic_rows"), py::arg("asic_cols"), py::arg("thr"), py::arg("maxcorr"), py::arg("npix_min"),
-        py::arg("flags"), py::arg("bank_cols"), py::arg("stream"));
+        py::arg("flags"), py::arg("bank_cols"), py::arg("stream"), py::arg("ped_sg") = 0);
   m.def("cm_lds_bytes", &pr::cm_lds_bytes, py::arg("asic_rows"), py::arg("asic_cols"), py::arg("kind"));
   m.def("cm_tile_cols", &pr::cm_tile_cols, py::arg("asic_rows"), py::arg("asic_cols"), py::arg("bank_cols"),
         py::arg("max_cols") = 0, py::arg("kind") = 0);
@@ -538,6 +540,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ped", &pr::CalibPlan::ped)
       .def_readwrite("gf", &pr::CalibPlan::gf)
       .def_readwrite("elig", &pr::CalibPlan::elig)
+      .def_readwrite("ped_sg", &pr::CalibPlan::ped_sg)
       .def_readwrite("n_panels", &pr::CalibPlan::n_panels)
       .def_readwrite("panel_rows", &pr::CalibPlan::panel_rows)
       .def_readwrite("panel_cols", &pr::CalibPlan::panel_cols)

@@ -326,35 +326,57 @@ __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
 // Decode one 8-pixel group: v = ADU - pedestal (0 for Jungfrau's invalid gain code), el = CM
 // eligibility bits, cbits = candidate bits for the store phase.
 //   rw: raw words (2 pixels each), pa: candidate pedestals, ep: eligibility bit-planes
-template <int KIND, int NT>
+// SG (signed pedestal tables, CalibConstants.cm_signed_pedestals): the pedestal of a pixel that is
+// not CM-eligible for that candidate is stored negated -- the tables carry the eligibility in their
+// sign bits (every pedestal is >= +0), so v = ADU - |p| and no bit-plane is loaded (ep unused).
+template <int KIND, int NT, bool SG = false>
 __device__ __forceinline__ void cm_decode8(const uint4 rw, const uint32_t ep, const float (&pa)[NT][8], float (&v)[8],
                                            uint32_t& el, uint32_t& cbits) {
   const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
   uint32_t c0 = 0, c1 = 0;   // candidate bit planes (bit j of pixel j): gain bit 14 / 15
+  uint32_t es = 0;           // SG: eligibility from the selected pedestal's sign
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const uint32_t wj = w[j >> 1];
     const int sh = 16 * (j & 1);
     if constexpr (KIND == kPlain) {
-      v[j] = (float)__builtin_amdgcn_ubfe(wj, sh, 16) - pa[0][j];
+      const float p = pa[0][j];
+      v[j] = (float)__builtin_amdgcn_ubfe(wj, sh, 16) - (SG ? fabsf(p) : p);
+      if constexpr (SG) es |= ((~__float_as_uint(p)) >> 31) << j;
     } else {
       const float adu = (float)__builtin_amdgcn_ubfe(wj, sh, 14);
       const uint32_t g0 = (uint32_t)__builtin_amdgcn_sbfe((int)wj, sh + 14, 1);   // all ones: gain bit 14
       if constexpr (KIND == kEpix10ka) {
-        v[j] = adu - __uint_as_float(bfi(g0, __float_as_uint(pa[1][j]), __float_as_uint(pa[0][j])));
+        const float p = __uint_as_float(bfi(g0, __float_as_uint(pa[1][j]), __float_as_uint(pa[0][j])));
+        v[j] = adu - (SG ? fabsf(p) : p);
+        if constexpr (SG) es |= ((~__float_as_uint(p)) >> 31) << j;
         c0 |= g0 & (1u << j);
       } else {   // Jungfrau: gain bits 0 -> G0, 1 -> G1, 3 -> G2, 2 -> invalid (never eligible, output 0)
         const uint32_t g1 = (uint32_t)__builtin_amdgcn_sbfe((int)wj, sh + 15, 1);
         const uint32_t p01 = (g0 & __float_as_uint(pa[1][j])) | (~g0 & __float_as_uint(pa[0][j]));
         const uint32_t sel2 = g0 & g1;
-        const float vj = adu - __uint_as_float((sel2 & __float_as_uint(pa[2][j])) | (~sel2 & p01));
+        const float p = __uint_as_float((sel2 & __float_as_uint(pa[2][j])) | (~sel2 & p01));
+        const float vj = adu - (SG ? fabsf(p) : p);
         v[j] = __uint_as_float(__float_as_uint(vj) & ~(~g0 & g1));
+        if constexpr (SG) es |= (((~__float_as_uint(p)) >> 31) & ~((~g0 & g1) >> 31)) << j;   // invalid: never
         c0 |= g0 & (1u << j);
         c1 |= g1 & (1u << j);
       }
     }
   }
-  if constexpr (NT == 1) {
+  if constexpr (SG) {
+    el = es;
+    if constexpr (NT == 1) {
+      cbits = 0;
+    } else if constexpr (NT == 2) {
+      cbits = c0;
+    } else {
+      uint32_t cb = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cb |= ((((c0 >> j) & 1u) + (((c0 & c1) >> j) & 1u)) << (2 * j));
+      cbits = cb;
+    }
+  } else if constexpr (NT == 1) {
     el = ep & 0xFFu;
     cbits = 0;
   } else if constexpr (NT == 2) {
@@ -395,6 +417,24 @@ __device__ __forceinline__ void cm_decode8_base(const uint4 rw, const uint32_t e
   for (int j = 0; j < 8; ++j)
     v[j] = (float)__builtin_amdgcn_ubfe(w[j >> 1], 16 * (j & 1), KIND == kPlain ? 16 : 14) - pa0[j];
   el = ep & 0xFFu;
+}
+
+// cm_decode8_base for signed pedestal tables: the tile values straight from the sign bits (v where
+// the pedestal is >= +0, NaN where it is negated); returns true when some pixel is not eligible
+template <int KIND>
+__device__ __forceinline__ bool cm_decode8_base_sg(const uint4 rw, const float (&pa0)[8], float (&v)[8], float (&x)[8]) {
+  const uint32_t w[4] = {rw.x, rw.y, rw.z, rw.w};
+  const uint32_t qnan = 0x7fc00000u;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float p = pa0[j];
+    v[j] = (float)__builtin_amdgcn_ubfe(w[j >> 1], 16 * (j & 1), KIND == kPlain ? 16 : 14) - fabsf(p);
+    const uint32_t m = (uint32_t)((int)__float_as_uint(p) >> 31);
+    x[j] = __uint_as_float(bfi(m, qnan, __float_as_uint(v[j])));
+    acc |= m;
+  }
+  return acc != 0u;
 }
 
 // tile value: v where eligible, NaN elsewhere
@@ -550,7 +590,7 @@ __device__ __forceinline__ float nan_fill(float x, float s) {
 #ifndef PR_CM_LDS_PROBE
 #define PR_CM_LDS_PROBE 0
 #endif
-template <int KIND, int NT, bool BASE = false>
+template <int KIND, int NT, bool BASE = false, bool SG = false>
 __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side, uint32_t cb, uint32_t slot,
                                         const float (&ga)[NT][8], const PR_GLOBAL uint16_t* raw,
                                         const float* __restrict__ ped, int64_t npix, int64_t pix, float (&o)[8]) {
@@ -575,7 +615,7 @@ __device__ __forceinline__ void cm_out8(const float* tile_row, const float* side
     load8<NT>(ped, npix, pix, need_from_raw<NT>(rw), pa);
     float v[8];
     uint32_t el, cb2;
-    cm_decode8<KIND, NT>(rw, 0u, pa, v, el, cb2);
+    cm_decode8<KIND, NT, SG>(rw, 0u, pa, v, el, cb2);
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = nan_fill(xv[j], v[j]);
   }
@@ -657,6 +697,9 @@ __device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C,
     const float4 v = *reinterpret_cast<const float4*>(tile + 4 * e);
 #else
     const float4 v = *reinterpret_cast<const float4*>(tile + r * P + 4 * j);
+#endif
+#if PR_CM_MEMPROBE & 8
+    if (__float_as_uint(v.x) == 0x7fc01234u)   // never: the flush's LDS reads and loop stay, the stores go
 #endif
     st_out4<1>((PR_GLOBAL float4*)(ob + (uint32_t)(r * panel_cols + 4 * j)), v);
     r += dr;
@@ -863,9 +906,8 @@ struct TileCoord {
 // off; an XCD-grouping remap of the table-major order changed nothing, 4.75 vs 4.65, and an
 // XCD-local frame-major order lost, 5.29 vs 4.90.)
 // With tg.fpw > 1 a workgroup takes fpw consecutive frames of its tile (t.f = the first).
-__device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C) {
+__device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C, const int id = (int)blockIdx.x) {
   TileCoord t;
-  const int id = (int)blockIdx.x;
   const int ng = (tg.nframes + tg.fpw - 1) / tg.fpw;
   const int tile = id / ng;
   t.f = (id - tile * ng) * tg.fpw;
@@ -876,6 +918,32 @@ __device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C)
   t.ac = (tile % per_panel) % tg.asics_per_row;
   t.base = (int64_t)t.panel * tg.panel_rows * tg.panel_cols + (int64_t)t.ar * R * tg.panel_cols + (int64_t)t.ac * C;
   return t;
+}
+
+// PR_CM_RAW_PF = D > 0: during the row phase the wave the medians leave idle (threads >= 192 of the
+// epix10k2M kernel: 176 row segments, 48 x 4 column lanes) touches every 128-B line of the raw tile of
+// workgroup blockIdx + D, which runs on the same XCD (workgroups go to XCDs round-robin, D % 8 == 0)
+// about D / (resident workgroups) lifetimes later, so its phase-1 raw loads hit in L2 instead of
+// waiting on HBM.  The idle wave waits for its own loads; no other wave's vmcnt sees them.
+#ifndef PR_CM_RAW_PF
+#define PR_CM_RAW_PF 0
+#endif
+template <int TR>
+__device__ __forceinline__ void cm_raw_prefetch(const FramePtrs& fp, const TileGeom& tg, int R, int C, int lane,
+                                                uint32_t (&pv)[2 * ((TR + 63) / 64)]) {
+  const int id = (int)blockIdx.x + PR_CM_RAW_PF;
+  if (id >= (int)gridDim.x) return;
+  const TileCoord n = cm_coords(tg, R, C, id);
+  const PR_GLOBAL uint32_t* raw = (const PR_GLOBAL uint32_t*)(gin<uint16_t>(fp.in[n.f]) + n.base);
+#pragma unroll
+  for (int k = 0; k < (TR + 63) / 64; ++k) {
+    const int r = 64 * k + lane;
+    if (r < TR) {
+      const uint32_t o = (uint32_t)(r * tg.panel_cols) >> 1;   // u16 row start, in dwords
+      pv[2 * k] = raw[o];                                        // first and last dword of the row
+      pv[2 * k + 1] = raw[o + ((uint32_t)C >> 1) - 1];
+    }
+  }
 }
 
 // Phase 1 (runtime-shape loop form): decode + pedestal into the tile, side slots for groups with
@@ -1084,11 +1152,51 @@ __device__ __forceinline__ uint4 ld_raw_u4(const PR_GLOBAL uint4* p) {
 #endif
 }
 
+// PR_CM_MEMPROBE (diagnostic, WRONG results; flags-0 timing of the memory phases): bit 1 = no pedestal
+// loads in phase 1, 2 = no gain-factor loads in phase 3, 4 = no raw loads, 8 = no flush stores,
+// 16 = no eligibility-plane loads.  A removed load is replaced by an opaque per-lane value (base
+// gain, every pixel eligible), so the rest of the kernel runs the same instruction stream.
+#ifndef PR_CM_MEMPROBE
+#define PR_CM_MEMPROBE 0
+#endif
+#if PR_CM_MEMPROBE
+template <int NT, bool RAW_IN>
+__device__ __forceinline__ void cm_probe_loads(const PR_GLOBAL uint16_t* raw_t, const PR_GLOBAL uint8_t* pl_t,
+                                               const PR_GLOBAL float* const (&ped_t)[NT], uint32_t o, int tid,
+                                               uint4& rw, uint32_t& ep, float (&pa0)[1][8]) {
+  if constexpr (!RAW_IN) {
+    if constexpr (PR_CM_MEMPROBE & 4) {
+      uint32_t z = 0x01000100u + ((uint32_t)tid & 0xffu) * 0x00010001u;
+      asm volatile("" : "+v"(z));
+      rw = make_uint4(z, z ^ 0x00010001u, z ^ 0x00020002u, z ^ 0x00030003u);
+    } else {
+      rw = ld_raw_u4((const PR_GLOBAL uint4*)(raw_t + o));
+    }
+  }
+  if constexpr (PR_CM_MEMPROBE & 16) {
+    uint32_t z = 0xFFFFFFFFu;
+    asm volatile("" : "+v"(z));
+    ep = z;
+  } else {
+    ep = load_planes_o<NT>(pl_t, o);
+  }
+  if constexpr (PR_CM_MEMPROBE & 1) {
+    for (int j = 0; j < 8; ++j) {
+      uint32_t z = 0x42c80000u + (uint32_t)j;   // ~100.0
+      asm volatile("" : "+v"(z));
+      pa0[0][j] = __uint_as_float(z);
+    }
+  } else {
+    load8o<1>(reinterpret_cast<const PR_GLOBAL float* const(&)[1]>(ped_t), o, 1u, pa0);
+  }
+}
+#endif
+
 // TR / TC: the tile rows / columns as compile-time constants for the production shapes (0 = from
 // TileGeom): every LDS address in the unrolled loops is then a base VGPR + immediate offset.
 // Phase 1, compile-time tile shape: decode + pedestal of the tile into LDS by BLOCK threads
 // (thread index tid in [0, BLOCK)).
-template <int KIND, int NT, int BLOCK, int TR, int TC, bool RAW_IN>
+template <int KIND, int NT, int BLOCK, int TR, int TC, bool RAW_IN, bool SG>
 __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int P, const TileGeom& tg,
                                             const PR_GLOBAL uint16_t* raw, const float* __restrict__ ped,
                                             const uint8_t* __restrict__ planes, const int64_t base, const int tid,
@@ -1119,9 +1227,14 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
       const int r = i / C8, c = (i % C8) * 8;
 #if PR_CM_OFF32
       const uint32_t o = (uint32_t)(r * tg.panel_cols + c);
+#if PR_CM_MEMPROBE
+      cm_probe_loads<NT, RAW_IN>(raw_t, pl_t, ped_t, o, tid, rw[u], ep[u], pa0[u]);
+#else
       if constexpr (!RAW_IN) rw[u] = ld_raw_u4((const PR_GLOBAL uint4*)(raw_t + o));
-      ep[u] = load_planes_o<NT>(pl_t, o);
+      if constexpr (SG) ep[u] = 0u;   // eligibility rides in the pedestals' sign bits
+      else ep[u] = load_planes_o<NT>(pl_t, o);
       load8o<1>(reinterpret_cast<const PR_GLOBAL float* const(&)[1]>(ped_t), o, 1u, pa0[u]);
+#endif
 #else
       const int64_t pix = base + (int64_t)r * tg.panel_cols + c;
       if constexpr (!RAW_IN) rw[u] = ld_raw_u4((const PR_GLOBAL uint4*)(raw + pix));
@@ -1136,10 +1249,17 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
     const bool act = (u + 1) * BLOCK <= NITEMS || i < NITEMS;
     const int r = act ? i / C8 : 0, k = act ? i % C8 : 0, c = k * 8;
     float v[8];
+    float x[8];
     uint32_t el = 0xFFu, cb = 0;
     if (act) {
       if (PR_CM_BASE_FAST && NT > 1 && __builtin_amdgcn_ballot_w64(!cm_base_only<KIND>(rw[u])) == 0) {
-        cm_decode8_base<KIND>(rw[u], ep[u], pa0[u][0], v, el);   // wave-uniform: no switched pixel
+        // wave-uniform: no switched pixel
+        if constexpr (SG) {
+          el = cm_decode8_base_sg<KIND>(rw[u], pa0[u][0], v, x) ? 0u : 0xFFu;   // only el != 0xFF is read
+        } else {
+          cm_decode8_base<KIND>(rw[u], ep[u], pa0[u][0], v, el);
+          cm_tile_values(v, el, x);
+        }
       } else {
         float pa[NT][8];
 #pragma unroll
@@ -1151,10 +1271,9 @@ __device__ __forceinline__ void cm_load_net(float* tile, SideCtx& sc, const int 
           load8<NT>(ped, tg.npix, base + (int64_t)r * tg.panel_cols + c, need_from_raw<NT>(rw[u]), pa, 1);
 #endif
         }
-        cm_decode8<KIND, NT>(rw[u], ep[u], pa, v, el, cb);
+        cm_decode8<KIND, NT, SG>(rw[u], ep[u], pa, v, el, cb);
+        cm_tile_values(v, el, x);
       }
-      float x[8];
-      cm_tile_values(v, el, x);
       float* trow = tile + r * P + c;
       *reinterpret_cast<float4*>(trow) = make_float4(x[0], x[1], x[2], x[3]);
       *reinterpret_cast<float4*>(trow + 4) = make_float4(x[4], x[5], x[6], x[7]);
@@ -1360,7 +1479,7 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
 #else
 #define PR_CM_VGPR_ATTR
 #endif
-template <int KIND, int L, int M, int BLOCK, int TR = 0, int TC = 0>
+template <int KIND, int L, int M, int BLOCK, int TR = 0, int TC = 0, bool SG = false>
 __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_CU / 4 : 2) PR_CM_VGPR_ATTR void calib_cm_net_kernel(
     const FramePtrs fp, const float* __restrict__ ped, const float* __restrict__ gf,
     const uint8_t* __restrict__ planes, const TileGeom tg, const CmParams cp, const ImgOut io) {
@@ -1377,6 +1496,8 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
   constexpr int NITEMS = (TR > 0 && TC > 0) ? TR * (TC / 8) : 0;
   constexpr int NI = NITEMS > 0 ? (NITEMS + BLOCK - 1) / BLOCK : 0;
   constexpr bool kNet = NI > 0 && NI <= 6;
+  // signed pedestals (no bit-planes, `planes` may be null) only in the compile-time phase-1 / store form
+  static_assert(!SG || kNet, "calib_cm_net_kernel: signed pedestal tables need the compile-time tile form");
   // frames of this workgroup (tg.fpw consecutive frames of one tile; the compile-time production
   // shapes prefetch frame k+1's raw words during frame k's medians)
   const int nf = min(tg.fpw, tg.nframes - t.f);
@@ -1410,9 +1531,9 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
     if constexpr (kNet) {
       const PR_GLOBAL uint16_t* raw_next = fi + 1 < nf ? gin<uint16_t>(fp.in[f + 1]) : nullptr;
       if (fi == 0)
-        cm_load_net<KIND, NT, BLOCK, TR, TC, false>(tile, sc, P, tg, raw, pedp, plp, tb, tid, rw, raw_next);
+        cm_load_net<KIND, NT, BLOCK, TR, TC, false, SG>(tile, sc, P, tg, raw, pedp, plp, tb, tid, rw, raw_next);
       else
-        cm_load_net<KIND, NT, BLOCK, TR, TC, true>(tile, sc, P, tg, raw, pedp, plp, tb, tid, rw, raw_next);
+        cm_load_net<KIND, NT, BLOCK, TR, TC, true, SG>(tile, sc, P, tg, raw, pedp, plp, tb, tid, rw, raw_next);
     } else {
       cm_phase1<KIND, NT>(tile, sc, P, R, C, tg, raw, pedp, plp, tb);
     }
@@ -1433,8 +1554,20 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
     PR_STAMP(2);
 
     // ---- phase 2a: rows by bank, one lane per segment ------------------------------------
+    // (PR_CM_RAW_PF: the prefetched words stay unused until the end of the frame, so no wave waits
+    // for them before its later loads would anyway)
+    uint32_t pfv[2 * (((TR > 0 ? TR : 1) + 63) / 64)];
     if (cp.flags & 1) {
+#if PR_CM_RAW_PF > 0
+      if constexpr (kNet && TR > 0 && TC > 0 && TR * (TC / L) <= 192 && BLOCK == 256) {
+        if (tid >= 192) cm_raw_prefetch<TR>(fp, tg, R, C, tid - 192, pfv);
+        else cm_rows<L>(tile, P, R, C, cp, rows_t0, rows_nt);
+      } else {
+        cm_rows<L>(tile, P, R, C, cp, rows_t0, rows_nt);
+      }
+#else
       cm_rows<L>(tile, P, R, C, cp, rows_t0, rows_nt);
+#endif
       PR_STAMP(3);
       __syncthreads();
       PR_STAMP(4);
@@ -1467,9 +1600,17 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
           const int r = i / C8, k = i % C8, c = k * 8;
           cm_get_meta<NT>(reinterpret_cast<const uint8_t*>(tile + r * P + C), C, k, cbs[u], slots[u]);
 #if PR_CM_OFF32
+#if PR_CM_MEMPROBE & 2
+          for (int j = 0; j < 8; ++j) {
+            uint32_t z = 0x3f800000u + (uint32_t)j;
+            asm volatile("" : "+v"(z));
+            g0[u][0][j] = __uint_as_float(z);
+          }
+#else
           if constexpr (!PR_CM_GPRE)
             load8o<1>(reinterpret_cast<const PR_GLOBAL float* const(&)[1]>(gf_t), (uint32_t)(r * tg.panel_cols + c), 1u,
                       g0[u]);
+#endif
 #else
           if constexpr (!PR_CM_GPRE) load8<1>(gfp, tg.npix, tb + (int64_t)r * tg.panel_cols + c, 1u, g0[u]);
 #endif
@@ -1487,14 +1628,14 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
           float o[8];
           if (PR_CM_BASE_FAST && NT > 1 && __builtin_amdgcn_ballot_w64(cbs[u] != 0u) == 0) {
             // wave-uniform: every pixel of the item takes the table-0 gain factor
-            cm_out8<KIND, NT, true>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, pedp, tg.npix, pix, o);
+            cm_out8<KIND, NT, true, SG>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, pedp, tg.npix, pix, o);
           } else {
 #if PR_CM_OFF32
             if constexpr (NT > 1) load8o<NT>(gf_t, (uint32_t)(r * tg.panel_cols + c), cm_need<NT>(cbs[u]), ga, 1);
 #else
             if constexpr (NT > 1) load8<NT>(gfp, tg.npix, pix, cm_need<NT>(cbs[u]), ga, 1);
 #endif
-            cm_out8<KIND, NT>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, pedp, tg.npix, pix, o);
+            cm_out8<KIND, NT, false, SG>(tile + r * P + c, side, cbs[u], slots[u], ga, raw, pedp, tg.npix, pix, o);
           }
           cm_put8(tile + r * P + c, o);
         }
@@ -1505,6 +1646,10 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
                    [&](int k) { st_[k] = __builtin_amdgcn_s_memtime(); });
 #else
       cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out);
+#endif
+#if PR_CM_RAW_PF > 0
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(pfv) / sizeof(pfv[0])); ++k) asm volatile("" ::"v"(pfv[k]));
 #endif
       PR_STAMP(8);
     } else {
@@ -1562,7 +1707,7 @@ static void cm_launch(K kernel, dim3 grid, int block, size_t lds, hipStream_t s,
 void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t planes, int kind,
                      int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
                      float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream, uint64_t img_desc,
-                     uint64_t gap_runs, int n_gap_runs) {
+                     uint64_t gap_runs, int n_gap_runs, uint64_t ped_sg) {
   check(nframes >= 1 && nframes <= kMaxFrames, "calib_cm: nframes out of range");
   check(asic_rows >= 1 && asic_rows <= 256, "calib_cm: ASIC rows must be in [1, 256]");
   check(asic_cols % 8 == 0 && asic_cols >= 8, "calib_cm: ASIC cols must be a multiple of 8");
@@ -1600,7 +1745,8 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   if (asic_cols == 0) asic_cols = cm_tile_cols(asic_rows, full_cols, bank_cols, 0, kind);
   check(asic_cols > 0, "calib_cm: no full-height ASIC stripe fits in 160 KiB of LDS");
   const size_t lds = cm_lds_bytes(asic_rows, asic_cols, kind);
-  check(aligned16(ped) && aligned16(gf) && (planes & 3) == 0, "calib_cm: misaligned constant tables");
+  check(aligned16(ped) && aligned16(gf) && aligned16(ped_sg) && (planes & 3) == 0,
+        "calib_cm: misaligned constant tables");
   for (int f = 0; f < nframes; ++f)
     check(aligned16(fp.in[f]) && aligned16(fp.out[f]), "calib_cm: frame buffers must be 16-B aligned");
   check(n_gap_runs == 0 || (img_desc != 0 && gap_runs != 0 && gap_runs % 4 == 0), "calib_cm: bad gap table");
@@ -1635,7 +1781,21 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   const uint8_t* F = reinterpret_cast<const uint8_t*>(planes);
   const bool narrow = asic_cols <= 128;
   const size_t lds_all = lds + 32 * (size_t)side_slots;
-  if (epix_prod && asic_cols == 48) {
+  // signed pedestal tables (eligibility in the sign bits, no bit-plane loads): the epix10k2M production
+  // kernel, whose phase 1 is the compile-time form (cm_load_net); the Jungfrau 256x128 stripe has 8
+  // items per lane and runs the loop form (cm_phase1 / cm_store), which reads the bit-planes
+  // (-DPR_CM_SG=0: always the bit-planes, the A/B build)
+#ifndef PR_CM_SG
+#define PR_CM_SG 1
+#endif
+  if (!PR_CM_SG) ped_sg = 0;
+  const float* PS = reinterpret_cast<const float*>(ped_sg);
+  const bool sg_kernel = epix_prod && asic_cols == 48 && ped_sg != 0;
+  check(sg_kernel || planes != 0, "calib_cm: this shape needs the eligibility bit-planes");
+  if (sg_kernel) {
+    cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, PR_CM_EPIX_BLOCK, 176, 48, true>, grid, PR_CM_EPIX_BLOCK, lds_all, s,
+              fp, PS, G, nullptr, tg, cp, io);
+  } else if (epix_prod && asic_cols == 48) {
     cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, PR_CM_EPIX_BLOCK, 176, 48>, grid, PR_CM_EPIX_BLOCK, lds_all, s, fp, P,
               G, F, tg, cp, io);
   } else if (jf_prod && asic_cols == 128) {

@@ -40,7 +40,7 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
       case kPlanCalibCm:
         launch_calib_cm(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.elig, p.kind, p.n_panels, p.panel_rows,
                         p.panel_cols, p.asic_rows, p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags,
-                        p.bank_cols, stream);
+                        p.bank_cols, stream, 0, 0, 0, p.ped_sg);
         break;
       case kPlanImageFused:
         if (p.use_tiles)
@@ -53,7 +53,8 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
         check(p.use_cm && p.img_desc != 0, "run_calib_plan: fused image plan without common mode / placement");
         const FramePtrs fp = ptrs_of(in, out, a, b);
         launch_calib_cm(fp, n, p.ped, p.gf, p.elig, p.kind, p.n_panels, p.panel_rows, p.panel_cols, p.asic_rows,
-                        p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags, p.bank_cols, stream, p.img_desc, p.gap_runs, p.n_gap_runs);
+                        p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags, p.bank_cols, stream, p.img_desc, p.gap_runs,
+                        p.n_gap_runs, p.ped_sg);
         break;
       }
       case kPlanImageScratch: {
@@ -64,7 +65,7 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
         if (p.use_cm)
           launch_calib_cm(ptrs_of(ina, tmp, 0, n), n, p.ped, p.gf, p.elig, p.kind, p.n_panels, p.panel_rows,
                           p.panel_cols, p.asic_rows, p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags,
-                          p.bank_cols, stream);
+                          p.bank_cols, stream, 0, 0, 0, p.ped_sg);
         else
           launch_calib_basic(ptrs_of(ina, tmp, 0, n), n, p.ped, p.gf, p.npix, p.kind, stream);
         if (p.use_tiles)

@@ -37,6 +37,7 @@ struct CalibPlan {
   int kind = 0;
   int64_t npix = 0;
   uint64_t ped = 0, gf = 0, elig = 0;
+  uint64_t ped_sg = 0;  // common mode: pedestals with the eligibility in their sign bits (0 = bit-planes)
   int n_panels = 0, panel_rows = 0, panel_cols = 0, asic_rows = 0, asic_cols = 0;
   float thr = 0, maxcorr = 0;
   int npix_min = 0, cm_flags = 0, bank_cols = 0;

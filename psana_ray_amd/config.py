@@ -169,6 +169,12 @@ class CommonModeParams:
         return cm
 
 
+# Common-mode kernel tables: carry each pixel's CM eligibility in the sign bit of its pedestal
+# (CalibConstants.cm_signed_pedestals) instead of a separate bit-plane array, which saves one global
+# load per 8-pixel group in the kernel's first phase.  Used when every pedestal is >= 0 (otherwise
+# the bit-planes); False forces the bit-planes.
+CM_SIGNED_PEDESTALS = True
+
 # Common mode by detector family when the CLI says "auto" (the producer's default): psana's calib of
 # an ePix10ka includes common mode (SURVEY E-03 / Appendix B), Jungfrau has none by default.
 CM_AUTO_FAMILIES = ("epix10ka",)

@@ -19,6 +19,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 import torch
 
+from .. import config
 from ..config import CommonModeParams
 from ..ops import kernels, reference
 from .constants import CalibConstants
@@ -65,6 +66,12 @@ class Calibrator:
             self.ped = torch.from_numpy(ped).to(self.device)
             self.gf = torch.from_numpy(gf).to(self.device)
             self.elig = torch.from_numpy(elig).to(self.device)
+            # pedestals carrying the CM eligibility in their sign bits (None: some pedestal < 0)
+            self.ped_sg = None
+            if common_mode is not None and config.CM_SIGNED_PEDESTALS:
+                sg = consts.cm_signed_pedestals(ped)
+                if sg is not None:
+                    self.ped_sg = torch.from_numpy(sg).to(self.device)
             self.idx = None
             self.omask = None
             self.tile_map = None
@@ -134,6 +141,7 @@ class Calibrator:
         p.kind = spec.kernel_kind
         p.npix = spec.npix
         p.ped, p.gf, p.elig = int(self.ped.data_ptr()), int(self.gf.data_ptr()), int(self.elig.data_ptr())
+        p.ped_sg = 0 if self.ped_sg is None else int(self.ped_sg.data_ptr())
         p.n_panels, p.panel_rows, p.panel_cols = spec.n_panels, spec.panel_rows, spec.panel_cols
         p.asic_rows, p.asic_cols = spec.asic_rows, spec.asic_cols
         p.raw_frame_bytes = spec.raw_frame_bytes

@@ -134,3 +134,25 @@ class CalibConstants:
         return (np.ascontiguousarray(ped.reshape(-1, npix)),
                 np.ascontiguousarray(gf.reshape(-1, npix)),
                 np.ascontiguousarray(planes.reshape(-1)))
+
+    def cm_eligibility(self) -> np.ndarray:
+        """[NC, npix] bool: pixel p is common-mode eligible when it decodes to candidate c (status
+        good and the candidate's gain range in the CM set) -- the bits of ``device_tables``' planes."""
+        s = self.spec
+        cand = self.candidate_gain_index()
+        cm_set = np.zeros(max(s.n_gains, 1), bool)
+        cm_set[list(self.cm_gains)] = True
+        return (((self.status == 0)[None] & cm_set[cand])).reshape(cand.shape[0], s.npix)
+
+    def cm_signed_pedestals(self, ped: np.ndarray) -> Optional[np.ndarray]:
+        """The common-mode kernel's pedestal tables with the eligibility in the sign bits: ``ped[c, p]``
+        where pixel p is eligible for candidate c, ``-ped[c, p]`` elsewhere (csrc/common_mode.hip
+        cm_decode8 SG: v = ADU - |p|, eligible = sign clear).  ``ped`` is ``device_tables``' [NC,
+        npix] table.  -0.0 pedestals become +0.0 first (ADU - 0 is the same either way); None when a
+        pedestal is negative or NaN, which the sign cannot carry (the kernel then loads bit-planes)."""
+        p = np.asarray(ped, np.float32)
+        if not np.all(p >= 0):          # also catches NaN
+            return None
+        p = np.where(p == 0, np.float32(0.0), p).astype(np.float32)   # -0.0 -> +0.0
+        sg = np.where(self.cm_eligibility(), p, -p).astype(np.float32)
+        return np.ascontiguousarray(sg)

@@ -83,7 +83,9 @@ def calib_image(raw, out, ped, gf, kind, idx: torch.Tensor, stream=None):
                       _ptr(idx), nout, s)
 
 
-def calib_cm(raw, out, ped, gf, elig, kind, spec, cm, stream=None):
+def calib_cm(raw, out, ped, gf, elig, kind, spec, cm, stream=None, ped_sg=None):
+    """``ped_sg``: optional signed pedestal tables (CalibConstants.cm_signed_pedestals); the production
+    shapes then read the eligibility from their sign bits instead of ``elig``."""
     C = _ext.load()
     npix = ped.shape[1]
     dev = ped.device
@@ -93,6 +95,9 @@ def calib_cm(raw, out, ped, gf, elig, kind, spec, cm, stream=None):
     if elig.dtype != torch.uint8 or elig.numel() != (npix // 8) * stride:
         raise ValueError("calib_cm: elig must be the uint8 eligibility bit-planes [npix / 8, stride] "
                          "(CalibConstants.device_tables)")
+    if ped_sg is not None and (ped_sg.dtype != torch.float32 or ped_sg.shape != ped.shape or ped_sg.device != dev
+                               or not ped_sg.is_contiguous()):
+        raise ValueError("calib_cm: ped_sg must be a contiguous float32 table shaped like ped on its device")
     bank = cm.bank_cols or spec.bank_cols
     if C.cm_tile_cols(spec.asic_rows, spec.asic_cols, int(bank), 0, int(kind)) == 0:
         raise ValueError(f"common mode: no full-height stripe of the {spec.asic_rows}x{spec.asic_cols} ASIC "
@@ -101,7 +106,8 @@ def calib_cm(raw, out, ped, gf, elig, kind, spec, cm, stream=None):
     for a, b in _chunks(len(raw)):
         C.calib_cm([_ptr(t) for t in raw[a:b]], [_ptr(t) for t in out[a:b]], _ptr(ped), _ptr(gf), _ptr(elig), kind,
                    spec.n_panels, spec.panel_rows, spec.panel_cols, spec.asic_rows, spec.asic_cols,
-                   float(cm.thr), float(cm.maxcorr), int(cm.npix_min), int(cm.flags), int(bank), s)
+                   float(cm.thr), float(cm.maxcorr), int(cm.npix_min), int(cm.flags), int(bank), s,
+                   0 if ped_sg is None else _ptr(ped_sg))
 
 
 def assemble(frames, out, idx: torch.Tensor, npix: int, omask: Optional[torch.Tensor] = None, stream=None):

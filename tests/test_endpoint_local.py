@@ -89,5 +89,7 @@ def test_ring_slots_are_256_byte_strided_for_odd_frames(native):
     for i in range(ring.n_slots):
         v = ring.slot(i)
         assert v.shape == (1, 9, 17) and v.is_contiguous() and v.data_ptr() == ptrs[i]
+    for i in range(ring.n_slots):   # host ring memory is not zero-initialised
+        ring.slot(i).fill_(0.0)
     ring.slot(1).fill_(7.0)
     assert float(ring.slot(0).sum()) == 0.0 and float(ring.slot(2).sum()) == 0.0

@@ -106,6 +106,46 @@ def test_common_mode_switched_and_unswitched_waves_bitwise(cuda_device, det):
     _assert_equal(out, ref, f"switched / unswitched waves {det}")
 
 
+@pytest.mark.parametrize("det", ["epix10k2M", "jungfrau05M"])
+@pytest.mark.parametrize("peds", ["random", "zeros_and_negative"])
+def test_common_mode_signed_pedestals_match_bit_planes(cuda_device, det, peds, monkeypatch):
+    """The production kernels read the CM eligibility from the pedestal sign bits
+    (config.CM_SIGNED_PEDESTALS, CalibConstants.cm_signed_pedestals) instead of bit-planes: both
+    encodings bitwise equal to each other and to the golden, with gain-switched pixels; a table with
+    +0 / -0 pedestals still encodes, one negative pedestal falls back to the planes."""
+    from psana_ray_amd import config
+    spec, consts, raw = _setup(det, 2, seed=21, gain_config="mixed")
+    r = raw.view(torch.int16).numpy().astype(np.int32) & 0xFFFF
+    rng = np.random.default_rng(8)
+    sw = rng.random(r.shape) < 0.03
+    r = np.where(sw, (r & 0x3FFF) | (1 << 14), r)
+    raw = torch.from_numpy(r.astype(np.uint16).view(np.int16)).view(torch.uint16)
+    if peds == "zeros_and_negative":
+        consts.pedestals[..., :3, :5] = 0.0
+        consts.pedestals[..., 3:5, :5] = -0.0
+    cm = CommonModeParams(flags=3, thr=30.0, maxcorr=50.0, npix_min=5)
+    mask = _mask(spec)
+    outs = {}
+    for signed in (True, False):
+        monkeypatch.setattr(config, "CM_SIGNED_PEDESTALS", signed)
+        cal = Calibrator(consts, cuda_device, Mode.calib, mask=mask, common_mode=cm)
+        assert (cal.ped_sg is not None) == signed
+        outs[signed] = cal(raw.to(cuda_device))
+    torch.cuda.synchronize()
+    ref = reference.calibrate_reference(raw.to(torch.int32), consts, mask, cal.cm)
+    _assert_equal(outs[True], outs[False], f"signed vs planes {det} {peds}")
+    _assert_equal(outs[True], ref, f"signed {det} {peds}")
+    if peds == "zeros_and_negative":   # one negative pedestal: the sign cannot carry eligibility
+        monkeypatch.setattr(config, "CM_SIGNED_PEDESTALS", True)
+        consts.pedestals[(slice(None),) + (0,) * (consts.pedestals.ndim - 1)] = -1.0   # every gain range
+        cal = Calibrator(consts, cuda_device, Mode.calib, mask=mask, common_mode=cm)
+        assert cal.ped_sg is None
+        out = cal(raw.to(cuda_device))
+        torch.cuda.synchronize()
+        _assert_equal(out, reference.calibrate_reference(raw.to(torch.int32), consts, mask, cal.cm),
+                      f"negative pedestal fallback {det}")
+
+
 def test_common_mode_even_odd_and_empty_segments(cuda_device):
     """Hand-built tile: even/odd participant counts, all-masked rows, |median| > maxcorr."""
     spec = get_detector("tiny_epix")

@@ -182,3 +182,26 @@ def test_cm_quad_lane_algorithm_emulation():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.run(trials=600, seed=3) == 0
+
+
+@pytest.mark.parametrize("det", ["epix10k2M", "jungfrau05M", "tiny_epix"])
+def test_cm_signed_pedestals_encode_eligibility(det):
+    """CalibConstants.cm_signed_pedestals: |table| is the pedestal table, the sign bit is set exactly
+    where device_tables' eligibility planes have a 0 bit, -0.0 pedestals encode like +0.0, and a
+    negative pedestal makes the encoding unavailable (None)."""
+    spec = get_detector(det)
+    consts = CalibConstants.random(spec, seed=4, gain_config="mixed", bad_fraction=0.05)
+    consts.pedestals[..., 0, :4] = -0.0
+    ped, _, planes = consts.device_tables(None)
+    sg = consts.cm_signed_pedestals(ped)
+    assert sg is not None and sg.dtype == np.float32 and sg.shape == ped.shape
+    np.testing.assert_array_equal(np.abs(sg), np.where(ped == 0, np.float32(0), ped))
+    nc = ped.shape[0]
+    stride = {1: 1, 2: 2, 3: 4}[nc]
+    pl = planes.reshape(-1, stride)
+    for c in range(nc):
+        elig = ((pl[:, c][:, None] >> np.arange(8)) & 1).astype(bool).reshape(-1)
+        np.testing.assert_array_equal(~np.signbit(sg[c]), elig)
+    assert 0 < np.signbit(sg).mean() < 1
+    ped[0, 7] = -1.0
+    assert consts.cm_signed_pedestals(ped) is None

@@ -47,7 +47,7 @@ def main():
         # the stream is read at call time: under graph capture it is the capture stream
         C.calib_cm(rp, op, p.ped, p.gf, p.elig, spec.kernel_kind, spec.n_panels, spec.panel_rows,
                    spec.panel_cols, spec.asic_rows, spec.asic_cols, float(cm.thr), float(cm.maxcorr),
-                   int(cm.npix_min), int(flags), int(p.bank_cols), _ext.stream_handle())
+                   int(cm.npix_min), int(flags), int(p.bank_cols), _ext.stream_handle(), p.ped_sg)
 
     # correctness of the full kernel against the golden model (1 frame)
     launch(3)

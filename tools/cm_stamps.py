@@ -110,7 +110,7 @@ def main():
     def launch(flags):
         C.calib_cm(rp, op, p.ped, p.gf, p.elig, spec.kernel_kind, spec.n_panels, spec.panel_rows,
                    spec.panel_cols, spec.asic_rows, spec.asic_cols, float(cm.thr), float(cm.maxcorr),
-                   int(cm.npix_min), int(flags), int(p.bank_cols), _ext.stream_handle())
+                   int(cm.npix_min), int(flags), int(p.bank_cols), _ext.stream_handle(), p.ped_sg)
 
     res = {"frames": F, "tiles": ntiles}
     # image mode (production geometry): the same kernel placing the tile into the assembled image
