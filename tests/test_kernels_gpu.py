@@ -114,7 +114,7 @@ def test_common_mode_signed_pedestals_match_bit_planes(cuda_device, det, peds, m
     encodings bitwise equal to each other and to the golden, with gain-switched pixels; a table with
     +0 / -0 pedestals still encodes, one negative pedestal falls back to the planes."""
     from psana_ray_amd import config
-    spec, consts, raw = _setup(det, 2, seed=21, gain_config="mixed")
+    spec, consts, raw = _setup(det, 3, seed=21, gain_config="mixed")   # odd: a one-frame tail workgroup
     r = raw.view(torch.int16).numpy().astype(np.int32) & 0xFFFF
     rng = np.random.default_rng(8)
     sw = rng.random(r.shape) < 0.03
