@@ -757,6 +757,15 @@ __device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, const GapPre& g, 
     cm_gap_store(out, io.gaps[e]);   // shares beyond kGapPre entries per thread (not the production shapes)
 }
 
+// PR_CM_PLACEPROBE (diagnostic, WRONG results): bit 1 drops the ragged 4-B stores, bit 2 the
+// full-chunk stores of row-run panels, bit 4 those of column-run panels (the LDS reads stay).
+#ifndef PR_CM_PLACEPROBE
+#define PR_CM_PLACEPROBE 0
+#endif
+#ifndef PR_CM_PLACE_CQ
+#define PR_CM_PLACE_CQ 4
+#endif
+#define PR_PLACE_KEEP(bit, v) (!(PR_CM_PLACEPROBE & (bit)) || __float_as_uint((v)) == 0x7fc01234u)
 __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C, const ImgOut& io, int panel, int y0,
                                          int x0, PR_GLOBAL float* out) {
   const int32_t* d = io.desc + 3 * panel;
@@ -807,7 +816,8 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
       const int drun = nb / nfull, dk = nb - drun * nfull;
       for (; run < nruns;) {
         const float* tp = tb + run * P + 4 * k * di;
-        st_out4<2>((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)), make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
+        const float4 v4 = make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]);
+        if (PR_PLACE_KEEP(2, v4.x)) st_out4<2>((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)), v4);
         run += drun;
         k += dk;
         if (k >= nfull) {
@@ -816,16 +826,18 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
         }
       }
     } else {
-      // a wave takes 4 chunks (64 B of image) of 16 neighbouring columns (see the general form)
-      const int per = 4 * nruns, nq = (nfull + 3) >> 2;
+      // a wave takes PR_CM_PLACE_CQ chunks (16 B each) of 64 / PR_CM_PLACE_CQ neighbouring columns
+      // (see the general form)
+      constexpr int CQ = PR_CM_PLACE_CQ;
+      const int per = CQ * nruns, nq = (nfull + CQ - 1) / CQ;
       int a = (int)threadIdx.x / per, w = (int)threadIdx.x - a * per;
       const int da = nb / per, dw = nb - da * per;
       for (; a < nq;) {
-        const int run = w >> 2, k = 4 * a + (w & 3);
+        const int run = w / CQ, k = CQ * a + (w % CQ);
         if (k < nfull) {
           const float* tp = tb + run + 4 * k * di;
-          st_out4<2>((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)),
-                     make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]));
+          const float4 v4 = make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]);
+          if (PR_PLACE_KEEP(4, v4.x)) st_out4<2>((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)), v4);
         }
         a += da;
         w += dw;
@@ -842,7 +854,8 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
     for (int e = threadIdx.x; e < nruns * n_rag; e += nb) {
       const int run = e / n_rag, j = e - run * n_rag;
       const int t = j < n_head ? j : t_hi + (j - n_head);
-      out[lo + (int64_t)run * outer + t] = *tile_at(run, t);
+      const float v1 = *tile_at(run, t);
+      if (PR_PLACE_KEEP(1, v1)) out[lo + (int64_t)run * outer + t] = v1;
     }
   }
 }
@@ -906,7 +919,16 @@ struct TileCoord {
 // off; an XCD-grouping remap of the table-major order changed nothing, 4.75 vs 4.65, and an
 // XCD-local frame-major order lost, 5.29 vs 4.90.)
 // With tg.fpw > 1 a workgroup takes fpw consecutive frames of its tile (t.f = the first).
-__device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C, const int id = (int)blockIdx.x) {
+// Image layout (desc != null, PR_CM_IMG_ORDER): in a panel whose tile COLUMNS are image rows (90 / 270
+// degree placements) the tile that continues an image row is the next ASIC row, so those panels
+// number their tiles ASIC-row fastest: the two tiles sharing the 128-B lines at a run's ends then run
+// 64 workgroups apart on the same XCD (as row-run panels' neighbours do) instead of 64 x ASICs per
+// row, and the L2 merges the halves before a partial line is written back.
+#ifndef PR_CM_IMG_ORDER
+#define PR_CM_IMG_ORDER 0
+#endif
+__device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C, const int id = (int)blockIdx.x,
+                                               const int32_t* desc = nullptr) {
   TileCoord t;
   const int ng = (tg.nframes + tg.fpw - 1) / tg.fpw;
   const int tile = id / ng;
@@ -916,6 +938,13 @@ __device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C,
   t.panel = tile / per_panel;
   t.ar = (tile % per_panel) / tg.asics_per_row;
   t.ac = (tile % per_panel) % tg.asics_per_row;
+  if (PR_CM_IMG_ORDER && desc != nullptr) {
+    const int sx = desc[3 * t.panel + 2];
+    if (sx != 1 && sx != -1) {   // column runs: ASIC rows fastest
+      t.ar = (tile % per_panel) % tg.asics_per_col;
+      t.ac = (tile % per_panel) / tg.asics_per_col;
+    }
+  }
   t.base = (int64_t)t.panel * tg.panel_rows * tg.panel_cols + (int64_t)t.ar * R * tg.panel_cols + (int64_t)t.ac * C;
   return t;
 }
@@ -1491,7 +1520,7 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
   float* tile = reinterpret_cast<float*>(smem);
   float* side = tile + R * P;
   SideCtx sc = side_ctx(side, tg.side_slots);
-  const TileCoord t = cm_coords(tg, R, C);
+  const TileCoord t = cm_coords(tg, R, C, (int)blockIdx.x, io.desc);
   const int tid = threadIdx.x;
   constexpr int NITEMS = (TR > 0 && TC > 0) ? TR * (TC / 8) : 0;
   constexpr int NI = NITEMS > 0 ? (NITEMS + BLOCK - 1) / BLOCK : 0;

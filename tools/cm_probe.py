@@ -5,7 +5,10 @@ graph-replayed and event-timed.  Under ``rocprofv3 --pmc SQ_INSTS_VALU ...`` the
 the order flags 0,1,2,3 (``--pmc-pass``: each flag value launched 3 times, no graphs), so per-phase
 VALU / LDS instruction counts can be read off the counter CSV.
 
-    python tools/cm_probe.py [--pmc-pass]
+    python tools/cm_probe.py [--pmc-pass] [--mode image] [--no-gaps]
+
+``--mode image``: the same kernel writing the assembled image (fused K-05 placement, the plan's
+gap table unless ``--no-gaps`` -- the producer's zero-filled HBM ring launches without it).
 """
 import argparse
 import json
@@ -29,6 +32,8 @@ def main():
     ap.add_argument("--detector", default="epix10k2M")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--repeat", type=int, default=1, help="timing rounds (one JSON line each)")
+    ap.add_argument("--mode", default="calib", choices=["calib", "image"])
+    ap.add_argument("--no-gaps", action="store_true", help="image mode: no gap fill (ring launches)")
     a = ap.parse_args()
     C = _ext.load()
     dev = torch.device("cuda:0")
@@ -36,15 +41,23 @@ def main():
     src = SyntheticRun("synthetic", 0, a.detector, pool_frames=8, pinned=False, gen_device="cuda")
     pool = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(dev)
     raw = pool.repeat((F + 7) // 8, 1, 1, 1)[:F].contiguous()
-    out = torch.empty((F, *src.spec.frame_shape), dtype=torch.float32, device=dev)
+    cm = CommonModeParams()
+    image = a.mode == "image"
+    cal = Calibrator(src.consts, dev, Mode.image if image else Mode.calib, common_mode=cm)
+    out = torch.empty((F, *cal.out_shape), dtype=torch.float32, device=dev)
     rp = [int(raw[i].data_ptr()) for i in range(F)]
     op = [int(out[i].data_ptr()) for i in range(F)]
-    cm = CommonModeParams()
-    cal = Calibrator(src.consts, dev, Mode.calib, common_mode=cm)
     p = cal.plan
     spec = src.spec
+    if image and a.no_gaps:
+        out.zero_()
+        p.n_gap_runs = 0
     def launch(flags):
         # the stream is read at call time: under graph capture it is the capture stream
+        if image:
+            p.cm_flags = int(flags)
+            C.run_calib_plan(p, rp, op, _ext.stream_handle())
+            return
         C.calib_cm(rp, op, p.ped, p.gf, p.elig, spec.kernel_kind, spec.n_panels, spec.panel_rows,
                    spec.panel_cols, spec.asic_rows, spec.asic_cols, float(cm.thr), float(cm.maxcorr),
                    int(cm.npix_min), int(flags), int(p.bank_cols), _ext.stream_handle(), p.ped_sg)
@@ -53,7 +66,10 @@ def main():
     launch(3)
     torch.cuda.synchronize()
     ref = reference.calibrate_reference(torch.from_numpy(src.pool[:1].astype(np.int32)), src.consts, None, cal.cm)
-    exact = bool(torch.equal(out[0].cpu(), ref[0]))
+    if image:
+        g = cal.geometry
+        ref = reference.assemble_reference(ref, g.rows, g.cols, g.image_shape, None)
+    exact = bool(torch.equal(out[0].cpu().view(-1), ref[0].reshape(-1)))
     if a.pmc_pass:
         for flags in (0, 1, 2, 3):
             for _ in range(3):
