@@ -219,13 +219,17 @@ __global__ __launch_bounds__(256) PR_PF_WAVES_ATTR void peakfind_range_kernel(co
                               : nullptr;
   const int cap = kPfCandCap + (spill != nullptr ? kPfSpillCap : 0);
   f32x4_t v[K];
+#ifndef PR_PF_DEPTH
+#define PR_PF_DEPTH 1
+#endif
+  f32x4_t v2[PR_PF_DEPTH > 1 ? K : 1];   // PR_PF_DEPTH 2: a second chunk in flight
   #ifndef PR_PF_FASTLOAD
 #define PR_PF_FASTLOAD 1
 #endif
 // chunk g's float4s: a uniform base (SGPR) + a 32-bit lane offset; interior chunks (all but a
   // frame's last) load without per-load bounds checks (each cost a 64-bit compare, an exec-mask
   // branch and four NaN moves: ~1/3 of the stream loop's VALU)
-  auto load = [&](int64_t g) {
+  auto load_to = [&](f32x4_t(&v)[K], int64_t g) {
     const int f = (int)(g / ncpf);
     const int64_t c0 = (g - (int64_t)f * ncpf) * 256 * K;   // first float4 of the chunk (uniform)
     const PR_GLOBAL f32x4_t* cp = reinterpret_cast<const PR_GLOBAL f32x4_t*>(gin<float>(fp.in[f])) + c0;
@@ -251,6 +255,7 @@ __global__ __launch_bounds__(256) PR_PF_WAVES_ATTR void peakfind_range_kernel(co
       }
     }
   };
+  auto load = [&](int64_t g) { load_to(v, g); };
   // A candidate's (2H+1)^2 neighbourhood, H = RAD + 2, as THREE aligned 16-B loads per row (the
   // 4-float groups holding columns x-H .. x+H; panels are a multiple of 4 wide, so a group is wholly
   // inside or outside its row) instead of (2H+1) 4-B loads: 21 vector loads for RAD 1 where 49 scalar
@@ -329,8 +334,9 @@ __global__ __launch_bounds__(256) PR_PF_WAVES_ATTR void peakfind_range_kernel(co
   float above_sum = 0.0f;
   int above_cnt = 0;
   int fcur = (int)(g0 / ncpf);
-  if (g0 < g1) load(g0);
-  for (int64_t g = g0; g < g1; ++g) {
+  // one chunk: candidate bits and hit statistics from its registers, the next load issued (`refill`),
+  // then the candidates parked
+  auto chunk = [&](f32x4_t(&cv)[K], int64_t g, auto refill) {
     const int f = (int)(g / ncpf);   // wave-uniform
     if (f != fcur) {
       flush(fcur, above_sum, above_cnt);
@@ -343,7 +349,7 @@ __global__ __launch_bounds__(256) PR_PF_WAVES_ATTR void peakfind_range_kernel(co
     for (int k = 0; k < K; ++k) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float val = v[k][e];
+        const float val = cv[k][e];
         const bool hit = val > pp.thr_peak;
         above_sum += hit ? val : 0.0f;
         above_cnt += hit ? 1 : 0;
@@ -351,7 +357,7 @@ __global__ __launch_bounds__(256) PR_PF_WAVES_ATTR void peakfind_range_kernel(co
       }
     }
     const int64_t q0 = (g - (int64_t)f * ncpf) * 256 * K + threadIdx.x;
-    if (g + 1 < g1) load(g + 1);
+    refill();
 #ifdef PR_PF_DIAG_STREAM_ONLY
     cand = 0;   // diagnostic builds only: the stream without any candidate handling
 #endif
@@ -372,7 +378,18 @@ __global__ __launch_bounds__(256) PR_PF_WAVES_ATTR void peakfind_range_kernel(co
         ++slot;
       }
     }
+  };
+#if PR_PF_DEPTH > 1
+  if (g0 < g1) load_to(v, g0);
+  if (g0 + 1 < g1) load_to(v2, g0 + 1);
+  for (int64_t g = g0; g < g1; g += 2) {
+    chunk(v, g, [&] { if (g + 2 < g1) load_to(v, g + 2); });
+    if (g + 1 < g1) chunk(v2, g + 1, [&] { if (g + 3 < g1) load_to(v2, g + 3); });
   }
+#else
+  if (g0 < g1) load(g0);
+  for (int64_t g = g0; g < g1; ++g) chunk(v, g, [&] { if (g + 1 < g1) load(g + 1); });
+#endif
   if (g0 < g1) flush(fcur, above_sum, above_cnt);
   __syncthreads();
   // Parked, then spilled candidates, one per thread and round (the spill stores above are visible:
