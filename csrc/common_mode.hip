@@ -1386,6 +1386,10 @@ __device__ __forceinline__ void cm_rows(float* tile, const int P, const int R, c
   }
 }
 
+// PR_CM_COL_ONELOAD = 1: the column phase reads its values from LDS once (pass 2 from registers)
+#ifndef PR_CM_COL_ONELOAD
+#define PR_CM_COL_ONELOAD 1
+#endif
 // PR_CM_PK_COLSUB = 0: the column correction one v_sub_f32 per row (A/B of the packed form)
 #ifndef PR_CM_PK_COLSUB
 #define PR_CM_PK_COLSUB 1
@@ -1424,6 +1428,18 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
     auto row_of = [&](int i) { return 8 * (i >> 1) + 2 * q + (i & 1); };
     auto off_of = [&](int i) { return (8 * (i >> 1) + (i & 1)) * P; };
     auto load = [&](int i) { return (act && row_of(i) < R) ? colp[off_of(i)] : QNAN; };
+    float x[M];
+#if PR_CM_COL_ONELOAD
+    // ONE pass over LDS: the column into registers, participants counted on the way (inactive lanes
+    // -- whole quads past the tile's columns -- read column 0 and never write: no per-element select)
+    int my_cnt = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      x[i] = row_of(i) < R ? colp[off_of(i)] : QNAN;
+      my_cnt += fabsf(x[i]) < cp.thr ? 1 : 0;
+      if ((i & 15) == 15) asm volatile("" ::: "memory");
+    }
+#else
     // pass 1: participants of this lane
     int my_cnt = 0;
 #pragma unroll
@@ -1431,6 +1447,7 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
       my_cnt += fabsf(load(i)) < cp.thr ? 1 : 0;
       if ((i & 15) == 15) asm volatile("" ::: "memory");
     }
+#endif
     // quad totals + exclusive prefix of the non-participants: balanced +-inf padding
     const int my_inv = M - my_cnt;
     const int i0 = dpp_quad_i<0x00>(my_inv), i1 = dpp_quad_i<0x55>(my_inv);
@@ -1444,10 +1461,9 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
     const uint32_t flip = (q & 1) ? 0x80000000u : 0u;
     uint32_t pad_base = 0xff800000u ^ flip;
     asm volatile("" : "+v"(pad_base));   // one v_bitop3 per pad below, not bitop3 + xor
-    float x[M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      const float v = load(i);
+      const float v = PR_CM_COL_ONELOAD ? x[i] : load(i);
       const bool pt = fabsf(v) < cp.thr;
       const uint32_t padb = ((uint32_t)s & 0x80000000u) ^ pad_base;
       x[i] = __uint_as_float(pt ? (__float_as_uint(v) ^ flip) : padb);
