@@ -66,9 +66,12 @@ class Calibrator:
             self.ped = torch.from_numpy(ped).to(self.device)
             self.gf = torch.from_numpy(gf).to(self.device)
             self.elig = torch.from_numpy(elig).to(self.device)
-            # pedestals carrying the CM eligibility in their sign bits (None: some pedestal < 0)
+            # pedestals carrying the CM eligibility in their sign bits (None: some pedestal < 0); only
+            # the epix10k2M-shaped production kernel reads them (csrc/common_mode.hip launch_calib_cm)
             self.ped_sg = None
-            if common_mode is not None and config.CM_SIGNED_PEDESTALS:
+            sg_shape = spec.kind == "epix10ka" and spec.asic_rows == 176 and spec.asic_cols % 48 == 0 and \
+                int(self.cm.bank_cols if self.cm is not None else 0) == 48
+            if common_mode is not None and config.CM_SIGNED_PEDESTALS and sg_shape:
                 sg = consts.cm_signed_pedestals(ped)
                 if sg is not None:
                     self.ped_sg = torch.from_numpy(sg).to(self.device)
