@@ -80,7 +80,7 @@ def frames(recs):
     return [r["gevt"] for r in fr]
 
 
-def finish(p, timeout=90):
+def finish(p, timeout=180):
     try:
         out, _ = p.communicate(timeout=timeout)
     except subprocess.TimeoutExpired:
