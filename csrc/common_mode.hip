@@ -1524,6 +1524,14 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
 #else
 #define PR_CM_VGPR_ATTR
 #endif
+#ifndef PR_CM_NET_MAXNI
+#define PR_CM_NET_MAXNI 8
+#endif
+// Jungfrau stripe width: 128 (one 256x128 tile per CU, 512 threads) or 64 (two 256x64 tiles per CU,
+// 256 threads each -- one workgroup's median phases overlap the other's memory phases)
+#ifndef PR_CM_JF_W
+#define PR_CM_JF_W 64
+#endif
 template <int KIND, int L, int M, int BLOCK, int TR = 0, int TC = 0, bool SG = false>
 __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_CU / 4 : 2) PR_CM_VGPR_ATTR void calib_cm_net_kernel(
     const FramePtrs fp, const float* __restrict__ ped, const float* __restrict__ gf,
@@ -1540,7 +1548,10 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
   const int tid = threadIdx.x;
   constexpr int NITEMS = (TR > 0 && TC > 0) ? TR * (TC / 8) : 0;
   constexpr int NI = NITEMS > 0 ? (NITEMS + BLOCK - 1) / BLOCK : 0;
-  constexpr bool kNet = NI > 0 && NI <= 6;
+  // compile-time phase-1 / store form when every lane's items fit in registers: up to 6 items at the
+  // epix10k2M kernel's 128-VGPR budget (four workgroups per CU), up to PR_CM_NET_MAXNI (8) for the
+  // Jungfrau 256x128 stripe, whose 135-KB tile allows one workgroup per CU (256 VGPRs)
+  constexpr bool kNet = NI > 0 && NI <= (M <= 48 ? 6 : PR_CM_NET_MAXNI);
   // signed pedestals (no bit-planes, `planes` may be null) only in the compile-time phase-1 / store form
   static_assert(!SG || kNet, "calib_cm_net_kernel: signed pedestal tables need the compile-time tile form");
   // frames of this workgroup (tg.fpw consecutive frames of one tile; the compile-time production
@@ -1923,7 +1934,8 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   // Tile shape (one decision per shape, no run-time knobs):
   //  * epix10k2M (176-row ASICs, 48-column banks): one-bank 176x48 stripes on 256-thread blocks,
   //    four workgroups per CU (round 1: 8.8 us/frame vs 9.2 for 176x96, 15.8 full width);
-  //  * Jungfrau (256x256 ASICs, 64-column banks): 256x128 stripes, 512-thread blocks;
+  //  * Jungfrau (256x256 ASICs, 64-column banks): 256x64 stripes (one bank), 256-thread blocks, two
+  //    workgroups per CU (PR_CM_JF_W; 256x128 on 512 threads, one per CU: 52.8 vs 37.3 us/frame);
   //  * otherwise: the widest stripe <= 128 columns whose tile fits half the LDS (two blocks per CU)
   //    when a compile-time network exists for the shape, else the widest that fits at all.
   const int M4 = (asic_rows + 3) / 4;
@@ -1935,7 +1947,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   if (epix_prod) {
     max_w = 48;
   } else if (jf_prod) {
-    max_w = 128;
+    max_w = PR_CM_JF_W;
   } else if (net) {
     for (int w = std::min(asic_cols, 128); w >= bank_cols; --w)
       if (asic_cols % w == 0 && w % bank_cols == 0 && w % 8 == 0 && cm_lds_bytes(asic_rows, w, kind) <= 80 * 1024) {
@@ -1955,16 +1967,17 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   check(n_gap_runs == 0 || (img_desc != 0 && gap_runs != 0 && gap_runs % 4 == 0), "calib_cm: bad gap table");
   const ImgOut io{reinterpret_cast<const int32_t*>(img_desc), reinterpret_cast<const int32_t*>(gap_runs),
                   img_desc != 0 ? n_gap_runs : 0};
-  // signed pedestal tables (eligibility in the sign bits, no bit-plane loads): the epix10k2M production
-  // kernel, whose phase 1 is the compile-time form (cm_load_net); the Jungfrau 256x128 stripe has 8
-  // items per lane and runs the loop form (cm_phase1 / cm_store), which reads the bit-planes
+  // signed pedestal tables (eligibility in the sign bits, no bit-plane loads): the production kernels,
+  // whose phase 1 is the compile-time form (cm_load_net); the loop form (cm_phase1 / cm_store) of the
+  // other shapes reads the bit-planes
   // (-DPR_CM_SG=0: always the bit-planes, the A/B build)
 #ifndef PR_CM_SG
 #define PR_CM_SG 1
 #endif
   if (!PR_CM_SG) ped_sg = 0;
   const float* PS = reinterpret_cast<const float*>(ped_sg);
-  const bool sg_kernel = epix_prod && asic_cols == 48 && ped_sg != 0;
+  const bool sg_kernel = ((epix_prod && asic_cols == 48) ||
+                          (jf_prod && asic_cols == PR_CM_JF_W && PR_CM_NET_MAXNI >= 8)) && ped_sg != 0;
   check(sg_kernel || planes != 0, "calib_cm: this shape needs the eligibility bit-planes");
   // two frames per workgroup with shared table loads (PR_CM_DUAL): two 2-tile workgroups per CU
   const bool dual = PR_CM_DUAL && sg_kernel;
@@ -1974,6 +1987,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   const size_t lds_tiles = dual ? 2 * lds : lds;
   const size_t budget = dual ? 80 * 1024
                         : (epix_prod && asic_cols == 48) ? (160 * 1024) / PR_CM_EPIX_WG_PER_CU
+                        : (jf_prod && asic_cols == 64) ? 80 * 1024     // two 256x64 Jungfrau stripes per CU
                         : (net && !jf_prod && asic_cols <= 128) ? 80 * 1024
                                                                 : 160 * 1024;
   const int side_slots = (int)std::min<size_t>(kMaxSideSlots, lds_tiles < budget ? (budget - lds_tiles) / 32 : 0);
@@ -2004,14 +2018,20 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
     cm_launch(calib_cm_dual_kernel<kEpix10ka, 48, 44, 176, 48>, grid, 512, lds_all, s, fp, PS, G, nullptr, tg, cp, io);
   } else
 #endif
-  if (sg_kernel) {
+  if (sg_kernel && epix_prod) {
     cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, PR_CM_EPIX_BLOCK, 176, 48, true>, grid, PR_CM_EPIX_BLOCK, lds_all, s,
               fp, PS, G, nullptr, tg, cp, io);
+  } else if (sg_kernel) {
+#if PR_CM_NET_MAXNI >= 8
+    cm_launch(calib_cm_net_kernel<kJungfrau, 64, 64, 4 * PR_CM_JF_W, 256, PR_CM_JF_W, true>, grid, 4 * PR_CM_JF_W,
+              lds_all, s, fp, PS, G, nullptr, tg, cp, io);
+#endif
   } else if (epix_prod && asic_cols == 48) {
     cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, PR_CM_EPIX_BLOCK, 176, 48>, grid, PR_CM_EPIX_BLOCK, lds_all, s, fp, P,
               G, F, tg, cp, io);
-  } else if (jf_prod && asic_cols == 128) {
-    cm_launch(calib_cm_net_kernel<kJungfrau, 64, 64, 512, 256, 128>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
+  } else if (jf_prod && asic_cols == PR_CM_JF_W) {
+    cm_launch(calib_cm_net_kernel<kJungfrau, 64, 64, 4 * PR_CM_JF_W, 256, PR_CM_JF_W>, grid, 4 * PR_CM_JF_W, lds_all, s,
+              fp, P, G, F, tg, cp, io);
   } else if (kind == kEpix10ka && bank_cols == 48 && M4 == 44 && narrow) {
     cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, 512>, grid, 512, lds_all, s, fp, P, G, F, tg, cp, io);
   } else if (kind == kEpix10ka && bank_cols == 8 && M4 == 4 && narrow) {

@@ -69,8 +69,9 @@ class Calibrator:
             # pedestals carrying the CM eligibility in their sign bits (None: some pedestal < 0); only
             # the epix10k2M-shaped production kernel reads them (csrc/common_mode.hip launch_calib_cm)
             self.ped_sg = None
-            sg_shape = spec.kind == "epix10ka" and spec.asic_rows == 176 and spec.asic_cols % 48 == 0 and \
-                int(self.cm.bank_cols if self.cm is not None else 0) == 48
+            bank = int(self.cm.bank_cols if self.cm is not None else 0)
+            sg_shape = (spec.kind == "epix10ka" and spec.asic_rows == 176 and spec.asic_cols % 48 == 0 and bank == 48) or \
+                (spec.kind == "jungfrau" and spec.asic_rows == 256 and spec.asic_cols % 128 == 0 and bank == 64)
             if common_mode is not None and config.CM_SIGNED_PEDESTALS and sg_shape:
                 sg = consts.cm_signed_pedestals(ped)
                 if sg is not None:
