@@ -949,32 +949,6 @@ __device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C,
   return t;
 }
 
-// PR_CM_RAW_PF = D > 0: during the row phase the wave the medians leave idle (threads >= 192 of the
-// epix10k2M kernel: 176 row segments, 48 x 4 column lanes) touches every 128-B line of the raw tile of
-// workgroup blockIdx + D, which runs on the same XCD (workgroups go to XCDs round-robin, D % 8 == 0)
-// about D / (resident workgroups) lifetimes later, so its phase-1 raw loads hit in L2 instead of
-// waiting on HBM.  The idle wave waits for its own loads; no other wave's vmcnt sees them.
-#ifndef PR_CM_RAW_PF
-#define PR_CM_RAW_PF 0
-#endif
-template <int TR>
-__device__ __forceinline__ void cm_raw_prefetch(const FramePtrs& fp, const TileGeom& tg, int R, int C, int lane,
-                                                uint32_t (&pv)[2 * ((TR + 63) / 64)]) {
-  const int id = (int)blockIdx.x + PR_CM_RAW_PF;
-  if (id >= (int)gridDim.x) return;
-  const TileCoord n = cm_coords(tg, R, C, id);
-  const PR_GLOBAL uint32_t* raw = (const PR_GLOBAL uint32_t*)(gin<uint16_t>(fp.in[n.f]) + n.base);
-#pragma unroll
-  for (int k = 0; k < (TR + 63) / 64; ++k) {
-    const int r = 64 * k + lane;
-    if (r < TR) {
-      const uint32_t o = (uint32_t)(r * tg.panel_cols) >> 1;   // u16 row start, in dwords
-      pv[2 * k] = raw[o];                                        // first and last dword of the row
-      pv[2 * k + 1] = raw[o + ((uint32_t)C >> 1) - 1];
-    }
-  }
-}
-
 // Phase 1 (runtime-shape loop form): decode + pedestal into the tile, side slots for groups with
 // non-eligible pixels.  Whole waves iterate together (side_put is a wave-wide ballot).
 template <int KIND, int NT>
@@ -1610,20 +1584,8 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
     PR_STAMP(2);
 
     // ---- phase 2a: rows by bank, one lane per segment ------------------------------------
-    // (PR_CM_RAW_PF: the prefetched words stay unused until the end of the frame, so no wave waits
-    // for them before its later loads would anyway)
-    uint32_t pfv[2 * (((TR > 0 ? TR : 1) + 63) / 64)];
     if (cp.flags & 1) {
-#if PR_CM_RAW_PF > 0
-      if constexpr (kNet && TR > 0 && TC > 0 && TR * (TC / L) <= 192 && BLOCK == 256) {
-        if (tid >= 192) cm_raw_prefetch<TR>(fp, tg, R, C, tid - 192, pfv);
-        else cm_rows<L>(tile, P, R, C, cp, rows_t0, rows_nt);
-      } else {
-        cm_rows<L>(tile, P, R, C, cp, rows_t0, rows_nt);
-      }
-#else
       cm_rows<L>(tile, P, R, C, cp, rows_t0, rows_nt);
-#endif
       PR_STAMP(3);
       __syncthreads();
       PR_STAMP(4);
@@ -1703,10 +1665,6 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
 #else
       cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out);
 #endif
-#if PR_CM_RAW_PF > 0
-#pragma unroll
-      for (int k = 0; k < (int)(sizeof(pfv) / sizeof(pfv[0])); ++k) asm volatile("" ::"v"(pfv[k]));
-#endif
       PR_STAMP(8);
     } else {
       cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, pedp, gfp, tb, out, io, t.tile, t.panel, t.ar * R,
@@ -1734,163 +1692,6 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
 #endif
 }
 
-
-// ---- two frames per workgroup, shared table loads (PR_CM_DUAL) --------------------------------
-// The epix10k2M production shape with signed pedestal tables, 512 threads, two workgroups per CU:
-// every workgroup takes one tile of TWO consecutive frames (two LDS tiles), and each lane handles
-// the same 8-pixel groups of both frames, so a pedestal / gain-factor table load serves two frames
-// (the memory-phase probes, profiles/r5/README.md section 6, put the table loads at ~16 % of the
-// kernel).  Median phases: frame 0 on threads 0-255, frame 1 on threads 256-511, the same
-// per-wave instruction streams as the one-frame kernel.
-// Measured and NOT the default (profiles/r5/README.md section 9): the memory phases get 8.5 % faster
-// (flags 0: 3.35 vs 3.66 us/frame) but a workgroup's median phases now hold six busy waves on three
-// SIMDs, and with two workgroups per CU instead of four the medians no longer hide behind other
-// workgroups' memory phases: flags 3 4.88 vs 4.61, device-resident pipelines -8 %.
-#ifndef PR_CM_DUAL
-#define PR_CM_DUAL 0
-#endif
-template <int KIND, int L, int M, int TR, int TC>
-__global__ __launch_bounds__(512, 2) void calib_cm_dual_kernel(const FramePtrs fp, const float* __restrict__ ped,
-                                                               const float* __restrict__ gf,
-                                                               const uint8_t* __restrict__ planes, const TileGeom tg,
-                                                               const CmParams cp, const ImgOut io) {
-  constexpr int BLOCK = 512;
-  constexpr int NT = KIND == kEpix10ka ? 2 : (KIND == kJungfrau ? 3 : 1);
-  static_assert(NT == 2, "calib_cm_dual_kernel: two candidate tables (epix10ka)");
-  constexpr int P = cm_pitch(TC, CmLayout<NT>::kCandBits);
-  constexpr int R = TR, C = TC, C8 = TC / 8;
-  constexpr int NITEMS = TR * C8;
-  constexpr int NI = (NITEMS + BLOCK - 1) / BLOCK;
-  static_assert(R * (C / L) <= 256 && 4 * C <= 256, "calib_cm_dual_kernel: one frame's medians on 256 threads");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* const tile0 = reinterpret_cast<float*>(smem);
-  float* const side = tile0 + 2 * R * P;
-  SideCtx sc = side_ctx(side, tg.side_slots);
-  const TileCoord t = cm_coords(tg, R, C);   // tg.fpw == 2: frames t.f and t.f + 1
-  const int tid = threadIdx.x;
-  const int nf = min(2, tg.nframes - t.f);
-  int64_t tb = t.base;
-  const float* pedp = ped;
-  const float* gfp = gf;
-  asm volatile("" : "+s"(tb), "+s"(pedp), "+s"(gfp));
-  const PR_GLOBAL uint16_t* raw[2] = {gin<uint16_t>(fp.in[t.f]), gin<uint16_t>(fp.in[t.f + (nf > 1 ? 1 : 0)])};
-  const PR_GLOBAL float* ped_t[NT];
-  const PR_GLOBAL float* gf_t[NT];
-#pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    ped_t[k] = (const PR_GLOBAL float*)pedp + k * tg.npix + tb;
-    gf_t[k] = (const PR_GLOBAL float*)gfp + k * tg.npix + tb;
-  }
-  auto active = [&](int u) { return (u + 1) * BLOCK <= NITEMS || tid + u * BLOCK < NITEMS; };
-
-  // ---- phase 1: both frames' raw words + one pedestal table load per group ------------------
-  uint4 rw[2][NI];
-  float pa0[NI][1][8];
-#pragma unroll
-  for (int u = 0; u < NI; ++u) {
-    if (active(u)) {
-      const int i = tid + u * BLOCK;
-      const uint32_t o = (uint32_t)((i / C8) * tg.panel_cols + (i % C8) * 8);
-      rw[0][u] = ld_raw_u4((const PR_GLOBAL uint4*)(raw[0] + tb + o));
-      if (nf > 1) rw[1][u] = ld_raw_u4((const PR_GLOBAL uint4*)(raw[1] + tb + o));
-      load8o<1>(reinterpret_cast<const PR_GLOBAL float* const(&)[1]>(ped_t), o, 1u, pa0[u]);
-    }
-  }
-#pragma unroll
-  for (int fi = 0; fi < 2; ++fi) {
-    if (fi >= nf) break;   // workgroup-uniform
-    float* const tile = tile0 + fi * R * P;
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      const bool act = active(u);
-      const int i = tid + u * BLOCK;
-      const int r = act ? i / C8 : 0, k = act ? i % C8 : 0, c = k * 8;
-      float v[8], x[8];
-      uint32_t el = 0xFFu, cb = 0;
-      if (act) {
-        if (__builtin_amdgcn_ballot_w64(!cm_base_only<KIND>(rw[fi][u])) == 0) {
-          el = cm_decode8_base_sg<KIND>(rw[fi][u], pa0[u][0], v, x) ? 0u : 0xFFu;
-        } else {
-          float pa[NT][8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pa[0][j] = pa0[u][0][j];
-          load8o<NT>(ped_t, (uint32_t)(r * tg.panel_cols + c), need_from_raw<NT>(rw[fi][u]), pa, 1);
-          cm_decode8<KIND, NT, true>(rw[fi][u], 0u, pa, v, el, cb);
-          cm_tile_values(v, el, x);
-        }
-        float* trow = tile + r * P + c;
-        *reinterpret_cast<float4*>(trow) = make_float4(x[0], x[1], x[2], x[3]);
-        *reinterpret_cast<float4*>(trow + 4) = make_float4(x[4], x[5], x[6], x[7]);
-      }
-      const uint32_t slot = side_put(sc, act && el != 0xFFu, v);   // convergent: whole wave
-      if (act) cm_put_meta<NT>(reinterpret_cast<uint8_t*>(tile + r * P + C), C, k, cb, slot);
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 2: medians, frame 0 on threads 0-255, frame 1 on 256-511 -------------------------
-  const int half = tid >> 8, ht = tid & 255;
-  float* const mtile = tile0 + half * R * P;
-  const bool mine = half < nf;
-  if (cp.flags & 1) {
-    if (mine) cm_rows<L>(mtile, P, R, C, cp, ht, 256);
-    __syncthreads();
-  }
-  if (cp.flags & 2) {
-    if (mine) cm_cols<M>(mtile, P, R, C, cp, ht, 256);
-    __syncthreads();
-  }
-
-  // ---- phase 3: one gain-factor table load per group for both frames, output into LDS ---------
-  uint32_t cbs[2][NI], slots[2][NI];
-  float g0[NI][1][8];
-#pragma unroll
-  for (int u = 0; u < NI; ++u) {
-    if (active(u)) {
-      const int i = tid + u * BLOCK;
-      const int r = i / C8, k = i % C8;
-#pragma unroll
-      for (int fi = 0; fi < 2; ++fi)
-        if (fi < nf)
-          cm_get_meta<NT>(reinterpret_cast<const uint8_t*>(tile0 + fi * R * P + r * P + C), C, k, cbs[fi][u],
-                          slots[fi][u]);
-      load8o<1>(reinterpret_cast<const PR_GLOBAL float* const(&)[1]>(gf_t), (uint32_t)(r * tg.panel_cols + k * 8), 1u,
-                g0[u]);
-    }
-  }
-#pragma unroll
-  for (int fi = 0; fi < 2; ++fi) {
-    if (fi >= nf) break;
-    float* const tile = tile0 + fi * R * P;
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      if (active(u)) {
-        const int i = tid + u * BLOCK;
-        const int r = i / C8, c = (i % C8) * 8;
-        const int64_t pix = tb + (int64_t)r * tg.panel_cols + c;
-        float ga[NT][8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ga[0][j] = g0[u][0][j];
-        float o[8];
-        if (__builtin_amdgcn_ballot_w64(cbs[fi][u] != 0u) == 0) {
-          cm_out8<KIND, NT, true, true>(tile + r * P + c, side, cbs[fi][u], slots[fi][u], ga, raw[fi], pedp, tg.npix,
-                                        pix, o);
-        } else {
-          load8o<NT>(gf_t, (uint32_t)(r * tg.panel_cols + c), cm_need<NT>(cbs[fi][u]), ga, 1);
-          cm_out8<KIND, NT, false, true>(tile + r * P + c, side, cbs[fi][u], slots[fi][u], ga, raw[fi], pedp, tg.npix,
-                                         pix, o);
-        }
-        cm_put8(tile + r * P + c, o);
-      }
-    }
-  }
-#pragma unroll
-  for (int fi = 0; fi < 2; ++fi) {
-    if (fi >= nf) break;
-    cm_write_out(tile0 + fi * R * P, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb,
-                 gout<float>(fp.out[t.f + fi]));
-  }
-}
 
 size_t cm_lds_bytes(int asic_rows, int asic_cols, int kind) {
   const int cand_bits = kind == kJungfrau ? 2 : 1;
@@ -1979,14 +1780,11 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   const bool sg_kernel = ((epix_prod && asic_cols == 48) ||
                           (jf_prod && asic_cols == PR_CM_JF_W && PR_CM_NET_MAXNI >= 8)) && ped_sg != 0;
   check(sg_kernel || planes != 0, "calib_cm: this shape needs the eligibility bit-planes");
-  // two frames per workgroup with shared table loads (PR_CM_DUAL): two 2-tile workgroups per CU
-  const bool dual = PR_CM_DUAL && sg_kernel;
   // LDS budget of one workgroup: the epix10k2M 176x48 stripe runs PR_CM_EPIX_WG_PER_CU workgroups
-  // per CU (the dual-frame form two, each with two tiles), the narrow compile-time kernels two,
+  // per CU, the two 256x64 Jungfrau stripes two, the narrow compile-time kernels two,
   // everything else one; what the tiles leave is side slots
-  const size_t lds_tiles = dual ? 2 * lds : lds;
-  const size_t budget = dual ? 80 * 1024
-                        : (epix_prod && asic_cols == 48) ? (160 * 1024) / PR_CM_EPIX_WG_PER_CU
+  const size_t lds_tiles = lds;
+  const size_t budget = (epix_prod && asic_cols == 48) ? (160 * 1024) / PR_CM_EPIX_WG_PER_CU
                         : (jf_prod && asic_cols == 64) ? 80 * 1024     // two 256x64 Jungfrau stripes per CU
                         : (net && !jf_prod && asic_cols <= 128) ? 80 * 1024
                                                                 : 160 * 1024;
@@ -2002,7 +1800,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   tg.nframes = nframes;
   // frames per workgroup: the epix10k2M production kernel takes PR_CM_FPW consecutive frames of
   // its tile (next frame's raw words prefetched during the medians); everything else one
-  tg.fpw = dual ? 2 : (epix_prod && asic_cols == 48) ? PR_CM_FPW : 1;
+  tg.fpw = (epix_prod && asic_cols == 48) ? PR_CM_FPW : 1;
   tg.side_slots = side_slots;
   tg.pitch = cm_pitch(asic_cols, kind == kJungfrau ? 2 : 1);
   const CmParams cp{thr, maxcorr, npix_min, flags, bank_cols};
@@ -2013,11 +1811,6 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   const uint8_t* F = reinterpret_cast<const uint8_t*>(planes);
   const bool narrow = asic_cols <= 128;
   const size_t lds_all = lds_tiles + 32 * (size_t)side_slots;
-#if PR_CM_DUAL
-  if (dual) {
-    cm_launch(calib_cm_dual_kernel<kEpix10ka, 48, 44, 176, 48>, grid, 512, lds_all, s, fp, PS, G, nullptr, tg, cp, io);
-  } else
-#endif
   if (sg_kernel && epix_prod) {
     cm_launch(calib_cm_net_kernel<kEpix10ka, 48, 44, PR_CM_EPIX_BLOCK, 176, 48, true>, grid, PR_CM_EPIX_BLOCK, lds_all, s,
               fp, PS, G, nullptr, tg, cp, io);
