@@ -207,6 +207,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("asic_rows"), py::arg("asic_cols"), py::arg("thr"), py::arg("maxcorr"), py::arg("npix_min"),
         py::arg("flags"), py::arg("bank_cols"), py::arg("stream"), py::arg("ped_sg") = 0);
   m.def("cm_lds_bytes", &pr::cm_lds_bytes, py::arg("asic_rows"), py::arg("asic_cols"), py::arg("kind"));
+  m.def("cm_signed_shape", &pr::cm_signed_shape, py::arg("kind"), py::arg("asic_rows"), py::arg("asic_cols"),
+        py::arg("bank_cols"));
   m.def("cm_tile_cols", &pr::cm_tile_cols, py::arg("asic_rows"), py::arg("asic_cols"), py::arg("bank_cols"),
         py::arg("max_cols") = 0, py::arg("kind") = 0);
   m.def("image_tile_shape", [] { return py::make_tuple(pr::image_tile_h(), pr::image_tile_w(), pr::image_tile_stage()); });

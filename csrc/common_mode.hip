@@ -1501,6 +1501,10 @@ __device__ __forceinline__ void cm_cols(float* tile, const int P, const int R, c
 #ifndef PR_CM_NET_MAXNI
 #define PR_CM_NET_MAXNI 8
 #endif
+// signed pedestal tables for the production shapes (0: always the bit-planes, the A/B build)
+#ifndef PR_CM_SG
+#define PR_CM_SG 1
+#endif
 // Jungfrau stripe width: 128 (one 256x128 tile per CU, 512 threads) or 64 (two 256x64 tiles per CU,
 // 256 threads each -- one workgroup's median phases overlap the other's memory phases)
 #ifndef PR_CM_JF_W
@@ -1693,6 +1697,15 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
 }
 
 
+// The production shapes whose compile-time kernels read the signed pedestal tables (launch_calib_cm
+// picks them with the same predicate); Calibrator builds the tables only for these.
+bool cm_signed_shape(int kind, int asic_rows, int asic_cols, int bank_cols) {
+  if (!PR_CM_SG) return false;
+  if (kind == kEpix10ka) return bank_cols == 48 && asic_rows == 176 && asic_cols % 48 == 0;
+  if (kind == kJungfrau) return PR_CM_NET_MAXNI >= 8 && bank_cols == 64 && asic_rows == 256 && asic_cols % 128 == 0;
+  return false;
+}
+
 size_t cm_lds_bytes(int asic_rows, int asic_cols, int kind) {
   const int cand_bits = kind == kJungfrau ? 2 : 1;
   return (size_t)asic_rows * cm_pitch(asic_cols, cand_bits) * 4;
@@ -1772,9 +1785,6 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   // whose phase 1 is the compile-time form (cm_load_net); the loop form (cm_phase1 / cm_store) of the
   // other shapes reads the bit-planes
   // (-DPR_CM_SG=0: always the bit-planes, the A/B build)
-#ifndef PR_CM_SG
-#define PR_CM_SG 1
-#endif
   if (!PR_CM_SG) ped_sg = 0;
   const float* PS = reinterpret_cast<const float*>(ped_sg);
   const bool sg_kernel = ((epix_prod && asic_cols == 48) ||

@@ -18,6 +18,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
                      int n_gap_runs = 0,    // img_desc: fused K-05 (ImgOut); gap runs zeroed by the same kernel
                      uint64_t ped_sg = 0);  // signed pedestal tables (eligibility in the sign bits), 0 = planes
 size_t cm_lds_bytes(int asic_rows, int asic_cols, int kind);
+bool cm_signed_shape(int kind, int asic_rows, int asic_cols, int bank_cols);   // reads signed pedestal tables
 void launch_image_tiles(const FramePtrs& fp, int nframes, bool calib, int kind, uint64_t ped, uint64_t gf,
                         int64_t npix, int panel_rows, int panel_cols, uint64_t tiles, int n_tiles, int tiles_x,
                         uint64_t codes, int img_h, int img_w, uint64_t stream);

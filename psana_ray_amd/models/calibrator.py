@@ -66,12 +66,11 @@ class Calibrator:
             self.ped = torch.from_numpy(ped).to(self.device)
             self.gf = torch.from_numpy(gf).to(self.device)
             self.elig = torch.from_numpy(elig).to(self.device)
-            # pedestals carrying the CM eligibility in their sign bits (None: some pedestal < 0); only
-            # the epix10k2M-shaped production kernel reads them (csrc/common_mode.hip launch_calib_cm)
+            # pedestals carrying the CM eligibility in their sign bits (None: some pedestal < 0), for
+            # the production kernels that read them (the launcher's predicate, _C.cm_signed_shape)
             self.ped_sg = None
-            bank = int(self.cm.bank_cols if self.cm is not None else 0)
-            sg_shape = (spec.kind == "epix10ka" and spec.asic_rows == 176 and spec.asic_cols % 48 == 0 and bank == 48) or \
-                (spec.kind == "jungfrau" and spec.asic_rows == 256 and spec.asic_cols % 128 == 0 and bank == 64)
+            sg_shape = self.cm is not None and bool(C.cm_signed_shape(spec.kernel_kind, spec.asic_rows, spec.asic_cols,
+                                                                      int(self.cm.bank_cols)))
             if common_mode is not None and config.CM_SIGNED_PEDESTALS and sg_shape:
                 sg = consts.cm_signed_pedestals(ped)
                 if sg is not None:

@@ -48,3 +48,16 @@ def test_device_topology_on_a_cpu_box(native):
     t = native.device_topology()
     assert set(t) == {"n", "can_access", "link_type", "hops"}
     assert len(t["can_access"]) == t["n"]
+
+
+def test_cm_signed_shape_matches_the_production_kernels():
+    """Calibrator builds signed pedestal tables only where launch_calib_cm reads them: the epix10k2M
+    176x48 and Jungfrau 256x64 compile-time kernels (csrc/common_mode.hip cm_signed_shape)."""
+    from psana_ray_amd.ops import _ext
+
+    C = _ext.load()
+    assert C.cm_signed_shape(0, 176, 384, 48)        # epix10ka, epix10k2M ASICs
+    assert C.cm_signed_shape(1, 256, 256, 64)        # jungfrau
+    assert not C.cm_signed_shape(0, 44, 48, 16)      # generic kernel shapes read bit-planes
+    assert not C.cm_signed_shape(1, 64, 64, 32)
+    assert not C.cm_signed_shape(2, 176, 384, 48)    # plain kind
