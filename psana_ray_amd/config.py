@@ -76,12 +76,12 @@ def pipeline_shape(where: str, ranks_per_gpu: int = 1) -> dict:
             "consumer_batch": SHARED_GPU_CONSUMER_BATCH if shared else CONSUMER_BATCH}
 
 
-# Consumer: the peak finder's two alternating streams.  Round 3 gave each its own hardware queue
-# (ordinary streams landed both on ONE queue: rocprofv3 Queue_Id, profiles/r3/streams2/); with the
-# round-5 kernels ordinary streams are as fast or faster in every interleaved round
-# (profiles/r5/sweep2/, sweep3/: device-resident calib +0.7-1.3 %, image +0.1 %, host-staged +0.3 %;
-# high-priority streams -7 %), so they share the process's queues again.
-CONSUMER_STREAM_KIND = "shared"
+# Consumer: the peak finder's two alternating streams, each on its own hardware queue (ordinary
+# streams landed both on ONE queue: rocprofv3 Queue_Id, profiles/r3/streams2/).  Round 5: ordinary
+# streams are within the noise for one rank per GPU (+0.3-1.3 %, profiles/r5/sweep2/, sweep3/) but
+# lose where ranks share a GPU or frames cross processes (2 ranks on one GPU: host-staged -2.5 %,
+# cross windows -3.6 / -3.8 %, profiles/r5/n2ab/), so the queues stay dedicated.
+CONSUMER_STREAM_KIND = "dedicated"
 CONSUMER_STREAMS = 2
 # Frames per peak-finder launch of the in-process consumer (bench.py --batch, the producer CLI's
 # co-consumer): one full launch (kernels.MAX_FRAMES) -- half as many launch ramps and drains per
