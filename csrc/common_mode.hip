@@ -245,6 +245,7 @@ struct TileGeom {
   int fpw;                           // frames per workgroup (grid = n_tiles * ceil(nframes / fpw), 1-D)
   int side_slots;                    // LDS side slots after the tile (SideCtx)
   int pitch;                         // LDS floats per tile row (values + candidate bits + pad)
+  int xcd_map;                       // XCD-grouped tile order (cm_coords): few frames per launch
 };
 
 // Fused K-05 output (image mode with common mode).  Every panel is placed by an integer rotation
@@ -927,14 +928,31 @@ struct TileCoord {
 #ifndef PR_CM_IMG_ORDER
 #define PR_CM_IMG_ORDER 0
 #endif
+// XCD-grouped order for launches of at most PR_CM_XCD_MAX_FRAMES frames (TileGeom.xcd_map): with few
+// frames per launch a tile's constant tables are re-read per frame group on every XCD and dominate
+// the traffic (Jungfrau-16M, 8-frame chunks: 43.4 -> 37.7 us/frame; epix10k2M at 8 frames 6.35 ->
+// 5.76), while at 32-64 frames the plain table-major order spreads the raw / output streams better
+// (epix10k2M 64 frames: 4.59 vs 4.72), profiles/r5/README.md section 20
+#ifndef PR_CM_XCD_MAX_FRAMES
+#define PR_CM_XCD_MAX_FRAMES 12
+#endif
 __device__ __forceinline__ TileCoord cm_coords(const TileGeom& tg, int R, int C, const int id = (int)blockIdx.x,
                                                const int32_t* desc = nullptr) {
   TileCoord t;
   const int ng = (tg.nframes + tg.fpw - 1) / tg.fpw;
-  const int tile = id / ng;
-  t.f = (id - tile * ng) * tg.fpw;
-  t.tile = tile;
   const int per_panel = tg.asics_per_col * tg.asics_per_row;
+  int tile = id / ng;
+  t.f = (id - tile * ng) * tg.fpw;
+  if (tg.xcd_map) {
+    // XCD-grouped table-major order: workgroups go to the 8 XCDs round-robin, so ids 8j + x of a
+    // block of 8 tiles x ng frame groups run tile (block, x) on XCD x -- every frame of a tile on
+    // ONE XCD, whose L2 then fetches the tile's tables once per launch instead of once per XCD
+    // (the launcher sets xcd_map only when the tiles per frame are a multiple of 8)
+    const int blk = id / (8 * ng), rem = id - blk * 8 * ng;
+    tile = blk * 8 + (rem & 7);
+    t.f = (rem >> 3) * tg.fpw;
+  }
+  t.tile = tile;
   t.panel = tile / per_panel;
   t.ar = (tile % per_panel) / tg.asics_per_row;
   t.ac = (tile % per_panel) % tg.asics_per_row;
@@ -1813,6 +1831,8 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   tg.fpw = (epix_prod && asic_cols == 48) ? PR_CM_FPW : 1;
   tg.side_slots = side_slots;
   tg.pitch = cm_pitch(asic_cols, kind == kJungfrau ? 2 : 1);
+  tg.xcd_map = (nframes <= PR_CM_XCD_MAX_FRAMES &&
+                ((int64_t)n_panels * tg.asics_per_col * tg.asics_per_row) % 8 == 0) ? 1 : 0;
   const CmParams cp{thr, maxcorr, npix_min, flags, bank_cols};
   const dim3 grid((unsigned)(n_panels * tg.asics_per_col * tg.asics_per_row * ((nframes + tg.fpw - 1) / tg.fpw)));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
