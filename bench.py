@@ -181,8 +181,84 @@ def resolve_shape(args, gpu: bool):
     return share, resolve_consumer_batch(args.batch, share), resolve_producer_streams(where, args.compute_streams, share)
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def self_launch(n: int, argv) -> int:
+    """``python bench.py --gpus N`` with N > 1 and no launcher around it: start the N ranks here, as
+    CHILD processes with the env a torchrun / mpirun launch gives them (RANK, WORLD_SIZE,
+    LOCAL_RANK, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), one per GPU.  The reference's
+    launch shape is the same (``mpirun -n 4 psana-ray-producer``, README.md:20; every rank reads
+    its own rank and size, psana_ray/producer.py:138-140).
+
+    This parent never touches the GPU (no torch.cuda call, no HIP runtime) and never execs: it
+    waits for the children, forwards nothing itself (rank 0 prints the one JSON line on the
+    inherited stdout), and returns the worst child exit code.  When one rank fails, the others are
+    given 30 s to notice (their collectives fail) and are then killed by PID, so a lost rank cannot
+    hang the job until gloo's 600-s timeout."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    script = os.path.abspath(__file__)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(n),
+                    "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                    "PSANA_RAY_SELF_LAUNCHED": "1"})
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=env, stdout=subprocess.PIPE,
+                                      text=True, bufsize=1))
+    print(f"bench.py: self-launched {n} ranks (pids {[p.pid for p in procs]}, rendezvous 127.0.0.1:{port})",
+          file=sys.stderr, flush=True)
+
+    def forward(p):
+        # the result line to stdout; everything else a rank writes there (gloo's "[Gloo] Rank r is
+        # connected to ..." banner) to stderr, so stdout carries exactly ONE line
+        for line in p.stdout:
+            dst = sys.stdout if line.startswith("{") else sys.stderr
+            dst.write(line)
+            dst.flush()
+
+    fwd = [threading.Thread(target=forward, args=(p,), daemon=True) for p in procs]
+    for t in fwd:
+        t.start()
+    rcs = [None] * n
+    first_fail = None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+                if rcs[i] not in (None, 0) and first_fail is None:
+                    first_fail = time.monotonic()
+                    print(f"bench.py: rank {i} exited with {rcs[i]}", file=sys.stderr, flush=True)
+        if first_fail is not None and time.monotonic() - first_fail > 30.0:
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.send_signal(signal.SIGKILL)
+                    rcs[i] = p.wait()
+                    print(f"bench.py: killed rank {i} (pid {p.pid}) after a peer failed", file=sys.stderr, flush=True)
+        time.sleep(0.05)
+    for t in fwd:
+        t.join(timeout=10)
+    bad = [rc for rc in rcs if rc != 0]
+    if not bad:
+        return 0
+    # a signal death (negative rc) maps to 128 + signo, like a shell
+    return max((128 - rc) if rc < 0 else rc for rc in bad)
+
+
 def main(argv=None):
     args = parse(argv)
+    from psana_ray_amd.parallel.launch import detect as _detect
+
+    if args.gpus > 1 and _detect().launcher == "single":
+        return self_launch(args.gpus, sys.argv[1:] if argv is None else list(argv))
     from psana_ray_amd.utils.runtime_env import select_copy_engine
 
     select_copy_engine(args.copy_engine)   # before the HIP runtime initialises (first torch.cuda call)
@@ -223,6 +299,9 @@ def main(argv=None):
     # shape (config.pipeline_shape: 3 producer streams and 32-frame batches there), the same
     # resolution psana-ray-producer / psana-ray-consumer make
     gpu_share, args.batch, compute_streams = resolve_shape(args, gpu)
+    if gpu and gpu_share > 1 and rank == 0:
+        print(f"bench.py: WARNING: {world} ranks on {torch.cuda.device_count()} visible GPU(s): {gpu_share} ranks "
+              f"share a GPU (config.ranks_per_gpu); n_gpus reports distinct devices", file=sys.stderr, flush=True)
 
     coord = None
     store = None
@@ -233,7 +312,17 @@ def main(argv=None):
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         import datetime
 
-        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
+        # gloo prints its "[Gloo] Rank r is connected to ..." banner on fd 1 while connecting: send
+        # it to stderr so stdout carries only the result line (torchrun launches included)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         coord = dist.group.WORLD
         store = dist.distributed_c10d._get_default_store()
 
@@ -555,6 +644,10 @@ def main(argv=None):
         consumed_per_rank = allsum(got)
         recv_share = [round(x, 3) for x in allsum(int(st.get("frames_recv", 0)) / max(1, got))]
     copies = prod.engine.copy_stats() if (prod is not None and prod.engine is not None) else None
+    # n_gpus = DISTINCT devices the ranks ran on (2 ranks sharing the one GPU of a box report 1);
+    # n_ranks = world size
+    devs = topology["device_per_rank"] if topology is not None else [device.index if gpu else -1]
+    n_devices = len({d for d in devs if d is not None and d >= 0})
     if not gpu:
         staging = "host memory (CPU rehearsal)"
     elif args.source == "device":
@@ -568,7 +661,8 @@ def main(argv=None):
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "frames/s",
-        "n_gpus": world,
+        "n_gpus": n_devices,
+        "n_ranks": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * dt / args.steps, 4),
@@ -592,6 +686,8 @@ def main(argv=None):
             "source": args.source,
             "chunk": args.chunk,
             "ranks_per_gpu": gpu_share,
+            "launch": "self-launched children" if os.environ.get("PSANA_RAY_SELF_LAUNCHED") == "1"
+                      else li.launcher,
             "producer_ranks": n_prod,
             "queue": "local (single process)" if sess is None else "elastic fabric session",
         },
