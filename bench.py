@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Flagship benchmark: detector frames/sec (whole node) through the shared queue, epix10k2M.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched by
-``torch.distributed.run`` with one rank per GPU.  One STEP = every rank's consumer takes
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.  For N > 1 it runs either
+under a launcher (``torch.distributed.run`` / mpirun / Slurm: one rank per GPU) or, typed as is,
+starts its N ranks itself as child processes before any GPU call (``self_launch``).  One STEP = every rank's consumer takes
 ``--batch`` frames out of its shard of the shared queue and runs the on-GPU peak finder on them.
 Behind it, every producer rank streams raw epix10k2M frames from a pinned host pool into HBM
 (our copy kernel on a side stream), calibrates them with the HIP kernels (pedestal + gain
@@ -21,7 +22,10 @@ window runs with ``route=remote_only`` (a producer never keeps a frame on its ow
 consumer on another GPU is linked: every frame crosses xGMI as a HIP-IPC peer copy); its frames/s,
 cross-GPU GB/s and bytes per rank are reported under ``extra.xgmi_phase`` (``--cross-steps 0``
 skips it).  The run is self-validating: it exits non-zero (after printing its line) when a link
-failed or never attached, or when less than 90% of that window's frames crossed GPUs.
+failed or never attached, when less than 90% of that window's frames crossed GPUs, or when a frame
+arrived with contents that differ from what its producer sent (every 64th frame a producer sends
+to another process carries a content checksum the consumer re-sums from its own ring,
+``extra.frame_checks``; csrc/verify.h).
 
 Synthetic data: random-init calibration constants and a pre-generated pool of raw frames
 (cycled), because no LCLS data / psana exists offline (BASELINE.json).
@@ -635,7 +639,26 @@ def main(argv=None):
     ep.join(timeout=60)
     topology = _topology(ep, device, allsum) if sess is not None or gpu else None
     peaks = consumer.synchronize() if consumer is not None else 0
+    if gpu:
+        torch.cuda.synchronize(device)   # every verify launch on the consumer streams has completed
     st = ep.stats()
+    # end-to-end checks of frames that crossed processes (csrc/verify.h): consumer-side re-sums of the
+    # frames whose producer attached a checksum, and the acquires issued before peer-written reads
+    checks = None
+    if sess is not None:
+        vc = allsum(ep.verify_counts())
+        checks = {"verify_every": ep._fabric.verify_every() if ep._fabric is not None else None,
+                  "frames_verified": sum(v["verified"] for v in vc),
+                  "frames_mismatched": sum(v["mismatched"] for v in vc),
+                  "verified_per_rank": [v["verified"] for v in vc],
+                  "mismatched_per_rank": [v["mismatched"] for v in vc],
+                  "last_bad_gevt_per_rank": [v["last_bad_gevt"] for v in vc],
+                  "acquires_per_rank": [v["acquires"] for v in vc],
+                  "checksummed_sent_per_rank": allsum(int(st.get("frames_checksummed", 0))),
+                  "corrupted_injected_per_rank": allsum(int(st.get("frames_corrupted", 0)))}
+        if cross is not None:
+            cross["frames_verified"] = checks["frames_verified"]
+            cross["frames_mismatched"] = checks["frames_mismatched"]
     # per rank over the whole run: the share of the frames it consumed that arrived from another
     # process (consumer-only ranks of BASELINE config 3 receive every frame over the fabric)
     recv_share = consumed_per_rank = None
@@ -708,6 +731,7 @@ def main(argv=None):
             "frames_sent_rank0_headline": int(c1.get("frames_sent", 0) - c0.get("frames_sent", 0)),
             "bytes_sent_rank0": st.get("bytes_sent", 0),
             "xgmi_phase": cross,
+            "frame_checks": checks,
             "links_rank0": linking,
             "topology": topology,
             "steady_gate": gate,
@@ -731,6 +755,9 @@ def main(argv=None):
             problems.append(f"{failed_links} fabric link(s) failed")
         if linking is not None and not all(allsum(bool(linking.get("complete")))):
             problems.append("some rank's links never completed")
+        if checks is not None and checks["frames_mismatched"] > 0:
+            problems.append(f"{checks['frames_mismatched']} frame(s) arrived with contents that differ from what "
+                            f"their producer sent (last gevt per rank {checks['last_bad_gevt_per_rank']})")
         if cross is not None and cross["cross_gpu_fraction"] < 0.9:
             problems.append(f"only {cross['cross_gpu_fraction']:.3f} of the cross window's frames crossed GPUs")
     result["extra"]["validation"] = problems or "ok"

@@ -23,6 +23,7 @@ namespace py = pybind11;
 #include "kernels.h"
 #include "streams.h"
 #include "trace.h"
+#include "verify.h"
 #include "xtc2.h"
 
 
@@ -173,6 +174,18 @@ PYBIND11_MODULE(_C, m) {
         "peer access (hipDeviceCanAccessPeer) and link type / hop count (hipExtGetLinkTypeAndHopCount) "
         "between every pair of visible GPUs");
   m.def("install_segv_trace", &maybe_install_segv_trace);
+  m.def("frame_checksum_host", [](uint64_t ptr, int64_t bytes) {
+        return pr::frame_checksum_host(reinterpret_cast<const void*>(ptr), bytes);
+      }, py::arg("ptr"), py::arg("bytes"), "content checksum of a host buffer (csrc/verify.h)");
+  m.def("checksum_tag", [](uint64_t sum) { return pr::ck_tag(sum); }, py::arg("sum"));
+  py::class_<pr::FrameVerifier, std::shared_ptr<pr::FrameVerifier>>(m, "FrameVerifier")
+      .def(py::init<int, int64_t>(), py::arg("device"), py::arg("frame_bytes"))
+      .def("checksum_async", &pr::FrameVerifier::checksum_async, py::arg("ptrs"), py::arg("stream"))
+      .def("result", &pr::FrameVerifier::result, py::arg("index"))
+      .def("verify", &pr::FrameVerifier::verify, py::arg("ptrs"), py::arg("expect"), py::arg("gevt"),
+           py::arg("stream"))
+      .def("acquire", &pr::FrameVerifier::acquire, py::arg("stream"))
+      .def("counts", &pr::FrameVerifier::counts);
   m.doc() = "psana_ray_amd native extension: gfx950 HIP kernels + host runtime";
   m.attr("MAX_FRAMES_PER_LAUNCH") = pr::kMaxFrames;
   m.attr("KIND_EPIX10KA") = (int)pr::kEpix10ka;
@@ -375,7 +388,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("copy_dev_ms", &pr::FabricStats::copy_dev_ms)
       .def_readonly("copy_dev_bytes", &pr::FabricStats::copy_dev_bytes)
       .def_readonly("taken_local", &pr::FabricStats::taken_local)
-      .def_readonly("taken_remote", &pr::FabricStats::taken_remote);
+      .def_readonly("taken_remote", &pr::FabricStats::taken_remote)
+      .def_readonly("frames_checksummed", &pr::FabricStats::frames_checksummed)
+      .def_readonly("frames_corrupted", &pr::FabricStats::frames_corrupted);
   py::class_<pr::CopySample>(m, "CopySample")
       .def_readonly("dev_ms", &pr::CopySample::dev_ms)
       .def_readonly("issue_to_done_ms", &pr::CopySample::issue_to_done_ms)
@@ -433,6 +448,9 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("copy_engine", &pr::QueueFabric::copy_engine)
       .def_property_readonly("copy_workgroups", &pr::QueueFabric::copy_workgroups)
       .def("copy_samples", &pr::QueueFabric::copy_samples)
+      .def("set_verify_every", &pr::QueueFabric::set_verify_every, py::arg("every"))
+      .def("verify_every", &pr::QueueFabric::verify_every)
+      .def("verify_counts", &pr::QueueFabric::verify_counts)
       .def_static("copy_grid_for", &pr::QueueFabric::copy_grid_for, py::arg("consumer_devices"), py::arg("device"),
                   py::arg("per_peer"))
       .def("links", &pr::QueueFabric::links);
@@ -500,6 +518,8 @@ PYBIND11_MODULE(_C, m) {
       .def("n_ready", &SP::n_ready)
       .def("consumer_held", &SP::consumer_held)
       .def("wait_ready_on", &SP::wait_ready_on, py::arg("slot"), py::arg("stream"))
+      .def("check_frames", &SP::check_frames, py::arg("slots"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
       .def("wait_free_on", &SP::wait_free_on, py::arg("slot"), py::arg("stream"))
       .def("sync_ready", &SP::sync_ready, py::call_guard<py::gil_scoped_release>())
       .def("header", &SP::header)

@@ -567,8 +567,12 @@ __device__ __forceinline__ float cm_gain(const float (&ga)[NT][8], uint32_t cb, 
 // NaN-fill: x if x is a number, else s -- ONE v_med3_f32 instead of v_cmp_u + v_cndmask.  With no
 // NaN operand med3(x, s, x) = x; with a NaN operand v_med3_f32 returns v_min3_f32 of its operands,
 // whose minNum semantics drop the NaNs: med3(NaN, s, NaN) = s (s is never NaN: a raw value or a
-// recomputed ADU - pedestal).  The third operand is an opaque copy of x, so the compiler cannot fold
-// med3(x, s, x) to x.
+// recomputed ADU - pedestal).  The third operand is x itself (no opaque copy: an asm barrier would
+// cost a v_mov per pixel in a VALU-bound kernel).  That relies on LLVM keeping
+// amdgcn.fmed3(x, s, x) as a med3 and not folding it to x, which
+// tests/test_med3_fill_isa.py checks on the compiled gfx950 code (v_med3_f32 vA, vX, vS, vX
+// present) and the bitwise GPU tests check numerically; PR_CM_MED3_FILL=0 builds the compare +
+// select reference.
 #ifndef PR_CM_MED3_FILL
 #define PR_CM_MED3_FILL 1
 #endif

@@ -288,6 +288,7 @@ struct QueueFabric::Batch {
   hipEvent_t ev = nullptr;                 // runtime engine / reclaims: this batch's own event
   std::shared_ptr<CopyGroup> grp;          // kernel engine: the dispatch it rode in
   double t_issue = 0;
+  std::vector<std::pair<int, int64_t>> ck;  // (frame of the batch, pinned checksum result index)
 };
 
 QueueFabric::QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is_producer, bool is_consumer,
@@ -304,7 +305,77 @@ QueueFabric::QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate (fabric)");
   }
   if (!is_producer) drained_.store(true);
+  if (device_ < 0 || slot_bytes_ % 16 == 0) {   // the device checksum reads whole 16-B words
+    verifier_ = std::make_shared<FrameVerifier>(device_, slot_bytes_);
+    if (is_consumer) pool_->set_verifier(verifier_);
+  }
+  if (const char* e = getenv("PSANA_RAY_AMD_FAULT_CORRUPT")) corrupt_every_ = std::max(0L, atol(e));
   register_native_thread_owner(this, [this] { halt(); });
+}
+
+void QueueFabric::set_verify_every(int every) {
+  check(!running_.load(), "QueueFabric: set_verify_every before start()");
+  verify_every_ = std::max(0, every);
+}
+
+std::array<int64_t, 4> QueueFabric::verify_counts() const {
+  return verifier_ ? verifier_->counts() : std::array<int64_t, 4>{0, 0, -1, 0};
+}
+
+// Producer: the frames of `b` that carry a content checksum to their consumer (every
+// verify_every_-th frame of this producer by its rank-local idx -- so every producer's links are
+// sampled, which gevt % N would not do for N producers sharing one gevt sequence -- and only
+// frames that have none yet: a frame handed back by a closing consumer keeps its producer's
+// checksum).  GPU: queued on `stream` ahead of the copy, results read
+// when the copy completes (finish_checksums); host: computed now.
+void QueueFabric::start_checksums(Batch& b, uint64_t stream) {
+  if (verify_every_ <= 0 || !verifier_) return;
+  std::vector<uint64_t> ptrs;
+  std::vector<int> which;
+  for (size_t i = 0; i < b.slots.size(); ++i) {
+    const SlotHeader& h = b.hdrs[i];
+    if (h.idx < 0 || h.idx % verify_every_ != 0 || ck_tagged(h.aux)) continue;
+    if (device_ < 0) {
+      b.hdrs[i].aux = ck_tag(frame_checksum_host(reinterpret_cast<const void*>(pool_->slot_ptr(b.slots[i])), slot_bytes_));
+      continue;
+    }
+    ptrs.push_back(pool_->slot_ptr(b.slots[i]));
+    which.push_back((int)i);
+  }
+  for (size_t a = 0; a < ptrs.size(); a += kMaxFrames) {
+    const size_t n = std::min(ptrs.size() - a, (size_t)kMaxFrames);
+    const int64_t base =
+        verifier_->checksum_async(std::vector<uint64_t>(ptrs.begin() + a, ptrs.begin() + a + n), stream);
+    for (size_t k = 0; k < n; ++k) b.ck.emplace_back(which[a + k], base + (int64_t)k);
+  }
+}
+
+void QueueFabric::finish_checksums(Batch& b) {
+  for (const auto& c : b.ck) b.hdrs[(size_t)c.first].aux = verifier_->result(c.second);
+  int64_t n = 0;
+  for (const SlotHeader& h : b.hdrs) n += ck_tagged(h.aux) ? 1 : 0;
+  b.ck.clear();
+  std::lock_guard<std::mutex> lk(mu_);
+  st_.frames_checksummed += n;
+}
+
+// Test-only fault injection (PSANA_RAY_AMD_FAULT_CORRUPT=N): every N-th frame this producer sends to
+// another process is damaged in the consumer's ring after its copy, so the consumer's checks must
+// catch it (tests/test_fabric_verify.py).  Off (0) unless the variable is set.
+void QueueFabric::inject_corruption(const Batch& b, uint64_t stream) {
+  if (corrupt_every_ <= 0) return;
+  const Link& l = *b.link;
+  for (size_t i = 0; i < b.slots.size(); ++i) {
+    if (++corrupt_count_ % corrupt_every_ != 0) continue;
+    const uint64_t dst = l.remote[b.rslots[i]] + (uint64_t)(slot_bytes_ / 2 / 16 * 16);
+    if (device_ < 0)
+      memset(reinterpret_cast<void*>(dst), 0x5A, 16);
+    else
+      hip_check(hipMemsetAsync(reinterpret_cast<void*>(dst), 0x5A, 16, reinterpret_cast<hipStream_t>(stream)),
+                "hipMemsetAsync (fault injection)");
+    std::lock_guard<std::mutex> lk(mu_);
+    ++st_.frames_corrupted;
+  }
 }
 
 void QueueFabric::halt() {
@@ -1196,6 +1267,7 @@ int64_t QueueFabric::producer_pass(double now) {
     const int n = (int)b.slots.size();
     l.inflight -= n;
     if (l.attached && !l.dead && !l.closed) {
+      finish_checksums(b);
       for (int i = 0; i < n; ++i) post_notice(l, make_notice(b.rslots[i], 0, b.hdrs[i]));
       l.seg->n_head.store(l.n_head, std::memory_order_release);
       // the copy is complete (host-observed): free the slots with no device wait, and count the
@@ -1347,6 +1419,7 @@ int64_t QueueFabric::producer_pass(double now) {
         trace::Range tr("fabric.copy_batch");
         b.stream = l.stream != nullptr ? l.stream : stream_;
         pool_->begin_send_batch(slots, reinterpret_cast<uint64_t>(b.stream));   // stream waits for the frames
+        start_checksums(b, reinterpret_cast<uint64_t>(b.stream));
         int a = 0;
         const uint64_t sb = (uint64_t)slot_bytes_;
         while (a < n) {   // coalesce runs contiguous on both sides
@@ -1360,13 +1433,16 @@ int64_t QueueFabric::producer_pass(double now) {
                     "hipMemcpyAsync (frame -> consumer ring)");
           a = e;
         }
+        inject_corruption(b, reinterpret_cast<uint64_t>(b.stream));
         b.ev = take_event();
         hip_check(hipEventRecord(b.ev, b.stream), "hipEventRecord (frame copy)");
       } else {
         pool_->begin_send_batch(slots, 0);
+        start_checksums(b, 0);
         for (int j = 0; j < n; ++j)
           memcpy(reinterpret_cast<void*>(l.remote[b.rslots[j]]), reinterpret_cast<const void*>(pool_->slot_ptr(slots[j])),
                  (size_t)slot_bytes_);
+        inject_corruption(b, 0);
       }
       l.inflight += n;
       inflight_.push_back(std::move(b));
@@ -1472,6 +1548,7 @@ void QueueFabric::issue_copies(std::vector<Batch>& kb, double now) {
   std::vector<int> all;
   for (const Batch& b : kb) all.insert(all.end(), b.slots.begin(), b.slots.end());
   pool_->begin_send_batch(all, reinterpret_cast<uint64_t>(xstream_));   // xstream_ waits for their data
+  for (Batch& b : kb) start_checksums(b, reinterpret_cast<uint64_t>(xstream_));   // ahead of the copy
   auto g = std::make_shared<CopyGroup>();
   g->start = take_timed_event();
   g->end = take_timed_event();
@@ -1513,6 +1590,7 @@ void QueueFabric::issue_copies(std::vector<Batch>& kb, double now) {
     g->bytes += (int64_t)n * slot_bytes_;
   }
   flush();
+  for (const Batch& b : kb) inject_corruption(b, reinterpret_cast<uint64_t>(xstream_));
   hip_check(hipEventRecord(g->end, xstream_), "hipEventRecord (copy end)");
   g->pending = (int)kb.size();
   for (Batch& b : kb) {

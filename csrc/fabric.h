@@ -74,6 +74,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <array>
 #include <atomic>
 #include <deque>
 #include <memory>
@@ -83,6 +84,7 @@
 #include <vector>
 
 #include "runtime.h"
+#include "verify.h"
 
 namespace pr {
 
@@ -132,6 +134,8 @@ struct FabricStats {
   int64_t copy_dev_bytes = 0;    // bytes those timed copies moved
   int64_t taken_local = 0;       // consumer: frames taken (get) that its own process produced
   int64_t taken_remote = 0;      // consumer: frames taken that another process produced
+  int64_t frames_checksummed = 0;  // producer: frames sent with a content checksum (verify.h)
+  int64_t frames_corrupted = 0;    // producer: test-only fault injection (PSANA_RAY_AMD_FAULT_CORRUPT)
 };
 
 // One timed copy dispatch (fabric pass): device time of the copy, bytes, frames, host time from
@@ -219,6 +223,15 @@ class QueueFabric {
   std::vector<CopySample> copy_samples() const;
   static constexpr int kMaxSamples = 4096;
 
+  // End-to-end frame checks (verify.h).  Producer: every `every`-th frame (idx % every == 0, rank-local) sent
+  // to another process carries a content checksum in its notice (0 = none).  Consumer: frames taken
+  // from other processes get a system-scope acquire on the reader's stream, checksummed ones are
+  // re-summed and compared.  Before start().
+  void set_verify_every(int every);
+  int verify_every() const { return verify_every_; }
+  // consumer: {verified, mismatched, last mismatching gevt, acquires} (verify.h counts())
+  std::array<int64_t, 4> verify_counts() const;
+
   void start();
   void request_stop() { stop_.store(true); }
   bool join(double timeout_s);
@@ -267,6 +280,9 @@ class QueueFabric {
   void issue_copies(std::vector<Batch>& kb, double now);
   int copy_grid(const std::vector<Batch>& kb) const;
   void finish_group(const std::shared_ptr<CopyGroup>& g);
+  void start_checksums(Batch& b, uint64_t stream);
+  void finish_checksums(Batch& b);
+  void inject_corruption(const Batch& b, uint64_t stream);
 
   SlotPool* pool_;
   int64_t slot_bytes_;
@@ -288,6 +304,9 @@ class QueueFabric {
   hipStream_t xstream_ = nullptr;   // kernel engine: the copy stream (own hardware queue, pooled)
   int copy_engine_ = kCopyKernel;
   int copy_wgs_ = 128;
+  int verify_every_ = 0;
+  std::shared_ptr<FrameVerifier> verifier_;
+  int64_t corrupt_every_ = 0, corrupt_count_ = 0;   // test-only fault injection
   int xstream_kind_ = 1;            // kStreamDedicated
   std::vector<hipEvent_t> free_events_, all_events_;
   std::vector<hipEvent_t> free_timed_;          // timing-enabled events (copy groups)

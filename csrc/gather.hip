@@ -172,9 +172,15 @@ bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgro
 // chunk (256 lanes x U x 16 B in flight); the grid strides over the chunks of all runs, so the
 // writes to different consumers (different xGMI links) are in flight at the same time.  Loads are
 // nontemporal (the producer slot is freed right after); stores are plain (a same-GPU consumer reads
-// the slot next).  Visibility: the consumer is told only after this kernel's completion event
-// (end-of-kernel release), see csrc/fabric.h.
+// the slot next).  Visibility: the consumer is told only after this kernel's completion event, and
+// every wave ends with an explicit SYSTEM-scope release (buffer_wbl2 sc0 sc1: lines of peer memory
+// this XCD's L2 may hold dirty are written back over xGMI before the completion signal), instead of
+// relying on the dispatch packet's release scope; the consumer issues the matching acquire
+// (verify.h).  PR_COPY_RELEASE=0 builds the A/B variant without it.
 // ---------------------------------------------------------------------------------------------
+#ifndef PR_COPY_RELEASE
+#define PR_COPY_RELEASE 1
+#endif
 template <int U>
 __global__ __launch_bounds__(256) void copy_runs_kernel(const CopyRuns cr, const int total_chunks) {
   constexpr int kChunk16 = 256 * U;
@@ -197,6 +203,9 @@ __global__ __launch_bounds__(256) void copy_runs_kernel(const CopyRuns cr, const
       if (q < n16) dst[q] = v[u];
     }
   }
+#if PR_COPY_RELEASE
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+#endif
 }
 
 int launch_copy_runs(CopyRuns& cr, int workgroups, uint64_t stream) {

@@ -1,4 +1,5 @@
 #include "runtime.h"
+#include "verify.h"
 
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -673,7 +674,41 @@ std::vector<int> SlotPool::get_batch(int max_n, double timeout_s, uint64_t strea
     DeviceGuard dg(device_);
     for (const auto& w : waits) wait_ref(w, stream);
   }
+  if (!out.empty()) check_frames(out, stream);
   return out;
+}
+
+void SlotPool::set_verifier(std::shared_ptr<FrameVerifier> v) {
+  std::lock_guard<std::mutex> lk(mu_);
+  verifier_ = std::move(v);
+}
+
+std::shared_ptr<FrameVerifier> SlotPool::verifier() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return verifier_;
+}
+
+void SlotPool::check_frames(const std::vector<int>& slots, uint64_t stream) {
+  std::shared_ptr<FrameVerifier> v;
+  std::vector<uint64_t> ptrs;
+  std::vector<int64_t> expect, gevt;
+  bool remote = false;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!verifier_) return;
+    v = verifier_;
+    for (int s : slots) {
+      check_slot(s);
+      remote |= origin_[s] >= 0;
+      if (ck_tagged(hdr_[s].aux) && !ptrs_.empty()) {
+        ptrs.push_back(ptrs_[(size_t)s]);
+        expect.push_back(hdr_[s].aux);
+        gevt.push_back(hdr_[s].gevt);
+      }
+    }
+  }
+  if (remote || !ptrs.empty()) v->acquire(stream);
+  if (!ptrs.empty()) v->verify(ptrs, expect, gevt, stream);
 }
 
 void SlotPool::release_batch(const std::vector<int>& slots, uint64_t stream) {

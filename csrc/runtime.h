@@ -19,12 +19,15 @@
 
 #include <condition_variable>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 namespace pr {
+
+class FrameVerifier;   // verify.h
 
 // ---------------------------------------------------------------------------------------
 class PinnedBuffer {
@@ -46,7 +49,7 @@ class PinnedBuffer {
 // One hipMalloc allocation of HBM (ring segments).  Ring memory is allocated here, not by the torch
 // caching allocator, so every allocation is exactly one segment: HIP IPC export works per
 // allocation, and opening an IPC handle of an allocation above 2 GiB hangs on this ROCm stack
-// (measured: 2.08 GB attaches in 0.2 ms, 2.16 GB never returns; tools/diag_ipc_attach.py).
+// (measured: 2.08 GB attaches in 0.2 ms, 2.16 GB never returns; profiles/r2/ipc_attach.md).
 class DeviceBuffer {
  public:
   DeviceBuffer(int64_t bytes, int device);
@@ -169,6 +172,14 @@ class SlotPool {
   void end_recv_batch(const std::vector<int>& slots, const std::vector<SlotHeader>& hdrs, uint64_t stream);
   int64_t event_records() const { return ev_records_; }
 
+  // End-to-end checks of frames other processes wrote into this (consumer) ring (verify.h): every
+  // get_batch -- and check_frames, which the single-frame get path calls -- issues a system-scope
+  // acquire on the caller's stream when a taken frame came from another process, and re-sums the
+  // frames whose header carries a producer checksum (aux tag), compared on the device.
+  void set_verifier(std::shared_ptr<FrameVerifier> v);
+  std::shared_ptr<FrameVerifier> verifier() const;
+  void check_frames(const std::vector<int>& slots, uint64_t stream);
+
   // elastic fabric (fabric.h): another PROCESS writes granted slots, so a grant needs the slot's
   // previous readers to have finished on the host's view (event query), not just stream order
   std::vector<int> grant_batch(int max_n);                                    // FREE -> RECEIVING
@@ -234,6 +245,7 @@ class SlotPool {
   std::vector<int64_t> got_origins_;
   bool closed_ = false;
   bool auto_route_ = false;
+  std::shared_ptr<FrameVerifier> verifier_;
   PoolStats st_;
 };
 

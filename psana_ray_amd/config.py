@@ -115,6 +115,19 @@ def fabric_copy_setting(engine: Optional[str] = None, workgroups: Optional[int] 
         raise ValueError(f"unknown stream kind {kind!r} ({' | '.join(STREAM_KINDS)})")
     return eng, int(wgs), kind
 
+# End-to-end frame checks of the fabric (csrc/verify.h): a producer attaches a content checksum to
+# every FABRIC_VERIFY_EVERY-th frame (rank-local idx % N == 0) it sends to another process; the consumer re-sums
+# it from its own ring before the caller reads it and counts matches / mismatches on the device.
+# 1/64 of the routed frames = one extra 8.65-MB read per 64 frames on each side.  0 disables.
+# Env override: PSANA_RAY_AMD_VERIFY_EVERY.
+FABRIC_VERIFY_EVERY = 64
+
+
+def fabric_verify_every() -> int:
+    v = os.environ.get("PSANA_RAY_AMD_VERIFY_EVERY", "")
+    return max(0, int(v)) if v.strip() else FABRIC_VERIFY_EVERY
+
+
 # --- rendezvous ---------------------------------------------------------------------------
 DEFAULT_STORE_PORT = 6379             # the Ray head port of README.md:15, reused for the store
 ENV_ADDRESS = "PSANA_RAY_ADDRESS"

@@ -7,9 +7,12 @@ rank come from the launcher's environment (MPICH/Hydra ``PMI_*``/``MPI_LOCALRANK
 """
 from __future__ import annotations
 
+import logging
 import os
 from dataclasses import dataclass
 from typing import Optional
+
+log = logging.getLogger(__name__)
 
 _RANK = ("RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK", "SLURM_PROCID")
 _SIZE = ("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS")
@@ -60,7 +63,10 @@ def detect() -> LaunchInfo:
         launcher = "single"
     local_size = _first_int(_LOCAL_SIZE, None)
     if local_size is None:
-        local_size = size if launcher != "slurm" else 1
+        # no launcher told how many of its ranks share this node: assume one (the
+        # global size would make a multi-node PMI launch take the shared-GPU pipeline shape).
+        # torchrun, Open MPI, MPICH/Hydra and bench.py's self-launch all set a local size.
+        local_size = 1
     return LaunchInfo(rank, size, local, launcher, max(1, local_size))
 
 
@@ -74,7 +80,9 @@ def ranks_per_gpu(n_gpus: Optional[int] = None, local_size: Optional[int] = None
         import torch
 
         n_gpus = torch.cuda.device_count()
-    return max(1, -(-int(local_size) // max(1, int(n_gpus))))
+    share = max(1, -(-int(local_size) // max(1, int(n_gpus))))
+    log.debug("ranks per GPU: %d (%d local ranks on %d GPU(s))", share, int(local_size), int(n_gpus))
+    return share
 
 
 def device_for(local_rank: int, requested: Optional[str] = None):

@@ -64,6 +64,14 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--psana_calibrated", action="store_true",
                    help="psana_wrapper runs: take psana's CPU-calibrated frames even when the wrapper can provide "
                         "raw frames and constants (default: raw frames calibrated by the HIP kernels)")
+    g.add_argument("--psana_private_constants", action="store_true",
+                   help="psana_wrapper runs without a calib_constants() hook: read psana2's calibration constants "
+                        "through its PRIVATE detector accessors (det.raw._pedestals / _gain / _status / ...); "
+                        "without it such a run falls back to psana's CPU calibration")
+    g.add_argument("--psana_handle_shard", default="explicit", choices=["explicit", "psana"],
+                   help="psana_wrapper runs whose raw frames come from the run's own event loop (no raw retrieval "
+                        "mode): explicit = rank r keeps every size-th event from r (default); psana = the loop is "
+                        "already sharded over the MPI ranks by psana")
     g.add_argument("--num_events", type=int, default=None, help="events in a synthetic run (default: endless)")
     g.add_argument("--data_dir", type=str, default=None, help="raw-run files directory (or $PSANA_RAY_DATA)")
     g.add_argument("--chunk", type=int, default=64, help="frames per H2D copy / kernel launch (<= 64)")
@@ -210,6 +218,10 @@ def main(argv=None) -> int:
     if device.type == "cuda":
         torch.cuda.set_device(device)
         bind_numa_to_device(device)
+        from .parallel.launch import ranks_per_gpu
+
+        log.info("Rank %d: %s launch, %d local rank(s), %d rank(s) per GPU", rank, li.launcher, li.local_size,
+                 ranks_per_gpu(local_size=li.local_size))
     stop = threading.Event()
 
     def signal_handler(sig, frame):   # every rank (Q-14): stop producing, advertise EOS, exit cleanly
@@ -238,7 +250,8 @@ def main(argv=None) -> int:
         try:
             source = open_source(args.exp, args.run, args.detector_name, rank=group, size=n_groups,
                                  n_events=args.num_events, pinned=device.type == "cuda", data_dir=args.data_dir,
-                                 mode=Mode.raw, prefer_raw=True)
+                                 mode=Mode.raw, prefer_raw=True, psana_private_constants=args.psana_private_constants,
+                                 psana_handle_shard=args.psana_handle_shard)
         except NoSourceError as e:
             log.error("Rank %d: %s", rank, e)
             return 2
@@ -253,7 +266,9 @@ def main(argv=None) -> int:
             source = open_source(args.exp, args.run, args.detector_name, rank=rank, size=size,
                                  n_events=args.num_events, pinned=device.type == "cuda", data_dir=args.data_dir,
                                  mode=read_mode if not args.calibrate_on_read else Mode.raw,
-                                 prefer_raw=not args.psana_calibrated)
+                                 prefer_raw=not args.psana_calibrated,
+                                 psana_private_constants=args.psana_private_constants,
+                                 psana_handle_shard=args.psana_handle_shard)
         except NoSourceError as e:
             log.error("Rank %d: %s", rank, e)
             return 2

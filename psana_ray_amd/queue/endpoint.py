@@ -147,6 +147,9 @@ class QueueEndpoint:
 
         eng, wgs, kind = fabric_copy_setting(copy_engine, copy_workgroups, copy_stream)
         self._fabric.set_copy_engine(FABRIC_COPY_ENGINES[eng], int(wgs), STREAM_KINDS[kind])
+        from ..config import fabric_verify_every
+
+        self._fabric.set_verify_every(fabric_verify_every())
         self.copy_engine = (eng, int(wgs), kind)
         if self.is_consumer:
             if self.gpu:
@@ -274,6 +277,8 @@ class QueueEndpoint:
                 raise EndOfStream("all producers finished and the queue shard is drained")
             return None
         self.pool.wait_ready_on(s, self._stream(stream))
+        if self._fabric is not None:
+            self.pool.check_frames([s], self._stream(stream))   # acquire / checksum of a peer-written frame
         h = self.pool.header(s)
         pe = None if math.isnan(h.photon_energy) else h.photon_energy
         return FrameItem(self, s, h.rank, h.idx, h.gevt, pe, self._views[s])
@@ -367,6 +372,7 @@ class QueueEndpoint:
         final = "done" if (not self.is_producer or self._drained_published) else "failed"
         self.session.close(final if self.is_producer else "closed")
         self._final = self._counters()
+        self._final["verify"] = self.verify_counts()
         fab.request_stop()
         if not fab.join(timeout):
             log.warning("queue fabric thread did not stop within %.0f s", timeout)
@@ -391,6 +397,7 @@ class QueueEndpoint:
                 "copy_launches": st.copy_launches, "copy_dev_ms": st.copy_dev_ms,
                 "copy_dev_bytes": st.copy_dev_bytes, "taken_local": st.taken_local,
                 "taken_remote": st.taken_remote,
+                "frames_checksummed": st.frames_checksummed, "frames_corrupted": st.frames_corrupted,
                 "iterations": st.iterations, "idle_iterations": st.idle_iterations}
 
     def links(self) -> list:
@@ -403,6 +410,17 @@ class QueueEndpoint:
         if self._fabric is None:
             return []
         return [(c.dev_ms, c.issue_to_done_ms, c.bytes, c.frames, c.links) for c in self._fabric.copy_samples()]
+
+    def verify_counts(self) -> dict:
+        """End-to-end checks of frames other processes wrote into this consumer's ring (csrc/verify.h):
+        frames re-summed and compared with their producer's checksum, mismatches (and the last
+        mismatching gevt), and the system-scope acquires issued before reading peer-written frames.
+        On a GPU ring, synchronise the streams the frames were read on first for an exact count."""
+        if self._fabric is None:
+            return dict(self._final.get("verify", {"verified": 0, "mismatched": 0, "last_bad_gevt": -1,
+                                                   "acquires": 0}))
+        v, m, g, a = self._fabric.verify_counts()
+        return {"verified": int(v), "mismatched": int(m), "last_bad_gevt": int(g), "acquires": int(a)}
 
     def metrics(self) -> dict:
         """Gauges + cumulative counters for utils.metrics."""

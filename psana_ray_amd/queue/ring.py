@@ -57,7 +57,7 @@ class FrameRing:
     HBM rings are NOT one tensor: they are made of segments of at most ``SEGMENT_BYTES``, each its
     own ``hipMalloc`` (``_C.DeviceBuffer``, wrapped zero-copy with DLPack).  A consumer exports
     every segment to producer processes as a HIP IPC handle, and opening the handle of an
-    allocation above 2 GiB hangs on this ROCm stack (tools/diag_ipc_attach.py: 2.08 GB attaches in
+    allocation above 2 GiB hangs on this ROCm stack (profiles/r2/ipc_attach.md: 2.08 GB attaches in
     0.2 ms, 2.16 GB never returns).  The pool knows every slot's address (``slot_ptrs``), so
     kernels, copies and the fabric never assume one contiguous ring.  Host rings are one region:
     named shared memory when producer processes must write into them (``shm_name``)."""

@@ -18,7 +18,8 @@ SYNTHETIC_EXPS = ("synthetic",)
 
 def open_source(exp: str, run: int, detector_name: str, rank: int = 0, size: int = 1,
                 n_events: Optional[int] = None, pinned: bool = False, pool_frames: int = 32,
-                data_dir: Optional[str] = None, mode=None, prefer_raw: bool = True, **kw):
+                data_dir: Optional[str] = None, mode=None, prefer_raw: bool = True,
+                psana_private_constants: bool = False, psana_handle_shard: str = "explicit", **kw):
     """Pick the event source for ``(exp, run, detector_name)``:
 
     1. an XTC2-style run ``$PSANA_RAY_DATA/<exp>/xtc/<exp>-r<run>-s000-c000.xtc2`` (+ its
@@ -47,7 +48,8 @@ def open_source(exp: str, run: int, detector_name: str, rank: int = 0, size: int
                             pool_frames=pool_frames, pinned=pinned, **kw)
     if psana_available():
         return PsanaWrapperSource(exp, run, detector_name, mode=Mode.image if mode is None else Mode(mode),
-                                  rank=rank, size=size, pinned=pinned, prefer_raw=prefer_raw, n_events=n_events)
+                                  rank=rank, size=size, pinned=pinned, prefer_raw=prefer_raw, n_events=n_events,
+                                  private_constants=psana_private_constants, handle_shard=psana_handle_shard)
     where = f" and no run file under {data_dir}" if data_dir else f" and ${ENV_DATA_DIR} is not set"
     raise NoSourceError(f"no event source for exp={exp!r} run={run} detector={detector_name!r}: psana_wrapper is "
                         f"not importable{where}.  Use --exp synthetic for the synthetic detector "

@@ -12,16 +12,28 @@ Two ways frames enter the GPU pipeline:
   common mode, masks, geometry) -- the same path as the synthetic and file sources; psana's CPU
   calibration never runs.  It needs raw frames AND the run's calibration constants, probed by
   attribute (nothing is fetched, nothing guessed over a network):
-    raw frames  1. the wrapper's own ``ImageRetrievalMode.raw`` through ``iter_events`` (keeps its
-                   photon energies), else
-                2. the psana detector handle the wrapper holds (``det`` / ``detector`` / ...):
+    raw frames  1. the wrapper's own ``ImageRetrievalMode.raw`` through ``iter_events`` -- the
+                   preferred path: it keeps the wrapper's SMD sharding and its photon energies;
+                2. else the psana detector handle the wrapper holds (``det`` / ``detector`` / ...):
                    psana2 ``det.raw.raw(evt)`` or psana1 ``det.raw(evt)``, over the events of the
                    run it holds (``run.events()`` / ``ds.events()``; photon energy from a wrapper
-                   ``get_photon_energy(evt)`` when it has one);
+                   ``get_photon_energy(evt)`` when it has one).  That loop bypasses the wrapper, so
+                   it is sharded EXPLICITLY: rank r of size keeps the loop's events i with
+                   i % size == r (``handle_shard="explicit"``, the default), unless the operator
+                   says psana already shards it (``--psana_handle_shard psana``); the path taken is
+                   logged and reported as ``raw_via``;
     constants   1. an adapter hook ``calib_constants()`` on the wrapper (mapping below), else
-                2. the detector handle's constant accessors: psana2 ``det.raw._pedestals()``,
-                   ``_gain()`` (ADU/keV), ``_status()``, ``_pixel_coord_indexes()``; psana1
-                   ``det.pedestals(run)``, ``gain(run)``, ``status(run)``, ``indexes_xy(run)``.
+                2. the detector handle's PUBLIC psana1 accessors ``det.pedestals(run)``,
+                   ``gain(run)``, ``status(run)``, ``gain_config(run)``, ``indexes_xy(run)``, else
+                3. only when the operator opts in (``--psana_private_constants``): psana2's private
+                   ``det.raw._pedestals()``, ``_gain()`` (ADU/keV), ``_status()``, ``_gain_config()``,
+                   ``_pixel_coord_indexes()`` (names that may change between psana releases);
+                   without the opt-in the source falls back to psana's CPU calibration with a
+                   WARNING that names the flag.
+                An ePix10ka's per-pixel gain configuration must come with constants read from a
+                detector handle: without it the gain range each pixel auto-switches through is
+                unknown, so the source falls back to psana's CPU calibration instead of guessing.
+                Only the ``calib_constants()`` hook may omit it (documented default: AHL).
 * **calibrated** (fallback, ``source_path = "psana_cpu"``, logged once at WARNING): frames arrive
   calibrated by psana in the requested mode and are uploaded in pinned batches (one H2D copy per
   frame of a chunk, no per-frame synchronisation); masks are applied by one kernel per chunk.
@@ -100,17 +112,25 @@ def _call(fn, *alts):
     raise err
 
 
-def _constants_from_detector(det, run: int):
-    """The calib_constants() mapping from a psana detector handle, or (None, why)."""
+PRIVATE_FLAG = "--psana_private_constants"
+
+
+def _constants_from_detector(det, run: int, private_ok: bool = False):
+    """The calib_constants() mapping from a psana detector handle, or (None, why).  psana1's public
+    accessors are used as is; psana2's private ones (``det.raw._pedestals`` ...) only when
+    ``private_ok`` (the operator's opt-in)."""
     r = getattr(det, "raw", None)
-    if r is not None and hasattr(r, "_pedestals"):        # psana2 AreaDetector (det.raw.*)
-        acc = {"pedestals": "_pedestals", "gains": "_gain", "status": "_status", "coords": "_pixel_coord_indexes",
-               "gain_config": "_gain_config"}
-        obj, style = r, "psana2"
-    elif hasattr(det, "pedestals"):                       # psana1 Detector
+    if hasattr(det, "pedestals") and callable(getattr(det, "pedestals")):   # psana1 Detector (public API)
         acc = {"pedestals": "pedestals", "gains": "gain", "status": "status", "coords": "indexes_xy",
                "gain_config": "gain_config"}
         obj, style = det, "psana1"
+    elif r is not None and hasattr(r, "_pedestals"):      # psana2 AreaDetector (det.raw._* : private)
+        if not private_ok:
+            return None, (f"the psana2 detector handle exposes its constants only through private accessors "
+                          f"(det.raw._pedestals / _gain / _status); pass {PRIVATE_FLAG} to use them")
+        acc = {"pedestals": "_pedestals", "gains": "_gain", "status": "_status", "coords": "_pixel_coord_indexes",
+               "gain_config": "_gain_config"}
+        obj, style = r, "psana2"
     else:
         return None, "the psana detector handle exposes no calibration constants"
     out = {}
@@ -164,13 +184,17 @@ class PsanaWrapperSource:
 
     def __init__(self, exp: str, run: int, detector_name: str, mode: Mode = Mode.image, rank: int = 0,
                  size: int = 1, pinned: bool = False, prefer_raw: bool = True, staging: int = 128,
-                 n_events: Optional[int] = None):
+                 n_events: Optional[int] = None, private_constants: bool = False, handle_shard: str = "explicit"):
         import psana_wrapper  # type: ignore
 
         self.exp, self.run, self.detector_name = exp, int(run), detector_name
         self.rank, self.size = int(rank), int(size)
         self.mode = Mode(mode)
         self.n_events = n_events
+        if handle_shard not in ("explicit", "psana"):
+            raise ValueError(f"handle_shard must be 'explicit' or 'psana', not {handle_shard!r}")
+        self.private_constants = bool(private_constants)
+        self.handle_shard = handle_shard
         self._modes = psana_wrapper.ImageRetrievalMode
         self.wrapper = psana_wrapper.PsanaWrapperSmd(exp=exp, run=run, detector_name=detector_name)
         self._skip = 0
@@ -225,7 +249,11 @@ class PsanaWrapperSource:
         if hasattr(self._modes, "raw"):
             self.raw_via = "iter_events(raw)"
         elif det is not None and _raw_accessor(det) is not None and _find_events(self.wrapper) is not None:
-            self.raw_via = f"{det_attr}.raw(evt)"
+            # the run's own event loop bypasses the wrapper's SMD sharding: shard it here unless the
+            # operator says psana already does
+            shard = f"every {self.size}th event from {self.rank}" if (self.handle_shard == "explicit"
+                                                                     and self.size > 1) else "as psana yields them"
+            self.raw_via = f"{det_attr}.raw(evt) over the run's events ({shard})"
             self._raw_fn = _raw_accessor(det)
             self._events_fn = _find_events(self.wrapper)
             self._pe_fn = next((getattr(self.wrapper, a) for a in _PE_ATTRS if callable(getattr(self.wrapper, a, None))),
@@ -239,7 +267,7 @@ class PsanaWrapperSource:
             c = hook()
             self.constants_via = "calib_constants() hook"
         elif det is not None:
-            c, style = _constants_from_detector(det, self.run)
+            c, style = _constants_from_detector(det, self.run, self.private_constants)
             if c is None:
                 return style
             self.constants_via = f"{style} detector handle ({det_attr})"
@@ -264,9 +292,15 @@ class PsanaWrapperSource:
         status = status.astype(np.uint8)
         cfg = c.get("gain_config")
         if spec.kind == "epix10ka":
+            if cfg is None and not callable(hook):
+                # a fixed-gain or AML run would select the wrong pedestal / gain range
+                # under an AHL guess -- psana's own CPU calibration knows the configuration
+                return (f"the {self.constants_via} gives no per-pixel gain configuration for the ePix10ka "
+                        f"(needed to decode its gain ranges)")
             if cfg is None:
-                log.warning("psana_wrapper %s: no per-pixel gain configuration among the constants; assuming AHL "
-                            "(auto high-to-low) for every pixel", self.detector_name)
+                log.warning("psana_wrapper %s: calib_constants() gives no per-pixel gain configuration; assuming "
+                            "AHL (auto high-to-low) for every pixel (the hook's documented default)",
+                            self.detector_name)
             cfg = np.full(spec.frame_shape, 3, np.uint8) if cfg is None else \
                 np.asarray(cfg).astype(np.uint8).reshape(spec.frame_shape)
         cmg = {"epix10ka": EPIX_CM_GAINS, "jungfrau": JUNGFRAU_CM_GAINS}.get(spec.kind, (0,))
@@ -303,8 +337,12 @@ class PsanaWrapperSource:
         return self._cursor
 
     def _raw_from_handle(self):
-        """(raw frame, photon energy) per event of the run through the psana detector handle."""
-        for evt in self._events_fn():
+        """(raw frame, photon energy) per event of the run through the psana detector handle; with
+        explicit sharding this rank keeps the loop's events i with i % size == rank."""
+        explicit = self.handle_shard == "explicit" and self.size > 1
+        for i, evt in enumerate(self._events_fn()):
+            if explicit and i % self.size != self.rank:
+                continue
             data = self._raw_fn(evt)
             if data is None:   # the detector is not in this event (psana returns None)
                 continue

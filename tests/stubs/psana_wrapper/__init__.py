@@ -22,6 +22,12 @@ Knobs (environment):
                             (detector.raw(evt), pedestals(run), gain(run), status(run)) over
                             ``wrapper.ds.events()``
   PSANA_STUB_EVENTS=N     events in the run (default 24)
+  PSANA_STUB_GAINCFG=...  the ePix10ka per-pixel gain configuration (AHL default, "mixed": random
+                          FH/FM/FL/AHL/AML per pixel)
+  PSANA_STUB_NO_GAINCFG=1 the detector handles expose no gain-configuration accessor
+  PSANA_STUB_HANDLE_SHARDED=1  the handle styles' run / DataSource event loop yields only this
+                          rank's events (default: every event of the run -- the loop bypasses the
+                          wrapper's SMD sharding, so the adapter shards it explicitly)
   PSANA_STUB_CM=text      common mode "psana" applies (default: "default"; "off" disables)
 SMD sharding: the rank / size come from the same launcher variables the producer reads, and rank
 r yields global events r, r + size, ... (psana's SMD mode distributes events over MPI ranks).
@@ -63,7 +69,8 @@ class PsanaWrapperSmd:
         self.rank, self.size = _rank_size()
         self.n_events = int(os.environ.get("PSANA_STUB_EVENTS", "24"))
         # one generator for the whole run (seeded by exp/run), sharded like SMD mode
-        self._syn = SyntheticRun(exp, run, detector_name, rank=0, size=1, pool_frames=8, gen_device="cpu")
+        self._syn = SyntheticRun(exp, run, detector_name, rank=0, size=1, pool_frames=8, gen_device="cpu",
+                                 gain_config=os.environ.get("PSANA_STUB_GAINCFG", "AHL"))
         self.consts = self._syn.consts
         if STYLE in ("psana2", "psana2_events"):
             self.det = _Psana2Det(self)
@@ -117,7 +124,8 @@ class _Run:
         self._w = w
 
     def events(self):
-        for g in self._w.local_events():
+        sharded = os.environ.get("PSANA_STUB_HANDLE_SHARDED", "0") == "1"
+        for g in (self._w.local_events() if sharded else range(self._w.n_events)):
             yield _Evt(g)
 
 
@@ -139,6 +147,10 @@ class _Psana2Raw:
     def _status(self):
         st = self._w.consts.status
         return np.broadcast_to(st, (self._w.consts.pedestals.shape[0], *st.shape)).copy()
+
+    if os.environ.get("PSANA_STUB_NO_GAINCFG", "0") != "1":
+        def _gain_config(self):
+            return self._w.consts.gain_config
 
     def _pixel_coord_indexes(self):
         from psana_ray_amd.models.geometry import make_geometry
@@ -170,6 +182,10 @@ class _Psana1Det:
 
     def status(self, run):
         return self._w.consts.status
+
+    if os.environ.get("PSANA_STUB_NO_GAINCFG", "0") != "1":
+        def gain_config(self, run):
+            return self._w.consts.gain_config
 
 
 def stub_common_mode():

@@ -3,7 +3,7 @@
 
 Needs an extension built with -DPR_CM_STAMPS=1:
     python tools/build_variant.py stamps common_mode.hip -DPR_CM_STAMPS=1
-and run with that .so in place of the shipped one (tools/gpu_cm_stamps.sh does both steps on the box).
+and run with that .so in place of the shipped one (tools/gpu_stamps.sh does both steps on the box).
 
 Every wave of the production kernel records the shader clock at its phase boundaries; this tool
 launches one 64-frame dispatch per flag mix (after warm-up launches) and reports, per phase, the

@@ -17,7 +17,7 @@ esac
 # side only, with the sanitizer on the host pass and never on a GPU pass
 $CXX -x hip --offload-host-only --offload-arch=gfx950 -fno-gpu-sanitize -std=c++17 -O1 -g $FLAGS \
   -I"$R/csrc" \
-  "$R/tests/cpp/slotpool_stress.cpp" "$R/csrc/runtime.cpp" "$R/csrc/fabric.cpp" "$R/csrc/lifecycle.cpp" "$R/csrc/trace.cpp" \
+  "$R/tests/cpp/slotpool_stress.cpp" "$R/csrc/runtime.cpp" "$R/csrc/fabric.cpp" "$R/csrc/lifecycle.cpp" "$R/csrc/verify.cpp" "$R/csrc/trace.cpp" \
   "$R/csrc/streams.cpp" "$R/tests/cpp/host_stubs.cpp" \
   -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64 -lpthread -lrt -o "$OUT"
 "$OUT" "$N"

@@ -24,8 +24,13 @@ where three comparators are six, so networks are built from them where they pay:
 Virtual +inf padding (positions past the real values) is tracked symbolically: an op against a pad
 is a no-op or a relabelling, never an instruction.
 
-Checks (every run): sorts and selections against ``sorted`` on random permutations, inputs with
-duplicates and random 0-1 vectors; V-merges exhaustively on 0-1 V-shaped inputs.
+Checks (every run): every merge node of every sort tree EXHAUSTIVELY on 0-1 inputs (a merge of
+sorted runs of lengths a and b needs only the (a + 1)(b + 1) pairs of sorted 0-1 runs; with 3-sorter
+and pair leaves this proves each whole sort by induction and the 0-1 principle, and a selection is
+a backward cone of such a sort); sorts and selections also against ``sorted`` on random
+permutations, inputs with duplicates and random 0-1 vectors; V-merges exhaustively on 0-1 V-shaped
+inputs.  ``--check --diff`` also fails when the committed header differs from what this generator
+writes (tests/test_sortnet_gen.py).
 """
 from __future__ import annotations
 
@@ -240,6 +245,28 @@ def check_select(n, mops, order, ranks, trials=2000):
     return True
 
 
+def merge_nodes(n):
+    """(na, nb, kind) of every internal merge of tree_sort(n)'s tree."""
+    if n <= 3:
+        return []
+    _, h, kind = sort_plan(n)
+    return merge_nodes(h) + merge_nodes(n - h) + [(h, n - h, kind)]
+
+
+def check_merge_exhaustive(na, nb, kind):
+    """The merge network of sorted runs of lengths na, nb on every pair of sorted 0-1 runs."""
+    a, b = list(range(na)), list(range(na, na + nb))
+    ops, order = oem_merge(a, b) if kind == "oem" else b3_merge(a, b)
+    mops = full_mask(ops)
+    for i in range(na + 1):
+        for j in range(nb + 1):
+            v = [0] * i + [1] * (na - i) + [0] * j + [1] * (nb - j)
+            y = run(mops, v)
+            if [y[k] for k in order] != sorted(v):
+                return False
+    return True
+
+
 def check_vmerge(n, mops, order):
     # every 0-1 V-shaped input 1^a 0^b 1^c: by the 0-1 principle the network sorts every V-shaped input
     for a in range(n + 1):
@@ -260,12 +287,16 @@ VMERGES = (4, 44, 64)        # column phase: V-shaped merge-split halves (M)
 def sort_net(n):
     ops, order = tree_sort(list(range(n)))
     mops = full_mask(ops)
+    for na, nb, kind in merge_nodes(n):
+        assert check_merge_exhaustive(na, nb, kind), f"sort {n}: merge {na}+{nb} ({kind})"
     assert check_sort(n, mops, order), f"sort {n}"
     return mops, order
 
 
 def select_net(n):
     ops, order = tree_sort(list(range(n)))
+    for na, nb, kind in merge_nodes(n):
+        assert check_merge_exhaustive(na, nb, kind), f"select {n}: merge {na}+{nb} ({kind})"
     pa, pb = (n - 1) // 2 if n & 1 else n // 2 - 1, ((n - 1) // 2 if n & 1 else n // 2 - 1) + 1
     mops = cone(ops, {order[pa], order[pb]})
     assert check_select(n, mops, order, (pa, pb)), f"select {n}"
@@ -320,6 +351,7 @@ def emit(name, n, mops, order, note):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--check", action="store_true", help="verify and print op counts, write nothing")
+    ap.add_argument("--diff", action="store_true", help="with --check: fail if csrc/sortnet_gen.h is stale")
     args = ap.parse_args()
     out = ["// GENERATED by tools/sortnet_gen.py -- do not edit.  Three-input sorting / selection networks",
            "// of the common-mode kernel (see the generator's docstring for the constructions and checks).",
@@ -350,9 +382,14 @@ def main():
         out += ["template <>", f"struct GenVMerge<{n}> : GenVMergeNet{n} {{", "  static constexpr bool kHave = true;",
                 "};", ""]
     out += ["}  // namespace pr", ""]
+    text = "\n".join(out)
     if not args.check:
-        OUT.write_text("\n".join(out))
+        OUT.write_text(text)
         print(f"wrote {OUT}")
+    elif args.diff:
+        if OUT.read_text() != text:
+            raise SystemExit(f"{OUT} differs from the generator's output: regenerate it")
+        print(f"{OUT} matches the generator")
 
 
 if __name__ == "__main__":
