@@ -610,6 +610,10 @@ def main(argv=None):
             "received_cross_per_consumed": round(sum(fr_recv) / max(1, sum(allsum(cross_steps * B if takes else 0))),
                                                  3),
             "bytes_sent_per_rank": sent, "frames_sent_per_rank": fr_sent, "frames_local_per_rank": fr_local,
+            # of the frames sent: calibrated straight into the consumer's slot (no copy pass;
+            # csrc/fabric.h take_direct), and direct frames lost to a consumer that left
+            "frames_direct_per_rank": allsum(int(x1.get("frames_direct", 0) - x0.get("frames_direct", 0))),
+            "frames_lost_direct_per_rank": allsum(int(x1.get("frames_lost_direct", 0))),
             "copy_ms_per_batch_per_rank": cms,
             "copy_dispatch_per_rank": copy_detail,
             "link_GB_total_per_rank": per_link,

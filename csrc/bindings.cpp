@@ -390,6 +390,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("taken_local", &pr::FabricStats::taken_local)
       .def_readonly("taken_remote", &pr::FabricStats::taken_remote)
       .def_readonly("frames_checksummed", &pr::FabricStats::frames_checksummed)
+      .def_readonly("frames_direct", &pr::FabricStats::frames_direct)
+      .def_readonly("frames_lost_direct", &pr::FabricStats::frames_lost_direct)
       .def_readonly("frames_corrupted", &pr::FabricStats::frames_corrupted);
   py::class_<pr::CopySample>(m, "CopySample")
       .def_readonly("dev_ms", &pr::CopySample::dev_ms)
@@ -449,6 +451,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("copy_workgroups", &pr::QueueFabric::copy_workgroups)
       .def("copy_samples", &pr::QueueFabric::copy_samples)
       .def("set_verify_every", &pr::QueueFabric::set_verify_every, py::arg("every"))
+      .def("set_direct", &pr::QueueFabric::set_direct, py::arg("on"))
+      .def("direct", &pr::QueueFabric::direct)
       .def("verify_every", &pr::QueueFabric::verify_every)
       .def("verify_counts", &pr::QueueFabric::verify_counts)
       .def_static("copy_grid_for", &pr::QueueFabric::copy_grid_for, py::arg("consumer_devices"), py::arg("device"),
@@ -602,6 +606,8 @@ PYBIND11_MODULE(_C, m) {
       .def("start", &pr::ProducerEngine::start, py::arg("n_local_events"), py::arg("max_steps"), py::arg("k0") = 0)
       .def("set_file_source", &pr::ProducerEngine::set_file_source, py::arg("reader"), py::keep_alive<1, 2>())
       .def("set_header_rank", &pr::ProducerEngine::set_header_rank, py::arg("rank"))
+      .def("set_fabric", &pr::ProducerEngine::set_fabric, py::arg("fabric").none(true))
+      .def_property_readonly("direct_frames", &pr::ProducerEngine::direct_frames)
       .def("set_compute_streams", &pr::ProducerEngine::set_compute_streams, py::arg("n"), py::arg("kind") = 0)
       .def_property_readonly("compute_streams", &pr::ProducerEngine::compute_streams)
       .def("request_stop", &pr::ProducerEngine::request_stop)

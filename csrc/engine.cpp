@@ -1,4 +1,5 @@
 #include "engine.h"
+#include "fabric.h"
 #include "trace.h"
 
 #include <chrono>
@@ -505,6 +506,11 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
         for (int q = 0; q < n; ++q) in[q] = dev_in_[b][q];
       }
       for (int q = 0; q < n; ++q) out[q] = pool_->slot_ptr(slots[q]);
+      // frames with a direct grant are calibrated straight into that consumer's slot (the local slot
+      // only carries the header and the queue_size accounting; QueueFabric::take_direct)
+      std::vector<QueueFabric::DirectGrant> dg;
+      if (fabric_ != nullptr) dg = fabric_->take_direct(n);
+      for (size_t q = 0; q < dg.size(); ++q) out[q] = dg[q].ptr;
       if (gpu_timing_) {
         if (device_resident_) harvest(b, false);
         hip_check(hipEventRecord(calib_start_[b], cs), "record calib start");
@@ -528,6 +534,13 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
           hdrs[q].gevt = rank_ + (k + q) * size_;
           hdrs[q].photon_energy = src_pe_[(k + q) % src_pe_.size()];
         }
+      }
+      if (!dg.empty()) {   // bound BEFORE the commit: the fabric must never route these as copies
+        std::vector<int> ds(slots.begin(), slots.begin() + (int64_t)dg.size());
+        std::vector<int64_t> tk(dg.size());
+        for (size_t q = 0; q < dg.size(); ++q) tk[q] = dg[q].token;
+        fabric_->bind_direct(ds, tk);
+        direct_frames_.fetch_add((int64_t)dg.size());
       }
       pool_->commit_batch(slots, hdrs, stream_c);   // one ready event for the whole chunk
       record_chunk_done(n, cs);

@@ -23,6 +23,8 @@
 
 namespace pr {
 
+class QueueFabric;   // fabric.h
+
 enum PlanMode : int {
   kPlanRawCopy = 0,     // mode=raw: copy raw frames into the slot
   kPlanCalib = 1,       // K-01/02/04
@@ -84,6 +86,10 @@ class ProducerEngine {
   // producers (SURVEY P-04) shard EVENTS over rank groups but tag frames with their own rank, so a
   // consumer can tell the panel shard (rank % shards) apart from the event (gevt).
   void set_header_rank(int64_t r) { hdr_rank_ = r; }
+  // Calibrate straight into consumer slots the queue fabric offers (QueueFabric::take_direct; null =
+  // off).  Before start(); the fabric must outlive the run (ProducerPipeline clears it after join).
+  void set_fabric(QueueFabric* f) { fabric_ = f; }
+  int64_t direct_frames() const { return direct_frames_.load(); }
   // rank-local events [k0, n_local_events) (n_local_events < 0: endless), at most max_steps of them
   void start(int64_t n_local_events, int64_t max_steps, int64_t k0 = 0);
   void request_stop() { stop_.store(true); }
@@ -130,6 +136,8 @@ class ProducerEngine {
   int chunk_;
   int n_raw_bufs_;
   int64_t rank_, size_, hdr_rank_;
+  QueueFabric* fabric_ = nullptr;
+  std::atomic<int64_t> direct_frames_{0};
   std::vector<uint64_t> src_frames_;
   std::vector<double> src_pe_;
   bool device_resident_ = false;   // source frames live in this GPU's HBM: no staging copies

@@ -233,6 +233,7 @@ struct QueueFabric::Link {
   hipStream_t stream = nullptr;       // this link's copy stream: copies to different consumers
                                       // (different xGMI links) run concurrently
   int inflight = 0;
+  int direct = 0;                     // grants of this link in the direct pool (offered / taken / bound)
   bool eos_posted = false, acked_close = false;
   uint64_t r_tail = 0;
   int64_t noticed = 0;                // frames noticed on this link
@@ -289,6 +290,7 @@ struct QueueFabric::Batch {
   std::shared_ptr<CopyGroup> grp;          // kernel engine: the dispatch it rode in
   double t_issue = 0;
   std::vector<std::pair<int, int64_t>> ck;  // (frame of the batch, pinned checksum result index)
+  bool direct = false;                      // calibrated straight into the consumer's slots (no copy)
 };
 
 QueueFabric::QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is_producer, bool is_consumer,
@@ -322,6 +324,131 @@ std::array<int64_t, 4> QueueFabric::verify_counts() const {
   return verifier_ ? verifier_->counts() : std::array<int64_t, 4>{0, 0, -1, 0};
 }
 
+void QueueFabric::set_direct(bool on) {
+  check(!running_.load(), "QueueFabric: set_direct before start()");
+  direct_on_ = on && is_producer_ && device_ >= 0 && copy_engine_ == kCopyKernel;
+}
+
+std::vector<QueueFabric::DirectGrant> QueueFabric::take_direct(int max_n) {
+  std::vector<DirectGrant> out;
+  if (!direct_on_ || max_n <= 0) return out;
+  std::lock_guard<std::mutex> lk(dmu_);
+  while ((int)out.size() < max_n && !d_free_.empty()) {
+    auto e = std::move(d_free_.front());
+    d_free_.pop_front();
+    out.push_back({e.first, e.second.link->remote[(size_t)e.second.rslot]});
+    d_taken_.push_back(std::move(e));
+  }
+  return out;
+}
+
+void QueueFabric::bind_direct(const std::vector<int>& local_slots, const std::vector<int64_t>& tokens) {
+  check(local_slots.size() == tokens.size(), "QueueFabric::bind_direct: size mismatch");
+  std::lock_guard<std::mutex> lk(dmu_);
+  for (size_t i = 0; i < tokens.size(); ++i) {
+    auto it = std::find_if(d_taken_.begin(), d_taken_.end(), [&](const auto& e) { return e.first == tokens[i]; });
+    check(it != d_taken_.end(), "QueueFabric::bind_direct: unknown token");
+    d_bound_.emplace_back(local_slots[i], std::move(it->second));
+    d_taken_.erase(it);
+  }
+}
+
+void QueueFabric::cancel_direct(const std::vector<int64_t>& tokens) {
+  std::lock_guard<std::mutex> lk(dmu_);
+  for (int64_t t : tokens) {
+    auto it = std::find_if(d_taken_.begin(), d_taken_.end(), [&](const auto& e) { return e.first == t; });
+    if (it == d_taken_.end()) continue;
+    d_cancel_.push_back(std::move(*it));
+    d_taken_.erase(it);
+  }
+}
+
+// Fabric thread, every producer pass: cancelled grants back to their links, the offer pool purged
+// of links that can no longer take frames, emptied when the policy keeps frames local (balanced /
+// local_first / relay) or the producer finished, else refilled from the live remote consumers'
+// grants (the link holding the most grants first, so the offers spread over the consumers).
+int64_t QueueFabric::direct_pass() {
+  const int policy = policy_.load();
+  // spread / remote_only send frames to other processes by policy; a producer with no consumer of
+  // its own (or one that closed) sends every frame away
+  const bool want = direct_on_ && !finished_.load() &&
+                    (policy == 2 || policy == 4 || !is_consumer_ || consumer_closed_.load());
+  auto usable = [](const Link& l) {
+    return l.attached && !l.dead && !l.closed && !l.eos_posted && !l.keeper && l.kcopy;
+  };
+  int64_t work = 0;
+  std::lock_guard<std::mutex> lk(dmu_);
+  for (auto& e : d_cancel_) {
+    Link& l = *e.second.link;
+    if (!l.dead && !l.closed) l.grants.push_front(e.second.rslot);
+    --l.direct;
+    ++work;
+  }
+  d_cancel_.clear();
+  for (auto it = d_free_.begin(); it != d_free_.end();) {
+    Link& l = *it->second.link;
+    if (want && usable(l)) {
+      ++it;
+      continue;
+    }
+    if (!l.dead && !l.closed) l.grants.push_front(it->second.rslot);   // EOS: returned with the others
+    --l.direct;
+    it = d_free_.erase(it);
+    ++work;
+  }
+  if (!want) return work;
+  // frames already produced without a grant (copy path) get the consumers' grants first: the offer
+  // pool refills only when none of them waits
+  if ((int64_t)pool_->n_produced() > (int64_t)d_bound_.size()) return work;
+  while ((int)d_free_.size() < kDirectPool) {
+    Link* best = nullptr;
+    std::shared_ptr<Link> bp;
+    for (auto& lp : links_)
+      if (lp->outgoing && usable(*lp) && !lp->grants.empty() && (best == nullptr || lp->grants.size() > best->grants.size())) {
+        best = lp.get();
+        bp = lp;
+      }
+    if (best == nullptr) break;
+    const int rs = best->grants.front();
+    best->grants.pop_front();
+    ++best->direct;
+    d_free_.emplace_back(d_next_++, DirectRec{bp, rs});
+    ++work;
+  }
+  return work;
+}
+
+// Produced frames that were calibrated straight into consumer slots: no copy, only ordering.  The
+// fabric's copy stream waits for their calibration (the slots' ready events), a system-scope release
+// on every XCD writes back L2 lines of peer memory the calibration kernels left dirty, optional
+// checksums read the frames back from the consumer rings, and each link's batch gets a completion
+// event; step 3 notices the frames when it completes (or counts them lost if the consumer left).
+void QueueFabric::issue_direct(std::vector<Batch>& db) {
+  trace::Range tr("fabric.direct_dispatch");
+  if (xstream_ == nullptr) xstream_ = acquire_stream(device_, xstream_kind_);
+  std::vector<int> all;
+  for (const Batch& b : db) all.insert(all.end(), b.slots.begin(), b.slots.end());
+  pool_->begin_send_batch(all, reinterpret_cast<uint64_t>(xstream_));
+  launch_release_fence(reinterpret_cast<uint64_t>(xstream_));
+  int64_t n = 0;
+  for (Batch& b : db) {
+    start_checksums(b, reinterpret_cast<uint64_t>(xstream_));
+    inject_corruption(b, reinterpret_cast<uint64_t>(xstream_));
+  }
+  for (Batch& b : db) {
+    b.stream = xstream_;
+    b.direct = true;
+    b.ev = take_event();
+    hip_check(hipEventRecord(b.ev, xstream_), "hipEventRecord (direct frames)");
+    b.link->inflight += (int)b.slots.size();
+    n += (int64_t)b.slots.size();
+    inflight_.push_back(std::move(b));
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  st_.frames_direct += n;
+  st_.batches += (int64_t)db.size();
+}
+
 // Producer: the frames of `b` that carry a content checksum to their consumer (every
 // verify_every_-th frame of this producer by its rank-local idx -- so every producer's links are
 // sampled, which gevt % N would not do for N producers sharing one gevt sequence -- and only
@@ -336,10 +463,11 @@ void QueueFabric::start_checksums(Batch& b, uint64_t stream) {
     const SlotHeader& h = b.hdrs[i];
     if (h.idx < 0 || h.idx % verify_every_ != 0 || ck_tagged(h.aux)) continue;
     if (device_ < 0) {
-      b.hdrs[i].aux = ck_tag(frame_checksum_host(reinterpret_cast<const void*>(pool_->slot_ptr(b.slots[i])), slot_bytes_));
+      const uint64_t src = b.direct ? b.link->remote[b.rslots[i]] : pool_->slot_ptr(b.slots[i]);
+      b.hdrs[i].aux = ck_tag(frame_checksum_host(reinterpret_cast<const void*>(src), slot_bytes_));
       continue;
     }
-    ptrs.push_back(pool_->slot_ptr(b.slots[i]));
+    ptrs.push_back(b.direct ? b.link->remote[b.rslots[i]] : pool_->slot_ptr(b.slots[i]));
     which.push_back((int)i);
   }
   for (size_t a = 0; a < ptrs.size(); a += kMaxFrames) {
@@ -1280,6 +1408,33 @@ int64_t QueueFabric::producer_pass(double now) {
       st_.frames_sent += n;
       st_.bytes_sent += (int64_t)n * slot_bytes_;
       st_.copy_s += now - b.t_issue;
+    } else if (b.direct && l.closed && !l.dead && l.attached) {
+      // a consumer that CLOSED keeps its ring mapped until we acknowledge: copy the frames back
+      // into their local slots (still ours, SENDING) and requeue them at the FIFO front, like a
+      // copy that completed after the close (rare path: the fabric thread waits for it)
+      CopyRuns cr{};
+      cr.n = 0;
+      for (int i = 0; i < n; ++i) {
+        if (cr.n == kMaxCopyRuns) {
+          launch_copy_runs(cr, kLocalCopyWgs, reinterpret_cast<uint64_t>(xstream_));
+          cr.n = 0;
+        }
+        cr.src[cr.n] = l.remote[b.rslots[i]];
+        cr.dst[cr.n] = pool_->slot_ptr(b.slots[i]);
+        cr.n16[cr.n] = slot_bytes_ / 16;
+        ++cr.n;
+      }
+      if (cr.n > 0) launch_copy_runs(cr, kLocalCopyWgs, reinterpret_cast<uint64_t>(xstream_));
+      hip_check(hipStreamSynchronize(xstream_), "hipStreamSynchronize (direct frames back from a closed consumer)");
+      pool_->unsend_batch(b.slots);
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.frames_requeued += n;
+    } else if (b.direct) {
+      // the frame's data exists only in the ring of the consumer that died: lost (never noticed),
+      // like the rest of that consumer's read-ahead
+      pool_->end_send_completed(b.slots, false);
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.frames_lost_direct += n;
     } else {
       pool_->unsend_batch(b.slots);
       std::lock_guard<std::mutex> lk(mu_);
@@ -1296,7 +1451,44 @@ int64_t QueueFabric::producer_pass(double now) {
   // 4. route produced frames (FIFO) to this process's own consumer or to granted remote slots.
   //    Keeper links are the last resort: a frame goes there only when no real consumer (and not
   //    this process's own) has credit for it.
-  const std::vector<int> offers = pool_->produced(kMaxDispatch);
+  std::vector<int> offers = pool_->produced(kMaxDispatch);
+  if (direct_on_) {
+    work += direct_pass();
+    // frames bound to a direct grant go to that grant's consumer, whatever the policy says now
+    std::vector<Batch> db;
+    {
+      std::lock_guard<std::mutex> lk(dmu_);
+      if (!d_bound_.empty()) {
+        std::vector<int> rest;
+        for (int sl : offers) {
+          auto it = std::find_if(d_bound_.begin(), d_bound_.end(), [&](const auto& e) { return e.first == sl; });
+          if (it == d_bound_.end()) {
+            rest.push_back(sl);
+            continue;
+          }
+          Batch* b = nullptr;
+          for (Batch& x : db)
+            if (x.link == it->second.link) b = &x;
+          if (b == nullptr) {
+            db.emplace_back();
+            b = &db.back();
+            b->link = it->second.link;
+            b->t_issue = now;
+          }
+          b->slots.push_back(sl);
+          b->rslots.push_back(it->second.rslot);
+          --it->second.link->direct;
+          d_bound_.erase(it);
+        }
+        offers.swap(rest);
+      }
+    }
+    if (!db.empty()) {
+      for (Batch& b : db) b.hdrs = pool_->headers(b.slots);
+      for (const Batch& b : db) work += (int64_t)b.slots.size();
+      issue_direct(db);
+    }
+  }
   int64_t local_credit = (is_consumer_ && !consumer_closed_.load() && policy != 3) ? pool_->credits() : 0;
   std::vector<Link*> cands;
   for (auto& lp : links_)
@@ -1472,7 +1664,12 @@ int64_t QueueFabric::producer_pass(double now) {
     st_.readahead = readahead;
   }
   const int64_t backlog = pool_->n_produced();
-  const bool all_routed = finished_.load() && backlog == 0 && inflight_.empty() && !returns_open;
+  bool direct_idle = true;
+  if (direct_on_) {
+    std::lock_guard<std::mutex> lk(dmu_);
+    direct_idle = d_free_.empty() && d_taken_.empty() && d_bound_.empty() && d_cancel_.empty();
+  }
+  const bool all_routed = finished_.load() && backlog == 0 && inflight_.empty() && !returns_open && direct_idle;
   bool drained = all_routed;
   for (auto& lp : links_) {
     Link& l = *lp;
@@ -1485,7 +1682,7 @@ int64_t QueueFabric::producer_pass(double now) {
     // a closed link is acknowledged once nothing is in flight towards it, every returned frame was
     // answered and the consumer read every notice (so it has handed back every frame it received)
     const bool settled =
-        l.inflight == 0 && l.returns.empty() && l.reclaiming == 0 &&
+        l.inflight == 0 && l.direct == 0 && l.returns.empty() && l.reclaiming == 0 &&
         (l.dead || (s->returns_final.load(std::memory_order_acquire) != 0 &&
                     s->r_head.load(std::memory_order_acquire) == l.r_tail &&
                     s->n_tail.load(std::memory_order_acquire) == l.n_head));
@@ -1611,7 +1808,7 @@ void QueueFabric::publish_status() {
   for (auto& lp : links_) {
     Link& l = *lp;
     // retire links that can never carry anything again
-    const bool out_done = l.outgoing && (l.dead || l.closed) && l.acked_close && l.inflight == 0;
+    const bool out_done = l.outgoing && (l.dead || l.closed) && l.acked_close && l.inflight == 0 && l.direct == 0;
     const bool out_never = l.outgoing && l.dead && !l.attached;
     const bool in_done = !l.outgoing && (l.dead || l.detached) && l.outstanding == 0 && !l.named;
     const bool in_never = !l.outgoing && l.dead && !l.attached;

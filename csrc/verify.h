@@ -68,6 +68,8 @@ void launch_frame_checksums(const CkFrames& a, int nframes, int64_t n16, uint64_
                             uint64_t out, uint64_t counters, uint64_t stream);
 // System-scope acquire on every XCD (64 one-wave workgroups, dealt round-robin over the 8 XCDs).
 void launch_acquire_fence(uint64_t stream);
+// System-scope release on every XCD (the direct-write path: calibration kernels wrote peer memory).
+void launch_release_fence(uint64_t stream);
 
 class FrameVerifier {
  public:

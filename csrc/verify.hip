@@ -75,6 +75,16 @@ void launch_frame_checksums(const CkFrames& a, int nframes, int64_t n16, uint64_
 // stale.  Workgroups are dealt round-robin over the 8 XCDs, so 64 of them reach every XCD's L2.
 __global__ __launch_bounds__(64) void acquire_fence_kernel() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
 
+// buffer_wbl2 sc0 sc1: writes back the dirty L2 lines of this XCD (peer memory included), so frames
+// that kernels of this GPU wrote into another GPU's ring reach it before the completion signal that
+// the notice is posted after.  64 workgroups reach every XCD's L2.
+__global__ __launch_bounds__(64) void release_fence_kernel() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); }
+
+void launch_release_fence(uint64_t stream) {
+  hipLaunchKernelGGL(release_fence_kernel, dim3(64), dim3(64), 0, reinterpret_cast<hipStream_t>(stream));
+  hip_check(hipGetLastError(), "release_fence launch");
+}
+
 void launch_acquire_fence(uint64_t stream) {
   hipLaunchKernelGGL(acquire_fence_kernel, dim3(64), dim3(64), 0, reinterpret_cast<hipStream_t>(stream));
   hip_check(hipGetLastError(), "acquire_fence launch");

@@ -123,6 +123,17 @@ def fabric_copy_setting(engine: Optional[str] = None, workgroups: Optional[int] 
 FABRIC_VERIFY_EVERY = 64
 
 
+# Direct writes (csrc/fabric.h set_direct): while frames are routed to other processes (spread /
+# remote_only), a GPU producer calibrates them straight into granted consumer slots instead of into
+# its own slot plus a copy pass.  Env override: PSANA_RAY_AMD_FABRIC_DIRECT=0|1.
+FABRIC_DIRECT = True
+
+
+def fabric_direct() -> bool:
+    v = os.environ.get("PSANA_RAY_AMD_FABRIC_DIRECT", "").strip()
+    return FABRIC_DIRECT if not v else v not in ("0", "false", "off")
+
+
 def fabric_verify_every() -> int:
     v = os.environ.get("PSANA_RAY_AMD_VERIFY_EVERY", "")
     return max(0, int(v)) if v.strip() else FABRIC_VERIFY_EVERY

@@ -164,6 +164,11 @@ class ProducerPipeline:
             kind = PRODUCER_STREAM_KIND[where] if stream_kind is None else stream_kind
             self.engine.set_compute_streams(n_cs, STREAM_KINDS[kind])
             self.stream_config = (n_cs, kind)
+            fab = getattr(endpoint, "_fabric", None)
+            if fab is not None and fab.direct():
+                # frames routed to other processes are calibrated straight into their consumer's
+                # slot (csrc/fabric.h take_direct); cleared after the engine stopped (_run_engine)
+                self.engine.set_fabric(fab)
 
     # --------------------------------------------------------------------------------
     def _acquire(self, n: int, stream) -> List[int]:
@@ -391,6 +396,7 @@ class ProducerPipeline:
         finally:
             self.engine.request_stop()
             self.engine.join(-1.0)
+            self.engine.set_fabric(None)   # the endpoint may close (and free the fabric) from here on
         err = self.engine.error()
         self.frames = int(self.engine.frames)
         self.full_waits = int(self.engine.full_waits)

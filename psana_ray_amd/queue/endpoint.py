@@ -147,9 +147,10 @@ class QueueEndpoint:
 
         eng, wgs, kind = fabric_copy_setting(copy_engine, copy_workgroups, copy_stream)
         self._fabric.set_copy_engine(FABRIC_COPY_ENGINES[eng], int(wgs), STREAM_KINDS[kind])
-        from ..config import fabric_verify_every
+        from ..config import fabric_direct, fabric_verify_every
 
         self._fabric.set_verify_every(fabric_verify_every())
+        self._fabric.set_direct(fabric_direct())   # GPU producers with the kernel engine only
         self.copy_engine = (eng, int(wgs), kind)
         if self.is_consumer:
             if self.gpu:
@@ -398,6 +399,7 @@ class QueueEndpoint:
                 "copy_dev_bytes": st.copy_dev_bytes, "taken_local": st.taken_local,
                 "taken_remote": st.taken_remote,
                 "frames_checksummed": st.frames_checksummed, "frames_corrupted": st.frames_corrupted,
+                "frames_direct": st.frames_direct, "frames_lost_direct": st.frames_lost_direct,
                 "iterations": st.iterations, "idle_iterations": st.idle_iterations}
 
     def links(self) -> list:

@@ -17,4 +17,5 @@ void launch_frame_checksums(const CkFrames&, int, int64_t, uint64_t, uint64_t, b
   check(false, "launch_frame_checksums: the host-only sanitizer build has no GPU kernels");
 }
 void launch_acquire_fence(uint64_t) { check(false, "launch_acquire_fence: no GPU kernels in this build"); }
+void launch_release_fence(uint64_t) { check(false, "launch_release_fence: no GPU kernels in this build"); }
 }  // namespace pr

@@ -106,3 +106,33 @@ def test_checksum_device_matches_host(native, cuda_device):
         stream.synchronize()
         ok, bad, last, acq = v.counts()
         assert (ok, bad, last, acq) == (2, 1, 11, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_two_ranks_one_gpu_frames_verified(native, direct):
+    """bench.py --gpus 2 (self-launched, two processes on the box's GPU, device-resident raw frames):
+    the route=remote_only window moves every frame between processes through HIP IPC -- calibrated
+    straight into the consumer's slot (direct) or copied by copy_runs_kernel -- and the consumers
+    verify every 4th frame's checksum bitwise."""
+    r, d = _run_gpu_bench(2, {"PSANA_RAY_AMD_VERIFY_EVERY": "4", "PSANA_RAY_AMD_FABRIC_DIRECT": direct})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert d["n_gpus"] == 1 and d["n_ranks"] == 2
+    fc, x = d["extra"]["frame_checks"], d["extra"]["xgmi_phase"]
+    assert fc["frames_verified"] > 0 and fc["frames_mismatched"] == 0, fc
+    assert x["cross_gpu_fraction"] >= 0.9
+    if direct == "1":
+        assert sum(x["frames_direct_per_rank"]) > 0, x
+    else:
+        assert sum(x["frames_direct_per_rank"]) == 0, x
+
+
+def _run_gpu_bench(nproc, extra_env):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.update(extra_env)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--steps", "20", "--warmup", "3",
+           "--source", "device", "--gate-max-s", "3"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200, cwd="/tmp")
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r, (json.loads(lines[0]) if lines else None)
