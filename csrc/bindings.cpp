@@ -594,8 +594,13 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("img_desc", &pr::CalibPlan::img_desc)
       .def_readwrite("gap_runs", &pr::CalibPlan::gap_runs)
       .def_readwrite("n_gap_runs", &pr::CalibPlan::n_gap_runs);
-  m.def("run_calib_plan", &pr::run_calib_plan, py::arg("plan"), py::arg("in_ptrs"), py::arg("out_ptrs"),
-        py::arg("stream"));
+  m.def("run_calib_plan",
+        [](const pr::CalibPlan& plan, const std::vector<uint64_t>& in, const std::vector<uint64_t>& out,
+           uint64_t stream, const std::vector<uint8_t>& plain) {
+          pr::run_calib_plan(plan, in, out, stream, plain.empty() ? nullptr : &plain);
+        },
+        py::arg("plan"), py::arg("in_ptrs"), py::arg("out_ptrs"), py::arg("stream"),
+        py::arg("plain") = std::vector<uint8_t>{});
 
   py::class_<pr::ProducerEngine>(m, "ProducerEngine")
       .def(py::init<pr::SlotPool*, int64_t, int, const pr::CalibPlan&, int, int, int64_t, int64_t, int, bool>(),

@@ -246,6 +246,10 @@ struct TileGeom {
   int side_slots;                    // LDS side slots after the tile (SideCtx)
   int pitch;                         // LDS floats per tile row (values + candidate bits + pad)
   int xcd_map;                       // XCD-grouped tile order (cm_coords): few frames per launch
+  uint64_t plain_mask;               // bit f: frame f's calib-layout stores are plain, not streaming
+                                     // (frames written into ANOTHER process's ring: QueueFabric direct
+                                     // grants -- streaming stores through an IPC mapping were seen stale
+                                     // by the ring's owner, profiles/r6/README.md)
 };
 
 // Fused K-05 output (image mode with common mode).  Every panel is placed by an integer rotation
@@ -674,8 +678,12 @@ __device__ __forceinline__ void cm_flush_cols(const float* tile, int P, int R, P
 // non-temporal (profiles/r5/README.md); the neighbour tile of the same frame runs on the same XCD
 // (table-major order, 64 frames per launch), so a plain store's half line waits in L2 for its partner.
 __device__ __forceinline__ void cm_flush(const float* tile, int P, int R, int C, PR_GLOBAL float* out, int64_t base,
-                                         int panel_cols) {
+                                         int panel_cols, bool nt = true) {
   const int C4 = C >> 2;
+  if (!nt) {   // plain stores (a frame for another process's ring), workgroup-uniform
+    cm_flush_cols<false>(tile, P, R, out + base, panel_cols, 0, C4);
+    return;
+  }
 #if PR_CM_NT_STORE == 3 && !PR_CM_LDS_PROBE
   if ((panel_cols & 31) == 0) {   // every tile row starts at the same offset within its 128-B line
     PR_GLOBAL float* const ob = out + base;
@@ -877,7 +885,7 @@ struct NoMark {
 template <typename Mark = NoMark>
 __device__ __forceinline__ void cm_write_out(const float* tile, int P, int R, int C, const TileGeom& tg,
                                              const ImgOut& io, int tile_id, int panel, int y0, int x0, int64_t base,
-                                             PR_GLOBAL float* out, const Mark& mark = Mark()) {
+                                             PR_GLOBAL float* out, bool nt, const Mark& mark = Mark()) {
   GapPre gp;
   if (io.desc != nullptr) gp = cm_gap_preload(io, tile_id, (int)gridDim.x / ((tg.nframes + tg.fpw - 1) / tg.fpw));
   __syncthreads();
@@ -887,7 +895,7 @@ __device__ __forceinline__ void cm_write_out(const float* tile, int P, int R, in
     mark(10);
     cm_fill_gaps(io, gp, out);
   } else {
-    cm_flush(tile, P, R, C, out, base, tg.panel_cols);
+    cm_flush(tile, P, R, C, out, base, tg.panel_cols, nt);
   }
 }
 
@@ -897,7 +905,7 @@ __device__ __forceinline__ void cm_store(float* tile, const float* side, const i
                                          const TileGeom& tg, const PR_GLOBAL uint16_t* raw,
                                          const float* __restrict__ ped, const float* __restrict__ gf, int64_t base,
                                          PR_GLOBAL float* out, const ImgOut& io, int tile_id, int panel, int y0,
-                                         int x0) {
+                                         int x0, bool nt) {
   const int C8 = C >> 3;
   for (int i = threadIdx.x; i < R * C8; i += blockDim.x) {
     const int r = i / C8, k = i - r * C8, c = k * 8;
@@ -910,7 +918,7 @@ __device__ __forceinline__ void cm_store(float* tile, const float* side, const i
     cm_out8<KIND, NT>(tile + r * P + c, side, cb, slot, ga, raw, ped, tg.npix, pix, o);
     cm_put8(tile + r * P + c, o);
   }
-  cm_write_out(tile, P, R, C, tg, io, tile_id, panel, y0, x0, base, out);
+  cm_write_out(tile, P, R, C, tg, io, tile_id, panel, y0, x0, base, out, nt);
 }
 
 // (tile, frame) of this workgroup and the tile's first pixel
@@ -1089,7 +1097,8 @@ __global__ __launch_bounds__(1024) void calib_cm_kernel(const FramePtrs fp, cons
     __syncthreads();
   }
 
-  cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.tile, t.panel, t.ar * R, t.ac * C);
+  cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, ped, gf, t.base, out, io, t.tile, t.panel, t.ar * R, t.ac * C,
+                     !((tg.plain_mask >> t.f) & 1));
 }
 
 // ==========================================================================================
@@ -1686,15 +1695,15 @@ __global__ __launch_bounds__(BLOCK, M <= 48 ? (BLOCK / 64) * PR_CM_EPIX_WG_PER_C
       }
       PR_STAMP(7);
 #if PR_CM_STAMPS
-      cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out,
+      cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out, !((tg.plain_mask >> f) & 1),
                    [&](int k) { st_[k] = __builtin_amdgcn_s_memtime(); });
 #else
-      cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out);
+      cm_write_out(tile, P, R, C, tg, io, t.tile, t.panel, t.ar * R, t.ac * C, tb, out, !((tg.plain_mask >> f) & 1));
 #endif
       PR_STAMP(8);
     } else {
       cm_store<KIND, NT>(tile, side, P, R, C, tg, raw, pedp, gfp, tb, out, io, t.tile, t.panel, t.ar * R,
-                         t.ac * C);
+                         t.ac * C, !((tg.plain_mask >> f) & 1));
     }
   };
   if constexpr (kNet) {
@@ -1757,7 +1766,7 @@ static void cm_launch(K kernel, dim3 grid, int block, size_t lds, hipStream_t s,
 void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf, uint64_t planes, int kind,
                      int n_panels, int panel_rows, int panel_cols, int asic_rows, int asic_cols, float thr,
                      float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream, uint64_t img_desc,
-                     uint64_t gap_runs, int n_gap_runs, uint64_t ped_sg) {
+                     uint64_t gap_runs, int n_gap_runs, uint64_t ped_sg, uint64_t plain_mask) {
   check(nframes >= 1 && nframes <= kMaxFrames, "calib_cm: nframes out of range");
   check(asic_rows >= 1 && asic_rows <= 256, "calib_cm: ASIC rows must be in [1, 256]");
   check(asic_cols % 8 == 0 && asic_cols >= 8, "calib_cm: ASIC cols must be a multiple of 8");
@@ -1828,6 +1837,7 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
   tg.asic_cols = asic_cols;
   tg.asics_per_col = panel_rows / asic_rows;
   tg.asics_per_row = panel_cols / asic_cols;
+  tg.plain_mask = plain_mask;
   tg.npix = (int64_t)n_panels * panel_rows * panel_cols;
   tg.nframes = nframes;
   // frames per workgroup: the epix10k2M production kernel takes PR_CM_FPW consecutive frames of

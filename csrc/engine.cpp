@@ -22,12 +22,16 @@ static FramePtrs ptrs_of(const std::vector<uint64_t>& in, const std::vector<uint
 }
 
 void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const std::vector<uint64_t>& out,
-                    uint64_t stream) {
+                    uint64_t stream, const std::vector<uint8_t>* plain) {
   check(in.size() == out.size(), "run_calib_plan: in/out size mismatch");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   for (size_t a = 0; a < in.size(); a += kMaxFrames) {
     const size_t b = std::min(in.size(), a + (size_t)kMaxFrames);
     const int n = (int)(b - a);
+    uint64_t plain_mask = 0;   // frames written into another process's ring: plain stores (fabric.h direct)
+    if (plain != nullptr)
+      for (size_t i = a; i < b && i < plain->size(); ++i)
+        if ((*plain)[i]) plain_mask |= 1ull << (i - a);
     switch (p.mode) {
       case kPlanRawCopy:
         for (size_t i = a; i < b; ++i)
@@ -41,7 +45,7 @@ void run_calib_plan(const CalibPlan& p, const std::vector<uint64_t>& in, const s
       case kPlanCalibCm:
         launch_calib_cm(ptrs_of(in, out, a, b), n, p.ped, p.gf, p.elig, p.kind, p.n_panels, p.panel_rows,
                         p.panel_cols, p.asic_rows, p.asic_cols, p.thr, p.maxcorr, p.npix_min, p.cm_flags,
-                        p.bank_cols, stream, 0, 0, 0, p.ped_sg);
+                        p.bank_cols, stream, 0, 0, 0, p.ped_sg, plain_mask);
         break;
       case kPlanImageFused:
         if (p.use_tiles)
@@ -518,7 +522,13 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       }
       {
         trace::Range r("producer.launch_calib");
-        run_calib_plan(plan_, in, out, stream_c);
+        if (dg.empty()) {
+          run_calib_plan(plan_, in, out, stream_c);
+        } else {
+          std::vector<uint8_t> plain(n, 0);
+          for (size_t q = 0; q < dg.size(); ++q) plain[q] = 1;
+          run_calib_plan(plan_, in, out, stream_c, &plain);
+        }
       }
       if (!device_resident_ || gpu_timing_) hip_check(hipEventRecord(buf_free_[b], cs), "record buf free");
       auto t3 = clk::now();

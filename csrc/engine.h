@@ -60,8 +60,9 @@ struct CalibPlan {
 };
 
 // Launch the plan for n frames (any n; split into kMaxFrames launches) on `stream`.
+// plain: per frame, 1 = plain (not streaming) output stores (frames for another process's ring)
 void run_calib_plan(const CalibPlan& plan, const std::vector<uint64_t>& in, const std::vector<uint64_t>& out,
-                    uint64_t stream);
+                    uint64_t stream, const std::vector<uint8_t>* plain = nullptr);
 
 class ProducerEngine {
  public:

@@ -398,9 +398,11 @@ int64_t QueueFabric::direct_pass() {
   }
   if (!want) return work;
   // frames already produced without a grant (copy path) get the consumers' grants first: the offer
-  // pool refills only when none of them waits
-  if ((int64_t)pool_->n_produced() > (int64_t)d_bound_.size()) return work;
-  while ((int)d_free_.size() < kDirectPool) {
+  // pool takes only the grants beyond that backlog
+  int64_t spare = -std::max<int64_t>(0, (int64_t)pool_->n_produced() - (int64_t)d_bound_.size());
+  for (auto& lp : links_)
+    if (lp->outgoing && usable(*lp)) spare += (int64_t)lp->grants.size();
+  while ((int)d_free_.size() < kDirectPool && spare-- > 0) {
     Link* best = nullptr;
     std::shared_ptr<Link> bp;
     for (auto& lp : links_)

@@ -16,7 +16,8 @@ void launch_calib_cm(const FramePtrs& fp, int nframes, uint64_t ped, uint64_t gf
                      float maxcorr, int npix_min, int flags, int bank_cols, uint64_t stream,
                      uint64_t img_desc = 0, uint64_t gap_runs = 0,
                      int n_gap_runs = 0,    // img_desc: fused K-05 (ImgOut); gap runs zeroed by the same kernel
-                     uint64_t ped_sg = 0);  // signed pedestal tables (eligibility in the sign bits), 0 = planes
+                     uint64_t ped_sg = 0,   // signed pedestal tables (eligibility in the sign bits), 0 = planes
+                     uint64_t plain_mask = 0);  // bit f: plain (not streaming) stores for frame f
 size_t cm_lds_bytes(int asic_rows, int asic_cols, int kind);
 bool cm_signed_shape(int kind, int asic_rows, int asic_cols, int bank_cols);   // reads signed pedestal tables
 void launch_image_tiles(const FramePtrs& fp, int nframes, bool calib, int kind, uint64_t ped, uint64_t gf,

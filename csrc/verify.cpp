@@ -30,61 +30,80 @@ FrameVerifier::FrameVerifier(int device, int64_t frame_bytes) : device_(device),
   if (device_ < 0) return;
   check(frame_bytes % 16 == 0, "FrameVerifier: frame size must be a multiple of 16 B on the GPU");
   DeviceGuard dg(device_);
-  const size_t rows = (size_t)kRows * kMaxFrames;
-  hip_check(hipMalloc(reinterpret_cast<void**>(&acc_), rows * sizeof(uint64_t)), "hipMalloc (verify scratch)");
-  hip_check(hipMalloc(reinterpret_cast<void**>(&cnt_), rows * sizeof(uint32_t)), "hipMalloc (verify tickets)");
-  hip_check(hipMalloc(reinterpret_cast<void**>(&counters_), 4 * sizeof(int64_t)), "hipMalloc (verify counters)");
-  hip_check(hipMemset(acc_, 0, rows * sizeof(uint64_t)), "hipMemset (verify scratch)");
-  hip_check(hipMemset(cnt_, 0, rows * sizeof(uint32_t)), "hipMemset (verify tickets)");
-  const int64_t init[4] = {0, 0, -1, 0};
-  hip_check(hipMemcpy(counters_, init, sizeof(init), hipMemcpyHostToDevice), "hipMemcpy (verify counters)");
+  const size_t rows = (size_t)kRows * kMaxFrames * kCkPartials;
+  hip_check(hipMalloc(reinterpret_cast<void**>(&part_), rows * sizeof(uint64_t)), "hipMalloc (verify scratch)");
   hip_check(hipHostMalloc(reinterpret_cast<void**>(&results_), kResults * sizeof(int64_t), hipHostMallocDefault),
             "hipHostMalloc (verify results)");
   memset(results_, 0, kResults * sizeof(int64_t));
-  hip_check(hipStreamCreateWithFlags(&rd_stream_, hipStreamNonBlocking), "hipStreamCreate (verify)");
 }
 
 FrameVerifier::~FrameVerifier() {
   if (device_ < 0) return;
   DeviceGuard dg(device_);
-  (void)hipDeviceSynchronize();   // no launch of ours may still use the scratch
-  if (rd_stream_) (void)hipStreamDestroy(rd_stream_);
-  if (acc_) (void)hipFree(acc_);
-  if (cnt_) (void)hipFree(cnt_);
-  if (counters_) (void)hipFree(counters_);
+  for (auto& p : pending_) {
+    (void)hipEventSynchronize(p.ev);   // no launch of ours may still use the scratch
+    (void)hipEventDestroy(p.ev);
+  }
+  for (auto e : free_ev_) (void)hipEventDestroy(e);
+  (void)hipDeviceSynchronize();
+  if (part_) (void)hipFree(part_);
   if (results_) (void)hipHostFree(results_);
 }
 
 int64_t FrameVerifier::take_row() {
-  std::lock_guard<std::mutex> lk(mu_);
   const int64_t r = row_;
   row_ = (row_ + 1) % kRows;
   return r;
 }
 
+int64_t FrameVerifier::take_results(int n) {
+  if (res_next_ + n > kResults) res_next_ = 0;
+  const int64_t base = res_next_;
+  res_next_ += n;
+  return base;
+}
+
 int64_t FrameVerifier::checksum_async(const std::vector<uint64_t>& ptrs, uint64_t stream) {
   check(device_ >= 0, "FrameVerifier::checksum_async: GPU rings only");
   check(!ptrs.empty() && (int)ptrs.size() <= kMaxFrames, "FrameVerifier::checksum_async: 1..kMaxFrames frames");
-  int64_t base;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (res_next_ + (int64_t)ptrs.size() > kResults) res_next_ = 0;
-    base = res_next_;
-    res_next_ += (int64_t)ptrs.size();
-  }
   CkFrames a{};
   for (size_t i = 0; i < ptrs.size(); ++i) a.ptr[i] = ptrs[i];
+  std::lock_guard<std::mutex> lk(mu_);
+  const int64_t base = take_results((int)ptrs.size());
   const int64_t row = take_row();
   DeviceGuard dg(device_);
-  launch_frame_checksums(a, (int)ptrs.size(), bytes_ / 16, reinterpret_cast<uint64_t>(acc_ + row * kMaxFrames),
-                         reinterpret_cast<uint64_t>(cnt_ + row * kMaxFrames), false,
-                         reinterpret_cast<uint64_t>(results_ + base), 0, stream);
+  launch_frame_checksums(a, (int)ptrs.size(), bytes_ / 16,
+                         reinterpret_cast<uint64_t>(part_ + row * kMaxFrames * kCkPartials),
+                         reinterpret_cast<uint64_t>(results_ + base), stream);
   return base;
 }
 
 int64_t FrameVerifier::result(int64_t index) const {
   check(device_ >= 0 && index >= 0 && index < kResults, "FrameVerifier::result: bad index");
   return reinterpret_cast<volatile int64_t*>(results_)[index];
+}
+
+void FrameVerifier::settle(bool wait) {
+  while (!pending_.empty()) {
+    Pending& p = pending_.front();
+    if (wait) {
+      hip_check(hipEventSynchronize(p.ev), "hipEventSynchronize (verify)");
+    } else {
+      const hipError_t q = hipEventQuery(p.ev);
+      if (q == hipErrorNotReady) return;
+      hip_check(q, "hipEventQuery (verify)");
+    }
+    for (size_t i = 0; i < p.expect.size(); ++i) {
+      if (result(p.base + (int64_t)i) == p.expect[i]) {
+        h_ok_.fetch_add(1);
+      } else {
+        h_bad_.fetch_add(1);
+        h_last_bad_.store(p.gevt[i]);
+      }
+    }
+    free_ev_.push_back(p.ev);
+    pending_.pop_front();
+  }
 }
 
 void FrameVerifier::verify(const std::vector<uint64_t>& ptrs, const std::vector<int64_t>& expect,
@@ -103,19 +122,34 @@ void FrameVerifier::verify(const std::vector<uint64_t>& ptrs, const std::vector<
     }
     return;
   }
+  std::lock_guard<std::mutex> lk(mu_);
   DeviceGuard dg(device_);
+  settle(false);
+  // results of pending launches may not be overwritten: with the ring nearly full, wait for the oldest
+  while (!pending_.empty() && ((int64_t)pending_.size() + 1) * kMaxFrames > kResults) {
+    hip_check(hipEventSynchronize(pending_.front().ev), "hipEventSynchronize (verify ring)");
+    settle(false);
+  }
   for (size_t a0 = 0; a0 < ptrs.size(); a0 += kMaxFrames) {
     const size_t n = std::min(ptrs.size() - a0, (size_t)kMaxFrames);
     CkFrames a{};
-    for (size_t i = 0; i < n; ++i) {
-      a.ptr[i] = ptrs[a0 + i];
-      a.expect[i] = expect[a0 + i];
-      a.gevt[i] = gevt[a0 + i];
-    }
+    for (size_t i = 0; i < n; ++i) a.ptr[i] = ptrs[a0 + i];
+    const int64_t base = take_results((int)n);
     const int64_t row = take_row();
-    launch_frame_checksums(a, (int)n, bytes_ / 16, reinterpret_cast<uint64_t>(acc_ + row * kMaxFrames),
-                           reinterpret_cast<uint64_t>(cnt_ + row * kMaxFrames), true, 0,
-                           reinterpret_cast<uint64_t>(counters_), stream);
+    launch_frame_checksums(a, (int)n, bytes_ / 16, reinterpret_cast<uint64_t>(part_ + row * kMaxFrames * kCkPartials),
+                           reinterpret_cast<uint64_t>(results_ + base), stream);
+    Pending p;
+    if (free_ev_.empty()) {
+      hip_check(hipEventCreateWithFlags(&p.ev, hipEventDisableTiming), "hipEventCreate (verify)");
+    } else {
+      p.ev = free_ev_.back();
+      free_ev_.pop_back();
+    }
+    hip_check(hipEventRecord(p.ev, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord (verify)");
+    p.base = base;
+    p.expect.assign(expect.begin() + (int64_t)a0, expect.begin() + (int64_t)(a0 + n));
+    p.gevt.assign(gevt.begin() + (int64_t)a0, gevt.begin() + (int64_t)(a0 + n));
+    pending_.push_back(std::move(p));
   }
 }
 
@@ -130,14 +164,13 @@ void FrameVerifier::acquire(uint64_t stream) {
   launch_acquire_fence(stream);
 }
 
-std::array<int64_t, 4> FrameVerifier::counts() const {
-  if (device_ < 0) return {h_ok_.load(), h_bad_.load(), h_last_bad_.load(), acquires_.load()};
-  DeviceGuard dg(device_);
-  int64_t c[4] = {0, 0, -1, 0};
-  hip_check(hipMemcpyAsync(c, counters_, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, rd_stream_),
-            "hipMemcpyAsync (verify counters)");
-  hip_check(hipStreamSynchronize(rd_stream_), "hipStreamSynchronize (verify counters)");
-  return {c[0], c[1], c[2], acquires_.load()};
+std::array<int64_t, 4> FrameVerifier::counts() {
+  if (device_ >= 0) {
+    std::lock_guard<std::mutex> lk(mu_);
+    DeviceGuard dg(device_);
+    settle(true);
+  }
+  return {h_ok_.load(), h_bad_.load(), h_last_bad_.load(), acquires_.load()};
 }
 
 }  // namespace pr

@@ -10,9 +10,9 @@
 //             exactly the bytes copied), carried to the consumer in the notice's `aux` field with a
 //             tag in the top byte;
 //   consumer: a frame it takes whose aux carries the tag is re-summed from ITS ring slot on the
-//             stream the caller will read it on, before that read, and compared on the device:
-//             verified / mismatched counters (plus the last mismatching gevt) stay in HBM and are
-//             read back only when asked (no host sync per frame).
+//             stream the caller will read it on, before that read; the sum lands in pinned host
+//             memory and is compared on the host once that launch's event completed (verified /
+//             mismatched counts plus the last mismatching gevt; no host sync per frame).
 //
 // The checksum is order-dependent (each 16-B word is mixed with its index, then the mixes are
 // summed), so a stale, shifted or partially written frame changes it; the sum is associative, so
@@ -28,6 +28,7 @@
 
 #include <array>
 #include <atomic>
+#include <deque>
 #include <mutex>
 #include <vector>
 
@@ -54,18 +55,16 @@ __host__ __device__ __forceinline__ bool ck_tagged(int64_t aux) {
 // The checksum of `bytes` bytes at host address p (a partial last 16-B word is zero-padded).
 uint64_t frame_checksum_host(const void* p, int64_t bytes);
 
-// Per-launch arguments of the device checksum kernel (kernarg block, 1.5 KB).
+// Per-launch arguments of the device checksum kernels (kernarg block).
 struct CkFrames {
   uint64_t ptr[kMaxFrames];
-  int64_t expect[kMaxFrames];   // consumer: tagged checksum the producer sent
-  int64_t gevt[kMaxFrames];
 };
 
-// Device launchers (verify.hip).  acc / cnt: kMaxFrames-entry scratch rows (zero, left zero).
-//   compare = false: out[f] = tagged checksum of frame f (pinned host memory)
-//   compare = true : counters[0] += matches, counters[1] += mismatches, counters[2] = last bad gevt
-void launch_frame_checksums(const CkFrames& a, int nframes, int64_t n16, uint64_t acc, uint64_t cnt, bool compare,
-                            uint64_t out, uint64_t counters, uint64_t stream);
+// Device launcher (verify.hip): out[f] = tagged checksum of frame f (pinned host memory), via a
+// scratch row `part` of kMaxFrames x kCkPartials uint64 partials.
+constexpr int kCkPartials = 128;
+void launch_frame_checksums(const CkFrames& a, int nframes, int64_t n16, uint64_t part, uint64_t out,
+                            uint64_t stream);
 // System-scope acquire on every XCD (64 one-wave workgroups, dealt round-robin over the 8 XCDs).
 void launch_acquire_fence(uint64_t stream);
 // System-scope release on every XCD (the direct-write path: calibration kernels wrote peer memory).
@@ -86,29 +85,36 @@ class FrameVerifier {
   // first result in the pinned result ring (result(i) is valid once the stream passed this point)
   int64_t checksum_async(const std::vector<uint64_t>& ptrs, uint64_t stream);
   int64_t result(int64_t index) const;
-  // consumer: compare frames against the tagged checksums their producer sent (GPU: queued on
-  // `stream` and counted on the device; host: now)
+  // consumer: compare frames against the tagged checksums their producer sent (GPU: the sums are
+  // queued on `stream` and compared on the host once that launch's event completed -- at a later
+  // verify() or counts(); host rings: now)
   void verify(const std::vector<uint64_t>& ptrs, const std::vector<int64_t>& expect,
               const std::vector<int64_t>& gevt, uint64_t stream);
   // consumer, GPU: explicit system-scope acquire on `stream` before reading peer-written frames
   void acquire(uint64_t stream);
-  // {verified, mismatched, last mismatching gevt (-1 none), acquires}; GPU: reads the device
-  // counters (the caller synchronises the streams it verified on first for an exact count)
-  std::array<int64_t, 4> counts() const;
+  // {verified, mismatched, last mismatching gevt (-1 none), acquires}; GPU: waits for every
+  // pending comparison's launch, so the count covers every frame verify() was called for
+  std::array<int64_t, 4> counts();
 
-  static constexpr int kRows = 256;         // scratch rows (rotating, one per launch)
-  static constexpr int kResults = 4096;     // pinned producer results (rotating)
+  static constexpr int kRows = 64;          // scratch rows (rotating, one per launch)
+  static constexpr int kResults = 16384;    // pinned results (rotating)
 
  private:
+  struct Pending {
+    hipEvent_t ev;
+    int64_t base;
+    std::vector<int64_t> expect, gevt;
+  };
   int64_t take_row();
+  int64_t take_results(int n);
+  void settle(bool wait);   // compare pending results whose launch completed (all, if wait); mu_ held
   int device_;
   int64_t bytes_;
-  uint64_t* acc_ = nullptr;        // device: kRows x kMaxFrames
-  uint32_t* cnt_ = nullptr;        // device: kRows x kMaxFrames
-  int64_t* counters_ = nullptr;    // device: [verified, mismatched, last bad gevt]
+  uint64_t* part_ = nullptr;       // device: kRows x kMaxFrames x kCkPartials
   int64_t* results_ = nullptr;     // pinned host: kResults
-  hipStream_t rd_stream_ = nullptr;
-  mutable std::mutex mu_;
+  std::deque<Pending> pending_;
+  std::vector<hipEvent_t> free_ev_;
+  std::mutex mu_;
   int64_t row_ = 0, res_next_ = 0;
   bool acquire_on_ = true;
   std::atomic<int64_t> h_ok_{0}, h_bad_{0}, h_last_bad_{-1}, acquires_{0};

@@ -7,16 +7,18 @@
 
 namespace pr {
 
-// Grid (blocks per frame, frames).  Each lane sums the mixes of a strided set of 16-B words, the
-// block reduces them (DPP-lowered shuffles, then LDS across its 4 waves), and one lane adds the
-// block's sum to the frame's scratch accumulator.  The LAST block of a frame (ticket) reads the
-// total, leaves the scratch zero for the next launch on this row, and publishes: the tagged sum
-// (producer, into pinned host memory) or the comparison (consumer, device counters).
-template <bool kCompare>
-__global__ __launch_bounds__(256) void frame_checksum_kernel(const CkFrames a, const int64_t n16,
-                                                             unsigned long long* __restrict__ acc,
-                                                             unsigned int* __restrict__ cnt, int64_t* out,
-                                                             unsigned long long* counters) {
+// Two launches: (blocks per frame, frames) blocks each sum the mixes of a strided set of 16-B words
+// (DPP-lowered shuffles, then LDS across the block's 4 waves) and store ONE partial per block; then
+// one block per frame adds its partials in a fixed order and stores the tagged sum into pinned host
+// memory, where the host reads it after the launch's event (producer: into the notice; consumer:
+// compared with the producer's -- no device-side counters, so no cross-XCD atomics at all).  The kernel boundary
+// orders the partials' stores before their reads on every XCD: a single-launch "last block adds
+// the others' atomics" form gave sums that differed from the host's on gfx950 (the blocks of a
+// frame run on all 8 XCDs, whose L2s are not coherent for device-scope atomics on plain memory).
+constexpr int kCkBlocks = kCkPartials;   // max blocks per frame (partials per frame)
+
+__global__ __launch_bounds__(256) void frame_partials_kernel(const CkFrames a, const int64_t n16,
+                                                             uint64_t* __restrict__ part) {
   const int f = blockIdx.y;
   const PR_GLOBAL u32x4_t* p = gin<u32x4_t>(a.ptr[f]);
   uint64_t s = 0;
@@ -27,47 +29,36 @@ __global__ __launch_bounds__(256) void frame_checksum_kernel(const CkFrames a, c
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor((unsigned long long)s, o);
-  __shared__ uint64_t part[4];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __shared__ uint64_t w[4];
+  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  s = part[0] + part[1] + part[2] + part[3];
-  atomicAdd(&acc[f], (unsigned long long)s);
-  __threadfence();
-  const unsigned t = atomicAdd(&cnt[f], 1u);
-  if (t != gridDim.x - 1) return;
-  __threadfence();
-  const uint64_t tot = atomicExch(&acc[f], 0ull);
-  atomicExch(&cnt[f], 0u);
-  const int64_t tg = ck_tag(tot);
-  if constexpr (!kCompare) {
-    out[f] = tg;   // pinned host memory: read by the fabric thread once the copy's event completed
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  } else if (tg == a.expect[f]) {
-    atomicAdd(&counters[0], 1ull);
-  } else {
-    atomicAdd(&counters[1], 1ull);
-    atomicExch(&counters[2], (unsigned long long)a.gevt[f]);
-  }
+  if (threadIdx.x == 0) part[(int64_t)f * kCkBlocks + blockIdx.x] = w[0] + w[1] + w[2] + w[3];
 }
 
-void launch_frame_checksums(const CkFrames& a, int nframes, int64_t n16, uint64_t acc, uint64_t cnt, bool compare,
-                            uint64_t out, uint64_t counters, uint64_t stream) {
+__global__ __launch_bounds__(64) void frame_finish_kernel(const int nblk, const uint64_t* __restrict__ part,
+                                                          int64_t* out) {
+  const int f = blockIdx.x;
+  uint64_t s = 0;
+  for (int b = threadIdx.x; b < nblk; b += 64) s += part[(int64_t)f * kCkBlocks + b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor((unsigned long long)s, o);
+  if (threadIdx.x != 0) return;
+  out[f] = ck_tag(s);   // pinned host memory: read on the host once the launch's event completed
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+void launch_frame_checksums(const CkFrames& a, int nframes, int64_t n16, uint64_t part, uint64_t out,
+                            uint64_t stream) {
   check(nframes >= 1 && nframes <= kMaxFrames, "frame_checksums: 1..kMaxFrames frames per launch");
-  check(n16 > 0 && acc != 0 && cnt != 0, "frame_checksums: empty frame or no scratch");
-  check(compare ? counters != 0 : out != 0, "frame_checksums: no result buffer");
+  check(n16 > 0 && part != 0 && out != 0, "frame_checksums: empty frame, no scratch or no result buffer");
   for (int i = 0; i < nframes; ++i) check(aligned16(a.ptr[i]), "frame_checksums: frames must be 16-B aligned");
-  const int64_t per = (n16 + 256 * 8 - 1) / (256 * 8);   // ~8 words per lane, at most 128 blocks a frame
-  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(128, per)), (unsigned)nframes);
+  const int64_t per = (n16 + 256 * 8 - 1) / (256 * 8);   // ~8 words per lane, at most kCkBlocks blocks a frame
+  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(kCkBlocks, per));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  auto* pa = reinterpret_cast<unsigned long long*>(acc);
-  auto* pc = reinterpret_cast<unsigned int*>(cnt);
-  if (compare)
-    hipLaunchKernelGGL(frame_checksum_kernel<true>, grid, dim3(256), 0, s, a, n16, pa, pc, nullptr,
-                       reinterpret_cast<unsigned long long*>(counters));
-  else
-    hipLaunchKernelGGL(frame_checksum_kernel<false>, grid, dim3(256), 0, s, a, n16, pa, pc,
-                       reinterpret_cast<int64_t*>(out), nullptr);
+  auto* pp = reinterpret_cast<uint64_t*>(part);
+  hipLaunchKernelGGL(frame_partials_kernel, dim3((unsigned)nblk, (unsigned)nframes), dim3(256), 0, s, a, n16, pp);
+  hipLaunchKernelGGL(frame_finish_kernel, dim3((unsigned)nframes), dim3(64), 0, s, nblk, pp,
+                     reinterpret_cast<int64_t*>(out));
   hip_check(hipGetLastError(), "frame_checksums launch");
 }
 

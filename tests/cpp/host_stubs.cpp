@@ -13,7 +13,7 @@ int launch_copy_runs(CopyRuns&, int, uint64_t) {
 
 namespace pr {
 // verify.hip launchers: the host-only sanitizer build runs host (CPU) rings only
-void launch_frame_checksums(const CkFrames&, int, int64_t, uint64_t, uint64_t, bool, uint64_t, uint64_t, uint64_t) {
+void launch_frame_checksums(const CkFrames&, int, int64_t, uint64_t, uint64_t, uint64_t) {
   check(false, "launch_frame_checksums: the host-only sanitizer build has no GPU kernels");
 }
 void launch_acquire_fence(uint64_t) { check(false, "launch_acquire_fence: no GPU kernels in this build"); }

@@ -97,7 +97,8 @@ def test_checksum_device_matches_host(native, cuda_device):
         base = v.checksum_async([int(f.data_ptr()) for f in frames], sh)
         stream.synchronize()
         got = [v.result(base + i) for i in range(3)]
-        want = [C.checksum_tag(C.frame_checksum_host(int(f.cpu().numpy().ctypes.data), nbytes)) for f in frames]
+        host = [f.cpu().numpy() for f in frames]   # kept alive while the host checksum reads them
+        want = [C.checksum_tag(C.frame_checksum_host(int(h.ctypes.data), nbytes)) for h in host]
         assert got == want
         # consumer mode: frame 1 damaged after its checksum was taken
         frames[1][nbytes // 8] ^= 1
@@ -136,3 +137,33 @@ def _run_gpu_bench(nproc, extra_env):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200, cwd="/tmp")
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     return r, (json.loads(lines[0]) if lines else None)
+
+
+@pytest.mark.gpu
+def test_plain_store_mask_is_bitwise_equal(native, cuda_device):
+    """Frames calibrated for ANOTHER process's ring (direct grants) use plain stores instead of the
+    streaming ones (CmParams plain_mask): the epix10k2M common-mode kernel's output is bit-identical
+    either way, for a mixed mask over a 64-frame launch."""
+    import numpy as np
+    import torch
+
+    from psana_ray_amd.models.calibrator import Calibrator
+    from psana_ray_amd.models.detector import Mode
+    from psana_ray_amd.config import resolve_common_mode
+    from psana_ray_amd.source import SyntheticRun
+
+    C = native
+    dev = cuda_device
+    src = SyntheticRun("synthetic", 0, "epix10k2M", pool_frames=8, gen_device="cuda")
+    cal = Calibrator(src.consts, dev, Mode.calib, common_mode=resolve_common_mode("auto", src.consts.spec))
+    raw = torch.from_numpy(src.pool.view(np.int16)).view(torch.uint16).to(dev)
+    n = 64
+    ins = [int(raw[i % raw.shape[0]].data_ptr()) for i in range(n)]
+    a = torch.empty((n, *cal.out_shape), dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    s = torch.cuda.current_stream(dev)
+    C.run_calib_plan(cal.plan, ins, [int(a[i].data_ptr()) for i in range(n)], s.cuda_stream)
+    C.run_calib_plan(cal.plan, ins, [int(b[i].data_ptr()) for i in range(n)], s.cuda_stream,
+                     [1 if i % 3 else 0 for i in range(n)])
+    s.synchronize()
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
