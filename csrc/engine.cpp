@@ -513,7 +513,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       // frames with a direct grant are calibrated straight into that consumer's slot (the local slot
       // only carries the header and the queue_size accounting; QueueFabric::take_direct)
       std::vector<QueueFabric::DirectGrant> dg;
-      if (fabric_ != nullptr) dg = fabric_->take_direct(n);
+      if (fabric_ != nullptr) dg = fabric_->take_direct(n);   // opportunistic: never waits for grants
       for (size_t q = 0; q < dg.size(); ++q) out[q] = dg[q].ptr;
       if (gpu_timing_) {
         if (device_resident_) harvest(b, false);

@@ -369,10 +369,11 @@ void QueueFabric::cancel_direct(const std::vector<int64_t>& tokens) {
 // grants (the link holding the most grants first, so the offers spread over the consumers).
 int64_t QueueFabric::direct_pass() {
   const int policy = policy_.load();
-  // spread / remote_only send frames to other processes by policy; a producer with no consumer of
-  // its own (or one that closed) sends every frame away
-  const bool want = direct_on_ && !finished_.load() &&
-                    (policy == 2 || policy == 4 || !is_consumer_ || consumer_closed_.load());
+  // only where the POLICY sends frames to other processes (spread, remote_only).  A producer with no
+  // consumer of its own keeps the copy path: its frames are routed at completion to whichever
+  // consumer has credit then, which keeps competing consumers balanced by their read speed (binding
+  // at launch time skewed a fast / slow pair towards the slow one, 77 vs 123 frames)
+  const bool want = direct_on_ && !finished_.load() && (policy == 2 || policy == 4);
   auto usable = [](const Link& l) {
     return l.attached && !l.dead && !l.closed && !l.eos_posted && !l.keeper && l.kcopy;
   };
@@ -385,9 +386,15 @@ int64_t QueueFabric::direct_pass() {
     ++work;
   }
   d_cancel_.clear();
+  // the pool never holds more grants than the engine can use now (its free producer budget): a
+  // budget full of frames waiting for a copy needs the consumers' grants for the copy path, or
+  // nothing moves (the pool would keep every grant while the engine cannot take one)
+  const int64_t target = want ? std::max<int64_t>(0, std::min<int64_t>(kDirectPool, pool_->producer_room())) : 0;
+  int64_t keep = 0;
   for (auto it = d_free_.begin(); it != d_free_.end();) {
     Link& l = *it->second.link;
-    if (want && usable(l)) {
+    if (want && usable(l) && keep < target) {
+      ++keep;
       ++it;
       continue;
     }
@@ -397,12 +404,9 @@ int64_t QueueFabric::direct_pass() {
     ++work;
   }
   if (!want) return work;
-  // frames already produced without a grant (copy path) get the consumers' grants first: the offer
-  // pool takes only the grants beyond that backlog
-  int64_t spare = -std::max<int64_t>(0, (int64_t)pool_->n_produced() - (int64_t)d_bound_.size());
-  for (auto& lp : links_)
-    if (lp->outgoing && usable(*lp)) spare += (int64_t)lp->grants.size();
-  while ((int)d_free_.size() < kDirectPool && spare-- > 0) {
+  // direct first: the offer pool refills (up to the engine's free budget) before the copy path
+  // routes this pass's produced frames
+  while ((int64_t)d_free_.size() < target) {
     Link* best = nullptr;
     std::shared_ptr<Link> bp;
     for (auto& lp : links_)
@@ -431,15 +435,17 @@ void QueueFabric::issue_direct(std::vector<Batch>& db) {
   std::vector<int> all;
   for (const Batch& b : db) all.insert(all.end(), b.slots.begin(), b.slots.end());
   pool_->begin_send_batch(all, reinterpret_cast<uint64_t>(xstream_));
-  launch_release_fence(reinterpret_cast<uint64_t>(xstream_));
+  bool peer_gpu = false;   // a ring on another GPU was written: write back L2 lines of peer memory
+  for (const Batch& b : db) peer_gpu |= b.link->consumer_device >= 0 && b.link->consumer_device != device_;
+  if (peer_gpu) launch_release_fence(reinterpret_cast<uint64_t>(xstream_));
   int64_t n = 0;
   for (Batch& b : db) {
+    b.direct = true;   // before the checksums: they must read the frames in the consumer's ring
     start_checksums(b, reinterpret_cast<uint64_t>(xstream_));
     inject_corruption(b, reinterpret_cast<uint64_t>(xstream_));
   }
   for (Batch& b : db) {
     b.stream = xstream_;
-    b.direct = true;
     b.ev = take_event();
     hip_check(hipEventRecord(b.ev, xstream_), "hipEventRecord (direct frames)");
     b.link->inflight += (int)b.slots.size();
@@ -1789,6 +1795,11 @@ void QueueFabric::issue_copies(std::vector<Batch>& kb, double now) {
     g->bytes += (int64_t)n * slot_bytes_;
   }
   flush();
+  // another GPU's ring written: one system-scope release on every XCD before the completion signal
+  // (a consumer on THIS GPU reads through the same L2: nothing to write back)
+  bool peer_gpu = false;
+  for (const Batch& b : kb) peer_gpu |= b.link->consumer_device >= 0 && b.link->consumer_device != device_;
+  if (peer_gpu) launch_release_fence(reinterpret_cast<uint64_t>(xstream_));
   for (const Batch& b : kb) inject_corruption(b, reinterpret_cast<uint64_t>(xstream_));
   hip_check(hipEventRecord(g->end, xstream_), "hipEventRecord (copy end)");
   g->pending = (int)kb.size();

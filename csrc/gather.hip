@@ -172,14 +172,16 @@ bool launch_copy_h2d(uint64_t dst, uint64_t host_src, int64_t bytes, int workgro
 // chunk (256 lanes x U x 16 B in flight); the grid strides over the chunks of all runs, so the
 // writes to different consumers (different xGMI links) are in flight at the same time.  Loads are
 // nontemporal (the producer slot is freed right after); stores are plain (a same-GPU consumer reads
-// the slot next).  Visibility: the consumer is told only after this kernel's completion event, and
-// every wave ends with an explicit SYSTEM-scope release (buffer_wbl2 sc0 sc1: lines of peer memory
-// this XCD's L2 may hold dirty are written back over xGMI before the completion signal), instead of
-// relying on the dispatch packet's release scope; the consumer issues the matching acquire
-// (verify.h).  PR_COPY_RELEASE=0 builds the A/B variant without it.
+// the slot next).  Visibility: the consumer is told only after this kernel's completion event; when
+// a dispatch writes another GPU's ring, the fabric follows it with ONE system-scope release on every
+// XCD (launch_release_fence, verify.hip: buffer_wbl2 sc0 sc1 writes back L2 lines of peer memory
+// before the completion signal) instead of relying on the dispatch packet's release scope, and the
+// consumer issues the matching acquire (verify.h).  PR_COPY_RELEASE=1 builds the round-6 variant with
+// a release at the end of every wave instead: 2 ranks on one GPU, route=remote_only window 83.0k /
+// 84.0k vs 108.2k / 109.7k fr/s without it (profiles/r6/README.md section 3).
 // ---------------------------------------------------------------------------------------------
 #ifndef PR_COPY_RELEASE
-#define PR_COPY_RELEASE 1
+#define PR_COPY_RELEASE 0
 #endif
 template <int U>
 __global__ __launch_bounds__(256) void copy_runs_kernel(const CopyRuns cr, const int total_chunks) {
