@@ -779,6 +779,23 @@ __device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, const GapPre& g, 
 #define PR_CM_PLACE_CQ 4
 #endif
 #define PR_PLACE_KEEP(bit, v) (!(PR_CM_PLACEPROBE & (bit)) || __float_as_uint((v)) == 0x7fc01234u)
+// PR_CM_IMG_NT = 1 (A/B): image placement stores streaming (non-temporal) for the 128-B lines that lie
+// wholly inside one image run, plain for the lines a run shares with a gap or a neighbour tile (the
+// image form of PR_CM_NT_STORE 3; all-streaming placement stores cost 13 %, partial lines)
+#ifndef PR_CM_IMG_NT
+#define PR_CM_IMG_NT 0
+#endif
+__device__ __forceinline__ void st_img4(PR_GLOBAL float* out, int32_t e, int32_t run_lo, int len, const float4 v) {
+#if PR_CM_IMG_NT
+  if ((e & ~31) >= run_lo && (e | 31) < run_lo + len) {
+    f32x4_t x;
+    x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
+    __builtin_nontemporal_store(x, (PR_GLOBAL f32x4_t*)(out + e));
+    return;
+  }
+#endif
+  st_out4<2>((PR_GLOBAL float4*)(out + e), v);
+}
 __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C, const ImgOut& io, int panel, int y0,
                                          int x0, PR_GLOBAL float* out) {
   const int32_t* d = io.desc + 3 * panel;
@@ -830,7 +847,7 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
       for (; run < nruns;) {
         const float* tp = tb + run * P + 4 * k * di;
         const float4 v4 = make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]);
-        if (PR_PLACE_KEEP(2, v4.x)) st_out4<2>((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)), v4);
+        if (PR_PLACE_KEEP(2, v4.x)) st_img4(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4);
         run += drun;
         k += dk;
         if (k >= nfull) {
@@ -850,7 +867,7 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
         if (k < nfull) {
           const float* tp = tb + run + 4 * k * di;
           const float4 v4 = make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]);
-          if (PR_PLACE_KEEP(4, v4.x)) st_out4<2>((PR_GLOBAL float4*)(out + (ob + run * oo + 4 * k)), v4);
+          if (PR_PLACE_KEEP(4, v4.x)) st_img4(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4);
         }
         a += da;
         w += dw;

@@ -6,8 +6,9 @@
 #   smoke      __graft_entry__.smoke()
 #   bench      the driver's line: bench.py --steps 20 --warmup 5 (and --steps 200)
 #   dev        device-resident calib / image pipelines, 200 steps
-#   rehearsal  the driver's N>1 launch on this one GPU: torch.distributed.run, 2 ranks, host-staged
-#              and device-resident (links, both windows, gate, topology record, teardown)
+#   rehearsal  the driver's N>1 launch on this one GPU, 2 ranks: plain `bench.py --gpus 2` (self-
+#              launched) host-staged, torch.distributed.run device-resident (links, both windows,
+#              gate, topology record, frame checks, teardown)
 #   prof       rocprofv3 --kernel-trace --stats of both device-resident pipelines (stats CSVs kept)
 #   configs    BASELINE config 4 (Jungfrau-16M, queue_size 400000; host-staged / device-resident,
 #              rocprofv3 stats) and config 1 (256x256, in-process CPU queue)
@@ -47,10 +48,15 @@ if has dev; then
 fi
 if has rehearsal; then
   for src in host device; do
-    timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) \
-      bench.py --gpus 2 --steps 40 --warmup 10 --source $src > $O/n2_$src.log 2>&1 || { tail -30 $O/n2_$src.log; exit 1; }
+    # host: the driver's plain command (bench.py self-launches its ranks); device: under torchrun
+    if [ $src = host ]; then
+      timeout -k 10 300 python3 bench.py --gpus 2 --steps 40 --warmup 10 --source $src > $O/n2_$src.log 2>&1 || { tail -30 $O/n2_$src.log; exit 1; }
+    else
+      timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) \
+        bench.py --gpus 2 --steps 40 --warmup 10 --source $src > $O/n2_$src.log 2>&1 || { tail -30 $O/n2_$src.log; exit 1; }
+    fi
     grep '"metric"' $O/n2_$src.log > $O/n2_$src.json
-    python3 -c "import json;d=json.load(open('$O/n2_$src.json'));x=d['extra'];c=x['xgmi_phase'];print('n2 $src', d['value'], 'cross', c['frames_per_s'], c['cross_gpu_fraction'], 'gate', x['steady_gate'], 'links', x['topology']['outgoing_links_per_rank'])"
+    python3 -c "import json;d=json.load(open('$O/n2_$src.json'));x=d['extra'];c=x['xgmi_phase'];print('n2 $src', d['value'], 'n_gpus', d['n_gpus'], 'n_ranks', d['n_ranks'], 'cross', c['frames_per_s'], c['cross_gpu_fraction'], 'checks', x['frame_checks']['frames_verified'], x['frame_checks']['frames_mismatched'], 'gate', x['steady_gate'], 'links', x['topology']['outgoing_links_per_rank'])"
   done
 fi
 if has prof; then
@@ -77,8 +83,7 @@ if has jfcm; then
   head -4 $O/prof_jf16m_cm/run_kernel_stats.csv | cut -c1-160
 fi
 if has rehearsal4; then
-  timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) \
-    bench.py --gpus 4 --steps 40 --warmup 10 --source device > $O/n4_device.log 2>&1 || { tail -30 $O/n4_device.log; exit 1; }
+  timeout -k 10 400 python3 bench.py --gpus 4 --steps 40 --warmup 10 --source device > $O/n4_device.log 2>&1 || { tail -30 $O/n4_device.log; exit 1; }
   grep '"metric"' $O/n4_device.log > $O/n4_device.json
   python3 -c "import json;d=json.load(open('$O/n4_device.json'));x=d['extra'];c=x['xgmi_phase'];print('n4 device', d['value'], 'rpg', d['config']['ranks_per_gpu'], 'batch', d['config']['global_batch'], 'streams', x['producer_streams'], 'cross', c['frames_per_s'], c['cross_gpu_fraction'], 'gate', x['steady_gate']['iterations'], x['steady_gate']['converged'])"
 fi
