@@ -779,9 +779,12 @@ __device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, const GapPre& g, 
 #define PR_CM_PLACE_CQ 4
 #endif
 #define PR_PLACE_KEEP(bit, v) (!(PR_CM_PLACEPROBE & (bit)) || __float_as_uint((v)) == 0x7fc01234u)
-// PR_CM_IMG_NT = 1 (A/B): image placement stores streaming (non-temporal) for the 128-B lines that lie
-// wholly inside one image run, plain for the lines a run shares with a gap or a neighbour tile (the
-// image form of PR_CM_NT_STORE 3; all-streaming placement stores cost 13 %, partial lines)
+// PR_CM_IMG_NT = 1 (A/B, not kept): image placement stores streaming (non-temporal) for the 128-B
+// lines that lie wholly inside one image run, plain for the lines a run shares with a gap or a
+// neighbour tile (the image form of PR_CM_NT_STORE 3; all-streaming placement stores cost 13 %).
+// Same box, 3 rounds: kernel (--mode image --no-gaps, flags 3) 5.778 / 5.795 / 5.796 vs 5.368-5.390
+// us/frame, device-resident image pipeline 125.2-126.5k vs 136.2-137.7k fr/s (profiles/r6/image/):
+// the per-chunk line test costs more issue slots than the streaming stores save.
 #ifndef PR_CM_IMG_NT
 #define PR_CM_IMG_NT 0
 #endif
