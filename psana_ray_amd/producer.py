@@ -374,6 +374,12 @@ def main(argv=None) -> int:
                     log.error("Rank %d: %d frames were not taken by any consumer within --timeout %.0f s; "
                               "exiting without them", rank, ep.undelivered(), args.timeout)
                 rc = 1
+            m = ep.metrics()
+            if m.get("frames_sent"):
+                log.info("Rank %d: fabric: %d frames sent to other processes (%d calibrated straight into the "
+                         "consumer's slot, %d of those lost with a consumer that died), %d requeued, %d checksummed",
+                         rank, m.get("frames_sent", 0), m.get("frames_direct", 0), m.get("frames_lost_direct", 0),
+                         m.get("frames_requeued", 0), m.get("frames_checksummed", 0))
             if cons_thread is not None:
                 cons_thread.join()
                 log.info("Rank %d: co-located consumer processed %d frames, %d peaks", rank,

@@ -160,3 +160,50 @@ def test_gpu_odd_sized_image_frames_cross_processes(store_port, tmp_path):  # no
     recs = records(tmp_path / "c.jsonl")
     assert sorted(frames(recs)) == list(range(30))
     assert recs[-1].get("eos") is True
+
+
+def test_gpu_direct_writes_consumer_that_leaves(store_port, tmp_path):  # noqa: F811
+    """Direct writes (csrc/fabric.h take_direct): with --route spread the producer calibrates frames
+    straight into its consumers' slots.  A consumer that CLOSES hands back the direct frames still in
+    flight by copy-back (requeued: the survivor receives them, every frame exactly once, bit-exact)."""
+    n = 200
+    prod = gpu_producer(store_port, n, "--route", "spread", queue_size=64)
+    a = consumer(store_port, tmp_path / "a.jsonl", *GPU_C, "--sleep", "0.02", "--stop_after", "10")
+    b = consumer(store_port, tmp_path / "b.jsonl", *GPU_C, "--sleep", "0.02")
+    rc_a, out_a = finish(a, 120)
+    rc_b, out_b = finish(b, 120)
+    rc_p, out_p = finish(prod, 120)
+    assert (rc_a, rc_b, rc_p) == (0, 0, 0), (out_a[-2000:], out_b[-2000:], out_p[-2000:])
+    ga, gb = frames(records(tmp_path / "a.jsonl")), frames(records(tmp_path / "b.jsonl"))
+    assert len(ga) == 10
+    assert sorted(ga + gb) == list(range(n))
+    assert _direct_frames(out_p) > 0, out_p[-2000:]
+
+
+def _direct_frames(out):
+    import re
+
+    m = re.search(r"\((\d+) calibrated straight into the consumer's slot", out)
+    return int(m.group(1)) if m else 0
+
+
+def test_gpu_direct_writes_killed_consumer(store_port, tmp_path):  # noqa: F811
+    """Direct writes with a consumer killed by -9: the frames in flight into its ring are lost with
+    its read-ahead (at most the prefetch bound), the survivor gets the rest exactly once."""
+    from psana_ray_amd.config import DEFAULT_PREFETCH
+
+    n = 240
+    prod = gpu_producer(store_port, n, "--route", "spread", queue_size=100)
+    a = consumer(store_port, tmp_path / "a.jsonl", *GPU_C, "--sleep", "0.01", "--die_after", "16")
+    b = consumer(store_port, tmp_path / "b.jsonl", *GPU_C, "--sleep", "0.01")
+    rc_a, _ = finish(a, 120)
+    assert rc_a == -9
+    rc_b, out_b = finish(b, 120)
+    rc_p, out_p = finish(prod, 120)
+    assert rc_b == 0, out_b[-3000:]
+    assert rc_p == 0, out_p[-3000:]
+    ga, gb = frames(records(tmp_path / "a.jsonl")), frames(records(tmp_path / "b.jsonl"))
+    assert not set(ga) & set(gb)
+    lost = set(range(n)) - set(ga) - set(gb)
+    assert len(lost) <= DEFAULT_PREFETCH, lost
+    assert _direct_frames(out_p) > 0, out_p[-2000:]
