@@ -25,7 +25,7 @@ namespace pr {
 namespace {
 
 constexpr uint64_t kLinkMagic = 0x314B4E494C525350ull;  // "PSRLINK1"
-constexpr int32_t kLinkVersion = 4;
+constexpr int32_t kLinkVersion = 5;
 constexpr int32_t kNoticeReturned = 1;   // the grant comes back unused (producer finished / closing)
 constexpr int32_t kNoticeReclaimed = 2;  // a returned frame was copied out: its slot is free again
 constexpr int32_t kNoticeRejected = 4;   // a returned frame was refused (EOS posted): route it elsewhere
@@ -75,6 +75,8 @@ struct alignas(64) LinkSeg {
   int32_t consumer_device;
   int32_t n_segs;
   int32_t consumer_kind;  // 0 consumer, 1 queue keeper
+  char consumer_pci[32];  // PCI bus id of the consumer ring's GPU (device indices differ between
+                          // processes whose launcher restricts the visible GPUs)
   char ring_name[128];
   SegDesc segs[QueueFabric::kMaxSegments];
   std::atomic<uint64_t> ready;
@@ -776,6 +778,10 @@ void QueueFabric::apply_ops() {
       s->consumer_pid = (int64_t)getpid();
       s->kind = export_kind_;
       s->consumer_device = device_;
+      if (device_ >= 0 && hipDeviceGetPCIBusId(s->consumer_pci, (int)sizeof(s->consumer_pci), device_) != hipSuccess) {
+        (void)hipGetLastError();
+        s->consumer_pci[0] = 0;
+      }
       s->consumer_kind = keeper_ ? 1 : 0;
       snprintf(s->ring_name, sizeof(s->ring_name), "%s", export_name_.c_str());
       s->n_segs = (int32_t)segs_.size();
@@ -841,7 +847,19 @@ bool QueueFabric::try_attach(Link& l, double now) {
       hip_check(hipSetDevice(device_), "hipSetDevice");
       int ndev = 0;
       hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
-      const int cdev = s->consumer_device;
+      // the consumer's GPU in THIS process's numbering: by PCI bus id (its own index is only
+      // meaningful when both processes see the same devices)
+      int cdev = s->consumer_device;
+      if (s->consumer_pci[0] != 0) {
+        char mine[32];
+        for (int d = 0; d < ndev; ++d)
+          if (hipDeviceGetPCIBusId(mine, (int)sizeof(mine), d) == hipSuccess && strncmp(mine, s->consumer_pci, sizeof(mine)) == 0) {
+            cdev = d;
+            break;
+          }
+        (void)hipGetLastError();
+      }
+      l.consumer_device = cdev;
       if (cdev >= 0 && cdev < ndev && cdev != device_) {
         // the copy engine / blit kernels of THIS GPU write the consumer GPU's HBM over xGMI
         int can = 0;
@@ -880,7 +898,7 @@ bool QueueFabric::try_attach(Link& l, double now) {
     return false;
   }
   l.ipc = s->kind == 1;
-  l.consumer_device = l.ipc ? s->consumer_device : -1;
+  if (!l.ipc) l.consumer_device = -1;   // IPC rings: set above, in this process's device numbering
   // the copy kernel moves 16-B words between 16-B aligned slots; a slot size that is not a multiple
   // of 16 B or a misaligned ring takes the runtime engine on this link instead -- decided here, once,
   // never after frames were handed to a copy (FrameRing pads its slots to 256 B, so its rings always
