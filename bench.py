@@ -105,6 +105,10 @@ def parse(argv=None):
                     help="hardware-queue placement of the fabric copy stream (default config.FABRIC_COPY_STREAM)")
     ap.add_argument("--fabric-copy-wgs", type=int, default=None,
                     help="fabric copy kernel workgroups per peer GPU link (default config.FABRIC_COPY_WORKGROUPS)")
+    ap.add_argument("--verify-every", type=int, default=None,
+                    help="every N-th frame a producer sends to another process carries a content checksum its "
+                         "consumer verifies (default config.FABRIC_VERIFY_EVERY = 64; 0 off; "
+                         "$PSANA_RAY_AMD_VERIFY_EVERY)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: protocol rehearsal with gloo and the golden models (tests only; not a benchmark)")
     return ap.parse_args(argv)
@@ -266,6 +270,8 @@ def main(argv=None):
     from psana_ray_amd.utils.runtime_env import select_copy_engine
 
     select_copy_engine(args.copy_engine)   # before the HIP runtime initialises (first torch.cuda call)
+    if args.verify_every is not None:
+        os.environ["PSANA_RAY_AMD_VERIFY_EVERY"] = str(max(0, args.verify_every))
     import numpy as np
     import torch
     import torch.distributed as dist
