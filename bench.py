@@ -215,13 +215,31 @@ def self_launch(n: int, argv) -> int:
     port = _free_port()
     script = os.path.abspath(__file__)
     procs = []
+
+    def die_with_parent():   # in the child, before exec: a parent killed by its caller takes its ranks along
+        try:
+            import ctypes
+
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL)   # PR_SET_PDEATHSIG
+        except Exception:
+            pass
+
     for r in range(n):
         env = dict(os.environ)
         env.update({"RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(n),
                     "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
                     "PSANA_RAY_SELF_LAUNCHED": "1"})
         procs.append(subprocess.Popen([sys.executable, script, *argv], env=env, stdout=subprocess.PIPE,
-                                      text=True, bufsize=1))
+                                      text=True, bufsize=1, preexec_fn=die_with_parent))
+
+    def on_signal(signo, frame):   # SIGTERM / SIGINT of the launcher: the ranks go too, then we do
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGKILL)
+        sys.exit(128 + signo)
+
+    signal.signal(signal.SIGTERM, on_signal)
+    signal.signal(signal.SIGINT, on_signal)
     print(f"bench.py: self-launched {n} ranks (pids {[p.pid for p in procs]}, rendezvous 127.0.0.1:{port})",
           file=sys.stderr, flush=True)
 

@@ -107,3 +107,38 @@ def test_bench_self_launch_failure_propagates(native):
            "tiny_epix", "--producers", "5"]   # invalid on every rank -> rc 2
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd="/tmp")
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+
+
+def test_bench_self_launch_ranks_die_with_the_launcher(native):
+    """A self-launched job whose parent is killed (a caller's timeout) leaves no rank running."""
+    import signal
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "100000", "--warmup", "2",
+           "--batch", "4", "--detector", "tiny_epix", "--device", "cpu", "--queue-size", "32", "--chunk", "4"]
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd="/tmp")
+    pids = []
+    t0 = time.time()
+    while time.time() - t0 < 60 and not pids:   # the parent announces its ranks' pids on stderr
+        line = p.stderr.readline()
+        if "self-launched" in line:
+            pids = [int(x) for x in line.split("pids [")[1].split("]")[0].split(",")]
+    assert len(pids) == 2, "no self-launch line"
+    time.sleep(3.0)
+    p.send_signal(signal.SIGKILL)   # the parent dies without a chance to clean up
+    p.wait(30)
+
+    def alive(pid):
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            return False
+        with open(f"/proc/{pid}/stat") as f:   # a zombie waiting for its reaper counts as gone
+            return f.read().split(")")[-1].split()[0] != "Z"
+
+    t1 = time.time()
+    while time.time() - t1 < 20 and any(alive(x) for x in pids):
+        time.sleep(0.2)
+    assert not any(alive(x) for x in pids), pids
