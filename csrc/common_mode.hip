@@ -788,6 +788,20 @@ __device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, const GapPre& g, 
 #ifndef PR_CM_IMG_NT
 #define PR_CM_IMG_NT 0
 #endif
+// PR_CM_IMG_T = 1 (A/B, not kept): column-run panels read each image chunk's four tile elements as
+// one ds_read_b128 of a tile ROW per lane and transpose 4x4 blocks in the quad with DPP (VERDICT r5
+// next #3: one LDS read per 16-B store instead of four ds_read_b32).  Bitwise (45 CM / image tests);
+// same box, 3 rounds: kernel (--mode image --no-gaps, flags 3) 5.44 / 5.44 / 5.46 vs 5.38 / 5.40 /
+// 5.40 us/frame, image pipeline 135.5k / 136.9k / 136.6k vs 139.9k / 137.8k / 136.4k fr/s
+// (profiles/r6/image_t/): the LDS reads are not what the placement waits on (cf. r5 sections 14, 19).
+#ifndef PR_CM_IMG_T
+#define PR_CM_IMG_T 0
+#endif
+// quad_perm exchange with bound_ctrl (no `old` operand to materialise)
+template <int CTRL>
+__device__ __forceinline__ float quad_x(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
 __device__ __forceinline__ void st_img4(PR_GLOBAL float* out, int32_t e, int32_t run_lo, int len, const float4 v) {
 #if PR_CM_IMG_NT
   if ((e & ~31) >= run_lo && (e | 31) < run_lo + len) {
@@ -857,6 +871,30 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
           k -= nfull;
           ++run;
         }
+      }
+    } else if (PR_CM_IMG_T && (nruns & 3) == 0) {
+      // quad transpose: lane q of a quad reads tile row (position t_lo + 4k + q) of 4 neighbouring
+      // columns as ONE ds_read_b128, the quad transposes the 4x4 block with DPP exchanges, and lane q
+      // stores chunk k of column c0 + q.  A wave takes 4 chunks x 16 columns (the shipped CQ 4 shape).
+      const int q = (int)threadIdx.x & 3, quad = ((int)threadIdx.x & 63) >> 2;
+      const int nq = (nfull + 3) >> 2, ncg = (nruns + 15) >> 4, nw = nb >> 6;
+      for (int u = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); u < ncg * nq; u += nw) {
+        const int g = u / nq, a = u - g * nq;
+        const int c0 = 16 * g + 4 * (quad & 3), k = 4 * a + (quad >> 2);
+        const bool ok = c0 < nruns && k < nfull;          // uniform over the quad
+        const int tq = t_lo + 4 * (ok ? k : 0) + q;
+        const int r = step > 0 ? tq : len - 1 - tq;
+        const float4 m = *reinterpret_cast<const float4*>(tile + r * P + (ok ? c0 : 0));
+        // (every exchange runs on all four lanes: the opaque asm keeps the compiler from sinking a
+        // DPP read into the lane-divergent select, where it would read a disabled partner)
+        const bool odd = q & 1, hi = q & 2;
+        float p0 = quad_x<0xB1>(m.x), p1 = quad_x<0xB1>(m.y), p2 = quad_x<0xB1>(m.z), p3 = quad_x<0xB1>(m.w);
+        asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3));
+        const float y0 = odd ? p1 : m.x, y1 = odd ? m.y : p0, y2 = odd ? p3 : m.z, y3 = odd ? m.w : p2;
+        float s0 = quad_x<0x4E>(y0), s1 = quad_x<0x4E>(y1), s2 = quad_x<0x4E>(y2), s3 = quad_x<0x4E>(y3);
+        asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3));
+        const float z0 = hi ? s2 : y0, z1 = hi ? s3 : y1, z2 = hi ? y2 : s0, z3 = hi ? y3 : s1;
+        if (ok) st_img4(out, ob + (c0 + q) * oo + 4 * k, (int32_t)lo + (c0 + q) * oo, len, make_float4(z0, z1, z2, z3));
       }
     } else {
       // a wave takes PR_CM_PLACE_CQ chunks (16 B each) of 64 / PR_CM_PLACE_CQ neighbouring columns
