@@ -376,6 +376,9 @@ def main(argv=None):
     share = max(1, math.ceil(args.queue_size / world))
     # slack for frames waiting to be routed / copied to another GPU
     producer_slots = (4 * args.chunk + args.batch + (64 if world > 1 else 0)) if is_prod else 0
+    if is_prod and world > 1 and gpu:
+        from psana_ray_amd.config import fabric_direct_headroom
+        producer_slots += fabric_direct_headroom(cal.out_frame_bytes)   # slots kept for direct frames (engine.h)
     # queue_size is the LOGICAL capacity (deque(maxlen), shared_queue.py:7); physical HBM slots are
     # capped by free memory (config 4: Jungfrau-16M x 400000 would need 26.8 TB)
     cslots = physical_slots(share, cal.out_frame_bytes, device, args.hbm_fraction, producer_slots)
@@ -638,6 +641,7 @@ def main(argv=None):
             # csrc/fabric.h take_direct), and direct frames lost to a consumer that left
             "frames_direct_per_rank": allsum(int(x1.get("frames_direct", 0) - x0.get("frames_direct", 0))),
             "frames_lost_direct_per_rank": allsum(int(x1.get("frames_lost_direct", 0))),
+            "direct_headroom_slots": int(getattr(getattr(prod, "engine", None), "direct_headroom", 0)),
             "copy_ms_per_batch_per_rank": cms,
             "copy_dispatch_per_rank": copy_detail,
             "link_GB_total_per_rank": per_link,

@@ -613,6 +613,9 @@ PYBIND11_MODULE(_C, m) {
       .def("set_header_rank", &pr::ProducerEngine::set_header_rank, py::arg("rank"))
       .def("set_fabric", &pr::ProducerEngine::set_fabric, py::arg("fabric").none(true))
       .def_property_readonly("direct_frames", &pr::ProducerEngine::direct_frames)
+      .def("set_direct_headroom", &pr::ProducerEngine::set_direct_headroom, py::arg("slots"), py::arg("wait_s") = 0.002)
+      .def_property_readonly("direct_wait_s", &pr::ProducerEngine::direct_wait_s)
+      .def_property_readonly("direct_headroom", &pr::ProducerEngine::direct_headroom)
       .def("set_compute_streams", &pr::ProducerEngine::set_compute_streams, py::arg("n"), py::arg("kind") = 0)
       .def_property_readonly("compute_streams", &pr::ProducerEngine::compute_streams)
       .def("request_stop", &pr::ProducerEngine::request_stop)

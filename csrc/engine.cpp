@@ -3,6 +3,7 @@
 #include "trace.h"
 
 #include <chrono>
+#include <thread>
 #include <stdexcept>
 
 #include "common.h"
@@ -488,6 +489,32 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       }
       auto t1 = clk::now();
       t_stage_ += secs(t0, t1);
+      // direct headroom: frames in LOCAL slots stay within budget - headroom, the producer budget the
+      // queue_size accounting gives (the headroom slots only carry direct frames' headers: their data
+      // sits in the consumer's ring).  While the fabric offers grants the engine takes them first,
+      // and a chunk whose local share would pass the cap waits for grants to cover it or for the
+      // local backlog to drain, whichever comes first (headroom_wait_s_ > 0: at most that long, then
+      // the chunk may use headroom slots for local frames).
+      std::vector<QueueFabric::DirectGrant> dg;
+      if (fabric_ != nullptr && headroom_ > 0) {
+        trace::Range r("producer.direct_wait");
+        const auto tw = clk::now();
+        const int64_t cap = (int64_t)pool_->producer_budget() - headroom_;
+        for (;;) {
+          const bool offering = fabric_->direct_offering();
+          if (offering) {
+            const auto more = fabric_->take_direct(n - (int)dg.size());
+            dg.insert(dg.end(), more.begin(), more.end());
+          }
+          const int64_t local =
+              (int64_t)(pool_->producer_budget() - pool_->producer_room()) - fabric_->direct_inflight();
+          if ((int)dg.size() >= n || local + (n - (int64_t)dg.size()) <= cap) break;
+          if (stop_.load() || pool_->closed()) break;
+          if (headroom_wait_s_ > 0 && offering && secs(tw, clk::now()) > headroom_wait_s_) break;
+          std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        direct_wait_s_.store(direct_wait_s_.load() + secs(tw, clk::now()));
+      }
       slots.clear();
       trace::push("producer.acquire");
       while (slots.empty() && !stop_.load()) {   // all n slots at once, one event wait per batch
@@ -500,7 +527,14 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       trace::pop();
       auto t2 = clk::now();
       t_acquire_ += secs(t1, t2);
-      if ((int)slots.size() < n) break;   // stopped while waiting
+      if ((int)slots.size() < n) {   // stopped while waiting
+        if (!dg.empty()) {
+          std::vector<int64_t> tk;
+          for (const auto& g : dg) tk.push_back(g.token);
+          fabric_->cancel_direct(tk);
+        }
+        break;
+      }
       in.resize(n);
       out.resize(n);
       if (device_resident_) {   // calibrate straight from the resident source frames
@@ -512,8 +546,7 @@ void ProducerEngine::loop(int64_t n_local_events, int64_t max_steps, int64_t k0)
       for (int q = 0; q < n; ++q) out[q] = pool_->slot_ptr(slots[q]);
       // frames with a direct grant are calibrated straight into that consumer's slot (the local slot
       // only carries the header and the queue_size accounting; QueueFabric::take_direct)
-      std::vector<QueueFabric::DirectGrant> dg;
-      if (fabric_ != nullptr) dg = fabric_->take_direct(n);   // opportunistic: never waits for grants
+      if (fabric_ != nullptr && headroom_ == 0) dg = fabric_->take_direct(n);   // opportunistic: never waits
       for (size_t q = 0; q < dg.size(); ++q) out[q] = dg[q].ptr;
       if (gpu_timing_) {
         if (device_resident_) harvest(b, false);

@@ -91,6 +91,18 @@ class ProducerEngine {
   // off).  Before start(); the fabric must outlive the run (ProducerPipeline clears it after join).
   void set_fabric(QueueFabric* f) { fabric_ = f; }
   int64_t direct_frames() const { return direct_frames_.load(); }
+  // Direct headroom (0 = off): `slots` of the producer budget are kept for direct frames; frames
+  // calibrated into LOCAL slots (the copy path's backlog) stay within budget - slots.  While the
+  // fabric offers grants, a chunk whose local share would pass that waits for grants to cover it
+  // (or for the backlog to drain) instead of queueing more frames for a second pass; wait_s > 0
+  // bounds that wait (then local frames may use headroom slots).  Before start().
+  void set_direct_headroom(int slots, double wait_s) {
+    headroom_ = slots;
+    headroom_wait_s_ = wait_s;
+  }
+  int direct_headroom() const { return headroom_; }
+  // seconds the engine waited for grants (direct headroom)
+  double direct_wait_s() const { return direct_wait_s_.load(); }
   // rank-local events [k0, n_local_events) (n_local_events < 0: endless), at most max_steps of them
   void start(int64_t n_local_events, int64_t max_steps, int64_t k0 = 0);
   void request_stop() { stop_.store(true); }
@@ -139,6 +151,9 @@ class ProducerEngine {
   int64_t rank_, size_, hdr_rank_;
   QueueFabric* fabric_ = nullptr;
   std::atomic<int64_t> direct_frames_{0};
+  int headroom_ = 0;
+  double headroom_wait_s_ = 0.002;
+  std::atomic<double> direct_wait_s_{0.0};
   std::vector<uint64_t> src_frames_;
   std::vector<double> src_pe_;
   bool device_resident_ = false;   // source frames live in this GPU's HBM: no staging copies

@@ -344,8 +344,14 @@ std::vector<QueueFabric::DirectGrant> QueueFabric::take_direct(int max_n) {
   return out;
 }
 
+bool QueueFabric::direct_offering() const {
+  const int policy = policy_.load();
+  return direct_on_ && !finished_.load() && (policy == 2 || policy == 4);
+}
+
 void QueueFabric::bind_direct(const std::vector<int>& local_slots, const std::vector<int64_t>& tokens) {
   check(local_slots.size() == tokens.size(), "QueueFabric::bind_direct: size mismatch");
+  d_inflight_.fetch_add((int64_t)tokens.size(), std::memory_order_relaxed);
   std::lock_guard<std::mutex> lk(dmu_);
   for (size_t i = 0; i < tokens.size(); ++i) {
     auto it = std::find_if(d_taken_.begin(), d_taken_.end(), [&](const auto& e) { return e.first == tokens[i]; });
@@ -1420,6 +1426,7 @@ int64_t QueueFabric::producer_pass(double now) {
     Link& l = *b.link;
     const int n = (int)b.slots.size();
     l.inflight -= n;
+    if (b.direct) d_inflight_.fetch_sub(n, std::memory_order_relaxed);   // noticed, copied back or lost
     if (l.attached && !l.dead && !l.closed) {
       finish_checksums(b);
       for (int i = 0; i < n; ++i) post_notice(l, make_notice(b.rslots[i], 0, b.hdrs[i]));
@@ -1477,42 +1484,52 @@ int64_t QueueFabric::producer_pass(double now) {
   // 4. route produced frames (FIFO) to this process's own consumer or to granted remote slots.
   //    Keeper links are the last resort: a frame goes there only when no real consumer (and not
   //    this process's own) has credit for it.
-  std::vector<int> offers = pool_->produced(kMaxDispatch);
   if (direct_on_) {
     work += direct_pass();
-    // frames bound to a direct grant go to that grant's consumer, whatever the policy says now
+    // frames bound to a direct grant go to that grant's consumer, whatever the policy says now --
+    // every committed one, wherever it sits in the produced FIFO (behind a copy backlog longer than
+    // one pass's kMaxDispatch offers, a bound frame would hold its grant until the backlog drained,
+    // and a backlog that needs those grants would never drain)
     std::vector<Batch> db;
     {
       std::lock_guard<std::mutex> lk(dmu_);
-      if (!d_bound_.empty()) {
-        std::vector<int> rest;
-        for (int sl : offers) {
-          auto it = std::find_if(d_bound_.begin(), d_bound_.end(), [&](const auto& e) { return e.first == sl; });
-          if (it == d_bound_.end()) {
-            rest.push_back(sl);
-            continue;
-          }
-          Batch* b = nullptr;
-          for (Batch& x : db)
-            if (x.link == it->second.link) b = &x;
-          if (b == nullptr) {
-            db.emplace_back();
-            b = &db.back();
-            b->link = it->second.link;
-            b->t_issue = now;
-          }
-          b->slots.push_back(sl);
-          b->rslots.push_back(it->second.rslot);
-          --it->second.link->direct;
-          d_bound_.erase(it);
+      for (auto it = d_bound_.begin(); it != d_bound_.end();) {
+        if (pool_->state(it->first) != kProduced) {   // not committed yet
+          ++it;
+          continue;
         }
-        offers.swap(rest);
+        Batch* b = nullptr;
+        for (Batch& x : db)
+          if (x.link == it->second.link) b = &x;
+        if (b == nullptr) {
+          db.emplace_back();
+          b = &db.back();
+          b->link = it->second.link;
+          b->t_issue = now;
+        }
+        b->slots.push_back(it->first);
+        b->rslots.push_back(it->second.rslot);
+        --it->second.link->direct;
+        it = d_bound_.erase(it);
       }
     }
     if (!db.empty()) {
       for (Batch& b : db) b.hdrs = pool_->headers(b.slots);
       for (const Batch& b : db) work += (int64_t)b.slots.size();
       issue_direct(db);
+    }
+  }
+  std::vector<int> offers = pool_->produced(kMaxDispatch);
+  if (direct_on_) {
+    // a frame bound after the scan above and committed before produced() is still in d_bound_ (the
+    // engine binds before it commits): never route it as a copy; the next pass issues it
+    std::lock_guard<std::mutex> lk(dmu_);
+    if (!d_bound_.empty()) {
+      std::vector<int> rest;
+      for (int sl : offers)
+        if (std::find_if(d_bound_.begin(), d_bound_.end(), [&](const auto& e) { return e.first == sl; }) == d_bound_.end())
+          rest.push_back(sl);
+      offers.swap(rest);
     }
   }
   int64_t local_credit = (is_consumer_ && !consumer_closed_.load() && policy != 3) ? pool_->credits() : 0;

@@ -244,6 +244,9 @@ class QueueFabric {
   // notice once its calibration completed -- no copy pass.  Frames produced without a direct grant
   // keep the copy path.  A consumer that dies or closes while a direct frame is in flight loses
   // that frame (its data exists only in that consumer's ring; counted as frames_lost_direct).
+  // Bound frames are issued as soon as they are committed, wherever they sit in the produced FIFO.
+  // With the engine's direct headroom (engine.h) the engine waits for grants rather than queue
+  // copies, which makes nearly every routed frame direct.
   struct DirectGrant {
     int64_t token;
     uint64_t ptr;
@@ -254,6 +257,10 @@ class QueueFabric {
   void bind_direct(const std::vector<int>& local_slots, const std::vector<int64_t>& tokens);
   void cancel_direct(const std::vector<int64_t>& tokens);   // taken and never launched
   static constexpr int kDirectPool = 128;
+  // grants are on offer now (direct on, policy spread / remote_only, producer not finished)
+  bool direct_offering() const;
+  // direct frames that hold a local slot (bound to a grant, or dispatched and not yet complete)
+  int64_t direct_inflight() const { return d_inflight_.load(std::memory_order_relaxed); }
 
   void start();
   void request_stop() { stop_.store(true); }
@@ -344,6 +351,7 @@ class QueueFabric {
   std::vector<std::pair<int64_t, DirectRec>> d_taken_, d_cancel_;
   std::vector<std::pair<int, DirectRec>> d_bound_;   // local slot -> grant
   int64_t d_next_ = 1;
+  std::atomic<int64_t> d_inflight_{0};
   int xstream_kind_ = 1;            // kStreamDedicated
   std::vector<hipEvent_t> free_events_, all_events_;
   std::vector<hipEvent_t> free_timed_;          // timing-enabled events (copy groups)

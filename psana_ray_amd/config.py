@@ -134,6 +134,33 @@ def fabric_direct() -> bool:
     return FABRIC_DIRECT if not v else v not in ("0", "false", "off")
 
 
+# Direct headroom (csrc/engine.h set_direct_headroom): producer slots kept for direct frames; frames
+# in local slots (the copy path's backlog) stay within the rest of the budget (the one queue_size
+# gives), and while grants are on offer a chunk that would pass it waits for grants (or for the
+# backlog to drain; FABRIC_DIRECT_WAIT_S > 0 bounds the wait).  Producers that route to other
+# processes add it to their slot budget (bench.py, psana-ray-producer), at most
+# FABRIC_DIRECT_HEADROOM_BYTES of HBM.  Env overrides: PSANA_RAY_AMD_FABRIC_DIRECT_HEADROOM (slots;
+# 0 = off: direct grants only when on offer at launch), PSANA_RAY_AMD_FABRIC_DIRECT_WAIT_S.
+FABRIC_DIRECT_HEADROOM = 384
+FABRIC_DIRECT_HEADROOM_BYTES = 8 << 30
+FABRIC_DIRECT_WAIT_S = 0.0
+
+
+def fabric_direct_headroom(frame_bytes: Optional[int] = None) -> int:
+    if not fabric_direct():
+        return 0
+    v = os.environ.get("PSANA_RAY_AMD_FABRIC_DIRECT_HEADROOM", "").strip()
+    n = max(0, int(v)) if v else FABRIC_DIRECT_HEADROOM
+    if frame_bytes:
+        n = min(n, FABRIC_DIRECT_HEADROOM_BYTES // max(1, int(frame_bytes)))
+    return n
+
+
+def fabric_direct_wait_s() -> float:
+    v = os.environ.get("PSANA_RAY_AMD_FABRIC_DIRECT_WAIT_S", "").strip()
+    return max(0.0, float(v)) if v else FABRIC_DIRECT_WAIT_S
+
+
 def fabric_verify_every() -> int:
     v = os.environ.get("PSANA_RAY_AMD_VERIFY_EVERY", "")
     return max(0, int(v)) if v.strip() else FABRIC_VERIFY_EVERY

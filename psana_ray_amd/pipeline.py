@@ -169,6 +169,10 @@ class ProducerPipeline:
                 # frames routed to other processes are calibrated straight into their consumer's
                 # slot (csrc/fabric.h take_direct); cleared after the engine stopped (_run_engine)
                 self.engine.set_fabric(fab)
+                from .config import fabric_direct_headroom, fabric_direct_wait_s
+                head = fabric_direct_headroom()
+                if head > 0 and ring.pool.producer_budget - head >= 2 * self.chunk:
+                    self.engine.set_direct_headroom(head, fabric_direct_wait_s())
 
     # --------------------------------------------------------------------------------
     def _acquire(self, n: int, stream) -> List[int]:

@@ -296,6 +296,9 @@ def main(argv=None) -> int:
     chunk = max(1, int(args.chunk))
     share = max(1, math.ceil(args.queue_size / size))
     pslots = args.producer_slots if args.producer_slots is not None else max(share, 2 * chunk)
+    if args.producer_slots is None and args.route == "spread" and device.type == "cuda":
+        from .config import fabric_direct_headroom
+        pslots += fabric_direct_headroom(frame_bytes)   # slots kept for direct frames (csrc/engine.h)
     try:
         if args.local or (size == 1 and args.num_consumers == 0):
             if not co_consumer:

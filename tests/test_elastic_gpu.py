@@ -12,10 +12,11 @@ from tests.test_elastic_queue import consumer, finish, frames, records, store_po
 pytestmark = pytest.mark.gpu
 
 
-def gpu_producer(port, n_events, *extra, queue_size=16, chunk=4, timeout=60):
+def gpu_producer(port, n_events, *extra, queue_size=16, chunk=4, timeout=60, env=None):
     from tests.test_elastic_queue import producer
 
-    p = producer(port, n_events, "--device", "cuda:0", *extra, queue_size=queue_size, chunk=chunk, timeout=timeout)
+    p = producer(port, n_events, "--device", "cuda:0", *extra, queue_size=queue_size, chunk=chunk, timeout=timeout,
+                 env=env)
     return p
 
 
@@ -162,12 +163,16 @@ def test_gpu_odd_sized_image_frames_cross_processes(store_port, tmp_path):  # no
     assert recs[-1].get("eos") is True
 
 
-def test_gpu_direct_writes_consumer_that_leaves(store_port, tmp_path):  # noqa: F811
+@pytest.mark.parametrize("headroom", ["", "0"])
+def test_gpu_direct_writes_consumer_that_leaves(store_port, tmp_path, headroom):  # noqa: F811
     """Direct writes (csrc/fabric.h take_direct): with --route spread the producer calibrates frames
     straight into its consumers' slots.  A consumer that CLOSES hands back the direct frames still in
-    flight by copy-back (requeued: the survivor receives them, every frame exactly once, bit-exact)."""
+    flight by copy-back (requeued: the survivor receives them, every frame exactly once, bit-exact).
+    headroom "" = the default (config.FABRIC_DIRECT_HEADROOM slots kept for direct frames, the engine
+    waits for grants, engine.h), "0" = grants only when on offer at launch."""
     n = 200
-    prod = gpu_producer(store_port, n, "--route", "spread", queue_size=64)
+    prod = gpu_producer(store_port, n, "--route", "spread", queue_size=64,
+                        env={"PSANA_RAY_AMD_FABRIC_DIRECT_HEADROOM": headroom})
     a = consumer(store_port, tmp_path / "a.jsonl", *GPU_C, "--sleep", "0.02", "--stop_after", "10")
     b = consumer(store_port, tmp_path / "b.jsonl", *GPU_C, "--sleep", "0.02")
     rc_a, out_a = finish(a, 120)
@@ -187,13 +192,15 @@ def _direct_frames(out):
     return int(m.group(1)) if m else 0
 
 
-def test_gpu_direct_writes_killed_consumer(store_port, tmp_path):  # noqa: F811
+@pytest.mark.parametrize("headroom", ["", "0"])
+def test_gpu_direct_writes_killed_consumer(store_port, tmp_path, headroom):  # noqa: F811
     """Direct writes with a consumer killed by -9: the frames in flight into its ring are lost with
     its read-ahead (at most the prefetch bound), the survivor gets the rest exactly once."""
     from psana_ray_amd.config import DEFAULT_PREFETCH
 
     n = 240
-    prod = gpu_producer(store_port, n, "--route", "spread", queue_size=100)
+    prod = gpu_producer(store_port, n, "--route", "spread", queue_size=100,
+                        env={"PSANA_RAY_AMD_FABRIC_DIRECT_HEADROOM": headroom})
     a = consumer(store_port, tmp_path / "a.jsonl", *GPU_C, "--sleep", "0.01", "--die_after", "16")
     b = consumer(store_port, tmp_path / "b.jsonl", *GPU_C, "--sleep", "0.01")
     rc_a, _ = finish(a, 120)

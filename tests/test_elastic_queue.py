@@ -52,13 +52,14 @@ def store_port():
         p.kill()
 
 
-def producer(port, n_events, *extra, queue_size=16, chunk=4, timeout=60, detector="tiny_epix", mode="calib"):
+def producer(port, n_events, *extra, queue_size=16, chunk=4, timeout=60, detector="tiny_epix", mode="calib", env=None):
     cmd = [sys.executable, "-m", "psana_ray_amd.producer", "--exp", "synthetic", "--run", "2", "--detector_name",
            detector, *(("--calib",) if mode == "calib" else ()), "--device", "cpu", "--ray_address", f"127.0.0.1:{port}",
            "--num_events",
            str(n_events), "--queue_size", str(queue_size), "--chunk", str(chunk), "--timeout", str(timeout),
            "--metrics_interval", "0", "--log_level", "INFO", *extra]
-    return subprocess.Popen(cmd, env=ENV, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    return subprocess.Popen(cmd, env={**ENV, **(env or {})}, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                            text=True)
 
 
 def consumer(port, out, *extra):
