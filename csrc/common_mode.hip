@@ -779,12 +779,15 @@ __device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, const GapPre& g, 
 #define PR_CM_PLACE_CQ 4
 #endif
 #define PR_PLACE_KEEP(bit, v) (!(PR_CM_PLACEPROBE & (bit)) || __float_as_uint((v)) == 0x7fc01234u)
-// PR_CM_IMG_NT = 1 (A/B, not kept): image placement stores streaming (non-temporal) for the 128-B
+// PR_CM_IMG_NT (A/B, not kept; bit 1 = row-run panels, bit 2 = column-run panels, 3 = both): image
+// placement stores streaming (non-temporal) for the 128-B
 // lines that lie wholly inside one image run, plain for the lines a run shares with a gap or a
 // neighbour tile (the image form of PR_CM_NT_STORE 3; all-streaming placement stores cost 13 %).
 // Same box, 3 rounds: kernel (--mode image --no-gaps, flags 3) 5.778 / 5.795 / 5.796 vs 5.368-5.390
 // us/frame, device-resident image pipeline 125.2-126.5k vs 136.2-137.7k fr/s (profiles/r6/image/):
-// the per-chunk line test costs more issue slots than the streaming stores save.
+// the per-chunk line test costs more issue slots than the streaming stores save.  Split by panel
+// kind (profiles/r6/image_ntrc/): row-run panels only 5.34-5.37 (neutral), column-run panels only
+// 5.88-5.97 -- there every line arrives as two half-line streaming writes from two instructions.
 #ifndef PR_CM_IMG_NT
 #define PR_CM_IMG_NT 0
 #endif
@@ -802,9 +805,10 @@ template <int CTRL>
 __device__ __forceinline__ float quad_x(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
+template <int NTMASK = 3>
 __device__ __forceinline__ void st_img4(PR_GLOBAL float* out, int32_t e, int32_t run_lo, int len, const float4 v) {
 #if PR_CM_IMG_NT
-  if ((e & ~31) >= run_lo && (e | 31) < run_lo + len) {
+  if ((PR_CM_IMG_NT & NTMASK) && (e & ~31) >= run_lo && (e | 31) < run_lo + len) {
     f32x4_t x;
     x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
     __builtin_nontemporal_store(x, (PR_GLOBAL f32x4_t*)(out + e));
@@ -864,7 +868,7 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
       for (; run < nruns;) {
         const float* tp = tb + run * P + 4 * k * di;
         const float4 v4 = make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]);
-        if (PR_PLACE_KEEP(2, v4.x)) st_img4(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4);
+        if (PR_PLACE_KEEP(2, v4.x)) st_img4<1>(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4);
         run += drun;
         k += dk;
         if (k >= nfull) {
@@ -908,7 +912,7 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
         if (k < nfull) {
           const float* tp = tb + run + 4 * k * di;
           const float4 v4 = make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]);
-          if (PR_PLACE_KEEP(4, v4.x)) st_img4(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4);
+          if (PR_PLACE_KEEP(4, v4.x)) st_img4<2>(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4);
         }
         a += da;
         w += dw;
