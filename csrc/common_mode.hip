@@ -779,17 +779,19 @@ __device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, const GapPre& g, 
 #define PR_CM_PLACE_CQ 4
 #endif
 #define PR_PLACE_KEEP(bit, v) (!(PR_CM_PLACEPROBE & (bit)) || __float_as_uint((v)) == 0x7fc01234u)
-// PR_CM_IMG_NT (A/B, not kept; bit 1 = row-run panels, bit 2 = column-run panels, 3 = both): image
-// placement stores streaming (non-temporal) for the 128-B
+// PR_CM_IMG_NT (bit 1 = row-run panels, bit 2 = column-run panels; shipped 3 with PR_CM_PLACE_LA):
+// image placement stores streaming (non-temporal) for the 128-B
 // lines that lie wholly inside one image run, plain for the lines a run shares with a gap or a
 // neighbour tile (the image form of PR_CM_NT_STORE 3; all-streaming placement stores cost 13 %).
-// Same box, 3 rounds: kernel (--mode image --no-gaps, flags 3) 5.778 / 5.795 / 5.796 vs 5.368-5.390
-// us/frame, device-resident image pipeline 125.2-126.5k vs 136.2-137.7k fr/s (profiles/r6/image/):
-// the per-chunk line test costs more issue slots than the streaming stores save.  Split by panel
-// kind (profiles/r6/image_ntrc/): row-run panels only 5.34-5.37 (neutral), column-run panels only
-// 5.88-5.97 -- there every line arrives as two half-line streaming writes from two instructions.
+// With the round-5 column walk (a wave: 4 chunks x 16 runs) it LOST: kernel (--mode image --no-gaps,
+// flags 3) 5.78-5.80 vs 5.37-5.39 us/frame, image pipeline 125.2-126.5k vs 136.2-137.7k fr/s
+// (profiles/r6/image/); split by panel kind (profiles/r6/image_ntrc/) row-run panels only 5.34-5.37
+// (neutral), column-run panels only 5.88-5.97: every line arrived as two half-line streaming writes
+// from two instructions.  With the line-aligned column walk (PR_CM_PLACE_LA: each store instruction
+// writes 8 whole lines) it WINS: flags 0 4.60-4.64 vs 5.05-5.08, flags 3 5.32 vs 5.38-5.40, image
+// pipeline 142.8-146.8k vs 136.0-137.8k (profiles/r6/image_la/; line-aligned alone: neutral).
 #ifndef PR_CM_IMG_NT
-#define PR_CM_IMG_NT 0
+#define PR_CM_IMG_NT 3
 #endif
 // PR_CM_IMG_T = 1 (A/B, not kept): column-run panels read each image chunk's four tile elements as
 // one ds_read_b128 of a tile ROW per lane and transpose 4x4 blocks in the quad with DPP (VERDICT r5
@@ -800,15 +802,21 @@ __device__ __forceinline__ void cm_fill_gaps(const ImgOut& io, const GapPre& g, 
 #ifndef PR_CM_IMG_T
 #define PR_CM_IMG_T 0
 #endif
+// Column-run panels, line-aligned walk (see cm_place); 0 = the round-5 walk (PR_CM_PLACE_CQ chunks
+// x 64 / CQ runs per wave, lines split between instructions)
+#ifndef PR_CM_PLACE_LA
+#define PR_CM_PLACE_LA 1
+#endif
 // quad_perm exchange with bound_ctrl (no `old` operand to materialise)
 template <int CTRL>
 __device__ __forceinline__ float quad_x(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 template <int NTMASK = 3>
-__device__ __forceinline__ void st_img4(PR_GLOBAL float* out, int32_t e, int32_t run_lo, int len, const float4 v) {
+__device__ __forceinline__ void st_img4(PR_GLOBAL float* out, int32_t e, int32_t run_lo, int len, const float4 v,
+                                        bool nt) {
 #if PR_CM_IMG_NT
-  if ((PR_CM_IMG_NT & NTMASK) && (e & ~31) >= run_lo && (e | 31) < run_lo + len) {
+  if ((PR_CM_IMG_NT & NTMASK) && nt && (e & ~31) >= run_lo && (e | 31) < run_lo + len) {
     f32x4_t x;
     x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
     __builtin_nontemporal_store(x, (PR_GLOBAL f32x4_t*)(out + e));
@@ -817,8 +825,9 @@ __device__ __forceinline__ void st_img4(PR_GLOBAL float* out, int32_t e, int32_t
 #endif
   st_out4<2>((PR_GLOBAL float4*)(out + e), v);
 }
+// nt = false: plain stores only (a frame for another process's ring, as cm_flush)
 __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C, const ImgOut& io, int panel, int y0,
-                                         int x0, PR_GLOBAL float* out) {
+                                         int x0, PR_GLOBAL float* out, bool nt) {
   const int32_t* d = io.desc + 3 * panel;
   const int sy = d[1], sx = d[2];
   const int64_t b0 = (int64_t)d[0] + (int64_t)y0 * sy + (int64_t)x0 * sx;
@@ -868,12 +877,29 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
       for (; run < nruns;) {
         const float* tp = tb + run * P + 4 * k * di;
         const float4 v4 = make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]);
-        if (PR_PLACE_KEEP(2, v4.x)) st_img4<1>(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4);
+        if (PR_PLACE_KEEP(2, v4.x)) st_img4<1>(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4, nt);
         run += drun;
         k += dk;
         if (k >= nfull) {
           k -= nfull;
           ++run;
+        }
+      }
+    } else if (PR_CM_PLACE_LA) {
+      // line-aligned: a wave takes 8 runs x one 128-B image line each (lane = run offset x chunk of
+      // the line), so a store instruction writes 8 whole lines instead of 16 half lines (the runs'
+      // line phases differ: each lane locates its chunk from its run's own phase)
+      const int lane = (int)threadIdx.x & 63, ro = lane >> 3, j = lane & 7;
+      const int nrg = (nruns + 7) >> 3, ng = (nfull + 14) >> 3, nw = nb >> 6;
+      for (int u = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); u < nrg * ng; u += nw) {
+        const int rg = u / ng, g = u - rg * ng;
+        const int run = 8 * rg + ro;
+        const int32_t a0 = ob + run * oo;             // chunk 0 of this run (16-B aligned)
+        const int k = 8 * g - ((a0 >> 2) & 7) + j;    // this lane's chunk: line g of the run
+        if (run < nruns && k >= 0 && k < nfull) {
+          const float* tp = tb + run + 4 * k * di;
+          const float4 v4 = make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]);
+          st_img4<2>(out, a0 + 4 * k, (int32_t)lo + run * oo, len, v4, nt);
         }
       }
     } else if (PR_CM_IMG_T && (nruns & 3) == 0) {
@@ -898,7 +924,7 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
         float s0 = quad_x<0x4E>(y0), s1 = quad_x<0x4E>(y1), s2 = quad_x<0x4E>(y2), s3 = quad_x<0x4E>(y3);
         asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3));
         const float z0 = hi ? s2 : y0, z1 = hi ? s3 : y1, z2 = hi ? y2 : s0, z3 = hi ? y3 : s1;
-        if (ok) st_img4(out, ob + (c0 + q) * oo + 4 * k, (int32_t)lo + (c0 + q) * oo, len, make_float4(z0, z1, z2, z3));
+        if (ok) st_img4(out, ob + (c0 + q) * oo + 4 * k, (int32_t)lo + (c0 + q) * oo, len, make_float4(z0, z1, z2, z3), nt);
       }
     } else {
       // a wave takes PR_CM_PLACE_CQ chunks (16 B each) of 64 / PR_CM_PLACE_CQ neighbouring columns
@@ -912,7 +938,7 @@ __device__ __forceinline__ void cm_place(const float* tile, int P, int R, int C,
         if (k < nfull) {
           const float* tp = tb + run + 4 * k * di;
           const float4 v4 = make_float4(tp[0], tp[di], tp[2 * di], tp[3 * di]);
-          if (PR_PLACE_KEEP(4, v4.x)) st_img4<2>(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4);
+          if (PR_PLACE_KEEP(4, v4.x)) st_img4<2>(out, ob + run * oo + 4 * k, (int32_t)lo + run * oo, len, v4, nt);
         }
         a += da;
         w += dw;
@@ -953,7 +979,7 @@ __device__ __forceinline__ void cm_write_out(const float* tile, int P, int R, in
   __syncthreads();
   mark(9);
   if (io.desc != nullptr) {
-    cm_place(tile, P, R, C, io, panel, y0, x0, out);
+    cm_place(tile, P, R, C, io, panel, y0, x0, out, nt);
     mark(10);
     cm_fill_gaps(io, gp, out);
   } else {
