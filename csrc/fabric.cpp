@@ -314,6 +314,7 @@ QueueFabric::QueueFabric(SlotPool* pool, int64_t slot_bytes, int device, bool is
     if (is_consumer) pool_->set_verifier(verifier_);
   }
   if (const char* e = getenv("PSANA_RAY_AMD_FAULT_CORRUPT")) corrupt_every_ = std::max(0L, atol(e));
+  if (const char* e = getenv("PSANA_RAY_AMD_DIRECT_FENCE")) direct_fence_ = atoi(e);
   register_native_thread_owner(this, [this] { halt(); });
 }
 
@@ -445,7 +446,8 @@ void QueueFabric::issue_direct(std::vector<Batch>& db) {
   pool_->begin_send_batch(all, reinterpret_cast<uint64_t>(xstream_));
   bool peer_gpu = false;   // a ring on another GPU was written: write back L2 lines of peer memory
   for (const Batch& b : db) peer_gpu |= b.link->consumer_device >= 0 && b.link->consumer_device != device_;
-  if (peer_gpu) launch_release_fence(reinterpret_cast<uint64_t>(xstream_));
+  if (peer_gpu || (direct_fence_ & 1)) launch_release_fence(reinterpret_cast<uint64_t>(xstream_));
+  if (direct_fence_ & 2) launch_acquire_fence(reinterpret_cast<uint64_t>(xstream_));
   int64_t n = 0;
   for (Batch& b : db) {
     b.direct = true;   // before the checksums: they must read the frames in the consumer's ring

@@ -339,6 +339,7 @@ class QueueFabric {
   int verify_every_ = 0;
   std::shared_ptr<FrameVerifier> verifier_;
   int64_t corrupt_every_ = 0, corrupt_count_ = 0;   // test-only fault injection
+  int direct_fence_ = 0;   // diagnostic (PSANA_RAY_AMD_DIRECT_FENCE): 1 release, 2 acquire around direct frames
   // direct grants (take_direct / bind_direct): offered, taken by the engine, bound to a local slot.
   // Every transition under dmu_; only the fabric thread adds offers or resolves them.
   struct DirectRec {

@@ -46,14 +46,25 @@ FrameVerifier::~FrameVerifier() {
   }
   for (auto e : free_ev_) (void)hipEventDestroy(e);
   (void)hipDeviceSynchronize();
+  for (auto e : row_ev_)
+    if (e != nullptr) (void)hipEventDestroy(e);
   if (part_) (void)hipFree(part_);
   if (results_) (void)hipHostFree(results_);
 }
 
-int64_t FrameVerifier::take_row() {
+void FrameVerifier::launch_row(const CkFrames& a, int n, int64_t base, uint64_t stream) {
   const int64_t r = row_;
   row_ = (row_ + 1) % kRows;
-  return r;
+  if (row_ev_.empty()) row_ev_.assign(kRows, nullptr);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (row_ev_[(size_t)r] != nullptr) {
+    hip_check(hipStreamWaitEvent(s, row_ev_[(size_t)r], 0), "hipStreamWaitEvent (verify row)");
+  } else {
+    hip_check(hipEventCreateWithFlags(&row_ev_[(size_t)r], hipEventDisableTiming), "hipEventCreate (verify row)");
+  }
+  launch_frame_checksums(a, n, bytes_ / 16, reinterpret_cast<uint64_t>(part_ + r * kMaxFrames * kCkPartials),
+                         reinterpret_cast<uint64_t>(results_ + base), stream);
+  hip_check(hipEventRecord(row_ev_[(size_t)r], s), "hipEventRecord (verify row)");
 }
 
 int64_t FrameVerifier::take_results(int n) {
@@ -70,11 +81,8 @@ int64_t FrameVerifier::checksum_async(const std::vector<uint64_t>& ptrs, uint64_
   for (size_t i = 0; i < ptrs.size(); ++i) a.ptr[i] = ptrs[i];
   std::lock_guard<std::mutex> lk(mu_);
   const int64_t base = take_results((int)ptrs.size());
-  const int64_t row = take_row();
   DeviceGuard dg(device_);
-  launch_frame_checksums(a, (int)ptrs.size(), bytes_ / 16,
-                         reinterpret_cast<uint64_t>(part_ + row * kMaxFrames * kCkPartials),
-                         reinterpret_cast<uint64_t>(results_ + base), stream);
+  launch_row(a, (int)ptrs.size(), base, stream);
   return base;
 }
 
@@ -135,9 +143,7 @@ void FrameVerifier::verify(const std::vector<uint64_t>& ptrs, const std::vector<
     CkFrames a{};
     for (size_t i = 0; i < n; ++i) a.ptr[i] = ptrs[a0 + i];
     const int64_t base = take_results((int)n);
-    const int64_t row = take_row();
-    launch_frame_checksums(a, (int)n, bytes_ / 16, reinterpret_cast<uint64_t>(part_ + row * kMaxFrames * kCkPartials),
-                           reinterpret_cast<uint64_t>(results_ + base), stream);
+    launch_row(a, (int)n, base, stream);
     Pending p;
     if (free_ev_.empty()) {
       hip_check(hipEventCreateWithFlags(&p.ev, hipEventDisableTiming), "hipEventCreate (verify)");

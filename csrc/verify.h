@@ -97,7 +97,7 @@ class FrameVerifier {
   std::array<int64_t, 4> counts();
 
   static constexpr int kRows = 64;          // scratch rows (rotating, one per launch)
-  static constexpr int kResults = 16384;    // pinned results (rotating)
+  static constexpr int kResults = 65536;    // pinned results (rotating)
 
  private:
   struct Pending {
@@ -105,7 +105,8 @@ class FrameVerifier {
     int64_t base;
     std::vector<int64_t> expect, gevt;
   };
-  int64_t take_row();
+  // one checksum launch (mu_ held): a scratch row, ordered after that row's previous launch
+  void launch_row(const CkFrames& a, int n, int64_t base, uint64_t stream);
   int64_t take_results(int n);
   void settle(bool wait);   // compare pending results whose launch completed (all, if wait); mu_ held
   int device_;
@@ -114,6 +115,11 @@ class FrameVerifier {
   int64_t* results_ = nullptr;     // pinned host: kResults
   std::deque<Pending> pending_;
   std::vector<hipEvent_t> free_ev_;
+  // per scratch row: an event after its last launch.  Producer checksums (the fabric's copy stream)
+  // and consumer checks (read streams) share the rows, so a row's next launch, on whatever stream,
+  // waits for its previous one on the device (rows recycled after kRows launches were otherwise
+  // overwritten by a launch on another stream while still in use: wrong sums, false mismatches)
+  std::vector<hipEvent_t> row_ev_;
   std::mutex mu_;
   int64_t row_ = 0, res_next_ = 0;
   bool acquire_on_ = true;
