@@ -123,7 +123,10 @@ def test_two_ranks_one_gpu_frames_verified(native, direct):
     assert fc["frames_verified"] > 0 and fc["frames_mismatched"] == 0, fc
     assert x["cross_gpu_fraction"] >= 0.9
     if direct == "1":
-        assert sum(x["frames_direct_per_rank"]) > 0, x
+        # direct headroom (engine.h): the producers wait for grants rather than queue copies, so
+        # most routed frames are calibrated straight into the consumer's slot (92-98 % measured)
+        assert x["direct_headroom_slots"] > 0, x
+        assert sum(x["frames_direct_per_rank"]) >= 0.6 * sum(x["frames_sent_per_rank"]), x
     else:
         assert sum(x["frames_direct_per_rank"]) == 0, x
 
