@@ -6,7 +6,7 @@ and every Markdown file stay as they are.  Every other file of a directory is pa
 directory's ``ARCHIVE.jsonl`` (one line per file: {"file": name, "text": contents}), so a cited
 directory still exists and still holds its numbers.
 
-    python tools/profiles_archive.py pack            # rewrite the tree (git rm / add by hand)
+    python tools/profiles_archive.py pack [DIR...]   # rewrite the tree, or only DIRs (git rm / add by hand)
     python tools/profiles_archive.py unpack DIR      # restore DIR's files next to its archive
     python tools/profiles_archive.py cat DIR/FILE    # print one packed file
 """
@@ -40,12 +40,16 @@ def cited(tracked):
     return keep
 
 
-def pack():
+def pack(dirs=()):
+    """Every directory of profiles/ (no ``dirs``), or only the given directories."""
     tracked = subprocess.run(["git", "ls-files"], cwd=ROOT, capture_output=True, text=True, check=True).stdout.split()
     keep = cited(tracked)
+    want = {d.rstrip("/") for d in dirs}
     groups = {}
     for f in tracked:
         if f.startswith("profiles/") and f not in keep and not f.endswith("ARCHIVE.jsonl"):
+            if want and not any(f.startswith(d + "/") for d in want):
+                continue
             groups.setdefault(os.path.dirname(f), []).append(f)
     for d, fs in sorted(groups.items()):
         arc = ROOT / d / "ARCHIVE.jsonl"
@@ -80,4 +84,4 @@ def cat(path):
 if __name__ == "__main__":
     if len(sys.argv) < 2:
         raise SystemExit(__doc__)
-    {"pack": lambda: pack(), "unpack": lambda: unpack(sys.argv[2]), "cat": lambda: cat(sys.argv[2])}[sys.argv[1]]()
+    {"pack": lambda: pack(sys.argv[2:]), "unpack": lambda: unpack(sys.argv[2]), "cat": lambda: cat(sys.argv[2])}[sys.argv[1]]()
