@@ -170,7 +170,7 @@ class ProducerPipeline:
                 # slot (csrc/fabric.h take_direct); cleared after the engine stopped (_run_engine)
                 self.engine.set_fabric(fab)
                 from .config import fabric_direct_headroom, fabric_direct_wait_s
-                head = fabric_direct_headroom()
+                head = fabric_direct_headroom(ring.frame_bytes)   # the byte cap bench / the CLI sized the ring with
                 if head > 0 and ring.pool.producer_budget - head >= 2 * self.chunk:
                     self.engine.set_direct_headroom(head, fabric_direct_wait_s())
 
